@@ -1,0 +1,431 @@
+// Torch bindings for the ps_amd HIP kernels (module ps_amd._C).
+//
+// Every op validates device / dtype / contiguity / sizes on the host BEFORE launching, so a
+// shape mismatch is a Python exception, never an out-of-bounds access on the GPU.  Launches
+// go to the caller's current HIP stream (c10::hip::getCurrentHIPStream), so the ops compose
+// with torch streams, events and HIP-graph capture.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "psamd_launch.h"
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+int dcode(const Tensor& t, const char* name) {
+  if (t.scalar_type() == torch::kFloat32) return 0;
+  if (t.scalar_type() == torch::kBFloat16) return 1;
+  TORCH_CHECK(false, name, ": dtype must be float32 or bfloat16, got ", t.scalar_type());
+  return -1;
+}
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_f32(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+}
+
+void check_i64(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kInt64, name, " must be int64");
+}
+
+template <typename T>
+T* opt_ptr(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? static_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------------------ optimizers
+void fused_opt(int64_t kind, Tensor w, c10::optional<Tensor> st0, c10::optional<Tensor> st1, Tensor g,
+               c10::optional<Tensor> wout, double lr, double beta1, double beta2, double eps, double wd,
+               double momentum, double dampening, bool nesterov, bool adamw, double bc1, double bc2, double l1,
+               double l2, double fbeta, int64_t ftrl_mode, double gscale, c10::optional<Tensor> gscale_t) {
+  check_f32(w, "w");
+  check_gpu(g, "g");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n, "grad numel ", g.numel(), " != weight numel ", n);
+  if (st0.has_value() && st0->defined()) { check_f32(*st0, "st0"); TORCH_CHECK(st0->numel() == n, "st0 size"); }
+  if (st1.has_value() && st1->defined()) { check_f32(*st1, "st1"); TORCH_CHECK(st1->numel() == n, "st1 size"); }
+  if ((kind == 1 || kind == 3)) {
+    TORCH_CHECK(st0.has_value() && st0->defined() && st1.has_value() && st1->defined(), "adam/ftrl need 2 states");
+  }
+  if (kind == 2) TORCH_CHECK(st0.has_value() && st0->defined(), "adagrad needs a state");
+  if (kind == 0 && momentum != 0.0) TORCH_CHECK(st0.has_value() && st0->defined(), "momentum sgd needs a buffer");
+  int wout_bf16 = 0;
+  if (wout.has_value() && wout->defined()) {
+    check_gpu(*wout, "wout");
+    TORCH_CHECK(wout->numel() == n, "wout size");
+    wout_bf16 = dcode(*wout, "wout");
+  }
+  if (gscale_t.has_value() && gscale_t->defined()) check_f32(*gscale_t, "gscale_t");
+  const c10::hip::HIPGuard guard(w.device());
+  psamd::FusedOptArgs a;
+  a.kind = static_cast<int>(kind);
+  a.w = w.data_ptr<float>();
+  a.st0 = opt_ptr<float>(st0);
+  a.st1 = opt_ptr<float>(st1);
+  a.g = g.data_ptr();
+  a.g_bf16 = dcode(g, "g");
+  a.wout = opt_ptr<void>(wout);
+  a.wout_bf16 = wout_bf16;
+  a.n = n;
+  a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = wd; a.momentum = momentum;
+  a.dampening = dampening; a.nesterov = nesterov; a.adamw = adamw; a.bc1 = bc1; a.bc2 = bc2;
+  a.l1 = l1; a.l2 = l2; a.fbeta = fbeta; a.ftrl_mode = static_cast<int>(ftrl_mode);
+  a.gscale = gscale;
+  a.gscale_ptr = opt_ptr<const float>(gscale_t);
+  psamd::launch_fused_opt(a, cur_stream(w));
+}
+
+void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::optional<Tensor> st1, Tensor rows,
+                Tensor grad, bool rowwise, bool skip_zero, double lr, double beta1, double beta2, double eps,
+                double wd, double momentum, double bc1, double bc2, double l1, double l2, double fbeta,
+                int64_t ftrl_mode, double gscale) {
+  check_f32(table, "table");
+  TORCH_CHECK(table.dim() == 2, "table must be [rows, dim]");
+  check_i64(rows, "rows");
+  check_gpu(grad, "grad");
+  const int64_t dim = table.size(1);
+  TORCH_CHECK(grad.numel() == rows.numel() * dim, "grad must be [nrows, dim]");
+  if (st0.has_value() && st0->defined()) {
+    check_f32(*st0, "st0");
+    const int64_t want = (kind == 2 && rowwise) ? table.size(0) : table.numel();
+    TORCH_CHECK(st0->numel() == want, "st0 size (rowwise adagrad state is [rows])");
+  }
+  if (st1.has_value() && st1->defined()) { check_f32(*st1, "st1"); TORCH_CHECK(st1->numel() == table.numel(), "st1"); }
+  if (kind == 1 || kind == 3) TORCH_CHECK(st0.has_value() && st1.has_value(), "adam/ftrl need 2 states");
+  if (kind == 2) TORCH_CHECK(st0.has_value(), "adagrad needs a state");
+  const c10::hip::HIPGuard guard(table.device());
+  psamd::SparseOptArgs a;
+  a.kind = static_cast<int>(kind);
+  a.table = table.data_ptr<float>();
+  a.st0 = opt_ptr<float>(st0);
+  a.st1 = opt_ptr<float>(st1);
+  a.rows = rows.data_ptr<int64_t>();
+  a.grad = grad.data_ptr();
+  a.g_bf16 = dcode(grad, "grad");
+  a.nrows = rows.numel();
+  a.dim = static_cast<int>(dim);
+  a.rowwise = rowwise;
+  a.skip_zero = skip_zero;
+  a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = wd; a.momentum = momentum;
+  a.bc1 = bc1; a.bc2 = bc2; a.l1 = l1; a.l2 = l2; a.fbeta = fbeta; a.ftrl_mode = static_cast<int>(ftrl_mode);
+  a.gscale = gscale;
+  psamd::launch_sparse_opt(a, cur_stream(table));
+}
+
+// ------------------------------------------------------------------------------ reductions
+void sumsq(Tensor x, Tensor out, bool accumulate) {
+  check_gpu(x, "x");
+  check_f32(out, "out");
+  TORCH_CHECK(out.numel() >= 1, "out must hold one float");
+  const c10::hip::HIPGuard guard(x.device());
+  const int nb = psamd::sumsq_blocks(x.numel());
+  auto partial = torch::empty({nb}, out.options());
+  auto s = cur_stream(x);
+  psamd::launch_sumsq_partial(x.data_ptr(), dcode(x, "x"), x.numel(), partial.data_ptr<float>(), nb, s);
+  psamd::launch_sumsq_finish(partial.data_ptr<float>(), nb, out.data_ptr<float>(), accumulate, s);
+}
+
+void clip_factor(Tensor sq, double max_norm, Tensor factor) {
+  check_f32(sq, "sumsq");
+  check_f32(factor, "factor");
+  const c10::hip::HIPGuard guard(sq.device());
+  psamd::launch_clip_factor(sq.data_ptr<float>(), static_cast<float>(max_norm), factor.data_ptr<float>(),
+                            cur_stream(sq));
+}
+
+void cast_(Tensor x, Tensor y, double scale) {
+  check_gpu(x, "x");
+  check_gpu(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "cast size mismatch");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_cast(x.data_ptr(), dcode(x, "x"), y.data_ptr(), dcode(y, "y"), x.numel(), static_cast<float>(scale),
+                     cur_stream(x));
+}
+
+void axpy_(double a, Tensor x, Tensor y) {
+  check_gpu(x, "x");
+  check_gpu(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "axpy size mismatch");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_axpy(static_cast<float>(a), x.data_ptr(), dcode(x, "x"), y.data_ptr(), dcode(y, "y"), x.numel(),
+                     cur_stream(x));
+}
+
+void reduce_n(Tensor x, Tensor y, double scale) {
+  check_gpu(x, "x");
+  check_gpu(y, "y");
+  TORCH_CHECK(x.dim() == 2, "x must be [k, n]");
+  TORCH_CHECK(x.size(1) == y.numel(), "reduce_n size mismatch");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_reduce_n(x.data_ptr(), dcode(x, "x"), static_cast<int>(x.size(0)), x.size(1), y.data_ptr(),
+                         dcode(y, "y"), static_cast<float>(scale), cur_stream(x));
+}
+
+void lerp(Tensor w0, Tensor w, double sc, Tensor out) {
+  check_f32(w0, "w0");
+  check_f32(w, "w");
+  check_gpu(out, "out");
+  TORCH_CHECK(w0.numel() == w.numel() && w.numel() == out.numel(), "lerp size mismatch");
+  const c10::hip::HIPGuard guard(w.device());
+  psamd::launch_lerp(w0.data_ptr<float>(), w.data_ptr<float>(), static_cast<float>(sc), out.data_ptr(),
+                     dcode(out, "out"), w.numel(), cur_stream(w));
+}
+
+// ------------------------------------------------------------------------------ compression
+void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
+  check_gpu(g, "g");
+  check_f32(err, "err");
+  check_gpu(words, "words");
+  check_f32(scales, "scales");
+  TORCH_CHECK(words.scalar_type() == torch::kInt64, "words must be int64 (bit-packed)");
+  const int64_t n = g.numel();
+  TORCH_CHECK(err.numel() == n, "err size");
+  TORCH_CHECK(words.numel() >= (n + 63) / 64, "words too small");
+  TORCH_CHECK(scales.numel() >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
+  const c10::hip::HIPGuard guard(g.device());
+  psamd::launch_onebit_pack(g.data_ptr(), dcode(g, "g"), err.data_ptr<float>(), n,
+                            reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), scales.data_ptr<float>(),
+                            cur_stream(g));
+}
+
+void onebit_unpack_reduce(Tensor words, Tensor scales, Tensor out, double mult, bool accumulate) {
+  check_gpu(words, "words");
+  check_f32(scales, "scales");
+  check_gpu(out, "out");
+  TORCH_CHECK(words.dim() == 2 && scales.dim() == 2 && words.size(0) == scales.size(0), "words/scales [W, *]");
+  const int64_t n = out.numel();
+  TORCH_CHECK(words.size(1) >= (n + 63) / 64, "words too small");
+  TORCH_CHECK(scales.size(1) >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
+  const c10::hip::HIPGuard guard(out.device());
+  psamd::launch_onebit_unpack_reduce(reinterpret_cast<const uint64_t*>(words.data_ptr<int64_t>()),
+                                     scales.data_ptr<float>(), static_cast<int>(words.size(0)), n, words.size(1),
+                                     scales.size(1), out.data_ptr(), dcode(out, "out"), static_cast<float>(mult),
+                                     accumulate, cur_stream(out));
+}
+
+// ------------------------------------------------------------------------------ sparse
+void gather_rows(Tensor table, Tensor rows, Tensor out, int64_t out_off, int64_t act) {
+  check_gpu(table, "table");
+  check_i64(rows, "rows");
+  check_gpu(out, "out");
+  TORCH_CHECK(table.dim() == 2 && out.dim() == 2, "table/out must be 2-D");
+  const int64_t dim = table.size(1);
+  TORCH_CHECK(out.size(0) == rows.numel(), "out rows != len(rows)");
+  TORCH_CHECK(out_off >= 0 && out_off + dim <= out.size(1), "out column slice out of range");
+  const c10::hip::HIPGuard guard(table.device());
+  psamd::launch_gather_rows(table.data_ptr(), dcode(table, "table"), rows.data_ptr<int64_t>(), rows.numel(),
+                            static_cast<int>(dim), out.data_ptr(), dcode(out, "out"), out.size(1), out_off,
+                            static_cast<int>(act), cur_stream(table));
+}
+
+void segment_reduce_rows(Tensor src, Tensor perm, Tensor seg_off, Tensor out, bool mean) {
+  check_gpu(src, "src");
+  check_i64(perm, "perm");
+  check_i64(seg_off, "seg_off");
+  check_gpu(out, "out");
+  TORCH_CHECK(src.dim() == 2 && out.dim() == 2 && src.size(1) == out.size(1), "src/out [*, dim]");
+  TORCH_CHECK(seg_off.numel() == out.size(0) + 1, "seg_off must have nseg+1 entries");
+  TORCH_CHECK(perm.numel() == src.size(0), "perm must index every src row");
+  const c10::hip::HIPGuard guard(src.device());
+  psamd::launch_segment_reduce_rows(src.data_ptr(), dcode(src, "src"), perm.data_ptr<int64_t>(),
+                                    seg_off.data_ptr<int64_t>(), out.size(0), static_cast<int>(src.size(1)),
+                                    out.data_ptr(), dcode(out, "out"), mean, cur_stream(src));
+}
+
+void scatter_add_rows(Tensor src, Tensor rows, Tensor table) {
+  check_gpu(src, "src");
+  check_i64(rows, "rows");
+  check_f32(table, "table");
+  TORCH_CHECK(table.dim() == 2 && src.dim() == 2 && src.size(1) == table.size(1), "shape");
+  TORCH_CHECK(src.size(0) == rows.numel(), "src rows != len(rows)");
+  const c10::hip::HIPGuard guard(src.device());
+  psamd::launch_scatter_add_rows(src.data_ptr(), dcode(src, "src"), rows.data_ptr<int64_t>(), rows.numel(),
+                                 static_cast<int>(src.size(1)), table.data_ptr<float>(), cur_stream(src));
+}
+
+void embedding_bag_fwd(Tensor table, Tensor ids, Tensor out, int64_t out_off, int64_t act) {
+  check_f32(table, "table");
+  check_i64(ids, "ids");
+  check_gpu(out, "out");
+  TORCH_CHECK(ids.dim() == 2 && out.dim() == 2 && table.dim() == 2, "ids [B,F], out [B,*], table [R,D]");
+  const int64_t fields = ids.size(1), dim = table.size(1);
+  TORCH_CHECK(out.size(0) == ids.size(0), "batch mismatch");
+  TORCH_CHECK(out_off >= 0 && out_off + fields * dim <= out.size(1), "out column slice out of range");
+  const c10::hip::HIPGuard guard(table.device());
+  psamd::launch_embedding_bag_fwd(table.data_ptr<float>(), ids.data_ptr<int64_t>(), ids.size(0),
+                                  static_cast<int>(fields), static_cast<int>(dim), out.data_ptr(), dcode(out, "out"),
+                                  out.size(1), out_off, static_cast<int>(act), cur_stream(table));
+}
+
+void sparse_lr_fwd(Tensor w, Tensor ids, c10::optional<Tensor> bias, Tensor out) {
+  check_f32(w, "w");
+  check_i64(ids, "ids");
+  check_f32(out, "out");
+  TORCH_CHECK(ids.dim() == 2 && out.numel() == ids.size(0), "ids [B,F], out [B]");
+  if (bias.has_value() && bias->defined()) check_f32(*bias, "bias");
+  const c10::hip::HIPGuard guard(w.device());
+  psamd::launch_sparse_lr_fwd(w.data_ptr<float>(), ids.data_ptr<int64_t>(), ids.size(0),
+                              static_cast<int>(ids.size(1)), w.numel(), opt_ptr<const float>(bias),
+                              out.data_ptr<float>(), cur_stream(w));
+}
+
+void lazy_init_rows(Tensor table, Tensor rows, Tensor flags, int64_t seed, int64_t row_base, double lo, double hi) {
+  check_f32(table, "table");
+  check_i64(rows, "rows");
+  check_gpu(flags, "flags");
+  TORCH_CHECK(flags.scalar_type() == torch::kUInt8 && flags.numel() == table.size(0), "flags uint8 [rows]");
+  const c10::hip::HIPGuard guard(table.device());
+  psamd::launch_lazy_init_rows(table.data_ptr<float>(), rows.data_ptr<int64_t>(), rows.numel(),
+                               static_cast<int>(table.size(1)), flags.data_ptr<uint8_t>(),
+                               static_cast<uint64_t>(seed), row_base, static_cast<float>(lo), static_cast<float>(hi),
+                               cur_stream(table));
+}
+
+// ------------------------------------------------------------------------------ reference ops
+void softmax_temp_fwd(Tensor x, Tensor y, double temp, double clamp_lo, double clamp_hi) {
+  check_f32(x, "x");
+  check_f32(y, "y");
+  TORCH_CHECK(x.dim() == 2 && x.sizes() == y.sizes(), "x,y [rows, cols]");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_softmax_temp_fwd(x.data_ptr<float>(), y.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)),
+                                 static_cast<float>(1.0 / temp), static_cast<float>(clamp_lo),
+                                 static_cast<float>(clamp_hi), cur_stream(x));
+}
+
+void softmax_xent(Tensor p, Tensor labels, Tensor loss, c10::optional<Tensor> grad) {
+  check_f32(p, "p");
+  check_i64(labels, "labels");
+  check_f32(loss, "loss");
+  TORCH_CHECK(p.dim() == 2 && labels.numel() == p.size(0), "p [B,C], labels [B]");
+  if (grad.has_value() && grad->defined()) { check_f32(*grad, "grad"); TORCH_CHECK(grad->sizes() == p.sizes(), "grad"); }
+  const c10::hip::HIPGuard guard(p.device());
+  psamd::launch_softmax_xent(p.data_ptr<float>(), labels.data_ptr<int64_t>(), p.size(0), static_cast<int>(p.size(1)),
+                             loss.data_ptr<float>(), opt_ptr<float>(grad), cur_stream(p));
+}
+
+void bce(Tensor p, Tensor y, Tensor loss, c10::optional<Tensor> grad) {
+  check_f32(p, "p");
+  check_f32(y, "y");
+  check_f32(loss, "loss");
+  TORCH_CHECK(p.numel() == y.numel(), "p/y size");
+  if (grad.has_value() && grad->defined()) { check_f32(*grad, "grad"); TORCH_CHECK(grad->numel() == p.numel(), "grad"); }
+  const c10::hip::HIPGuard guard(p.device());
+  psamd::launch_bce(p.data_ptr<float>(), y.data_ptr<float>(), p.numel(), loss.data_ptr<float>(), opt_ptr<float>(grad),
+                    cur_stream(p));
+}
+
+void maxpool2d_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad, Tensor y, Tensor argmax) {
+  check_gpu(x, "x");
+  check_gpu(y, "y");
+  check_gpu(argmax, "argmax");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4, "NCHW");
+  TORCH_CHECK(argmax.scalar_type() == torch::kInt32 && argmax.sizes() == y.sizes(), "argmax int32 like y");
+  TORCH_CHECK(x.scalar_type() == y.scalar_type(), "x/y dtype");
+  const int64_t h = x.size(2), w = x.size(3), oh = y.size(2), ow = y.size(3);
+  TORCH_CHECK(oh == (h + 2 * pad - k) / stride + 1 && ow == (w + 2 * pad - k) / stride + 1, "pool output shape");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_maxpool2d_fwd(x.data_ptr(), dcode(x, "x"), x.size(0) * x.size(1), static_cast<int>(h),
+                              static_cast<int>(w), static_cast<int>(k), static_cast<int>(stride),
+                              static_cast<int>(pad), y.data_ptr(), argmax.data_ptr<int32_t>(), static_cast<int>(oh),
+                              static_cast<int>(ow), cur_stream(x));
+}
+
+void maxpool2d_bwd(Tensor dy, Tensor argmax, int64_t k, int64_t stride, int64_t pad, Tensor dx) {
+  check_gpu(dy, "dy");
+  check_gpu(dx, "dx");
+  TORCH_CHECK(argmax.scalar_type() == torch::kInt32 && argmax.sizes() == dy.sizes(), "argmax");
+  TORCH_CHECK(dy.scalar_type() == dx.scalar_type(), "dtype");
+  TORCH_CHECK(dx.dim() == 4 && dy.dim() == 4 && dx.size(0) == dy.size(0) && dx.size(1) == dy.size(1), "NCHW");
+  const c10::hip::HIPGuard guard(dy.device());
+  psamd::launch_maxpool2d_bwd(dy.data_ptr(), dcode(dy, "dy"), argmax.data_ptr<int32_t>(), dx.size(0) * dx.size(1),
+                              static_cast<int>(dx.size(2)), static_cast<int>(dx.size(3)), static_cast<int>(dy.size(2)),
+                              static_cast<int>(dy.size(3)), static_cast<int>(k), static_cast<int>(stride),
+                              static_cast<int>(pad), dx.data_ptr(), cur_stream(dy));
+}
+
+void im2col(Tensor x, int64_t k, int64_t stride, int64_t pad, Tensor col) {
+  check_f32(x, "x");
+  check_f32(col, "col");
+  TORCH_CHECK(x.dim() == 4, "x NCHW");
+  const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3);
+  const int64_t oh = (h + 2 * pad - k) / stride + 1, ow = (w + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(col.numel() == n * oh * ow * c * k * k, "col must be [n*oh*ow, c*k*k]");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_im2col(x.data_ptr<float>(), n, static_cast<int>(c), static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(k), static_cast<int>(stride), static_cast<int>(pad), static_cast<int>(oh),
+                       static_cast<int>(ow), col.data_ptr<float>(), cur_stream(x));
+}
+
+void col2im(Tensor col, int64_t k, int64_t stride, int64_t pad, Tensor x) {
+  check_f32(x, "x");
+  check_f32(col, "col");
+  TORCH_CHECK(x.dim() == 4, "x NCHW");
+  const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3);
+  const int64_t oh = (h + 2 * pad - k) / stride + 1, ow = (w + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(col.numel() == n * oh * ow * c * k * k, "col must be [n*oh*ow, c*k*k]");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_col2im(col.data_ptr<float>(), n, static_cast<int>(c), static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(k), static_cast<int>(stride), static_cast<int>(pad), static_cast<int>(oh),
+                       static_cast<int>(ow), x.data_ptr<float>(), cur_stream(x));
+}
+
+void dropout(Tensor x, Tensor y, double p, int64_t seed, int64_t offset) {
+  check_gpu(x, "x");
+  check_gpu(y, "y");
+  TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "dropout shape/dtype");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "p in [0, 1)");
+  const c10::hip::HIPGuard guard(x.device());
+  psamd::launch_dropout_fwd(x.data_ptr(), dcode(x, "x"), y.data_ptr(), x.numel(), static_cast<float>(p),
+                            static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), cur_stream(x));
+}
+
+void uniform_init(Tensor w, int64_t seed, int64_t offset, double lo, double hi) {
+  check_f32(w, "w");
+  const c10::hip::HIPGuard guard(w.device());
+  psamd::launch_uniform_init(w.data_ptr<float>(), w.numel(), static_cast<uint64_t>(seed),
+                             static_cast<uint64_t>(offset), static_cast<float>(lo), static_cast<float>(hi),
+                             cur_stream(w));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "ps_amd HIP kernels for MI355X (gfx950)";
+  m.def("fused_opt", &fused_opt);
+  m.def("sparse_opt", &sparse_opt);
+  m.def("sumsq", &sumsq);
+  m.def("clip_factor", &clip_factor);
+  m.def("cast_", &cast_);
+  m.def("axpy_", &axpy_);
+  m.def("reduce_n", &reduce_n);
+  m.def("lerp", &lerp);
+  m.def("onebit_pack", &onebit_pack);
+  m.def("onebit_unpack_reduce", &onebit_unpack_reduce);
+  m.def("gather_rows", &gather_rows);
+  m.def("segment_reduce_rows", &segment_reduce_rows);
+  m.def("scatter_add_rows", &scatter_add_rows);
+  m.def("embedding_bag_fwd", &embedding_bag_fwd);
+  m.def("sparse_lr_fwd", &sparse_lr_fwd);
+  m.def("lazy_init_rows", &lazy_init_rows);
+  m.def("softmax_temp_fwd", &softmax_temp_fwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("bce", &bce);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im);
+  m.def("dropout", &dropout);
+  m.def("uniform_init", &uniform_init);
+  m.attr("ONEBIT_CHUNK") = psamd::kOnebitChunk;
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,118 @@
+// Host-side launcher declarations for the ps_amd HIP kernels.
+//
+// The kernels live in csrc/kernels/*.hip (compiled by hipcc for gfx950 only); the torch
+// bindings in csrc/bindings.cpp validate tensors and call these launchers on the current
+// HIP stream.  Keeping this header free of torch lets the kernel TUs build in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psamd {
+
+// ---------------------------------------------------------------- optim.hip
+struct FusedOptArgs {
+  int kind;  // 0 sgd, 1 adam, 2 adagrad, 3 ftrl
+  float* w;  // fp32 master shard (in/out)
+  float* st0;  // momentum / adam m / adagrad h / ftrl z (nullable for plain sgd)
+  float* st1;  // adam v / ftrl n (nullable)
+  const void* g;  // gradient, bf16 (g_bf16) or fp32
+  int g_bf16;
+  void* wout;  // optional weight copy-out (pull buffer), bf16 (wout_bf16) or fp32
+  int wout_bf16;
+  int64_t n;
+  float lr, beta1, beta2, eps, wd, momentum, dampening;
+  int nesterov, adamw;
+  float bc1, bc2;
+  float l1, l2, fbeta;
+  int ftrl_mode;
+  float gscale;
+  const float* gscale_ptr;
+};
+void launch_fused_opt(const FusedOptArgs& a, hipStream_t s);
+
+struct SparseOptArgs {
+  int kind;
+  float* table;  // [rows_total, dim] owner-local fp32 table
+  float* st0;
+  float* st1;
+  const int64_t* rows;  // [nrows] unique owner-local rows
+  const void* grad;     // [nrows, dim]
+  int g_bf16;
+  int64_t nrows;
+  int dim;
+  int rowwise;  // adagrad: one accumulator per row
+  int skip_zero;
+  float lr, beta1, beta2, eps, wd, momentum;
+  float bc1, bc2, l1, l2, fbeta;
+  int ftrl_mode;
+  float gscale;
+};
+void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- reduce.hip
+// dtype codes: 0 = fp32, 1 = bf16
+void launch_sumsq_partial(const void* x, int dtype, int64_t n, float* partial, int nblocks, hipStream_t s);
+void launch_sumsq_finish(const float* partial, int nblocks, float* out, int accumulate, hipStream_t s);
+void launch_clip_factor(const float* sumsq, float max_norm, float* factor, hipStream_t s);
+void launch_cast(const void* x, int xdtype, void* y, int ydtype, int64_t n, float scale, hipStream_t s);
+void launch_axpy(float a, const void* x, int xdtype, void* y, int ydtype, int64_t n, hipStream_t s);
+void launch_reduce_n(const void* x, int xdtype, int k, int64_t n, void* y, int ydtype, float scale, hipStream_t s);
+void launch_lerp(const float* w0, const float* w, float sc, void* out, int odtype, int64_t n, hipStream_t s);
+int sumsq_blocks(int64_t n);
+
+// ---------------------------------------------------------------- compress.hip
+// 1-bit sign compression with per-chunk scale and error feedback (K26).
+constexpr int kOnebitChunk = 1024;
+void launch_onebit_pack(const void* g, int gdtype, float* err, int64_t n, uint64_t* words, float* scales,
+                        hipStream_t s);
+void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int nworkers, int64_t n,
+                                 int64_t words_stride, int64_t scales_stride, void* out, int odtype, float mult,
+                                 int accumulate, hipStream_t s);
+
+// ---------------------------------------------------------------- sparse.hip
+void launch_gather_rows(const void* table, int tdtype, const int64_t* rows, int64_t nrows, int dim, void* out,
+                        int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s);
+void launch_segment_reduce_rows(const void* src, int sdtype, const int64_t* perm, const int64_t* seg_off,
+                                int64_t nseg, int dim, void* out, int odtype, int mean, hipStream_t s);
+void launch_scatter_add_rows(const void* src, int sdtype, const int64_t* rows, int64_t nrows, int dim, float* table,
+                             hipStream_t s);
+void launch_embedding_bag_fwd(const float* table, const int64_t* ids, int64_t batch, int fields, int dim,
+                              void* out, int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s);
+void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int fields, int64_t hash_size,
+                          const float* bias, float* out, hipStream_t s);
+void launch_lazy_init_rows(float* table, const int64_t* rows, int64_t nrows, int dim, uint8_t* init_flags,
+                           uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s);
+
+// ---------------------------------------------------------------- ref_ops.hip
+void launch_softmax_temp_fwd(const float* x, float* y, int64_t rows, int cols, float inv_temp, float clamp_lo,
+                             float clamp_hi, hipStream_t s);
+void launch_softmax_xent(const float* p, const int64_t* labels, int64_t rows, int cols, float* loss,
+                         float* grad, hipStream_t s);
+void launch_bce(const float* p, const float* y, int64_t n, float* loss, float* grad, hipStream_t s);
+void launch_maxpool2d_fwd(const void* x, int dtype, int64_t nc, int h, int w, int k, int stride, int pad,
+                          void* y, int32_t* argmax, int oh, int ow, hipStream_t s);
+void launch_maxpool2d_bwd(const void* dy, int dtype, const int32_t* argmax, int64_t nc, int h, int w, int oh,
+                          int ow, int k, int stride, int pad, void* dx, hipStream_t s);
+void launch_im2col(const float* x, int64_t n, int c, int h, int w, int k, int stride, int pad, int oh, int ow,
+                   float* col, hipStream_t s);
+void launch_col2im(const float* col, int64_t n, int c, int h, int w, int k, int stride, int pad, int oh, int ow,
+                   float* x, hipStream_t s);
+void launch_dropout_fwd(const void* x, int dtype, void* y, int64_t n, float p_drop, uint64_t seed,
+                        uint64_t offset, hipStream_t s);
+void launch_dropout_bwd(const void* dy, int dtype, void* dx, int64_t n, float p_drop, uint64_t seed,
+                        uint64_t offset, hipStream_t s);
+void launch_uniform_init(float* w, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi, hipStream_t s);
+
+// ---------------------------------------------------------------- dense.hip (MFMA)
+// Y[M,N] = act(X[M,K] @ W[N,K]^T + b[N]); bf16 in/out, fp32 accumulate.
+// act: 0 none, 1 relu, 2 leaky relu(0.01), 3 clipped sigmoid (0.001 + 0.998*sigmoid)
+void launch_linear_fwd_bf16(const uint16_t* x, const uint16_t* w, const float* b, uint16_t* y, uint16_t* z_pre,
+                            int M, int N, int K, int act, hipStream_t s);
+// generic C[M,N] (+)= A[M,K] @ B[K,N] with strides for transposes (bf16 in, fp32 or bf16 out)
+void launch_gemm_bf16(const uint16_t* a, int64_t lda_m, int64_t lda_k, const uint16_t* b, int64_t ldb_k,
+                      int64_t ldb_n, void* c, int c_bf16, int64_t ldc, int M, int N, int K, float alpha,
+                      int beta_accumulate, const float* bias, int act, hipStream_t s);
+void launch_act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t n, int act, hipStream_t s);
+void launch_colsum(const uint16_t* x, int64_t rows, int cols, float* out, float scale, hipStream_t s);
+
+}  // namespace psamd

@@ -1,0 +1,274 @@
+// Fused server-side optimizers for the parameter-server shards (K21-K24 in SURVEY §2.5).
+//
+// Every kernel is one pass over a flat, range-partitioned shard: fp32 master weights and
+// fp32 optimizer state live on the owning rank, the pushed gradient arrives as bf16 or fp32
+// (reduce-scatter output), and the kernel optionally writes the updated weights straight
+// into the bf16/fp32 "pull" buffer that the following all-gather broadcasts.  One read of
+// each operand and one write of each result: these kernels are HBM-bound, so the only
+// levers are 16-byte-per-lane accesses, a grid that fills 256 CUs, and fusing the gradient
+// scale (1/world, clip coefficient) into the same pass.
+//
+// Reference semantics (file:line in /root/reference/src/main/java):
+//   SGD          update/SimpleUpdater.java:20-22        w += -eta * dw
+//   Adam         update/AdamUpdater.java:57-70          bias correction by the CONSTANT (1-beta)
+//                                                        (Q5) -> bias_mode = 2; standard (1-beta^t) = 1
+//   FTRL         update/FtrlUpdater.java:51-76           reference ordering/sigma (Q6) -> ftrl_mode = 1;
+//                                                        canonical McMahan FTRL-proximal -> ftrl_mode = 0
+//   Adagrad      (north-star, DLRM tables)
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+
+enum OptKind : int { kSGD = 0, kAdam = 1, kAdagrad = 2, kFtrl = 3 };
+
+struct OptParams {
+  float lr;
+  float beta1, beta2, eps;
+  float wd;
+  float momentum, dampening;
+  int nesterov;
+  int adamw;
+  float bc1, bc2;      // multipliers applied to m and v (bias correction), host-computed
+  float l1, l2, fbeta; // FTRL
+  int ftrl_mode;       // 0 canonical, 1 reference
+  int skip_zero;       // FTRL: skip the update when the first grad element of the key is 0 (reference)
+  float gscale;        // host gradient multiplier
+  const float* gscale_ptr;  // optional device multiplier (global-norm clip factor)
+};
+
+template <int KIND>
+__device__ __forceinline__ void opt_apply(float& w, float g, float& s0, float& s1, const OptParams& p) {
+  if constexpr (KIND == kSGD) {
+    if (p.wd != 0.f) g += p.wd * w;
+    if (p.momentum != 0.f) {
+      s0 = p.momentum * s0 + (1.f - p.dampening) * g;
+      g = p.nesterov ? g + p.momentum * s0 : s0;
+    }
+    w -= p.lr * g;
+  } else if constexpr (KIND == kAdam) {
+    if (p.wd != 0.f && !p.adamw) g += p.wd * w;
+    s0 = p.beta1 * s0 + (1.f - p.beta1) * g;
+    s1 = p.beta2 * s1 + (1.f - p.beta2) * g * g;
+    const float mh = s0 * p.bc1;
+    const float vh = s1 * p.bc2;
+    float upd = mh / (sqrtf(vh) + p.eps);
+    if (p.wd != 0.f && p.adamw) upd += p.wd * w;
+    w -= p.lr * upd;
+  } else if constexpr (KIND == kAdagrad) {
+    if (p.wd != 0.f) g += p.wd * w;
+    s0 += g * g;
+    w -= p.lr * g / (sqrtf(s0) + p.eps);
+  } else {  // FTRL; s0 = z, s1 = n ; lr = alpha
+    const float z = s0, n = s1;
+    if (p.ftrl_mode == 1) {
+      // reference: w from (z, n_old), then sigma = sqrt(n+g^2) - sqrt(n/alpha), z += g - sigma*w
+      float wn;
+      if (fabsf(z) <= p.l1) wn = 0.f;
+      else {
+        const float sgn = z >= 0.f ? 1.f : -1.f;
+        wn = -(z - sgn * p.l1) / ((p.l2 + (p.fbeta + sqrtf(n))) / p.lr);
+      }
+      const float sigma = sqrtf(n + g * g) - sqrtf(n / p.lr);
+      s0 = z + (g - sigma * wn);
+      s1 = n + g * g;
+      w = wn;
+    } else {
+      const float nn = n + g * g;
+      const float sigma = (sqrtf(nn) - sqrtf(n)) / p.lr;
+      const float zn = z + g - sigma * w;
+      s0 = zn;
+      s1 = nn;
+      if (fabsf(zn) <= p.l1) w = 0.f;
+      else {
+        const float sgn = zn >= 0.f ? 1.f : -1.f;
+        w = -(zn - sgn * p.l1) / ((p.fbeta + sqrtf(nn)) / p.lr + p.l2);
+      }
+    }
+  }
+}
+
+template <int KIND> struct NState { static constexpr int v = (KIND == kAdam || KIND == kFtrl) ? 2 : ((KIND == kSGD) ? 1 : 1); };
+
+// OUT: 0 = no copy-out, 1 = bf16 copy-out, 2 = fp32 copy-out.
+template <int KIND, typename G, int OUT, bool VEC>
+__global__ __launch_bounds__(256) void fused_opt_kernel(float* __restrict__ w, float* __restrict__ st0,
+                                                         float* __restrict__ st1, const G* __restrict__ g,
+                                                         void* __restrict__ wout, int64_t n, OptParams p) {
+  float scale = p.gscale;
+  if (p.gscale_ptr) scale *= *p.gscale_ptr;
+  const bool use_st0 = st0 != nullptr;
+  const bool use_st1 = st1 != nullptr;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  if constexpr (VEC) {
+    const int64_t nv = n / 8;
+    for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv; v += stride) {
+      const int64_t i = v * 8;
+      float wr[8], gr[8], a[8], b[8];
+      load8(w, i, wr);
+      load8(g, i, gr);
+      if (use_st0) load8(st0, i, a); else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = 0.f;
+      }
+      if (use_st1) load8(st1, i, b); else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) opt_apply<KIND>(wr[j], gr[j] * scale, a[j], b[j], p);
+      store8(w, i, wr);
+      if (use_st0) store8(st0, i, a);
+      if (use_st1) store8(st1, i, b);
+      if constexpr (OUT == 1) store8(static_cast<uint16_t*>(wout), i, wr);
+      if constexpr (OUT == 2) store8(static_cast<float*>(wout), i, wr);
+    }
+    // tail (n % 8) handled by block 0
+    if (blockIdx.x == 0) {
+      for (int64_t i = nv * 8 + threadIdx.x; i < n; i += blockDim.x) {
+        float wr = w[i], a = use_st0 ? st0[i] : 0.f, b = use_st1 ? st1[i] : 0.f;
+        opt_apply<KIND>(wr, Elem<G>::load(g, i) * scale, a, b, p);
+        w[i] = wr;
+        if (use_st0) st0[i] = a;
+        if (use_st1) st1[i] = b;
+        if constexpr (OUT == 1) static_cast<uint16_t*>(wout)[i] = f32_to_bf16(wr);
+        if constexpr (OUT == 2) static_cast<float*>(wout)[i] = wr;
+      }
+    }
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+      float wr = w[i], a = use_st0 ? st0[i] : 0.f, b = use_st1 ? st1[i] : 0.f;
+      opt_apply<KIND>(wr, Elem<G>::load(g, i) * scale, a, b, p);
+      w[i] = wr;
+      if (use_st0) st0[i] = a;
+      if (use_st1) st1[i] = b;
+      if constexpr (OUT == 1) static_cast<uint16_t*>(wout)[i] = f32_to_bf16(wr);
+      if constexpr (OUT == 2) static_cast<float*>(wout)[i] = wr;
+    }
+  }
+}
+
+template <int KIND, typename G, int OUT>
+static void dispatch_vec(const FusedOptArgs& a, const OptParams& p, hipStream_t s) {
+  const bool aligned = ((reinterpret_cast<uintptr_t>(a.w) | reinterpret_cast<uintptr_t>(a.st0) |
+                         reinterpret_cast<uintptr_t>(a.st1) | reinterpret_cast<uintptr_t>(a.g) |
+                         reinterpret_cast<uintptr_t>(a.wout)) & 15) == 0 &&
+                       (sizeof(G) == 4 || (reinterpret_cast<uintptr_t>(a.g) & 15) == 0);
+  const int block = 256;
+  if (aligned) {
+    const int grid = stream_grid((a.n + 7) / 8, block);
+    hipLaunchKernelGGL((fused_opt_kernel<KIND, G, OUT, true>), dim3(grid), dim3(block), 0, s, a.w, a.st0, a.st1,
+                       static_cast<const G*>(a.g), a.wout, a.n, p);
+  } else {
+    const int grid = stream_grid(a.n, block);
+    hipLaunchKernelGGL((fused_opt_kernel<KIND, G, OUT, false>), dim3(grid), dim3(block), 0, s, a.w, a.st0, a.st1,
+                       static_cast<const G*>(a.g), a.wout, a.n, p);
+  }
+}
+
+template <int KIND, typename G>
+static void dispatch_out(const FusedOptArgs& a, const OptParams& p, hipStream_t s) {
+  if (a.wout == nullptr) dispatch_vec<KIND, G, 0>(a, p, s);
+  else if (a.wout_bf16) dispatch_vec<KIND, G, 1>(a, p, s);
+  else dispatch_vec<KIND, G, 2>(a, p, s);
+}
+
+template <int KIND>
+static void dispatch_grad(const FusedOptArgs& a, const OptParams& p, hipStream_t s) {
+  if (a.g_bf16) dispatch_out<KIND, uint16_t>(a, p, s);
+  else dispatch_out<KIND, float>(a, p, s);
+}
+
+void launch_fused_opt(const FusedOptArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  OptParams p;
+  p.lr = a.lr; p.beta1 = a.beta1; p.beta2 = a.beta2; p.eps = a.eps; p.wd = a.wd;
+  p.momentum = a.momentum; p.dampening = a.dampening; p.nesterov = a.nesterov; p.adamw = a.adamw;
+  p.bc1 = a.bc1; p.bc2 = a.bc2; p.l1 = a.l1; p.l2 = a.l2; p.fbeta = a.fbeta; p.ftrl_mode = a.ftrl_mode;
+  p.skip_zero = 0; p.gscale = a.gscale; p.gscale_ptr = a.gscale_ptr;
+  switch (a.kind) {
+    case kSGD: dispatch_grad<kSGD>(a, p, s); break;
+    case kAdam: dispatch_grad<kAdam>(a, p, s); break;
+    case kAdagrad: dispatch_grad<kAdagrad>(a, p, s); break;
+    case kFtrl: dispatch_grad<kFtrl>(a, p, s); break;
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-sparse variants (sparse embedding tables, K24): apply the optimizer only to the rows
+// named in `rows` (unique, owner-local row indices), with `grad` laid out [nrows, dim].
+// One wave per row when dim >= 64, otherwise several rows per wave.  Row-wise Adagrad
+// keeps ONE accumulator per row (mean of g^2 over the row), the DLRM convention.
+// ---------------------------------------------------------------------------------------
+template <int KIND, typename G>
+__global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ table, float* __restrict__ st0,
+                                                          float* __restrict__ st1, const int64_t* __restrict__ rows,
+                                                          const G* __restrict__ grad, int64_t nrows, int dim,
+                                                          OptParams p, int rowwise) {
+  float scale = p.gscale;
+  if (p.gscale_ptr) scale *= *p.gscale_ptr;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * blockDim.x / 64;
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    const int64_t row = rows[r];
+    float* wrow = table + row * dim;
+    const G* grow = grad + r * dim;
+    if (KIND == kAdagrad && rowwise) {
+      float ss = 0.f;
+      for (int c = lane; c < dim; c += 64) {
+        const float gv = Elem<G>::load(grow, c) * scale;
+        ss += gv * gv;
+      }
+      ss = wave_sum(ss) / static_cast<float>(dim);
+      const float h = st0[row] + ss;
+      if (lane == 0) st0[row] = h;
+      const float denom = sqrtf(h) + p.eps;
+      for (int c = lane; c < dim; c += 64) {
+        const float gv = Elem<G>::load(grow, c) * scale;
+        wrow[c] -= p.lr * gv / denom;
+      }
+    } else {
+      // skip_zero reproduces FtrlUpdater.java:52-54 (per key == per row).
+      if (p.skip_zero && Elem<G>::load(grow, 0) == 0.f) continue;
+      for (int c = lane; c < dim; c += 64) {
+        float wr = wrow[c];
+        float a = st0 ? st0[row * dim + c] : 0.f;
+        float b = st1 ? st1[row * dim + c] : 0.f;
+        opt_apply<KIND>(wr, Elem<G>::load(grow, c) * scale, a, b, p);
+        wrow[c] = wr;
+        if (st0) st0[row * dim + c] = a;
+        if (st1) st1[row * dim + c] = b;
+      }
+    }
+  }
+}
+
+void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
+  if (a.nrows <= 0) return;
+  OptParams p;
+  p.lr = a.lr; p.beta1 = a.beta1; p.beta2 = a.beta2; p.eps = a.eps; p.wd = a.wd;
+  p.momentum = a.momentum; p.dampening = 0.f; p.nesterov = 0; p.adamw = 0;
+  p.bc1 = a.bc1; p.bc2 = a.bc2; p.l1 = a.l1; p.l2 = a.l2; p.fbeta = a.fbeta; p.ftrl_mode = a.ftrl_mode;
+  p.skip_zero = a.skip_zero; p.gscale = a.gscale; p.gscale_ptr = nullptr;
+  const int block = 256;
+  const int grid = stream_grid(a.nrows * 64, block);
+#define PSAMD_SPARSE_LAUNCH(K)                                                                                 \
+  if (a.g_bf16)                                                                                                \
+    hipLaunchKernelGGL((sparse_opt_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1, \
+                       a.rows, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, p, a.rowwise);            \
+  else                                                                                                         \
+    hipLaunchKernelGGL((sparse_opt_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,    \
+                       a.rows, static_cast<const float*>(a.grad), a.nrows, a.dim, p, a.rowwise);
+  switch (a.kind) {
+    case kSGD: PSAMD_SPARSE_LAUNCH(kSGD); break;
+    case kAdam: PSAMD_SPARSE_LAUNCH(kAdam); break;
+    case kAdagrad: PSAMD_SPARSE_LAUNCH(kAdagrad); break;
+    case kFtrl: PSAMD_SPARSE_LAUNCH(kFtrl); break;
+    default: break;
+  }
+#undef PSAMD_SPARSE_LAUNCH
+}
+
+}  // namespace psamd

@@ -1,0 +1,236 @@
+// Sparse-row kernels for embedding / wide tables (K5-K8, K24, K28, K29 in SURVEY §2.5).
+//
+// Reference: each embedding row is its own PS key "<field>.<id>" pulled and pushed one RPC
+// at a time (layer/EmbeddingField.java:57-104, store/KVStore.java:74-127); each wide weight
+// is a 1x1 key "wide.weights.<id>" (layer/LRLayer.java:62-120).  Here a table is one dense
+// fp32 [rows, dim] array on its owner rank and rows move as batches:
+//
+//  gather_rows          owner side of pull_rows: out[r] = act(table[rows[r]])  (one wave/row,
+//                       16-B loads; writes into an arbitrary column slice of a wider output
+//                       buffer so the reference ConcatLayer copy is free, K9)
+//  segment_reduce_rows  worker side of push_rows: per unique id, sum (or mean) of its
+//                       occurrence rows, read through a sorted permutation; deterministic,
+//                       no atomics (cdna_hip_programming.md Appendix B, store-and-sum form)
+//  scatter_add_rows     owner side apply for plain accumulate (unique rows => no conflicts)
+//  embedding_bag_fwd    fused per-field lookup for the reference EmbeddingLayer: ids[b, f]
+//                       -> out[b, off + f*dim : off + (f+1)*dim] with ReLU (layer/EmbeddingLayer.java:36-46)
+//  sparse_lr_fwd        z[b] = sum_f w[ids[b,f] mod H] + bias (layer/LRLayer.java:62-98 with
+//                       the hash of util/MatrixUtil.java:27-33 fused in)
+//  lazy_init_rows       deterministic first-touch row init keyed by (seed, global row) with an
+//                       "initialized" byte map; replaces the upsert(replace=false) round trip
+//                       (store/KVStore.java:86-107, net/PServer.java:143-162)
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return v > 0.f ? v : 0.01f * v;
+  if (act == 3) return 0.001f + 0.998f / (1.f + __expf(-v));
+  return v;
+}
+
+template <typename T, typename O>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ table, const int64_t* __restrict__ rows,
+                                                          int64_t nrows, int dim, O* __restrict__ out, int64_t out_ld,
+                                                          int64_t out_off, int act) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    const T* src = table + rows[r] * dim;
+    O* dst = out + r * out_ld + out_off;
+    for (int c = lane; c < dim; c += 64) Elem<O>::store(dst, c, apply_act(Elem<T>::load(src, c), act));
+  }
+}
+
+// vectorized: dim % 4 == 0, fp32 table, fp32 out, 16-B aligned rows
+__global__ __launch_bounds__(256) void gather_rows_vec4_kernel(const float* __restrict__ table,
+                                                               const int64_t* __restrict__ rows, int64_t nrows,
+                                                               int dim, float* __restrict__ out, int64_t out_ld,
+                                                               int64_t out_off, int act) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  const int d4 = dim >> 2;
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(table + rows[r] * dim);
+    f32x4* dst = reinterpret_cast<f32x4*>(out + r * out_ld + out_off);
+    for (int c = lane; c < d4; c += 64) {
+      f32x4 v = src[c];
+      v.x = apply_act(v.x, act); v.y = apply_act(v.y, act); v.z = apply_act(v.z, act); v.w = apply_act(v.w, act);
+      dst[c] = v;
+    }
+  }
+}
+
+void launch_gather_rows(const void* table, int tdtype, const int64_t* rows, int64_t nrows, int dim, void* out,
+                        int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int grid = stream_grid(nrows * 64, 256);
+  const bool vec = tdtype == 0 && odtype == 0 && dim % 4 == 0 && out_ld % 4 == 0 && out_off % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (vec) {
+    hipLaunchKernelGGL(gather_rows_vec4_kernel, dim3(grid), dim3(256), 0, s, static_cast<const float*>(table), rows,
+                       nrows, dim, static_cast<float*>(out), out_ld, out_off, act);
+    return;
+  }
+#define PSAMD_G(T, O)                                                                                                \
+  hipLaunchKernelGGL((gather_rows_kernel<T, O>), dim3(grid), dim3(256), 0, s, static_cast<const T*>(table), rows, \
+                     nrows, dim, static_cast<O*>(out), out_ld, out_off, act);
+  if (tdtype == 1 && odtype == 1) PSAMD_G(uint16_t, uint16_t)
+  else if (tdtype == 1) PSAMD_G(uint16_t, float)
+  else if (odtype == 1) PSAMD_G(float, uint16_t)
+  else PSAMD_G(float, float)
+#undef PSAMD_G
+}
+
+// out[u] = (mean ? 1/cnt : 1) * sum_{j in [seg_off[u], seg_off[u+1])} src[perm[j]]
+template <typename S, typename O>
+__global__ __launch_bounds__(256) void segment_reduce_rows_kernel(const S* __restrict__ src,
+                                                                  const int64_t* __restrict__ perm,
+                                                                  const int64_t* __restrict__ seg_off, int64_t nseg,
+                                                                  int dim, O* __restrict__ out, int mean) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t u = wave; u < nseg; u += nwaves) {
+    const int64_t b = seg_off[u], e = seg_off[u + 1];
+    const float inv = mean ? 1.f / static_cast<float>(e - b) : 1.f;
+    for (int c = lane; c < dim; c += 64) {
+      float acc = 0.f;
+      for (int64_t j = b; j < e; ++j) acc += Elem<S>::load(src + perm[j] * dim, c);
+      Elem<O>::store(out + u * dim, c, acc * inv);
+    }
+  }
+}
+
+void launch_segment_reduce_rows(const void* src, int sdtype, const int64_t* perm, const int64_t* seg_off,
+                                int64_t nseg, int dim, void* out, int odtype, int mean, hipStream_t s) {
+  if (nseg <= 0) return;
+  const int grid = stream_grid(nseg * 64, 256);
+#define PSAMD_S(S, O)                                                                                           \
+  hipLaunchKernelGGL((segment_reduce_rows_kernel<S, O>), dim3(grid), dim3(256), 0, s, static_cast<const S*>(src), \
+                     perm, seg_off, nseg, dim, static_cast<O*>(out), mean);
+  if (sdtype == 1 && odtype == 1) PSAMD_S(uint16_t, uint16_t)
+  else if (sdtype == 1) PSAMD_S(uint16_t, float)
+  else if (odtype == 1) PSAMD_S(float, uint16_t)
+  else PSAMD_S(float, float)
+#undef PSAMD_S
+}
+
+template <typename S>
+__global__ __launch_bounds__(256) void scatter_add_rows_kernel(const S* __restrict__ src,
+                                                               const int64_t* __restrict__ rows, int64_t nrows,
+                                                               int dim, float* __restrict__ table) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    float* dst = table + rows[r] * dim;
+    for (int c = lane; c < dim; c += 64) dst[c] += Elem<S>::load(src + r * dim, c);
+  }
+}
+
+void launch_scatter_add_rows(const void* src, int sdtype, const int64_t* rows, int64_t nrows, int dim, float* table,
+                             hipStream_t s) {
+  if (nrows <= 0) return;
+  const int grid = stream_grid(nrows * 64, 256);
+  if (sdtype == 1)
+    hipLaunchKernelGGL(scatter_add_rows_kernel<uint16_t>, dim3(grid), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(src), rows, nrows, dim, table);
+  else
+    hipLaunchKernelGGL(scatter_add_rows_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<const float*>(src),
+                       rows, nrows, dim, table);
+}
+
+// ids[b, f] are owner-local row indices into table (per-field offsets already applied)
+template <typename O>
+__global__ __launch_bounds__(256) void embedding_bag_fwd_kernel(const float* __restrict__ table,
+                                                                const int64_t* __restrict__ ids, int64_t batch,
+                                                                int fields, int dim, O* __restrict__ out,
+                                                                int64_t out_ld, int64_t out_off, int act) {
+  const int64_t total = batch * fields * dim;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t b = i / (static_cast<int64_t>(fields) * dim);
+    const int64_t rem = i - b * fields * dim;
+    const int f = static_cast<int>(rem / dim);
+    const int d = static_cast<int>(rem - static_cast<int64_t>(f) * dim);
+    const float v = table[ids[b * fields + f] * dim + d];
+    Elem<O>::store(out, b * out_ld + out_off + rem, apply_act(v, act));
+  }
+}
+
+void launch_embedding_bag_fwd(const float* table, const int64_t* ids, int64_t batch, int fields, int dim, void* out,
+                              int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s) {
+  const int64_t total = batch * fields * dim;
+  if (total <= 0) return;
+  const int grid = stream_grid(total, 256);
+  if (odtype == 1)
+    hipLaunchKernelGGL(embedding_bag_fwd_kernel<uint16_t>, dim3(grid), dim3(256), 0, s, table, ids, batch, fields, dim,
+                       static_cast<uint16_t*>(out), out_ld, out_off, act);
+  else
+    hipLaunchKernelGGL(embedding_bag_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, table, ids, batch, fields, dim,
+                       static_cast<float*>(out), out_ld, out_off, act);
+}
+
+// one wave per sample; lanes stride over fields
+__global__ __launch_bounds__(256) void sparse_lr_fwd_kernel(const float* __restrict__ w, const int64_t* __restrict__ ids,
+                                                            int64_t batch, int fields, int64_t hash_size,
+                                                            const float* __restrict__ bias, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t b = wave; b < batch; b += nwaves) {
+    float acc = 0.f;
+    for (int f = lane; f < fields; f += 64) {
+      int64_t id = ids[b * fields + f] % hash_size;
+      if (id < 0) id += hash_size;
+      acc += w[id];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) out[b] = acc + (bias ? bias[0] : 0.f);
+  }
+}
+
+void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int fields, int64_t hash_size,
+                          const float* bias, float* out, hipStream_t s) {
+  if (batch <= 0) return;
+  const int grid = stream_grid(batch * 64, 256);
+  hipLaunchKernelGGL(sparse_lr_fwd_kernel, dim3(grid), dim3(256), 0, s, w, ids, batch, fields, hash_size, bias, out);
+}
+
+// rows: owner-local indices; row_base: global index of local row 0 (keys the RNG so the value of
+// a row does not depend on which rank owns it or when it is first touched)
+__global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__ table, const int64_t* __restrict__ rows,
+                                                             int64_t nrows, int dim, uint8_t* __restrict__ flags,
+                                                             uint64_t seed, int64_t row_base, float lo, float hi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = wave; r < nrows; r += nwaves) {
+    const int64_t row = rows[r];
+    if (flags[row]) continue;  // wave-uniform
+    const uint64_t grow = static_cast<uint64_t>(row + row_base);
+    for (int c = lane; c < dim; c += 64) {
+      uint32_t rnd[4];
+      Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(c), rnd);
+      table[row * dim + c] = lo + (hi - lo) * Philox::u01(rnd[0]);
+    }
+    // rows may repeat inside one launch only if the caller passed duplicates; flags is
+    // written after the row so a duplicate wave either re-inits identically or skips.
+    if (lane == 0) flags[row] = 1;
+  }
+}
+
+void launch_lazy_init_rows(float* table, const int64_t* rows, int64_t nrows, int dim, uint8_t* init_flags,
+                           uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int grid = stream_grid(nrows * 64, 256);
+  hipLaunchKernelGGL(lazy_init_rows_kernel, dim3(grid), dim3(256), 0, s, table, rows, nrows, dim, init_flags, seed,
+                     row_base, lo, hi);
+}
+
+}  // namespace psamd

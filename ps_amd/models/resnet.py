@@ -1,0 +1,113 @@
+"""ResNet-50 (v1.5: stride on the 3x3 conv) -- the BASELINE.json headline model.
+
+torchvision is not in the image, so the architecture is defined here (He et al. 2016,
+torchvision layer naming so state dicts line up).  Random init only (no checkpoints).
+
+MI355X notes: the model is run in channels_last bf16 (MIOpen NHWC convolutions on the
+MFMA cores); all parameters -- conv, BN and FC -- are bf16 replicas whose fp32 masters
+live on the parameter-server shards (parallel/colocated.py).  BN running statistics are
+fp32 buffers kept per worker (they are not trained parameters, so they are not pushed;
+the reference has no BN at all).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        width = planes
+        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = True):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make_layer(self, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        downsample = None
+        if stride != 1 or self.inplanes != planes * 4:
+            downsample = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                       nn.BatchNorm2d(planes * 4))
+        layers = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * 4
+        for _ in range(1, blocks):
+            layers.append(Bottleneck(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def resnet18_like(num_classes: int = 10, width: int = 16) -> nn.Module:
+    """Tiny bottleneck ResNet for CPU tests (same code path, few channels)."""
+    m = ResNet((1, 1, 1, 1), num_classes)
+    return m
+
+
+def prepare_for_mi355x(model: nn.Module, dtype=torch.bfloat16, bn_fp32: bool = True) -> nn.Module:
+    """channels_last + bf16 parameters.
+
+    bn_fp32=True keeps BatchNorm affine params and running stats in fp32 (the mixed
+    bf16-activation / fp32-BN-param path that MIOpen and the native kernels both support);
+    bn_fp32=False casts the whole module, BN included, to ``dtype``.
+    """
+    model = model.to(memory_format=torch.channels_last)
+    for mod in model.modules():
+        is_bn = isinstance(mod, nn.modules.batchnorm._BatchNorm)
+        if is_bn and bn_fp32:
+            continue
+        for _, p in list(mod.named_parameters(recurse=False)):
+            p.data = p.data.to(dtype)
+        for name, b in list(mod.named_buffers(recurse=False)):
+            if b.is_floating_point():
+                setattr(mod, name, b.to(dtype))
+    return model

@@ -1,0 +1,112 @@
+"""Sparse-row ops for embedding / wide tables (HIP on GPU, torch on CPU).
+
+``dedup_rows`` is the worker side of push_rows: it turns per-occurrence gradient rows into
+(unique ids, reduced rows).  The sort/unique step uses torch (rocPRIM radix sort on the
+GPU); the reduction itself is the deterministic ``segment_reduce_rows`` HIP kernel.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import native, use_native
+
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
+
+
+def _act_ref(x: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_LEAKY:
+        return torch.where(x > 0, x, 0.01 * x)
+    if act == ACT_SIGMOID:
+        return 0.001 + 0.998 * torch.sigmoid(x)
+    return x
+
+
+def gather_rows(table: torch.Tensor, rows: torch.Tensor, out: torch.Tensor | None = None, out_off: int = 0,
+                act: int = ACT_NONE) -> torch.Tensor:
+    """out[:, out_off:out_off+dim] = act(table[rows])."""
+    dim = table.shape[1]
+    if out is None:
+        out = torch.empty(rows.numel(), dim, dtype=table.dtype, device=table.device)
+    if use_native(table, rows):
+        native().gather_rows(table, rows.contiguous(), out, int(out_off), int(act))
+        return out
+    out[:, out_off:out_off + dim] = _act_ref(table[rows].float(), act).to(out.dtype)
+    return out
+
+
+def segment_reduce_rows(src: torch.Tensor, perm: torch.Tensor, seg_off: torch.Tensor, out: torch.Tensor,
+                        mean: bool = False) -> torch.Tensor:
+    if use_native(src, perm):
+        native().segment_reduce_rows(src, perm, seg_off, out, bool(mean))
+        return out
+    srt = src[perm].float()
+    cnt = (seg_off[1:] - seg_off[:-1])
+    seg_ids = torch.repeat_interleave(torch.arange(cnt.numel()), cnt)
+    acc = torch.zeros(out.shape, dtype=torch.float32)
+    acc.index_add_(0, seg_ids, srt)
+    if mean:
+        acc /= cnt.clamp(min=1).float()[:, None]
+    out.copy_(acc.to(out.dtype))
+    return out
+
+
+def dedup_rows(ids: torch.Tensor, grads: torch.Tensor, mean: bool = False, out_dtype=None):
+    """(unique_ids, reduced_grads[u]) where reduced = sum (or mean) over occurrences."""
+    ids = ids.reshape(-1)
+    grads = grads.reshape(ids.numel(), -1)
+    uniq, inverse, counts = torch.unique(ids, sorted=True, return_inverse=True, return_counts=True)
+    perm = torch.argsort(inverse, stable=True)
+    seg_off = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=ids.device)
+    torch.cumsum(counts, 0, out=seg_off[1:])
+    out = torch.empty(uniq.numel(), grads.shape[1], dtype=out_dtype or grads.dtype, device=grads.device)
+    segment_reduce_rows(grads.contiguous(), perm, seg_off, out, mean)
+    return uniq, out
+
+
+def scatter_add_rows(src: torch.Tensor, rows: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    if use_native(src, table):
+        native().scatter_add_rows(src.contiguous(), rows.contiguous(), table)
+        return table
+    table.index_add_(0, rows, src.float())
+    return table
+
+
+def embedding_bag_fwd(table: torch.Tensor, ids: torch.Tensor, out: torch.Tensor, out_off: int = 0,
+                      act: int = ACT_NONE) -> torch.Tensor:
+    """out[b, off + f*dim + d] = act(table[ids[b, f], d]) -- fused field lookup + concat."""
+    if use_native(table, ids):
+        native().embedding_bag_fwd(table, ids.contiguous(), out, int(out_off), int(act))
+        return out
+    b, f = ids.shape
+    dim = table.shape[1]
+    out[:, out_off:out_off + f * dim] = _act_ref(table[ids].reshape(b, f * dim), act).to(out.dtype)
+    return out
+
+
+def sparse_lr_fwd(w: torch.Tensor, ids: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> torch.Tensor:
+    """out[b] = sum_f w[ids[b,f] mod H] + bias (wide part)."""
+    if use_native(w, ids):
+        native().sparse_lr_fwd(w, ids.contiguous(), bias, out)
+        return out
+    h = w.numel()
+    idx = torch.remainder(ids, h)
+    z = w.reshape(-1)[idx].sum(1)
+    if bias is not None:
+        z = z + bias.reshape(())
+    out.copy_(z.reshape(out.shape))
+    return out
+
+
+def lazy_init_rows(table: torch.Tensor, rows: torch.Tensor, flags: torch.Tensor, seed: int, row_base: int,
+                   lo: float, hi: float) -> None:
+    """Initialise rows not yet touched (flags==0) deterministically from (seed, global row)."""
+    if use_native(table, rows):
+        native().lazy_init_rows(table, rows.contiguous(), flags, int(seed), int(row_base), float(lo), float(hi))
+        return
+    new = rows[flags[rows] == 0].unique()
+    for r in new.tolist():
+        g = torch.Generator().manual_seed((int(seed) * 1000003 + r + row_base) & 0x7FFFFFFFFFFFFFFF)
+        table[r] = lo + (hi - lo) * torch.rand(table.shape[1], generator=g)
+        flags[r] = 1

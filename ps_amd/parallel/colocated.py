@@ -1,0 +1,333 @@
+"""Co-located parameter server over collectives -- the MI355X hot path.
+
+Reference architecture (structure.png): W worker processes push per-key
+gradients to S server processes over gRPC, the servers apply the optimizer, workers pull
+the weights back and meet at a barrier (store/KVStore.java:240-268, net/PServer.java:164-283).
+
+MI355X-native design: every GPU process is a worker AND the server of a range partition
+(registry.py).  Per bucket, in the order buckets become ready during backward:
+
+    push  = reduce-scatter of the bf16 gradient bucket       (RCCL over xGMI, comm stream)
+    serve = fused HIP optimizer on the owned fp32 master chunk; it writes the updated
+            weights straight into the owned chunk of the bf16 pull buffer   (same stream)
+    pull  = all-gather of the bucket from every owner         (RCCL, same stream)
+
+all overlapped with the rest of backward: the comm stream waits on an event recorded on the
+compute stream when the bucket's last gradient has been accumulated
+(``register_post_accumulate_grad_hook``), and the compute stream waits on the round's
+completion event only before the forward that needs the new weights.
+
+Consistency (SURVEY §2.3, quirks Q1-Q3 fixed):
+  * BSP  (staleness=0): forward t+1 sees exactly the weights after every push of step t.
+  * SSP  (staleness=s): forward t+1 uses weights version max(0, t+1-s); rounds stay in
+    flight for up to s steps.  Weight and gradient buffers are rings of s+1 slots so the
+    in-flight pull never writes the buffer the compute stream is reading.  A worker that
+    runs ahead blocks on the completion event of round t-s, i.e. when its clock leads the
+    slowest worker by more than s -- the SSP bound, enforced by the collective itself.
+  * Gradient accumulators are zeroed every round and averaged over exactly W workers.
+
+Options: global-norm clipping (two-phase: push all, norm, then serve+pull), 1-bit
+compressed push with error feedback (compress="onebit": bits all-to-all to the owners +
+owner-side unpack-reduce kernel), arbitrary per-key-prefix updaters (resolve_updater).
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+from functools import partial
+from typing import Dict, List, Optional, Union
+
+import torch
+
+from ..ops import compress as _cmp
+from ..ops import reduce as _red
+from .registry import Registry
+from .transport import Transport
+from .updaters import Updater, resolve_updater
+
+
+class ColocatedPS:
+    def __init__(self, model: torch.nn.Module, updaters: Union[Updater, Dict[str, Updater]],
+                 transport: Optional[Transport] = None, *, bucket_mb: float = 32.0, last_bucket_mb: float = 4.0,
+                 staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
+                 average: bool = True, broadcast_init: bool = True, overlap: bool = True):
+        self.model = model
+        self.t = transport or Transport()
+        self.world, self.rank = self.t.world, self.t.rank
+        self.updaters = updaters if isinstance(updaters, dict) else {"default": updaters}
+        self.staleness = int(staleness)
+        if self.staleness < 0:
+            raise ValueError("staleness must be >= 0")
+        self.nslots = self.staleness + 1
+        self.clip_norm = clip_norm
+        self.compress = compress
+        if compress not in (None, "onebit"):
+            raise ValueError(f"unknown compression {compress!r}")
+        self.average = average
+        self.overlap = overlap
+        params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("model has no trainable parameters")
+        self.device = params[0][1].device
+        self.gpu = self.device.type == "cuda"
+        align = 1024 if compress == "onebit" else 64
+        self.reg = Registry(self.world, int(bucket_mb * 2**20), align, int(last_bucket_mb * 2**20) or None)
+        for n, p in reversed(params):
+            self.reg.add(n, p.shape, p.dtype)
+        self.reg.finalize()
+        self.params = dict(params)
+        R = self.reg
+        # ---------------- replica buffers (rings of s+1 slots)
+        self.wbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
+                         for _ in range(self.nslots)] for g in R.group_size}
+        self.gbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
+                         for _ in range(self.nslots)] for g in R.group_size}
+        with torch.no_grad():
+            for n, p in params:
+                ki = R.keys[n]
+                self.wbuf[ki.group][0][ki.offset:ki.offset + ki.numel].copy_(p.detach().reshape(-1))
+            if broadcast_init:
+                for g in self.wbuf:
+                    self.t.broadcast(self.wbuf[g][0], src=0)
+            for g in self.wbuf:
+                for s in range(1, self.nslots):
+                    self.wbuf[g][s].copy_(self.wbuf[g][0])
+        # ---------------- server state: fp32 master + optimizer state for the owned chunks
+        self.master: List[torch.Tensor] = []
+        self.segs: List[List[tuple]] = []  # per bucket: [(updater, lo, hi)] chunk-local
+        self.states: List[List[List[torch.Tensor]]] = []
+        self.gshard: List[Optional[torch.Tensor]] = []
+        for b in R.buckets:
+            lo, hi = b.owner_range(self.rank)
+            m = self.wbuf[b.group][0][lo:hi].float().clone()
+            self.master.append(m)
+            segs = []
+            for k, a, z in R.segments(b.index, self.rank):
+                u = resolve_updater(k, self.updaters)
+                la, lz = a - lo, z - lo
+                if segs and segs[-1][0] is u and segs[-1][2] == la:
+                    segs[-1] = (u, segs[-1][1], lz)
+                else:
+                    segs.append((u, la, lz))
+            if not segs:  # chunk is pure padding: give it to the default updater
+                segs = [(resolve_updater(b.keys[0], self.updaters), 0, hi - lo)]
+            # extend first/last segment over leading/trailing padding
+            segs[0] = (segs[0][0], 0, segs[0][2])
+            segs[-1] = (segs[-1][0], segs[-1][1], hi - lo)
+            self.segs.append(segs)
+            self.states.append([u.new_states(m[a:z]) for (u, a, z) in segs])
+            if self.world > 1:
+                self.gshard.append(torch.empty(b.chunk, dtype=R.group_dtype[b.group], device=self.device))
+            else:
+                self.gshard.append(None)
+        # 1-bit compression state: error-feedback buffer per bucket (full bucket, fp32)
+        if compress == "onebit":
+            self.err = [torch.zeros(b.size, dtype=torch.float32, device=self.device) for b in R.buckets]
+            self.cwords = []
+            self.cscales = []
+            for b in R.buckets:
+                nw, ns = _cmp.packed_sizes(b.size)
+                self.cwords.append((torch.empty(nw, dtype=torch.int64, device=self.device),
+                                    torch.empty(nw, dtype=torch.int64, device=self.device)))
+                self.cscales.append((torch.empty(ns, dtype=torch.float32, device=self.device),
+                                     torch.empty(ns, dtype=torch.float32, device=self.device)))
+        # ---------------- clipping scratch
+        if clip_norm is not None:
+            self._sq = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._factor = torch.ones(1, dtype=torch.float32, device=self.device)
+        # ---------------- step state
+        self.round = 0  # PS clock: number of completed pushes
+        self.wslot = 0
+        self.gslot = 0
+        self.pending = [len(b.keys) for b in R.buckets]
+        self.launched = [False] * len(R.buckets)
+        self._key_bucket = {n: R.keys[n].bucket for n in self.params}
+        self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
+        self.round_events: deque = deque()
+        self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
+        self._bind(self.wslot, self.gslot)
+        self._hooks = [p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
+
+    # ------------------------------------------------------------------ views
+    def _view(self, buf: Dict[str, List[torch.Tensor]], slot: int, name: str) -> torch.Tensor:
+        ki = self.reg.keys[name]
+        return buf[ki.group][slot][ki.offset:ki.offset + ki.numel].view(ki.shape)
+
+    def _bind(self, wslot: int, gslot: int) -> None:
+        for n, p in self.params.items():
+            p.data = self._view(self.wbuf, wslot, n)
+            p.grad = self._view(self.gbuf, gslot, n)
+
+    def weight(self, name: str) -> torch.Tensor:
+        """Current replica weights of key ``name`` (the pulled version)."""
+        return self._view(self.wbuf, self.wslot, name)
+
+    # ------------------------------------------------------------------ push path
+    def _on_ready(self, name: str, p: torch.Tensor) -> None:
+        b = self._key_bucket[name]
+        self.pending[b] -= 1
+        if self.pending[b] == 0 and self.overlap:
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self._push(b)
+                if self.clip_norm is None:
+                    self._serve_pull(b)
+        else:
+            self._push(b)
+            if self.clip_norm is None:
+                self._serve_pull(b)
+
+    def _push(self, b: int) -> None:
+        bk = self.reg.buckets[b]
+        gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
+        if self.world == 1:
+            return
+        if self.compress == "onebit":
+            self._push_onebit(b, gin)
+        else:
+            self.t.reduce_scatter(self.gshard[b], gin)
+
+    def _push_onebit(self, b: int, gin: torch.Tensor) -> None:
+        """Compressed push: sign bits + chunk scales, all-to-all to the owners, owner decodes
+        and sums the W contributions in fixed rank order."""
+        bk = self.reg.buckets[b]
+        words, rwords = self.cwords[b]
+        scales, rscales = self.cscales[b]
+        _cmp.onebit_pack(gin, self.err[b], words, scales)
+        self.t.all_to_all(rwords, words)
+        self.t.all_to_all(rscales, scales)
+        nw_chunk = bk.chunk // 64
+        ns_chunk = bk.chunk // _cmp.CHUNK
+        _cmp.onebit_unpack_reduce(rwords.view(self.world, nw_chunk), rscales.view(self.world, ns_chunk),
+                                  self.gshard[b], 1.0, False)
+
+    def _grad_shard(self, b: int) -> torch.Tensor:
+        if self.world == 1:
+            bk = self.reg.buckets[b]
+            return self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
+        return self.gshard[b]
+
+    def _serve_pull(self, b: int) -> None:
+        bk = self.reg.buckets[b]
+        lo, hi = bk.owner_range(self.rank)
+        nxt = (self.round + 1) % self.nslots
+        wfull = self.wbuf[bk.group][nxt]
+        own = wfull[lo:hi]
+        g = self._grad_shard(b)
+        gscale = 1.0 / self.world if self.average else 1.0
+        gst = self._factor if self.clip_norm is not None else None
+        for (u, a, z), st in zip(self.segs[b], self.states[b]):
+            u.step_flat(self.master[b][a:z], st, g[a:z], wout=own[a:z], gscale=gscale, gscale_t=gst,
+                        step=self.round + 1)
+        self.t.all_gather(wfull[bk.start:bk.start + bk.size], own)
+
+    def _clip_and_serve(self) -> None:
+        self._sq.zero_()
+        for b in range(len(self.reg.buckets)):
+            _red.sumsq(self._grad_shard(b), self._sq, accumulate=True)
+        self.t.all_reduce(self._sq)
+        # norm of the averaged gradient = norm(sum) / W
+        scale = self.world if self.average else 1
+        _red.clip_factor(self._sq, float(self.clip_norm) * scale, self._factor)
+        for b in range(len(self.reg.buckets)):
+            self._serve_pull(b)
+
+    # ------------------------------------------------------------------ step boundary
+    def finish_step(self) -> None:
+        """End of a worker step: flush buckets that did not fire, run the round's remaining
+        phases, advance the PS clock and bind the weights the next forward may use."""
+        for b in range(len(self.reg.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        if self.clip_norm is not None:
+            if self.gpu:
+                with torch.cuda.stream(self.comm):
+                    self._clip_and_serve()
+            else:
+                self._clip_and_serve()
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record(self.comm)
+            self.round_events.append(ev)
+        r = self.round
+        self.round += 1
+        self.stats["rounds"] += 1
+        # weights version for the next forward
+        v = max(0, self.round - self.staleness)
+        need_round = v - 1  # round that produced version v
+        if self.gpu:
+            while self.round_events and (r - len(self.round_events) + 1) <= need_round:
+                ev = self.round_events.popleft()
+                torch.cuda.current_stream(self.device).wait_event(ev)
+        self.wslot = v % self.nslots
+        self.gslot = self.round % self.nslots
+        g = self.gbuf
+        for grp in g:
+            g[grp][self.gslot].zero_()
+        self.pending = [len(b.keys) for b in self.reg.buckets]
+        self.launched = [False] * len(self.reg.buckets)
+        self._bind(self.wslot, self.gslot)
+
+    def synchronize(self) -> None:
+        """Drain every in-flight round (checkpoint / eval boundary)."""
+        if self.gpu:
+            while self.round_events:
+                torch.cuda.current_stream(self.device).wait_event(self.round_events.popleft())
+
+    # ------------------------------------------------------------------ checkpoint
+    def shard_state(self) -> dict:
+        """This rank's server shard: fp32 master + optimizer state + clock."""
+        self.synchronize()
+        return {
+            "rank": self.rank, "world": self.world, "round": self.round, "staleness": self.staleness,
+            "master": [m.detach().cpu() for m in self.master],
+            "states": [[[s.detach().cpu() for s in st] for st in sts] for sts in self.states],
+            "manifest": {k: {"shape": list(ki.shape), "dtype": str(ki.dtype), "bucket": ki.bucket,
+                             "offset": ki.offset, "group": ki.group} for k, ki in self.reg.keys.items()},
+            "buckets": [{"group": b.group, "start": b.start, "size": b.size} for b in self.reg.buckets],
+        }
+
+    def load_shard_state(self, st: dict) -> None:
+        if st["world"] != self.world or st["rank"] != self.rank:
+            raise ValueError("checkpoint was written with a different world size / rank")
+        self.synchronize()
+        with torch.no_grad():
+            for m, src in zip(self.master, st["master"]):
+                m.copy_(src.to(m.device))
+            for sts, srcs in zip(self.states, st["states"]):
+                for s_list, src_list in zip(sts, srcs):
+                    for s, src in zip(s_list, src_list):
+                        s.copy_(src.to(s.device))
+            self.round = int(st["round"])
+            # rebuild every replica slot by one pull of the restored masters
+            for b, bk in enumerate(self.reg.buckets):
+                lo, hi = bk.owner_range(self.rank)
+                for slot in range(self.nslots):
+                    wfull = self.wbuf[bk.group][slot]
+                    wfull[lo:hi].copy_(self.master[b].to(wfull.dtype))
+                    self.t.all_gather(wfull[bk.start:bk.start + bk.size], wfull[lo:hi])
+        self.wslot = max(0, self.round - self.staleness) % self.nslots
+        self.gslot = self.round % self.nslots
+        for grp in self.gbuf:
+            self.gbuf[grp][self.gslot].zero_()
+        self._bind(self.wslot, self.gslot)
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def timed(fn):
+    t0 = time.perf_counter()
+    fn()
+    return (time.perf_counter() - t0) * 1e3
