@@ -6,7 +6,7 @@
 // with torch streams, events and HIP-graph capture.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "psamd_launch.h"
 
@@ -66,7 +66,7 @@ void fused_opt(int64_t kind, Tensor w, c10::optional<Tensor> st0, c10::optional<
     wout_bf16 = dcode(*wout, "wout");
   }
   if (gscale_t.has_value() && gscale_t->defined()) check_f32(*gscale_t, "gscale_t");
-  const c10::hip::HIPGuard guard(w.device());
+  const c10::DeviceGuard guard(w.device());
   psamd::FusedOptArgs a;
   a.kind = static_cast<int>(kind);
   a.w = w.data_ptr<float>();
@@ -103,7 +103,7 @@ void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::opti
   if (st1.has_value() && st1->defined()) { check_f32(*st1, "st1"); TORCH_CHECK(st1->numel() == table.numel(), "st1"); }
   if (kind == 1 || kind == 3) TORCH_CHECK(st0.has_value() && st1.has_value(), "adam/ftrl need 2 states");
   if (kind == 2) TORCH_CHECK(st0.has_value(), "adagrad needs a state");
-  const c10::hip::HIPGuard guard(table.device());
+  const c10::DeviceGuard guard(table.device());
   psamd::SparseOptArgs a;
   a.kind = static_cast<int>(kind);
   a.table = table.data_ptr<float>();
@@ -127,7 +127,7 @@ void sumsq(Tensor x, Tensor out, bool accumulate) {
   check_gpu(x, "x");
   check_f32(out, "out");
   TORCH_CHECK(out.numel() >= 1, "out must hold one float");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   const int nb = psamd::sumsq_blocks(x.numel());
   auto partial = torch::empty({nb}, out.options());
   auto s = cur_stream(x);
@@ -138,7 +138,7 @@ void sumsq(Tensor x, Tensor out, bool accumulate) {
 void clip_factor(Tensor sq, double max_norm, Tensor factor) {
   check_f32(sq, "sumsq");
   check_f32(factor, "factor");
-  const c10::hip::HIPGuard guard(sq.device());
+  const c10::DeviceGuard guard(sq.device());
   psamd::launch_clip_factor(sq.data_ptr<float>(), static_cast<float>(max_norm), factor.data_ptr<float>(),
                             cur_stream(sq));
 }
@@ -147,7 +147,7 @@ void cast_(Tensor x, Tensor y, double scale) {
   check_gpu(x, "x");
   check_gpu(y, "y");
   TORCH_CHECK(x.numel() == y.numel(), "cast size mismatch");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_cast(x.data_ptr(), dcode(x, "x"), y.data_ptr(), dcode(y, "y"), x.numel(), static_cast<float>(scale),
                      cur_stream(x));
 }
@@ -156,7 +156,7 @@ void axpy_(double a, Tensor x, Tensor y) {
   check_gpu(x, "x");
   check_gpu(y, "y");
   TORCH_CHECK(x.numel() == y.numel(), "axpy size mismatch");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_axpy(static_cast<float>(a), x.data_ptr(), dcode(x, "x"), y.data_ptr(), dcode(y, "y"), x.numel(),
                      cur_stream(x));
 }
@@ -166,7 +166,7 @@ void reduce_n(Tensor x, Tensor y, double scale) {
   check_gpu(y, "y");
   TORCH_CHECK(x.dim() == 2, "x must be [k, n]");
   TORCH_CHECK(x.size(1) == y.numel(), "reduce_n size mismatch");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_reduce_n(x.data_ptr(), dcode(x, "x"), static_cast<int>(x.size(0)), x.size(1), y.data_ptr(),
                          dcode(y, "y"), static_cast<float>(scale), cur_stream(x));
 }
@@ -176,7 +176,7 @@ void lerp(Tensor w0, Tensor w, double sc, Tensor out) {
   check_f32(w, "w");
   check_gpu(out, "out");
   TORCH_CHECK(w0.numel() == w.numel() && w.numel() == out.numel(), "lerp size mismatch");
-  const c10::hip::HIPGuard guard(w.device());
+  const c10::DeviceGuard guard(w.device());
   psamd::launch_lerp(w0.data_ptr<float>(), w.data_ptr<float>(), static_cast<float>(sc), out.data_ptr(),
                      dcode(out, "out"), w.numel(), cur_stream(w));
 }
@@ -192,7 +192,7 @@ void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
   TORCH_CHECK(err.numel() == n, "err size");
   TORCH_CHECK(words.numel() >= (n + 63) / 64, "words too small");
   TORCH_CHECK(scales.numel() >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   psamd::launch_onebit_pack(g.data_ptr(), dcode(g, "g"), err.data_ptr<float>(), n,
                             reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), scales.data_ptr<float>(),
                             cur_stream(g));
@@ -206,7 +206,7 @@ void onebit_unpack_reduce(Tensor words, Tensor scales, Tensor out, double mult, 
   const int64_t n = out.numel();
   TORCH_CHECK(words.size(1) >= (n + 63) / 64, "words too small");
   TORCH_CHECK(scales.size(1) >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
-  const c10::hip::HIPGuard guard(out.device());
+  const c10::DeviceGuard guard(out.device());
   psamd::launch_onebit_unpack_reduce(reinterpret_cast<const uint64_t*>(words.data_ptr<int64_t>()),
                                      scales.data_ptr<float>(), static_cast<int>(words.size(0)), n, words.size(1),
                                      scales.size(1), out.data_ptr(), dcode(out, "out"), static_cast<float>(mult),
@@ -222,7 +222,7 @@ void gather_rows(Tensor table, Tensor rows, Tensor out, int64_t out_off, int64_t
   const int64_t dim = table.size(1);
   TORCH_CHECK(out.size(0) == rows.numel(), "out rows != len(rows)");
   TORCH_CHECK(out_off >= 0 && out_off + dim <= out.size(1), "out column slice out of range");
-  const c10::hip::HIPGuard guard(table.device());
+  const c10::DeviceGuard guard(table.device());
   psamd::launch_gather_rows(table.data_ptr(), dcode(table, "table"), rows.data_ptr<int64_t>(), rows.numel(),
                             static_cast<int>(dim), out.data_ptr(), dcode(out, "out"), out.size(1), out_off,
                             static_cast<int>(act), cur_stream(table));
@@ -236,7 +236,7 @@ void segment_reduce_rows(Tensor src, Tensor perm, Tensor seg_off, Tensor out, bo
   TORCH_CHECK(src.dim() == 2 && out.dim() == 2 && src.size(1) == out.size(1), "src/out [*, dim]");
   TORCH_CHECK(seg_off.numel() == out.size(0) + 1, "seg_off must have nseg+1 entries");
   TORCH_CHECK(perm.numel() == src.size(0), "perm must index every src row");
-  const c10::hip::HIPGuard guard(src.device());
+  const c10::DeviceGuard guard(src.device());
   psamd::launch_segment_reduce_rows(src.data_ptr(), dcode(src, "src"), perm.data_ptr<int64_t>(),
                                     seg_off.data_ptr<int64_t>(), out.size(0), static_cast<int>(src.size(1)),
                                     out.data_ptr(), dcode(out, "out"), mean, cur_stream(src));
@@ -248,7 +248,7 @@ void scatter_add_rows(Tensor src, Tensor rows, Tensor table) {
   check_f32(table, "table");
   TORCH_CHECK(table.dim() == 2 && src.dim() == 2 && src.size(1) == table.size(1), "shape");
   TORCH_CHECK(src.size(0) == rows.numel(), "src rows != len(rows)");
-  const c10::hip::HIPGuard guard(src.device());
+  const c10::DeviceGuard guard(src.device());
   psamd::launch_scatter_add_rows(src.data_ptr(), dcode(src, "src"), rows.data_ptr<int64_t>(), rows.numel(),
                                  static_cast<int>(src.size(1)), table.data_ptr<float>(), cur_stream(src));
 }
@@ -261,7 +261,7 @@ void embedding_bag_fwd(Tensor table, Tensor ids, Tensor out, int64_t out_off, in
   const int64_t fields = ids.size(1), dim = table.size(1);
   TORCH_CHECK(out.size(0) == ids.size(0), "batch mismatch");
   TORCH_CHECK(out_off >= 0 && out_off + fields * dim <= out.size(1), "out column slice out of range");
-  const c10::hip::HIPGuard guard(table.device());
+  const c10::DeviceGuard guard(table.device());
   psamd::launch_embedding_bag_fwd(table.data_ptr<float>(), ids.data_ptr<int64_t>(), ids.size(0),
                                   static_cast<int>(fields), static_cast<int>(dim), out.data_ptr(), dcode(out, "out"),
                                   out.size(1), out_off, static_cast<int>(act), cur_stream(table));
@@ -273,7 +273,7 @@ void sparse_lr_fwd(Tensor w, Tensor ids, c10::optional<Tensor> bias, Tensor out)
   check_f32(out, "out");
   TORCH_CHECK(ids.dim() == 2 && out.numel() == ids.size(0), "ids [B,F], out [B]");
   if (bias.has_value() && bias->defined()) check_f32(*bias, "bias");
-  const c10::hip::HIPGuard guard(w.device());
+  const c10::DeviceGuard guard(w.device());
   psamd::launch_sparse_lr_fwd(w.data_ptr<float>(), ids.data_ptr<int64_t>(), ids.size(0),
                               static_cast<int>(ids.size(1)), w.numel(), opt_ptr<const float>(bias),
                               out.data_ptr<float>(), cur_stream(w));
@@ -284,7 +284,7 @@ void lazy_init_rows(Tensor table, Tensor rows, Tensor flags, int64_t seed, int64
   check_i64(rows, "rows");
   check_gpu(flags, "flags");
   TORCH_CHECK(flags.scalar_type() == torch::kUInt8 && flags.numel() == table.size(0), "flags uint8 [rows]");
-  const c10::hip::HIPGuard guard(table.device());
+  const c10::DeviceGuard guard(table.device());
   psamd::launch_lazy_init_rows(table.data_ptr<float>(), rows.data_ptr<int64_t>(), rows.numel(),
                                static_cast<int>(table.size(1)), flags.data_ptr<uint8_t>(),
                                static_cast<uint64_t>(seed), row_base, static_cast<float>(lo), static_cast<float>(hi),
@@ -296,7 +296,7 @@ void softmax_temp_fwd(Tensor x, Tensor y, double temp, double clamp_lo, double c
   check_f32(x, "x");
   check_f32(y, "y");
   TORCH_CHECK(x.dim() == 2 && x.sizes() == y.sizes(), "x,y [rows, cols]");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_softmax_temp_fwd(x.data_ptr<float>(), y.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)),
                                  static_cast<float>(1.0 / temp), static_cast<float>(clamp_lo),
                                  static_cast<float>(clamp_hi), cur_stream(x));
@@ -308,7 +308,7 @@ void softmax_xent(Tensor p, Tensor labels, Tensor loss, c10::optional<Tensor> gr
   check_f32(loss, "loss");
   TORCH_CHECK(p.dim() == 2 && labels.numel() == p.size(0), "p [B,C], labels [B]");
   if (grad.has_value() && grad->defined()) { check_f32(*grad, "grad"); TORCH_CHECK(grad->sizes() == p.sizes(), "grad"); }
-  const c10::hip::HIPGuard guard(p.device());
+  const c10::DeviceGuard guard(p.device());
   psamd::launch_softmax_xent(p.data_ptr<float>(), labels.data_ptr<int64_t>(), p.size(0), static_cast<int>(p.size(1)),
                              loss.data_ptr<float>(), opt_ptr<float>(grad), cur_stream(p));
 }
@@ -319,7 +319,7 @@ void bce(Tensor p, Tensor y, Tensor loss, c10::optional<Tensor> grad) {
   check_f32(loss, "loss");
   TORCH_CHECK(p.numel() == y.numel(), "p/y size");
   if (grad.has_value() && grad->defined()) { check_f32(*grad, "grad"); TORCH_CHECK(grad->numel() == p.numel(), "grad"); }
-  const c10::hip::HIPGuard guard(p.device());
+  const c10::DeviceGuard guard(p.device());
   psamd::launch_bce(p.data_ptr<float>(), y.data_ptr<float>(), p.numel(), loss.data_ptr<float>(), opt_ptr<float>(grad),
                     cur_stream(p));
 }
@@ -333,7 +333,7 @@ void maxpool2d_fwd(Tensor x, int64_t k, int64_t stride, int64_t pad, Tensor y, T
   TORCH_CHECK(x.scalar_type() == y.scalar_type(), "x/y dtype");
   const int64_t h = x.size(2), w = x.size(3), oh = y.size(2), ow = y.size(3);
   TORCH_CHECK(oh == (h + 2 * pad - k) / stride + 1 && ow == (w + 2 * pad - k) / stride + 1, "pool output shape");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_maxpool2d_fwd(x.data_ptr(), dcode(x, "x"), x.size(0) * x.size(1), static_cast<int>(h),
                               static_cast<int>(w), static_cast<int>(k), static_cast<int>(stride),
                               static_cast<int>(pad), y.data_ptr(), argmax.data_ptr<int32_t>(), static_cast<int>(oh),
@@ -346,7 +346,7 @@ void maxpool2d_bwd(Tensor dy, Tensor argmax, int64_t k, int64_t stride, int64_t 
   TORCH_CHECK(argmax.scalar_type() == torch::kInt32 && argmax.sizes() == dy.sizes(), "argmax");
   TORCH_CHECK(dy.scalar_type() == dx.scalar_type(), "dtype");
   TORCH_CHECK(dx.dim() == 4 && dy.dim() == 4 && dx.size(0) == dy.size(0) && dx.size(1) == dy.size(1), "NCHW");
-  const c10::hip::HIPGuard guard(dy.device());
+  const c10::DeviceGuard guard(dy.device());
   psamd::launch_maxpool2d_bwd(dy.data_ptr(), dcode(dy, "dy"), argmax.data_ptr<int32_t>(), dx.size(0) * dx.size(1),
                               static_cast<int>(dx.size(2)), static_cast<int>(dx.size(3)), static_cast<int>(dy.size(2)),
                               static_cast<int>(dy.size(3)), static_cast<int>(k), static_cast<int>(stride),
@@ -360,7 +360,7 @@ void im2col(Tensor x, int64_t k, int64_t stride, int64_t pad, Tensor col) {
   const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3);
   const int64_t oh = (h + 2 * pad - k) / stride + 1, ow = (w + 2 * pad - k) / stride + 1;
   TORCH_CHECK(col.numel() == n * oh * ow * c * k * k, "col must be [n*oh*ow, c*k*k]");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_im2col(x.data_ptr<float>(), n, static_cast<int>(c), static_cast<int>(h), static_cast<int>(w),
                        static_cast<int>(k), static_cast<int>(stride), static_cast<int>(pad), static_cast<int>(oh),
                        static_cast<int>(ow), col.data_ptr<float>(), cur_stream(x));
@@ -373,7 +373,7 @@ void col2im(Tensor col, int64_t k, int64_t stride, int64_t pad, Tensor x) {
   const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3);
   const int64_t oh = (h + 2 * pad - k) / stride + 1, ow = (w + 2 * pad - k) / stride + 1;
   TORCH_CHECK(col.numel() == n * oh * ow * c * k * k, "col must be [n*oh*ow, c*k*k]");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_col2im(col.data_ptr<float>(), n, static_cast<int>(c), static_cast<int>(h), static_cast<int>(w),
                        static_cast<int>(k), static_cast<int>(stride), static_cast<int>(pad), static_cast<int>(oh),
                        static_cast<int>(ow), x.data_ptr<float>(), cur_stream(x));
@@ -384,14 +384,14 @@ void dropout(Tensor x, Tensor y, double p, int64_t seed, int64_t offset) {
   check_gpu(y, "y");
   TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "dropout shape/dtype");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "p in [0, 1)");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   psamd::launch_dropout_fwd(x.data_ptr(), dcode(x, "x"), y.data_ptr(), x.numel(), static_cast<float>(p),
                             static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), cur_stream(x));
 }
 
 void uniform_init(Tensor w, int64_t seed, int64_t offset, double lo, double hi) {
   check_f32(w, "w");
-  const c10::hip::HIPGuard guard(w.device());
+  const c10::DeviceGuard guard(w.device());
   psamd::launch_uniform_init(w.data_ptr<float>(), w.numel(), static_cast<uint64_t>(seed),
                              static_cast<uint64_t>(offset), static_cast<float>(lo), static_cast<float>(hi),
                              cur_stream(w));

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t i = base + j * 256 + threadIdx.x;
-    const bool pos = c[j] >= 0.f;
+    const bool pos = (i < n) && c[j] >= 0.f;  // padded lanes contribute 0 bits
     const uint64_t m = __ballot(pos);
     if (i < n) err[i] = c[j] - (pos ? scale : -scale);
     const int64_t wbase = base + j * 256 + wid * 64;

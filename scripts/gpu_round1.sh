@@ -2,6 +2,7 @@
 # First GPU session: kernel numerics tests, smoke, ResNet-50 probe. Stops on any crash/timeout.
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export PYTHONPATH=$PWD:$PYTHONPATH
 rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
