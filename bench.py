@@ -40,13 +40,47 @@ def parse():
     ap.add_argument("--staleness", type=int, default=0)
     ap.add_argument("--bn-fp32", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
+                    help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
+                         "ResNet-50: 40.8 vs 39.4 ms, profiles/r1_graph_vs_eager.txt)")
+    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("PS_AMD_CONV_BENCHMARK", "1")),
+                    help="MIOpen find (exhaustive) for each conv shape during warm-up")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
 
 
+def setup_miopen_db():
+    """Point MIOpen at a writable copy of the in-repo find/perf db (miopen_db/udb: conv
+    algorithm choices for the ResNet-50 shapes, recorded by our own warm-up runs) so a
+    fresh box skips most of the exhaustive search.  Naive reference solvers are excluded
+    from find (they are never chosen and cost minutes to benchmark)."""
+    import shutil
+    import tempfile
+
+    for k in ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_BWD",
+              "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_WRW"):
+        os.environ.setdefault(k, "0")
+    if "MIOPEN_USER_DB_PATH" in os.environ:
+        return
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+    dst = os.path.join(tempfile.gettempdir(), f"ps_amd_miopen_{os.getuid()}_{os.environ.get('LOCAL_RANK', '0')}")
+    try:
+        for sub in ("udb", "cache"):
+            os.makedirs(os.path.join(dst, sub), exist_ok=True)
+            if os.path.isdir(os.path.join(src, sub)):
+                for f in os.listdir(os.path.join(src, sub)):
+                    if not os.path.exists(os.path.join(dst, sub, f)):
+                        shutil.copy2(os.path.join(src, sub, f), os.path.join(dst, sub, f))
+        os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(dst, "udb")
+        os.environ["MIOPEN_CUSTOM_CACHE_DIR"] = os.path.join(dst, "cache")
+    except OSError:
+        pass
+
+
 def main():
     args = parse()
+    setup_miopen_db()
     from ps_amd.parallel.transport import init_distributed
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import MomentumUpdater
@@ -69,7 +103,7 @@ def main():
     tp = init_distributed()
     rank, world = tp.rank, tp.world
     dev = torch.device("cuda", local)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.manual_seed(1234)
 
     model = prepare_for_mi355x(resnet50().to(dev), bn_fp32=bool(args.bn_fp32))
@@ -89,8 +123,21 @@ def main():
         ps.finish_step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    use_graph = args.graph == "1" or (args.graph == "auto" and world == 1)
+    tw0 = time.perf_counter()
+    if use_graph:
+        from ps_amd.train.graphs import GraphedStep
+
+        # eager warm-up (MIOpen find) inside GraphedStep, then capture; W counts warm-up steps
+        graphed = GraphedStep(step, warmup=max(1, args.warmup - 1))
+        step = graphed
+    else:
+        for _ in range(args.warmup):
+            step()
+    torch.cuda.synchronize()
+    if rank == 0:
+        print(f"[bench] warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
+              f"(includes MIOpen find/compile for new conv shapes)", file=sys.stderr, flush=True)
     tp.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -139,6 +186,7 @@ def main():
                 "optimizer": upd.name,
                 "bucket_mb": args.bucket_mb,
                 "staleness": args.staleness,
+                "hip_graph": bool(use_graph),
                 "final_loss": round(float(loss.item()), 4),
             },
         }
