@@ -173,6 +173,8 @@ class AdamUpdater(Updater):
 
     def spec_items(self):
         items = [("alfa", self.alfa), ("beta1", self.beta1), ("beta2", self.beta2), ("epsilon", self.epsilon)]
+        if self.bias_correction != "reference":  # reference spec strings imply the constant form
+            items.append(("bc", {"step": 1.0, "none": 0.0}[self.bias_correction]))
         return items
 
     def hyper(self, step):
@@ -230,7 +232,10 @@ class FtrlUpdater(Updater):
         self.mode = mode
 
     def spec_items(self):
-        return [("alfa", self.alfa), ("beta", self.beta), ("l1", self.l1), ("l2", self.l2)]
+        items = [("alfa", self.alfa), ("beta", self.beta), ("l1", self.l1), ("l2", self.l2)]
+        if self.mode == "reference":
+            items.append(("reference", 1.0))
+        return items
 
     def hyper(self, step):
         return dict(lr=self.alfa, fbeta=self.beta, l1=self.l1, l2=self.l2,
@@ -262,18 +267,20 @@ def parse_updater(spec: str) -> Updater:
     head = spec.split("@", 1)[0].strip().lower()
     g = lambda k, d=None: float(_between(spec, k)) if _between(spec, k) is not None else d  # noqa: E731
     if head == "adam" and _between(spec, "l1") is not None:
-        head = "ftrl"  # reference FtrlUpdater.getName() quirk (Q6)
+        # reference FtrlUpdater.getName() quirk (Q6): such strings come from the reference
+        return FtrlUpdater(g("alfa", 0.005), g("beta", 1.0), g("l1", 0.001), g("l2", 0.001), mode="reference")
     if head in ("simple", "sgd"):
         return SimpleUpdater(g("eta", 0.01))
     if head == "momentum":
         return MomentumUpdater(g("lr", 0.1), g("momentum", 0.9), g("wd", 0.0), bool(g("nesterov", 0.0)))
     if head == "adam":
-        bc = {0: "none", 1: "step", 2: "reference"}.get(int(g("bc", 1)), "step")
+        bc = {0: "none", 1: "step", 2: "reference"}.get(int(g("bc", 2)), "reference")
         return AdamUpdater(g("alfa", 0.001), g("beta1", 0.9), g("beta2", 0.999), g("epsilon", 1e-8), bc)
     if head == "adagrad":
         return AdagradUpdater(g("lr", 0.01), g("epsilon", 1e-10), rowwise=bool(g("rowwise", 0.0)))
     if head == "ftrl":
-        return FtrlUpdater(g("alfa", 0.005), g("beta", 1.0), g("l1", 0.001), g("l2", 0.001))
+        return FtrlUpdater(g("alfa", 0.005), g("beta", 1.0), g("l1", 0.001), g("l2", 0.001),
+                           mode="reference" if g("reference", 0.0) else "canonical")
     raise ValueError(f"unknown updater spec {spec!r}")
 
 
