@@ -114,6 +114,22 @@ class Model(nn.Module):
         return sum(layer.push_sparse() for layer in self.sparse_layers())
 
 
+def _scale_init(model: Model, scale: float) -> None:
+    """``init_scale`` != 1 shrinks the reference's 4*xavier uniform init (FcLayer.java:39)
+    -- at scale 1 a small synthetic problem needs the reference's 100 epochs to recover
+    from saturated sigmoids / dead ReLUs."""
+    if scale == 1.0:
+        return
+    with torch.no_grad():
+        for p in model.parameters():
+            p.mul_(scale)
+    for t in model.tables().values():
+        if hasattr(t, "init"):
+            t.init = (t.init[0] * scale, t.init[1] * scale)
+        elif hasattr(t, "local"):
+            t.local.init = (t.local.init[0] * scale, t.local.init[1] * scale)
+
+
 def _bind_table_updaters(model: Model):
     from ..parallel.updaters import resolve_updater
 
@@ -123,7 +139,7 @@ def _bind_table_updaters(model: Model):
 
 class DNN(Model):
     def __init__(self, fields, dim, numeric, fc_dims, table_factory=None, gen=None, grad_mode="exact",
-                 emb_rows: int = 100000):
+                 emb_rows: int = 100000, init_scale: float = 1.0):
         super().__init__()
         tf = table_factory or local_table_factory()
         bound = 4 * math.sqrt(6) / math.sqrt(1 + dim)
@@ -135,6 +151,7 @@ class DNN(Model):
         self.loss = CrossEntropy()
         self.updater["default"] = AdamUpdater(0.005, 0.9, 0.999, 1e-8, bias_correction="reference")
         _bind_table_updaters(self)
+        _scale_init(self, init_scale)
 
     def forward(self, batch):
         e = self.embedding(batch["E"])
@@ -155,7 +172,7 @@ class DNN(Model):
 
 class WideDeepNN(Model):
     def __init__(self, fields, dim, numeric, fc_dims, wide_size, table_factory=None, gen=None, grad_mode="exact",
-                 emb_rows: int = 100000):
+                 emb_rows: int = 100000, init_scale: float = 1.0):
         super().__init__()
         tf = table_factory or local_table_factory()
         bound = 4 * math.sqrt(6) / math.sqrt(1 + dim)
@@ -174,6 +191,7 @@ class WideDeepNN(Model):
         self.updater["wide.bias"] = ftrl
         self.updater["default"] = AdamUpdater(0.005, 0.9, 0.999, 1e-8, bias_correction="reference")
         _bind_table_updaters(self)
+        _scale_init(self, init_scale)
 
     def forward(self, batch):
         e = self.embedding(batch["E"])

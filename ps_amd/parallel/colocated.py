@@ -65,6 +65,7 @@ class ColocatedPS:
             raise ValueError(f"unknown compression {compress!r}")
         self.average = average
         self.overlap = overlap
+        self.accumulating = False  # micro-batch accumulation: hooks stay quiet until the last one
         params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         if not params:
             raise ValueError("model has no trainable parameters")
@@ -164,6 +165,8 @@ class ColocatedPS:
 
     # ------------------------------------------------------------------ push path
     def _on_ready(self, name: str, p: torch.Tensor) -> None:
+        if self.accumulating:
+            return
         b = self._key_bucket[name]
         self.pending[b] -= 1
         if self.pending[b] == 0 and self.overlap:

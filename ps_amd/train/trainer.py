@@ -1,0 +1,143 @@
+"""Training runtime (train/Trainer.java, TrainerThread.java, PredictThread.java).
+
+The reference runs ``nThreads`` model replicas on a CPU thread pool, averages their
+gradients in the shared KVStore and applies one optimizer step per round
+(Trainer.java:70-101).  On a GPU the replicas become micro-batches accumulated into the
+same gradient buckets (identical math: the average of the replica gradients), followed by
+ONE parameter-server round.  Engines:
+
+  CollectiveEngine  co-located PS over RCCL/gloo collectives (colocated.py) for dense keys
+                    + sharded sparse tables; BSP or SSP(s).  The MI355X path.
+  KVEngine          the reference KVStore API: standalone in-process store, or a worker of
+                    dedicated TCP servers (tcp.py) -- pull before the step, sum + push +
+                    barrier/clock after it.
+
+``Trainer.train(batches)`` returns the mean loss; failures of a replica are counted as the
+reference does (loss 0 + log) only when ``tolerate_failures`` is set -- by default they
+raise.  Per-step timings (fwd+bwd, push/update, exposed wait) go to the metrics stream.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..context import Stat, ctx
+from ..obs import metrics as _metrics
+from ..parallel.colocated import ColocatedPS
+from ..parallel.kvstore import KVStore
+from ..parallel.transport import Transport
+
+log = logging.getLogger("ps_amd.trainer")
+
+
+def _to(batch: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
+    return {k: (v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
+
+
+class CollectiveEngine:
+    def __init__(self, model, transport: Optional[Transport] = None, *, bucket_mb: float = 25.0,
+                 staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None):
+        self.model = model
+        self.t = transport or Transport()
+        dense = [p for p in model.parameters() if p.requires_grad]
+        self.ps = ColocatedPS(model, model.get_updater(), self.t, bucket_mb=bucket_mb, staleness=staleness,
+                              clip_norm=clip_norm, compress=compress) if dense else None
+
+    def accumulate(self, on: bool) -> None:
+        if self.ps is not None:
+            self.ps.accumulating = on
+
+    def end_step(self) -> None:
+        self.model.push_sparse()
+        if self.ps is not None:
+            self.ps.finish_step()
+
+    def pull(self) -> None:
+        self.model.pull_weights()
+
+    def synchronize(self) -> None:
+        if self.ps is not None:
+            self.ps.synchronize()
+
+
+class KVEngine:
+    def __init__(self, model, store: Optional[KVStore] = None):
+        self.model = model
+        self.kv = store or KVStore.ins()
+
+    def accumulate(self, on: bool) -> None:
+        pass
+
+    def pull(self) -> None:
+        self.model.pull_weights()
+        self.kv.pull_into(self.model)
+
+    def end_step(self) -> None:
+        self.kv.sum_from(self.model)
+        for p in self.model.parameters():
+            p.grad = None
+        self.model.push_sparse()
+        self.kv.update(self.model.get_updater())
+        self.kv.clear()
+
+    def synchronize(self) -> None:
+        pass
+
+
+class Trainer:
+    def __init__(self, model, engine=None, n_threads: int = 1, device=None, tolerate_failures: bool = False):
+        self.model = model
+        self.engine = engine or KVEngine(model)
+        self.n_threads = max(1, int(n_threads))
+        self.device = device
+        self.tolerate_failures = tolerate_failures
+        self.last_timing: Dict[str, float] = {}
+
+    def _dev(self, b):
+        return _to(b, self.device) if self.device is not None else b
+
+    def train(self, batches: Sequence[Dict[str, torch.Tensor]]) -> float:
+        """One PS round over up to ``n_threads`` micro-batches (Trainer.java:70-101)."""
+        ctx.status = Stat.TRAINING
+        batches = list(batches)[: self.n_threads] if self.n_threads > 1 else list(batches)[:1]
+        if not batches:
+            raise ValueError("no batches")
+        t0 = time.perf_counter()
+        self.engine.pull()
+        losses = []
+        for i, b in enumerate(batches):
+            ctx.model_index = i
+            self.engine.accumulate(i < len(batches) - 1)
+            try:
+                losses.append(self.model.train_batch(self._dev(b), scale=1.0 / len(batches)))
+            except Exception:
+                if not self.tolerate_failures:
+                    raise
+                log.exception("replica %d failed; counting loss 0 (reference TrainerThread.java:36-38)", i)
+                losses.append(0.0)
+        ctx.model_index = 0
+        t1 = time.perf_counter()
+        self.engine.end_step()
+        t2 = time.perf_counter()
+        loss = sum(losses) / len(losses)
+        step = ctx.incr_step()
+        _metrics.plot("loss", loss, step)
+        self.last_timing = {"fwd_bwd_ms": (t1 - t0) * 1e3, "ps_round_ms": (t2 - t1) * 1e3}
+        _metrics.log_step(step=step, loss=loss, **self.last_timing)
+        return loss
+
+    def predict(self, batches: Sequence[Dict[str, torch.Tensor]]) -> List[torch.Tensor]:
+        """Forward only (Trainer.java:44-68 / PredictThread)."""
+        prev = ctx.status
+        if prev == Stat.TRAINING:
+            ctx.status = Stat.PREDICTING
+        self.engine.synchronize()
+        out = []
+        for b in batches:
+            out.append(self.model.predict(self._dev(b)))
+            self.model.pull_weights()  # drop sparse leaves created by the forward
+        ctx.status = prev
+        return out
