@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--last-bucket-mb", type=float, default=2.0)
     ap.add_argument("--staleness", type=int, default=0)
     ap.add_argument("--bn-fp32", type=int, default=1)
+    ap.add_argument("--fused-bn", type=int, default=int(os.environ.get("PS_AMD_FUSED_BN", "1")),
+                    help="HIP fused BatchNorm+residual+ReLU kernels (ops/bn.py) instead of MIOpen BN")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
                     help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
@@ -106,7 +108,7 @@ def main():
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.manual_seed(1234)
 
-    model = prepare_for_mi355x(resnet50().to(dev), bn_fp32=bool(args.bn_fp32))
+    model = prepare_for_mi355x(resnet50(fused_bn=bool(args.fused_bn)).to(dev), bn_fp32=bool(args.bn_fp32))
     upd = MomentumUpdater(lr=args.lr, momentum=0.9, weight_decay=5e-5)
     ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
                      staleness=args.staleness)
@@ -187,6 +189,7 @@ def main():
                 "bucket_mb": args.bucket_mb,
                 "staleness": args.staleness,
                 "hip_graph": bool(use_graph),
+                "fused_bn": bool(args.fused_bn),
                 "final_loss": round(float(loss.item()), 4),
             },
         }

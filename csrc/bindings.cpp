@@ -397,6 +397,98 @@ void uniform_init(Tensor w, int64_t seed, int64_t offset, double lo, double hi) 
                              cur_stream(w));
 }
 
+// ------------------------------------------------------------------------------ batchnorm
+std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
+                               c10::optional<Tensor> beta, c10::optional<Tensor> rmean, c10::optional<Tensor> rvar,
+                               bool training, double momentum, double eps, int64_t act) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16, "x must be bf16 (NHWC-contiguous [R, C] view)");
+  TORCH_CHECK(x.dim() == 2, "x must be viewed as [R, C]");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  if (res.has_value() && res->defined()) {
+    check_gpu(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(), "res like x");
+  }
+  for (auto* t : {&gamma, &beta, &rmean, &rvar})
+    if (t->has_value() && (*t)->defined()) {
+      check_f32(**t, "bn param");
+      TORCH_CHECK((*t)->numel() == C, "bn param size");
+    }
+  if (!training) TORCH_CHECK(rmean.has_value() && rvar.has_value(), "eval mode needs running stats");
+  const c10::DeviceGuard guard(x.device());
+  auto y = torch::empty_like(x);
+  auto fopt = x.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({C}, fopt), invstd = torch::empty({C}, fopt);
+  auto coef = torch::empty({2 * C}, fopt);
+  const int G = psamd::bn_red_blocks(R);
+  auto ws = torch::empty({training ? 2 * G * C : 1}, fopt);
+  psamd::BnFwdArgs a;
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.res = (res.has_value() && res->defined()) ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr;
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.gamma = opt_ptr<const float>(gamma);
+  a.beta = opt_ptr<const float>(beta);
+  a.rmean = opt_ptr<float>(rmean);
+  a.rvar = opt_ptr<float>(rvar);
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.scale = coef.data_ptr<float>();
+  a.shift = coef.data_ptr<float>() + C;
+  a.ws = ws.data_ptr<float>();
+  a.R = R;
+  a.C = static_cast<int>(C);
+  a.G = G;
+  a.act = static_cast<int>(act);
+  a.training = training;
+  a.eps = static_cast<float>(eps);
+  a.momentum = static_cast<float>(momentum);
+  psamd::launch_bn_fwd(a, cur_stream(x));
+  return {y, mean, invstd};
+}
+
+std::vector<Tensor> bn_act_bwd(Tensor dy, Tensor y, Tensor x, c10::optional<Tensor> gamma, Tensor mean,
+                               Tensor invstd, int64_t act, bool want_dres, bool affine) {
+  check_gpu(dy, "dy");
+  check_gpu(y, "y");
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && y.sizes() == x.sizes(), "dy/y/x [R, C]");
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && y.scalar_type() == torch::kBFloat16 &&
+                  x.scalar_type() == torch::kBFloat16, "bf16 tensors");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C % 8");
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  TORCH_CHECK(mean.numel() == C && invstd.numel() == C, "stats size");
+  if (gamma.has_value() && gamma->defined()) check_f32(*gamma, "gamma");
+  const c10::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(torch::kFloat32);
+  auto dx = torch::empty_like(x);
+  Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
+  Tensor dgamma = affine ? torch::empty({C}, fopt) : Tensor();
+  Tensor dbeta = affine ? torch::empty({C}, fopt) : Tensor();
+  const int G = psamd::bn_red_blocks(R);
+  auto ws = torch::empty({2 * G * C + 3 * C}, fopt);
+  psamd::BnBwdArgs a;
+  a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+  a.y = reinterpret_cast<const uint16_t*>(y.data_ptr());
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.gamma = opt_ptr<const float>(gamma);
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.dgamma = affine ? dgamma.data_ptr<float>() : nullptr;
+  a.dbeta = affine ? dbeta.data_ptr<float>() : nullptr;
+  a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+  a.dres = want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr;
+  a.ws = ws.data_ptr<float>();
+  a.R = R;
+  a.C = static_cast<int>(C);
+  a.G = G;
+  a.act = static_cast<int>(act);
+  psamd::launch_bn_bwd(a, cur_stream(x));
+  return {dx, dres, dgamma, dbeta};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -426,6 +518,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col2im", &col2im);
   m.def("dropout", &dropout);
   m.def("uniform_init", &uniform_init);
+  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd", &bn_act_bwd);
   m.attr("ONEBIT_CHUNK") = psamd::kOnebitChunk;
   m.attr("ARCH") = "gfx950";
 }

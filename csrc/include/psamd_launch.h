@@ -103,6 +103,50 @@ void launch_dropout_bwd(const void* dy, int dtype, void* dx, int64_t n, float p_
                         uint64_t offset, hipStream_t s);
 void launch_uniform_init(float* w, int64_t n, uint64_t seed, uint64_t offset, float lo, float hi, hipStream_t s);
 
+// ---------------------------------------------------------------- bn_act.hip
+// NHWC BatchNorm (+residual) + activation; x/y/dy/dx/res bf16 [R, C]; params/stats fp32 [C].
+struct BnFwdArgs {
+  const uint16_t* x;
+  const uint16_t* res;  // nullable
+  uint16_t* y;
+  const float* gamma;   // nullable (affine=False)
+  const float* beta;
+  float* rmean;         // nullable (no running stats)
+  float* rvar;
+  float* mean;          // [C] saved for backward
+  float* invstd;        // [C]
+  float* scale;         // [C] scratch
+  float* shift;         // [C] scratch
+  float* ws;            // [2, G, C] partials
+  int64_t R;
+  int C;
+  int G;
+  int act;
+  int training;
+  float eps, momentum;
+};
+void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s);
+
+struct BnBwdArgs {
+  const uint16_t* dy;
+  const uint16_t* y;
+  const uint16_t* x;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;  // nullable
+  float* dbeta;   // nullable
+  uint16_t* dx;
+  uint16_t* dres;  // nullable: gradient of the fused residual input (= dz)
+  float* ws;       // [2, G, C] partials + [3, C] coefficients
+  int64_t R;
+  int C;
+  int G;
+  int act;
+};
+void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s);
+int bn_red_blocks(int64_t R);
+
 // ---------------------------------------------------------------- dense.hip (MFMA)
 // Y[M,N] = act(X[M,K] @ W[N,K]^T + b[N]); bf16 in/out, fp32 accumulate.
 // act: 0 none, 1 relu, 2 leaky relu(0.01), 3 clipped sigmoid (0.001 + 0.998*sigmoid)

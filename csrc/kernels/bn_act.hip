@@ -1,0 +1,388 @@
+// Fused BatchNorm (+ residual add) + activation for NHWC (channels_last) activations.
+//
+// ResNet-50 under MIOpen spends ~37 % of its step in BatchNorm and another ~17 % in the
+// separate ReLU / residual-add / ReLU-backward passes (profiles/r1_resnet50_ps_kernel_breakdown.txt).
+// All of them are HBM-bound, so the lever is passes over memory:
+//
+//   forward   MIOpen: stats(read x) + norm(read x, write z) + [add(read z,r write s)] + relu(read, write)
+//             here:   stats(read x) + apply(read x [+ read r], write y)
+//   backward  MIOpen: relu'(read dy,y write dz) + dscale/dbias(read dz,x) + dx(read dz,x write dx)
+//             here:   reduce(read dy,y,x) + apply(read dy,y,x write dx [+ write dres])
+//
+// Layout: x, y, dy, dx, residual are [R, C] row-major bf16 (R = N*H*W, C channels, C % 8 == 0);
+// gamma/beta/stats fp32.  Every thread moves 8 channels (16 B) per access.  Channel reductions
+// are two-level and deterministic: block partials [G, C] in fp32 (no atomics) + a finalize
+// kernel that sums them in fixed order.  act: 0 none, 1 relu.
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+
+struct RedGeom {
+  int tpr;      // threads per row = C / 8 (capped at 256 per channel tile)
+  int rows_it;  // rows a block covers per iteration = 256 / tpr
+};
+
+__host__ __device__ inline RedGeom red_geom(int C) {
+  int tpr = C / 8;
+  if (tpr > 256) tpr = 256;
+  // round up to a power of two so rows_it * tpr == 256 (idle lanes if C/8 is not one)
+  int p = 1;
+  while (p < tpr) p <<= 1;
+  return {p, 256 / p};
+}
+
+int bn_red_blocks(int64_t R) {
+  int64_t g = (R + 63) / 64;  // >= 64 rows per block keeps the [G, C] partials <= 1/16 of the data
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  return static_cast<int>(g);
+}
+
+// ------------------------------------------------------------------------------ stats
+// partial_s[g, c] = sum_{rows of block g} x[r, c]; partial_q likewise for x^2
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t R, int C,
+                                                               float* __restrict__ ps, float* __restrict__ pq) {
+  __shared__ float lds_s[256 * 8];
+  __shared__ float lds_q[256 * 8];
+  const RedGeom gm = red_geom(C);
+  const int t = threadIdx.x;
+  const int cg = t % gm.tpr + blockIdx.y * 256;  // channel group (8 channels)
+  const int r0 = t / gm.tpr;
+  const int ngroups = C / 8;
+  const int64_t G = gridDim.x;
+  const int64_t rows_per_block = (R + G - 1) / G;
+  const int64_t rb = blockIdx.x * rows_per_block;
+  const int64_t re = (rb + rows_per_block < R) ? rb + rows_per_block : R;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cg < ngroups) {
+    for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
+      float v[8];
+      load8(x, r * C + cg * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] += v[j] * v[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lds_s[t * 8 + j] = s[j];
+    lds_q[t * 8 + j] = q[j];
+  }
+  __syncthreads();
+  if (r0 == 0 && cg < ngroups) {
+    for (int k = 1; k < gm.rows_it; ++k) {
+      const int src = (k * gm.tpr + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += lds_s[src + j];
+        q[j] += lds_q[src + j];
+      }
+    }
+    float* os = ps + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    float* oq = pq + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    *reinterpret_cast<f32x4*>(os) = f32x4{s[0], s[1], s[2], s[3]};
+    *reinterpret_cast<f32x4*>(os + 4) = f32x4{s[4], s[5], s[6], s[7]};
+    *reinterpret_cast<f32x4*>(oq) = f32x4{q[0], q[1], q[2], q[3]};
+    *reinterpret_cast<f32x4*>(oq + 4) = f32x4{q[4], q[5], q[6], q[7]};
+  }
+}
+
+// Sum the [G, C] partials of one 8-channel group per block: thread t reads rows g = t, t+256, ...
+// (8 consecutive channels = 32 B per row), then an LDS tree over the 256 threads.  Fixed
+// order -> deterministic.  Returns the 8 sums in threads 0..7 (one channel each).
+__device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const float* __restrict__ q, int G, int C,
+                                              int cg, float* lds, float& outp, float& outq) {
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    float u[8], v[8];
+    load8(p, static_cast<int64_t>(g) * C + cg * 8, u);
+    load8(q, static_cast<int64_t>(g) * C + cg * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] += u[j];
+      b[j] += v[j];
+    }
+  }
+  // wave reduce, then across the 4 waves through LDS
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = wave_sum(a[j]);
+    b[j] = wave_sum(b[j]);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lds[wid * 16 + j] = a[j];
+      lds[wid * 16 + 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    float sa = 0.f, sb = 0.f;
+    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) {
+      sa += lds[w * 16 + threadIdx.x];
+      sb += lds[w * 16 + 8 + threadIdx.x];
+    }
+    outp = sa;
+    outq = sb;
+  }
+}
+
+// per channel: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; running stats.
+// grid = C / 8 blocks of 256 threads.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
+                                                          int G, int C, int64_t R, float eps, float momentum,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar, float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out, float* __restrict__ scale,
+                                                          float* __restrict__ shift) {
+  __shared__ float lds[64];
+  float s = 0.f, q = 0.f;
+  sum_partials8(ps, pq, G, C, blockIdx.x, lds, s, q);
+  if (threadIdx.x >= 8) return;
+  const int c = blockIdx.x * 8 + threadIdx.x;
+  const float inv_r = 1.f / static_cast<float>(R);
+  const float mean = s * inv_r;
+  float var = q * inv_r - mean * mean;
+  if (var < 0.f) var = 0.f;
+  const float invstd = rsqrtf(var + eps);
+  const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+  mean_out[c] = mean;
+  invstd_out[c] = invstd;
+  scale[c] = ga * invstd;
+  shift[c] = be - mean * ga * invstd;
+  if (rmean) {
+    const float unbiased = R > 1 ? var * static_cast<float>(R) / static_cast<float>(R - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+  }
+}
+
+// eval mode: scale/shift from running stats
+__global__ __launch_bounds__(256) void bn_eval_coef_kernel(int C, float eps, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ rmean,
+                                                           const float* __restrict__ rvar, float* __restrict__ scale,
+                                                           float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rvar[c] + eps);
+  const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+  scale[c] = ga * invstd;
+  shift[c] = be - rmean[c] * ga * invstd;
+}
+
+// y = act(x * scale_c + shift_c [+ res])
+template <bool RES, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, uint16_t* __restrict__ y,
+                                                       int64_t nvec, int C) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int cvec = C / 8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c = static_cast<int>(v % cvec) * 8;
+    float a[8], b[8], sc[8], sh[8];
+    load8(x, v * 8, a);
+    load8(scale, c, sc);
+    load8(shift, c, sh);
+    if constexpr (RES) load8(res, v * 8, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = a[j] * sc[j] + sh[j];
+      if constexpr (RES) o += b[j];
+      if constexpr (ACT == 1) o = o > 0.f ? o : 0.f;
+      a[j] = o;
+    }
+    store8(y, v * 8, a);
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// partial_dz[g,c] = sum dz ; partial_dzx[g,c] = sum dz * (x - mean) * invstd ; dz = dy * act'(y)
+template <int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
+                                                            const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, int64_t R, int C,
+                                                            float* __restrict__ pd, float* __restrict__ px) {
+  __shared__ float lds_d[256 * 8];
+  __shared__ float lds_x[256 * 8];
+  const RedGeom gm = red_geom(C);
+  const int t = threadIdx.x;
+  const int cg = t % gm.tpr + blockIdx.y * 256;
+  const int r0 = t / gm.tpr;
+  const int ngroups = C / 8;
+  const int64_t G = gridDim.x;
+  const int64_t rows_per_block = (R + G - 1) / G;
+  const int64_t rb = blockIdx.x * rows_per_block;
+  const int64_t re = (rb + rows_per_block < R) ? rb + rows_per_block : R;
+  float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cg < ngroups) {
+    float mu[8], is[8];
+    load8(mean, cg * 8, mu);
+    load8(invstd, cg * 8, is);
+    for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
+      float g[8], xv[8];
+      load8(dy, r * C + cg * 8, g);
+      load8(x, r * C + cg * 8, xv);
+      if constexpr (ACT == 1) {
+        float yv[8];
+        load8(y, r * C + cg * 8, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += g[j];
+        sx[j] += g[j] * (xv[j] - mu[j]) * is[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lds_d[t * 8 + j] = sd[j];
+    lds_x[t * 8 + j] = sx[j];
+  }
+  __syncthreads();
+  if (r0 == 0 && cg < ngroups) {
+    for (int k = 1; k < gm.rows_it; ++k) {
+      const int src = (k * gm.tpr + t) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sd[j] += lds_d[src + j];
+        sx[j] += lds_x[src + j];
+      }
+    }
+    float* od = pd + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    float* ox = px + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    *reinterpret_cast<f32x4*>(od) = f32x4{sd[0], sd[1], sd[2], sd[3]};
+    *reinterpret_cast<f32x4*>(od + 4) = f32x4{sd[4], sd[5], sd[6], sd[7]};
+    *reinterpret_cast<f32x4*>(ox) = f32x4{sx[0], sx[1], sx[2], sx[3]};
+    *reinterpret_cast<f32x4*>(ox + 4) = f32x4{sx[4], sx[5], sx[6], sx[7]};
+  }
+}
+
+// dgamma = sum dz*xhat, dbeta = sum dz; dx = A dz + B x + Cc.  grid = C / 8 blocks.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pd,
+                                                              const float* __restrict__ px, int G, int C, int64_t R,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ ca, float* __restrict__ cb,
+                                                              float* __restrict__ cc) {
+  __shared__ float lds[64];
+  float sd = 0.f, sx = 0.f;
+  sum_partials8(pd, px, G, C, blockIdx.x, lds, sd, sx);
+  if (threadIdx.x >= 8) return;
+  const int c = blockIdx.x * 8 + threadIdx.x;
+  if (dgamma) dgamma[c] = sx;
+  if (dbeta) dbeta[c] = sd;
+  const float ga = gamma ? gamma[c] : 1.f;
+  const float is = invstd[c];
+  const float k = ga * is;
+  const float md = sd / static_cast<float>(R);
+  const float mx = sx / static_cast<float>(R);
+  ca[c] = k;
+  cb[c] = -k * is * mx;
+  cc[c] = -k * md + k * is * mx * mean[c];
+}
+
+template <int ACT, bool DRES>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                           const uint16_t* __restrict__ y,
+                                                           const uint16_t* __restrict__ x,
+                                                           const float* __restrict__ ca,
+                                                           const float* __restrict__ cb,
+                                                           const float* __restrict__ cc, uint16_t* __restrict__ dx,
+                                                           uint16_t* __restrict__ dres, int64_t nvec, int C) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int cvec = C / 8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c = static_cast<int>(v % cvec) * 8;
+    float g[8], xv[8], A[8], B[8], Cc[8];
+    load8(dy, v * 8, g);
+    load8(x, v * 8, xv);
+    if constexpr (ACT == 1) {
+      float yv[8];
+      load8(y, v * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    load8(ca, c, A);
+    load8(cb, c, B);
+    load8(cc, c, Cc);
+    if constexpr (DRES) store8(dres, v * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = A[j] * g[j] + B[j] * xv[j] + Cc[j];
+    store8(dx, v * 8, xv);
+  }
+}
+
+// ------------------------------------------------------------------------------ launchers
+void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
+  const int C = a.C;
+  const int64_t R = a.R;
+  const int cblocks = (C + 255) / 256;
+  if (a.training) {
+    const int G = a.G;
+    const int ctiles = (C / 8 + 255) / 256;
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(G, ctiles), dim3(256), 0, s, a.x, R, C, a.ws, a.ws + G * C);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, G, C, R, a.eps,
+                       a.momentum, a.gamma, a.beta, a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
+  } else {
+    hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(cblocks), dim3(256), 0, s, C, a.eps, a.gamma, a.beta, a.rmean,
+                       a.rvar, a.scale, a.shift);
+  }
+  const int64_t nvec = R * C / 8;
+  const int grid = stream_grid(nvec, 256);
+#define PSAMD_BN_APPLY(RES, ACT)                                                                                 \
+  hipLaunchKernelGGL((bn_apply_kernel<RES, ACT>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale, a.shift, a.y, \
+                     nvec, C)
+  if (a.res) {
+    if (a.act == 1) PSAMD_BN_APPLY(true, 1);
+    else PSAMD_BN_APPLY(true, 0);
+  } else {
+    if (a.act == 1) PSAMD_BN_APPLY(false, 1);
+    else PSAMD_BN_APPLY(false, 0);
+  }
+#undef PSAMD_BN_APPLY
+}
+
+void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
+  const int C = a.C;
+  const int64_t R = a.R;
+  const int G = a.G;
+  const int ctiles = (C / 8 + 255) / 256;
+  if (a.act == 1)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mean, a.invstd,
+                       R, C, a.ws, a.ws + G * C);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<0>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mean, a.invstd,
+                       R, C, a.ws, a.ws + G * C);
+  float* coef = a.ws + 2 * G * C;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, G, C, R,
+                     a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, coef, coef + C, coef + 2 * C);
+  const int64_t nvec = R * C / 8;
+  const int grid = stream_grid(nvec, 256);
+#define PSAMD_BN_BWD(ACT, DRES)                                                                                    \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x, coef, coef + C, \
+                     coef + 2 * C, a.dx, a.dres, nvec, C)
+  if (a.dres) {
+    if (a.act == 1) PSAMD_BN_BWD(1, true);
+    else PSAMD_BN_BWD(0, true);
+  } else {
+    if (a.act == 1) PSAMD_BN_BWD(1, false);
+    else PSAMD_BN_BWD(0, false);
+  }
+#undef PSAMD_BN_BWD
+}
+
+}  // namespace psamd

@@ -14,38 +14,48 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.bn import BatchNormAct2d
+
 
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None,
+                 fused_bn: bool = True):
         super().__init__()
         width = planes
+        self.fused_bn = fused_bn
+        BN = BatchNormAct2d if fused_bn else nn.BatchNorm2d
         self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BN(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BN(width)
         self.conv3 = nn.Conv2d(width, planes * 4, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.bn3 = BN(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x
+        identity = x if self.downsample is None else self.downsample(x)
+        if self.fused_bn:
+            # BN + ReLU fused; bn3 fuses the residual add and the final ReLU (ops/bn.py)
+            out = self.bn1(self.conv1(x))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), identity)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
         return self.relu(out + identity)
 
 
 class ResNet(nn.Module):
-    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = True):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = True,
+                 fused_bn: bool = True):
         super().__init__()
         self.inplanes = 64
+        self.fused_bn = fused_bn
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = BatchNormAct2d(64) if fused_bn else nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0])
@@ -68,29 +78,29 @@ class ResNet(nn.Module):
     def _make_layer(self, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
         downsample = None
         if stride != 1 or self.inplanes != planes * 4:
-            downsample = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
-                                       nn.BatchNorm2d(planes * 4))
-        layers = [Bottleneck(self.inplanes, planes, stride, downsample)]
+            bn = BatchNormAct2d(planes * 4, act="none") if self.fused_bn else nn.BatchNorm2d(planes * 4)
+            downsample = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False), bn)
+        layers = [Bottleneck(self.inplanes, planes, stride, downsample, self.fused_bn)]
         self.inplanes = planes * 4
         for _ in range(1, blocks):
-            layers.append(Bottleneck(self.inplanes, planes))
+            layers.append(Bottleneck(self.inplanes, planes, fused_bn=self.fused_bn))
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.bn1(self.conv1(x))
+        x = self.maxpool(x if self.fused_bn else self.relu(x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 
-def resnet50(num_classes: int = 1000) -> ResNet:
-    return ResNet((3, 4, 6, 3), num_classes)
+def resnet50(num_classes: int = 1000, fused_bn: bool = True) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes, fused_bn=fused_bn)
 
 
-def resnet18_like(num_classes: int = 10, width: int = 16) -> nn.Module:
-    """Tiny bottleneck ResNet for CPU tests (same code path, few channels)."""
-    m = ResNet((1, 1, 1, 1), num_classes)
-    return m
+def resnet_tiny(num_classes: int = 10, fused_bn: bool = True) -> ResNet:
+    """One bottleneck per stage: same code path as ResNet-50 for quick tests."""
+    return ResNet((1, 1, 1, 1), num_classes, fused_bn=fused_bn)
 
 
 def prepare_for_mi355x(model: nn.Module, dtype=torch.bfloat16, bn_fp32: bool = True) -> nn.Module:
