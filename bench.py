@@ -4,11 +4,15 @@
 BASELINE.json metric: "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X
 workers" -- one process per GPU (torchrun), every rank a worker + the server of its range
 partition, push = RCCL reduce-scatter, server = fused HIP momentum-SGD on the fp32 master
-shard, pull = RCCL all-gather, all overlapped with backward (ps_amd/parallel/colocated.py).
+shard, pull = RCCL all-gather, all overlapped with backward (ps_amd/parallel/colocated.py);
+BatchNorm+residual+ReLU run as fused HIP kernels (ps_amd/ops/bn.py).
 
-Weak scaling: ``--batch-per-gpu`` images per rank per step (default 256), synthetic
-ImageNet-shaped data resident on the GPU, random-init weights, bf16 compute (channels_last),
-full optimizer step inside the timed region.
+Weak scaling: ``--batch-per-gpu`` images per rank per step (default 512 -- sized for the
+288 GB HBM), synthetic ImageNet-shaped data resident on the GPU, random-init weights, bf16
+compute (channels_last), full optimizer step inside the timed region.
+
+Other BASELINE configs: ``--config bert-ssp | dlrm | llama-onebit | mlp-tcp`` (see
+ps_amd/bench_configs.py).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; W untimed steps, then
 exactly K timed steps bracketed by barrier + cuda.synchronize on both sides; the max
@@ -23,17 +27,17 @@ import sys
 import time
 
 import torch
-import torch.nn.functional as F
-
-METRIC = "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X workers"
 
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default=os.environ.get("PS_AMD_BENCH_CONFIG", "resnet50"),
+                    choices=["resnet50", "bert-ssp", "dlrm", "llama-onebit", "mlp-tcp"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("PS_AMD_BENCH_BATCH", "256")))
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="0 = config default")
+    ap.add_argument("--seq-len", type=int, default=0, help="0 = config default")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("PS_AMD_BUCKET_MB", "25")))
     ap.add_argument("--last-bucket-mb", type=float, default=2.0)
@@ -42,11 +46,13 @@ def parse():
     ap.add_argument("--fused-bn", type=int, default=int(os.environ.get("PS_AMD_FUSED_BN", "1")),
                     help="HIP fused BatchNorm+residual+ReLU kernels (ops/bn.py) instead of MIOpen BN")
     ap.add_argument("--lr", type=float, default=0.1)
-    ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
-                    help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
-                         "ResNet-50: 40.8 vs 39.4 ms, profiles/r1_graph_vs_eager.txt)")
+    ap.add_argument("--dlrm-rows", type=int, default=1000000)
+    ap.add_argument("--tiny", type=int, default=0, help="llama-onebit: tiny config (smoke only)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("PS_AMD_CONV_BENCHMARK", "1")),
                     help="MIOpen find (exhaustive) for each conv shape during warm-up")
+    ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
+                    help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
+                         "ResNet-50: 32.7 vs 31.6 ms, profiles/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
@@ -82,24 +88,32 @@ def setup_miopen_db():
 
 def main():
     args = parse()
-    setup_miopen_db()
-    from ps_amd.parallel.transport import init_distributed
-    from ps_amd.parallel.colocated import ColocatedPS
-    from ps_amd.parallel.updaters import MomentumUpdater
-    from ps_amd.models.resnet import resnet50, prepare_for_mi355x
-    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ps_amd import bench_configs as BC
 
+    if args.config == "mlp-tcp":  # CPU plumbing config: no GPU involved
+        rec = BC.run_mlp_tcp(args.steps)
+        rec["warmup"] = 2
+        print(json.dumps(rec), flush=True)
+        return 0
+    d = BC.DEFAULTS[args.config]
+    args.batch_per_gpu = args.batch_per_gpu or d["batch"]
+    args.seq_len = args.seq_len or d["seq"]
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world_env == 1:
-        # re-launch ourselves under torchrun as a CHILD process (never exec from a GPU process)
+        # launch ourselves under torchrun as a CHILD process (never exec from a GPU process)
         import subprocess
 
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-               "--master-addr=127.0.0.1", "--master-port=29533", __file__] + sys.argv[1:]
-        sys.exit(subprocess.call(cmd))
+               "--master-addr=127.0.0.1", "--master-port=29533", os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd)
+    setup_miopen_db()
     if not torch.cuda.is_available():
-        print(json.dumps({"metric": METRIC, "value": None, "error": "no GPU visible"}))
+        print(json.dumps({"metric": args.config, "value": None, "error": "no GPU visible"}))
         return 1
+    from ps_amd.parallel.transport import init_distributed
+    import torch.distributed as dist
+
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     tp = init_distributed()
@@ -107,38 +121,21 @@ def main():
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.manual_seed(1234)
-
-    model = prepare_for_mi355x(resnet50(fused_bn=bool(args.fused_bn)).to(dev), bn_fp32=bool(args.bn_fp32))
-    upd = MomentumUpdater(lr=args.lr, momentum=0.9, weight_decay=5e-5)
-    ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
-                     staleness=args.staleness)
-    B, S = args.batch_per_gpu, args.image_size
-    g = torch.Generator(device=dev).manual_seed(rank)
-    x = torch.randn(B, 3, S, S, device=dev, generator=g).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (B,), device=dev, generator=g)
-
-    def step():
-        out = model(x)
-        loss = F.cross_entropy(out.float(), y)
-        loss.backward()
-        ps.finish_step()
-        return loss
+    bench = BC.SETUPS[args.config](args, tp, dev)
+    step = bench.step
 
     use_graph = args.graph == "1" or (args.graph == "auto" and world == 1)
     tw0 = time.perf_counter()
     if use_graph:
         from ps_amd.train.graphs import GraphedStep
 
-        # eager warm-up (MIOpen find) inside GraphedStep, then capture; W counts warm-up steps
-        graphed = GraphedStep(step, warmup=max(1, args.warmup - 1))
-        step = graphed
+        step = GraphedStep(step, warmup=max(1, args.warmup - 1))
     else:
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
     if rank == 0:
-        print(f"[bench] warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
+        print(f"[bench] {args.config}: warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
               f"(includes MIOpen find/compile for new conv shapes)", file=sys.stderr, flush=True)
     tp.barrier()
     torch.cuda.synchronize()
@@ -153,10 +150,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
-    samples = B * world * args.steps
-    value = samples / elapsed
+    value = bench.samples_per_step * world * args.steps / elapsed
     if args.profile_steps and rank == 0:
-        from torch.profiler import profile, ProfilerActivity
+        from torch.profiler import ProfilerActivity, profile
 
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for _ in range(args.profile_steps):
@@ -166,32 +162,23 @@ def main():
         with open("gpurun_out/torch_profile.txt", "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     if rank == 0:
+        cfg = dict(bench.config)
+        cfg["hip_graph"] = bool(use_graph)
+        cfg["final_loss"] = round(float(loss.item()), 4)
         rec = {
-            "metric": METRIC,
+            "metric": bench.metric,
             "value": round(value, 2),
-            "unit": "samples/s",
+            "unit": bench.unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (random ImageNet-shaped images + labels, GPU resident); random-init weights",
-            "config": {
-                "model": "ResNet-50",
-                "global_batch": B * world,
-                "seq_len": None,
-                "image_size": S,
-                "parallelism": f"ps-bsp-colocated-dp{world}",
-                "optimizer": upd.name,
-                "bucket_mb": args.bucket_mb,
-                "staleness": args.staleness,
-                "hip_graph": bool(use_graph),
-                "fused_bn": bool(args.fused_bn),
-                "final_loss": round(float(loss.item()), 4),
-            },
+            "vs_baseline": None,  # the reference publishes no throughput number
+            "dtype": "bf16" if args.config != "dlrm" else "fp32",
+            "data": "synthetic (GPU-resident batches of the named shape); random-init weights",
+            "config": cfg,
         }
         line = json.dumps(rec)
         print(line, flush=True)

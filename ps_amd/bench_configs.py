@@ -1,0 +1,199 @@
+"""The BASELINE.json benchmark configs (bench.py ``--config``).
+
+  resnet50      ResNet-50 sync-BSP, co-located PS, fused HIP momentum SGD     (headline)
+  bert-ssp      BERT-base MLM, bounded staleness s=1 (SSP), fused HIP AdamW
+  dlrm          DLRM-style: 26 sharded embedding tables, sparse push/pull, row-wise
+                Adagrad on the owning server (HIP), dense MLPs on the co-located PS
+  llama-onebit  Llama-3-8B bf16, 1-bit compressed gradient push with error feedback
+  mlp-tcp       2-layer MLP, 1 dedicated server + 2 workers on CPU/TCP loopback (plumbing)
+
+Each ``setup_*`` returns a Bench with ``step()`` (one full PS round: forward, backward,
+push, server update, pull -- nothing skipped), the samples processed per step on THIS rank,
+and the metric/config metadata.  Synthetic data of the named shape, random-init weights.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Callable, Dict
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class Bench:
+    step: Callable[[], torch.Tensor]
+    samples_per_step: int
+    metric: str
+    unit: str
+    config: Dict = field(default_factory=dict)
+    engine: object = None
+
+
+def setup_resnet50(args, tp, dev) -> Bench:
+    from .models.resnet import prepare_for_mi355x, resnet50
+    from .parallel.colocated import ColocatedPS
+    from .parallel.updaters import MomentumUpdater
+
+    model = prepare_for_mi355x(resnet50(fused_bn=bool(args.fused_bn)).to(dev), bn_fp32=bool(args.bn_fp32))
+    upd = MomentumUpdater(lr=args.lr, momentum=0.9, weight_decay=5e-5)
+    ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
+                     staleness=args.staleness)
+    B, S = args.batch_per_gpu, args.image_size
+    g = torch.Generator(device=dev).manual_seed(tp.rank)
+    x = torch.randn(B, 3, S, S, device=dev, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev, generator=g)
+
+    def step():
+        loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        ps.finish_step()
+        return loss
+
+    return Bench(step, B, "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X workers", "samples/s",
+                 {"model": "ResNet-50", "global_batch": B * tp.world, "seq_len": None, "image_size": S,
+                  "parallelism": f"ps-bsp-colocated-dp{tp.world}", "optimizer": upd.name,
+                  "bucket_mb": args.bucket_mb, "staleness": args.staleness, "fused_bn": bool(args.fused_bn)}, ps)
+
+
+def setup_bert_ssp(args, tp, dev) -> Bench:
+    from .models.transformer import BertForMLM, mlm_batch
+    from .parallel.colocated import ColocatedPS
+    from .parallel.updaters import AdamUpdater
+
+    torch.manual_seed(0)
+    model = BertForMLM().to(dev).to(torch.bfloat16)
+    upd = AdamUpdater(1e-4, 0.9, 0.999, 1e-6, bias_correction="step", weight_decay=0.01, adamw=True)
+    stale = 1 if args.staleness == 0 else args.staleness
+    ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
+                     staleness=stale, clip_norm=None)
+    B, S = args.batch_per_gpu, args.seq_len
+    ids, labels = mlm_batch(B, S, seed=tp.rank, device=dev)
+
+    def step():
+        loss = model(ids, labels)
+        loss.backward()
+        ps.finish_step()
+        return loss
+
+    return Bench(step, B, "sequences/sec (whole node) BERT-base MLM async bounded-staleness s=1", "sequences/s",
+                 {"model": "BERT-base", "global_batch": B * tp.world, "seq_len": S,
+                  "parallelism": f"ps-ssp{stale}-colocated-dp{tp.world}", "optimizer": upd.name}, ps)
+
+
+def setup_dlrm(args, tp, dev) -> Bench:
+    from .models.dlrm import DLRM, dlrm_batch
+    from .parallel.colocated import ColocatedPS
+    from .parallel.updaters import AdagradUpdater
+
+    torch.manual_seed(0)
+    rows = [args.dlrm_rows] * 26
+    model = DLRM(table_rows=rows, transport=tp, device=dev,
+                 sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True)).to(dev)
+    ps = ColocatedPS(model, AdagradUpdater(0.01, 1e-8), tp, bucket_mb=args.bucket_mb,
+                     last_bucket_mb=args.last_bucket_mb)
+    B = args.batch_per_gpu
+    dense, sparse, y = dlrm_batch(B, rows, seed=tp.rank, device=dev)
+
+    def step():
+        loss = F.binary_cross_entropy_with_logits(model(dense, sparse).float(), y)
+        loss.backward()
+        model.push_sparse()
+        ps.finish_step()
+        return loss
+
+    return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",
+                 {"model": "DLRM-26x128", "global_batch": B * tp.world, "seq_len": None,
+                  "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}"}, ps)
+
+
+def setup_llama_onebit(args, tp, dev) -> Bench:
+    from .models.transformer import LlamaConfig, LlamaForCausalLM
+    from .parallel.colocated import ColocatedPS
+    from .parallel.updaters import AdamUpdater
+
+    cfg = LlamaConfig.tiny() if args.tiny else LlamaConfig.llama3_8b()
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = LlamaForCausalLM(cfg, checkpointing=True).to(torch.bfloat16)
+    upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
+    ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
+                     compress="onebit" if tp.world > 1 else None)
+    B, S = args.batch_per_gpu, args.seq_len
+    g = torch.Generator(device=dev).manual_seed(tp.rank)
+    ids = torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g)
+
+    def step():
+        loss = model(ids, ids)
+        loss.backward()
+        ps.finish_step()
+        return loss
+
+    return Bench(step, B * S, "tokens/sec (whole node) Llama-3-8B bf16 1-bit compressed push", "tokens/s",
+                 {"model": "Llama-3-8B" if not args.tiny else "Llama-tiny", "global_batch": B * tp.world,
+                  "seq_len": S, "parallelism": f"ps-bsp-onebit-colocated-dp{tp.world}",
+                  "compression": "onebit+error-feedback" if tp.world > 1 else "none (1 worker: nothing to push)"},
+                 ps)
+
+
+SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_dlrm,
+          "llama-onebit": setup_llama_onebit}
+
+DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not given
+    "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "512")), seq=0),
+    "bert-ssp": dict(batch=256, seq=128),
+    "dlrm": dict(batch=16384, seq=0),
+    "llama-onebit": dict(batch=1, seq=4096),
+}
+
+
+# ----------------------------------------------------------------------------- CPU plumbing
+def _mlp_worker(wid, port, steps, batch, q):
+    import time
+
+    torch.set_num_threads(2)
+    from .parallel.kvstore import KVStore
+    from .parallel.tcp import PSClient
+    from .parallel.updaters import SimpleUpdater
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(784, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10))
+    kv = KVStore(PSClient("127.0.0.1", port), worker_id=wid)
+    upd = {"default": SimpleUpdater(0.05)}
+    g = torch.Generator().manual_seed(wid)
+    x = torch.randn(batch, 784, generator=g)
+    y = torch.randint(0, 10, (batch,), generator=g)
+    for i in range(steps + 2):
+        if i == 2:
+            t0 = time.perf_counter()
+        kv.pull_into(m)
+        m.zero_grad()
+        F.cross_entropy(m(x), y).backward()
+        kv.sum_from(m)
+        kv.update(upd)
+        kv.clear()
+    q.put((wid, time.perf_counter() - t0))
+
+
+def run_mlp_tcp(steps: int, batch: int = 128) -> Dict:
+    import multiprocessing as mp
+
+    from .parallel.tcp import PServer
+
+    srv = PServer(0, workers=2, mode="bsp").start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mlp_worker, args=(w, srv.port, steps, batch, q)) for w in range(2)]
+    [p.start() for p in ps]
+    res = [q.get(timeout=600) for _ in ps]
+    [p.join() for p in ps]
+    srv.stop()
+    el = max(t for _, t in res)
+    return {"metric": "samples/sec 2-layer MLP, 1 server + 2 workers on CPU/TCP loopback (plumbing)",
+            "value": round(2 * batch * steps / el, 2), "unit": "samples/s", "n_gpus": 0, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"model": "MLP-784-256-10", "global_batch": 2 * batch, "seq_len": None,
+                       "parallelism": "ps-tcp-1server-2workers-bsp"}}

@@ -1,0 +1,223 @@
+"""BERT-base and Llama-3 models for the BASELINE.json north-star configs (random init, no
+checkpoints, no network).
+
+Compact in-repo definitions (transformers is not needed on the hot path): parameter shapes
+and counts match the published architectures -- BERT-base 110M (12 x 768, 12 heads, FFN
+3072, vocab 30522), Llama-3-8B 8.03B (32 x 4096, 32 q / 8 kv heads, FFN 14336, vocab
+128256, RoPE theta 500000).  Attention runs through torch SDPA (flash kernels on ROCm);
+everything is bf16 on the GPU with fp32 masters on the parameter-server shards.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+
+# ------------------------------------------------------------------------------------ BERT
+@dataclass
+class BertConfig:
+    vocab: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    max_pos: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    dropout: float = 0.1
+
+
+class BertLayer(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.c = c
+        self.qkv = nn.Linear(c.hidden, 3 * c.hidden)
+        self.proj = nn.Linear(c.hidden, c.hidden)
+        self.ln1 = nn.LayerNorm(c.hidden, eps=c.eps)
+        self.fc1 = nn.Linear(c.hidden, c.ffn)
+        self.fc2 = nn.Linear(c.ffn, c.hidden)
+        self.ln2 = nn.LayerNorm(c.hidden, eps=c.eps)
+
+    def forward(self, x, mask: Optional[torch.Tensor] = None):
+        b, s, h = x.shape
+        nh = self.c.heads
+        q, k, v = self.qkv(x).view(b, s, 3, nh, h // nh).permute(2, 0, 3, 1, 4)
+        p = self.c.dropout if self.training else 0.0
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
+        a = a.transpose(1, 2).reshape(b, s, h)
+        x = self.ln1(x + F.dropout(self.proj(a), p, self.training))
+        f = self.fc2(F.gelu(self.fc1(x)))
+        return self.ln2(x + F.dropout(f, p, self.training))
+
+
+class BertForMLM(nn.Module):
+    """BERT-base with the masked-LM head (decoder tied to the word embeddings)."""
+
+    def __init__(self, c: BertConfig = BertConfig()):
+        super().__init__()
+        self.c = c
+        self.word = nn.Embedding(c.vocab, c.hidden)
+        self.pos = nn.Embedding(c.max_pos, c.hidden)
+        self.tok_type = nn.Embedding(c.type_vocab, c.hidden)
+        self.ln = nn.LayerNorm(c.hidden, eps=c.eps)
+        self.layers = nn.ModuleList(BertLayer(c) for _ in range(c.layers))
+        self.head_dense = nn.Linear(c.hidden, c.hidden)
+        self.head_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+        self.head_bias = nn.Parameter(torch.zeros(c.vocab))
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, ids, labels=None):
+        b, s = ids.shape
+        pos = torch.arange(s, device=ids.device)
+        x = self.word(ids) + self.pos(pos)[None] + self.tok_type.weight[0]
+        x = F.dropout(self.ln(x), self.c.dropout, self.training)
+        for layer in self.layers:
+            x = layer(x)
+        h = self.head_ln(F.gelu(self.head_dense(x)))
+        logits = h @ self.word.weight.t() + self.head_bias
+        if labels is None:
+            return logits
+        return F.cross_entropy(logits.float().view(-1, self.c.vocab), labels.view(-1), ignore_index=-100)
+
+
+def mlm_batch(batch: int, seq: int, vocab: int = 30522, mask_prob: float = 0.15, seed: int = 0, device=None):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(min(1000, vocab // 2), vocab, (batch, seq), generator=g)
+    labels = torch.full_like(ids, -100)
+    m = torch.rand(batch, seq, generator=g) < mask_prob
+    labels[m] = ids[m]
+    ids = ids.masked_fill(m, 103)  # [MASK]
+    if device is not None:
+        ids, labels = ids.to(device), labels.to(device)
+    return ids, labels
+
+
+# ----------------------------------------------------------------------------------- Llama
+@dataclass
+class LlamaConfig:
+    vocab: int = 128256
+    hidden: int = 4096
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    ffn: int = 14336
+    rope_theta: float = 500000.0
+    eps: float = 1e-5
+    max_seq: int = 8192
+
+    @staticmethod
+    def llama3_8b() -> "LlamaConfig":
+        return LlamaConfig()
+
+    @staticmethod
+    def tiny() -> "LlamaConfig":
+        return LlamaConfig(vocab=512, hidden=64, layers=2, heads=4, kv_heads=2, ffn=128, max_seq=128)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, d, eps):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.eps = eps
+
+    def forward(self, x):
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).to(x.dtype) * self.weight
+
+
+def rope_cache(seq: int, dim: int, theta: float, device):
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, device=device).float() / dim))
+    t = torch.arange(seq, device=device).float()
+    f = torch.outer(t, inv)
+    return torch.cos(f), torch.sin(f)
+
+
+def apply_rope(x, cos, sin):
+    # x [b, h, s, d]; rotate halves (Llama/HF convention)
+    d = x.shape[-1]
+    x1, x2 = x[..., : d // 2], x[..., d // 2:]
+    c, s = cos[None, None].to(x.dtype), sin[None, None].to(x.dtype)
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+class LlamaBlock(nn.Module):
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.c = c
+        hd = c.hidden // c.heads
+        self.attn_norm = RMSNorm(c.hidden, c.eps)
+        self.wq = nn.Linear(c.hidden, c.heads * hd, bias=False)
+        self.wk = nn.Linear(c.hidden, c.kv_heads * hd, bias=False)
+        self.wv = nn.Linear(c.hidden, c.kv_heads * hd, bias=False)
+        self.wo = nn.Linear(c.heads * hd, c.hidden, bias=False)
+        self.mlp_norm = RMSNorm(c.hidden, c.eps)
+        self.w1 = nn.Linear(c.hidden, c.ffn, bias=False)
+        self.w3 = nn.Linear(c.hidden, c.ffn, bias=False)
+        self.w2 = nn.Linear(c.ffn, c.hidden, bias=False)
+
+    def forward(self, x, cos, sin):
+        b, s, _ = x.shape
+        c = self.c
+        hd = c.hidden // c.heads
+        h = self.attn_norm(x)
+        q = self.wq(h).view(b, s, c.heads, hd).transpose(1, 2)
+        k = self.wk(h).view(b, s, c.kv_heads, hd).transpose(1, 2)
+        v = self.wv(h).view(b, s, c.kv_heads, hd).transpose(1, 2)
+        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+        rep = c.heads // c.kv_heads
+        k = k.repeat_interleave(rep, dim=1)
+        v = v.repeat_interleave(rep, dim=1)
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        x = x + self.wo(a.transpose(1, 2).reshape(b, s, -1))
+        h = self.mlp_norm(x)
+        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, c: LlamaConfig = LlamaConfig(), checkpointing: bool = False):
+        super().__init__()
+        self.c = c
+        self.checkpointing = checkpointing
+        self.embed = nn.Embedding(c.vocab, c.hidden)
+        self.layers = nn.ModuleList(LlamaBlock(c) for _ in range(c.layers))
+        self.norm = RMSNorm(c.hidden, c.eps)
+        self.lm_head = nn.Linear(c.hidden, c.vocab, bias=False)
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=0.02)
+
+    def forward(self, ids, labels=None):
+        s = ids.shape[1]
+        cos, sin = rope_cache(s, self.c.hidden // self.c.heads, self.c.rope_theta, ids.device)
+        x = self.embed(ids)
+        for layer in self.layers:
+            if self.checkpointing and self.training:
+                x = checkpoint(layer, x, cos, sin, use_reentrant=False)
+            else:
+                x = layer(x, cos, sin)
+        logits = self.lm_head(self.norm(x))
+        if labels is None:
+            return logits
+        return F.cross_entropy(logits[:, :-1].float().reshape(-1, self.c.vocab), labels[:, 1:].reshape(-1))
+
+
+def param_count(m: nn.Module) -> int:
+    seen, n = set(), 0
+    for p in m.parameters():
+        if id(p) not in seen:
+            seen.add(id(p))
+            n += p.numel()
+    return n
