@@ -1,0 +1,67 @@
+"""Shared launcher logic for the demo apps: the reference's -D flag semantics
+(Context.java:60-88) mapped onto ps_amd engines.
+
+  -Dmode=stand (default)       standalone: one process, local co-located PS
+  torchrun (WORLD_SIZE > 1)    co-located PS over RCCL (GPU) / gloo (CPU), BSP or SSP
+  -Dmode=dist -Dps=1           dedicated TCP parameter server (native), waits for workers
+  -Dmode=dist                  TCP worker of the servers in -DpsAddrs (BSP/SSP/ASP)
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+
+import torch
+
+from ..config import Config
+from ..context import ctx
+from ..parallel.kvstore import KVStore
+from ..parallel.tcp import PServer, PSRouterClient
+from ..parallel.transport import init_distributed
+from ..train.trainer import CollectiveEngine, KVEngine, Trainer
+
+log = logging.getLogger("ps_amd.app")
+
+
+def setup(argv=None) -> Config:
+    cfg = Config.from_args(sys.argv[1:] if argv is None else argv)
+    ctx.init(cfg)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(message)s")
+    if cfg.metrics_path:
+        os.environ["PS_AMD_METRICS_PATH"] = cfg.metrics_path
+    return cfg
+
+
+def maybe_run_server(cfg: Config) -> bool:
+    """Reference PS branch (CTR.java:73-82): -Dmode=dist -Dps=1 runs a TCP server and blocks."""
+    if not (ctx.is_distributed() and cfg.ps):
+        return False
+    mode = "asp" if cfg.ps_async else cfg.consistency
+    srv = PServer(cfg.ps_port, cfg.worker_num, mode, cfg.staleness, bind_any=True).start()
+    log.info("PServer on port %d mode=%s workers=%d", srv.port, mode, cfg.worker_num)
+    srv.wait()
+    srv.stop()
+    return True
+
+
+def make_trainer(cfg: Config, model, device=None) -> Trainer:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if ctx.is_distributed() and world == 1:
+        client = PSRouterClient(cfg.ps_addr_list)
+        wid = int(os.environ.get("PS_AMD_WORKER_ID", os.environ.get("RANK", "0")))
+        cons = "asp" if cfg.ps_async else cfg.consistency
+        engine = KVEngine(model, KVStore(client, worker_id=wid, consistency=cons))
+    else:
+        tp = init_distributed() if world > 1 else None
+        engine = CollectiveEngine(model, tp, bucket_mb=cfg.bucket_mb, staleness=cfg.staleness,
+                                  clip_norm=cfg.clip_norm or None, compress=cfg.compress or None)
+    return Trainer(model, engine, n_threads=cfg.thread, device=device)
+
+
+def device() -> torch.device:
+    if torch.cuda.is_available():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        return torch.device("cuda", local)
+    return torch.device("cpu")

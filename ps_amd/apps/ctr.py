@@ -1,0 +1,66 @@
+"""CTR demo (reference CTR.java:70-158): DNN.buildModel(23, 10, 45, {150, 10, 1}), Adam 0.005,
+batch 1000, train -> test AUC -> loss surface each epoch.  ``--wide`` uses WideDeepNN
+(FTRL wide part, hash space 100000).
+
+The reference's CTR files (train.txt / test.txt) are not shipped; with no ``-Dtrain`` a
+synthetic CTR stream with a known logistic optimum is used (ps_amd.data.synthetic_ctr).
+With ``-Dtrain=file`` the native reader parses ``label|num,...|cat,...`` lines.
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from ..context import ctx
+from ..data.dataset import NativeBatchDataSet, synthetic_ctr
+from ..eval.loss_surface import LossSurface
+from ..eval.metrics import AUC
+from ..models.reference import DNN, WideDeepNN
+from ..obs import metrics
+from .common import device, make_trainer, maybe_run_server, setup
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--steps-per-epoch", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=1000)
+    ap.add_argument("--wide", action="store_true")
+    ap.add_argument("--init-scale", type=float, default=1.0)
+    ap.add_argument("--loss-surface", action="store_true")
+    a, rest = ap.parse_known_args(argv)
+    cfg = setup(rest)
+    if maybe_run_server(cfg):
+        return
+    dev = device()
+    gen = torch.Generator().manual_seed(cfg.seed)
+    if a.wide:
+        model = WideDeepNN.build_model(23, 10, 45, [150, 10, 1], 100000, gen=gen, init_scale=a.init_scale)
+    else:
+        model = DNN.build_model(23, 10, 45, [150, 10, 1], gen=gen, init_scale=a.init_scale)
+    model = model.to(dev)
+    trainer = make_trainer(cfg, model, dev)
+    w0 = {n: p.detach().clone() for n, p in model.named_parameters()}
+    test = synthetic_ctr(5000, wide_k=23 if a.wide else 0, seed=10 ** 6)
+    for epoch in range(a.epochs):
+        if cfg.train:
+            ds = NativeBatchDataSet(cfg.train, "ctr", a.batch, dims=45, fields=23)
+            batches = iter(ds)
+        else:
+            batches = (synthetic_ctr(a.batch, wide_k=23 if a.wide else 0, seed=epoch * 100000 + i)
+                       for i in range(a.steps_per_epoch))
+        for b in batches:
+            if "W" not in b and a.wide:
+                b["W"] = b["E"] % 100000
+            trainer.train([b])
+        p = trainer.predict([test])[0]
+        auc = AUC(p.cpu(), test["Y"]).calculate()
+        metrics.plot("test_auc", auc, epoch)
+        print(f"epoch {epoch} test auc {auc:.4f}", flush=True)
+        if a.loss_surface:
+            LossSurface({k: v.to(dev) for k, v in test.items()}, model, w0).plot()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+"""Sharded checkpoint / resume (the reference keeps everything in memory).
+
+Every rank writes ITS server shard -- fp32 master weights + optimizer state of the ranges
+it owns (ColocatedPS.shard_state), its sparse-table rows + init flags + optimizer state,
+the PS clock -- to ``<dir>/step<k>/rank<r>.pt``; rank 0 also writes ``manifest.json``
+(key -> bucket/offset/shape/dtype, bucket layout, world size, step, data cursors, seeds).
+Writes run on a background thread from host copies taken at a round boundary, so training
+continues while the file is written.  Loading is with ``torch.load(weights_only=True)``
+(tensors / plain containers only) and rebuilds every replica with one pull.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from typing import Dict, Optional
+
+import torch
+
+
+class CheckpointManager:
+    def __init__(self, directory: str, rank: int = 0, world: int = 1, keep: int = 2):
+        self.dir = directory
+        self.rank, self.world, self.keep = rank, world, keep
+        self._thread: Optional[threading.Thread] = None
+        os.makedirs(directory, exist_ok=True)
+
+    def _path(self, step: int) -> str:
+        return os.path.join(self.dir, f"step{step:08d}")
+
+    def save(self, step: int, ps=None, tables: Optional[Dict[str, object]] = None, extra: Optional[dict] = None,
+             blocking: bool = False) -> str:
+        """Snapshot now (host copies), write asynchronously."""
+        self.wait()
+        state = {"step": step, "world": self.world, "rank": self.rank}
+        if ps is not None:
+            state["ps"] = ps.shard_state()
+        if tables:
+            state["tables"] = {}
+            for name, t in tables.items():
+                local = getattr(t, "local", t)
+                state["tables"][name] = {"table": local.table.detach().cpu(), "flags": local.flags.detach().cpu(),
+                                         "states": [s.detach().cpu() for s in local.states], "round": local.round}
+        if extra:
+            state["extra"] = extra
+        path = self._path(step)
+
+        def write():
+            os.makedirs(path, exist_ok=True)
+            tmp = os.path.join(path, f"rank{self.rank}.pt.tmp")
+            torch.save(state, tmp)
+            os.replace(tmp, os.path.join(path, f"rank{self.rank}.pt"))
+            if self.rank == 0:
+                man = {"step": step, "world": self.world, "extra": extra or {}}
+                if ps is not None:
+                    man["keys"] = state["ps"]["manifest"]
+                    man["buckets"] = state["ps"]["buckets"]
+                with open(os.path.join(path, "manifest.json"), "w") as f:
+                    json.dump(man, f, indent=1)
+            self._gc()
+
+        if blocking:
+            write()
+        else:
+            self._thread = threading.Thread(target=write, daemon=True)
+            self._thread.start()
+        return path
+
+    def wait(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def _gc(self) -> None:
+        if self.rank != 0:
+            return
+        steps = sorted(d for d in os.listdir(self.dir) if d.startswith("step"))
+        for d in steps[:-self.keep]:
+            p = os.path.join(self.dir, d)
+            for f in os.listdir(p):
+                os.remove(os.path.join(p, f))
+            os.rmdir(p)
+
+    def latest(self) -> Optional[int]:
+        steps = []
+        for d in os.listdir(self.dir):
+            if d.startswith("step") and os.path.exists(os.path.join(self.dir, d, f"rank{self.rank}.pt")):
+                steps.append(int(d[4:]))
+        return max(steps) if steps else None
+
+    def load(self, step: Optional[int] = None, ps=None, tables: Optional[Dict[str, object]] = None) -> dict:
+        step = self.latest() if step is None else step
+        if step is None:
+            raise FileNotFoundError(f"no checkpoint in {self.dir}")
+        state = torch.load(os.path.join(self._path(step), f"rank{self.rank}.pt"), weights_only=True)
+        if state["world"] != self.world:
+            raise ValueError(f"checkpoint world {state['world']} != current world {self.world} (no elasticity)")
+        if ps is not None:
+            ps.load_shard_state(state["ps"])
+        for name, t in (tables or {}).items():
+            s = state["tables"][name]
+            local = getattr(t, "local", t)
+            local.table.copy_(s["table"])
+            local.flags.copy_(s["flags"])
+            for dst, src in zip(local.states, s["states"]):
+                dst.copy_(src)
+            local.round = int(s["round"])
+        return state
