@@ -489,6 +489,39 @@ std::vector<Tensor> bn_act_bwd(Tensor dy, Tensor y, Tensor x, c10::optional<Tens
   return {dx, dres, dgamma, dbeta};
 }
 
+// ------------------------------------------------------------------------------ MFMA linear
+void gemm_nt(Tensor a, Tensor b, Tensor c, c10::optional<Tensor> bias, int64_t act, double alpha, bool accumulate) {
+  check_gpu(a, "a");
+  check_gpu(b, "b");
+  check_gpu(c, "c");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "a, b must be bf16");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "inner dims differ: ", K, " vs ", b.size(1));
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "c must be [M, N]");
+  if (bias.has_value() && bias->defined()) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "bias must be [N]");
+  }
+  const c10::DeviceGuard guard(a.device());
+  psamd::launch_gemm_nt_bf16(reinterpret_cast<const uint16_t*>(a.data_ptr()), K,
+                             reinterpret_cast<const uint16_t*>(b.data_ptr()), K, c.data_ptr(), dcode(c, "c") == 0, N,
+                             static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<float>(alpha),
+                             accumulate, opt_ptr<const float>(bias), static_cast<int>(act), cur_stream(a));
+}
+
+Tensor act_bwd(Tensor dy, Tensor y, int64_t act) {
+  check_gpu(dy, "dy");
+  check_gpu(y, "y");
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && y.scalar_type() == torch::kBFloat16, "bf16");
+  TORCH_CHECK(dy.numel() == y.numel(), "dy/y size");
+  const c10::DeviceGuard guard(dy.device());
+  auto dz = torch::empty_like(dy);
+  psamd::launch_act_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(y.data_ptr()),
+                        reinterpret_cast<uint16_t*>(dz.data_ptr()), dy.numel(), static_cast<int>(act), cur_stream(dy));
+  return dz;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -518,6 +551,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col2im", &col2im);
   m.def("dropout", &dropout);
   m.def("uniform_init", &uniform_init);
+  m.def("gemm_nt", &gemm_nt);
+  m.def("act_bwd", &act_bwd);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.attr("ONEBIT_CHUNK") = psamd::kOnebitChunk;

@@ -148,15 +148,11 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s);
 int bn_red_blocks(int64_t R);
 
 // ---------------------------------------------------------------- dense.hip (MFMA)
-// Y[M,N] = act(X[M,K] @ W[N,K]^T + b[N]); bf16 in/out, fp32 accumulate.
-// act: 0 none, 1 relu, 2 leaky relu(0.01), 3 clipped sigmoid (0.001 + 0.998*sigmoid)
-void launch_linear_fwd_bf16(const uint16_t* x, const uint16_t* w, const float* b, uint16_t* y, uint16_t* z_pre,
-                            int M, int N, int K, int act, hipStream_t s);
-// generic C[M,N] (+)= A[M,K] @ B[K,N] with strides for transposes (bf16 in, fp32 or bf16 out)
-void launch_gemm_bf16(const uint16_t* a, int64_t lda_m, int64_t lda_k, const uint16_t* b, int64_t ldb_k,
-                      int64_t ldb_n, void* c, int c_bf16, int64_t ldc, int M, int N, int K, float alpha,
-                      int beta_accumulate, const float* bias, int act, hipStream_t s);
+// C[M,N] (+)= act(alpha * A[M,K] . B[N,K]^T + bias[N]); A, B bf16 K-contiguous; C bf16 or fp32.
+// act: 0 none, 1 relu, 2 leaky relu(0.01), 3 reference clipped sigmoid (0.001 + 0.998*sigmoid)
+void launch_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, void* c, int c_f32,
+                         int64_t ldc, int M, int N, int K, float alpha, int accumulate, const float* bias, int act,
+                         hipStream_t s);
 void launch_act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t n, int act, hipStream_t s);
-void launch_colsum(const uint16_t* x, int64_t rows, int cols, float* out, float scale, hipStream_t s);
 
 }  // namespace psamd

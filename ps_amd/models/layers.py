@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import dense as _dense
 from ..ops import nn_ops
 from ..utils.matrix import xavier_bound
 from . import activations as A
@@ -36,6 +37,9 @@ def _uniform_(t: torch.Tensor, bound: float, gen: Optional[torch.Generator] = No
     with torch.no_grad():
         t.copy_((torch.rand(t.shape, generator=gen) * 2 - 1) * bound)
     return t
+
+
+_FUSED_ACT = {A.Relu: 1, A.LeakyRelu: 2, A.Sigmoid: 3}
 
 
 class InputLayer(nn.Module):
@@ -69,6 +73,12 @@ class FcLayer(nn.Module):
         return self
 
     def forward(self, x):
+        if x.is_cuda and self.weights.dtype == torch.bfloat16:
+            # MFMA GEMM with bias + activation fused in the epilogue (ops/dense.py)
+            code = _FUSED_ACT.get(type(self.activation), None) if self.activation is not None else 0
+            if code is not None:
+                return _dense.linear_act(x, self.weights, self.bias, code)
+            return self.activation(_dense.linear_act(x, self.weights, self.bias, 0))
         z = F.linear(x.to(self.weights.dtype), self.weights, self.bias)
         return self.activation(z) if self.activation is not None else z
 

@@ -1,0 +1,68 @@
+"""MFMA fused linear (csrc/kernels/dense.hip): y = act(x @ w^T + b), bf16 in/out, fp32 acc.
+
+Forward is ONE kernel (GEMM + bias + activation epilogue).  Backward: dz = act'(y) * dy
+(one elementwise kernel, the reference activation backwards), dx = dz @ w and
+dw = dz^T @ x on the same NT MFMA kernel (operands transposed to K-contiguous copies --
+the reference-scale layers are small, the copies are cheap), db = column sum of dz.
+CPU / non-bf16 tensors use torch (the numerics oracle).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import native
+
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
+
+
+def _act_ref(z, act):
+    if act == ACT_RELU:
+        return torch.relu(z)
+    if act == ACT_LEAKY:
+        return F.leaky_relu(z, 0.01)
+    if act == ACT_SIGMOID:
+        return 0.001 + 0.998 * torch.sigmoid(z)
+    return z
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, act: int = 0,
+            out_dtype=torch.bfloat16) -> torch.Tensor:
+    """act(a @ b^T + bias) with a [M,K], b [N,K] bf16 (HIP MFMA on GPU)."""
+    if a.is_cuda:
+        c = torch.empty(a.shape[0], b.shape[0], dtype=out_dtype, device=a.device)
+        native().gemm_nt(a.contiguous(), b.contiguous(), c, bias, int(act), 1.0, False)
+        return c
+    z = a.float() @ b.float().t()
+    if bias is not None:
+        z = z + bias.float()
+    return _act_ref(z, act).to(out_dtype)
+
+
+class _LinearAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        y = gemm_nt(x2, w, b.float() if b is not None else None, act)
+        ctx.save_for_backward(x2, w, y)
+        ctx.act, ctx.has_b, ctx.xshape, ctx.bdtype = act, b is not None, x.shape, (b.dtype if b is not None else None)
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0]).contiguous().to(torch.bfloat16)
+        dz = native().act_bwd(dy2, y, int(ctx.act)) if ctx.act else dy2
+        dx = gemm_nt(dz, w.t().contiguous()) if ctx.needs_input_grad[0] else None  # [M,N]x[K,N]^T
+        dw = gemm_nt(dz.t().contiguous(), x2.t().contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
+        db = dz.float().sum(0).to(ctx.bdtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
+
+
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: int = 0) -> torch.Tensor:
+    if x.is_cuda and w.dtype == torch.bfloat16:
+        return _LinearAct.apply(x.to(torch.bfloat16), w, b, int(act))
+    z = F.linear(x.to(w.dtype), w, b)
+    return _act_ref(z, act)

@@ -84,7 +84,8 @@ def test_resnet_fused_matches_unfused_gpu():
     b = prepare_for_mi355x(b.cuda())
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     ya, yb, yr = a(x), b(x), ref(x.float())
-    torch.testing.assert_close(ya.float(), yr, rtol=5e-2, atol=5e-2)
+    rel = lambda u: ((u.float() - yr).norm() / yr.norm()).item()  # noqa: E731
+    assert rel(ya) < 0.05 and rel(ya) < rel(yb) + 0.01, (rel(ya), rel(yb))
     g = torch.randn_like(yr)
     ya.float().backward(g)
     yb.float().backward(g)

@@ -262,3 +262,40 @@ def test_dropout_and_init():
     w = torch.empty(100000, device=DEV)
     N.uniform_init_(w, 3, -0.2, 0.2)
     assert w.min().item() >= -0.2 and w.max().item() < 0.2 and abs(w.mean().item()) < 0.01
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 150, 784), (1000, 150, 275), (100, 10, 50), (64, 64, 32), (257, 33, 70),
+                                   (1000, 1, 10)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_mfma_linear_fwd_bwd(M, N, K, act):
+    from ps_amd.ops import dense as D
+
+    torch.manual_seed(M + N + K)
+    x = (torch.randn(M, K) * 0.5).bfloat16()
+    w = (torch.randn(N, K) * 0.1).bfloat16()
+    b = torch.randn(N) * 0.1
+    dy = torch.randn(M, N).bfloat16()
+    # fp32 reference on the same bf16-rounded inputs
+    xr, wr, br = x.float().requires_grad_(), w.float().requires_grad_(), b.clone().requires_grad_()
+    yr = D._act_ref(xr @ wr.t() + br, act)
+    yr.backward(dy.float())
+    xg, wg, bg = x.cuda().requires_grad_(), w.cuda().requires_grad_(), b.cuda().requires_grad_()
+    yg = D.linear_act(xg, wg, bg, act)
+    yg.backward(dy.cuda())
+    torch.cuda.synchronize()
+    tol = dict(rtol=2e-2, atol=2e-2 * max(1.0, (K ** 0.5) * 0.1))
+    torch.testing.assert_close(yg.float().cpu(), yr.detach(), **tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, rtol=3e-2, atol=3e-2 * max(1.0, N ** 0.5 * 0.1))
+    torch.testing.assert_close(wg.grad.float().cpu(), wr.grad, rtol=3e-2, atol=5e-2 * max(1.0, M ** 0.5 * 0.1))
+    torch.testing.assert_close(bg.grad.cpu(), br.grad, rtol=3e-2, atol=5e-2 * max(1.0, M ** 0.5 * 0.1))
+
+
+def test_mfma_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C-write (cdna guide §3)."""
+    from ps_amd.ops import dense as D
+
+    n = 48
+    eye = torch.eye(n).bfloat16().cuda()
+    b = torch.arange(n * n, dtype=torch.float32).view(n, n).remainder(97).bfloat16().cuda()
+    c = D.gemm_nt(eye, b, out_dtype=torch.float32)  # I @ B^T = B^T
+    torch.testing.assert_close(c, b.float().t())

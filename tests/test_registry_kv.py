@@ -79,9 +79,10 @@ def test_tcp_one_server_two_workers_bsp_equals_large_batch():
         y = torch.randint(0, 3, (64,))
         upd = {"default": AdamUpdater(0.01, bias_correction="reference")}
         losses = {}
+        models = [_mlp(), _mlp()]  # built in the main thread: torch's global RNG is not per-thread
 
         def worker(wid):
-            m = _mlp()
+            m = models[wid]
             kv = KVStore(PSClient("127.0.0.1", srv.port), worker_id=wid)
             xs, ys = x[wid::2], y[wid::2]
             for step in range(5):
