@@ -398,9 +398,10 @@ void uniform_init(Tensor w, int64_t seed, int64_t offset, double lo, double hi) 
 }
 
 // ------------------------------------------------------------------------------ batchnorm
-std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
-                               c10::optional<Tensor> beta, c10::optional<Tensor> rmean, c10::optional<Tensor> rvar,
-                               bool training, double momentum, double eps, int64_t act) {
+static std::vector<Tensor> bn_fwd_impl(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
+                                       c10::optional<Tensor> beta, c10::optional<Tensor> rmean,
+                                       c10::optional<Tensor> rvar, bool training, double momentum, double eps,
+                                       int64_t act, bool apply) {
   check_gpu(x, "x");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16, "x must be bf16 (NHWC-contiguous [R, C] view)");
   TORCH_CHECK(x.dim() == 2, "x must be viewed as [R, C]");
@@ -417,7 +418,7 @@ std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optiona
     }
   if (!training) TORCH_CHECK(rmean.has_value() && rvar.has_value(), "eval mode needs running stats");
   const c10::DeviceGuard guard(x.device());
-  auto y = torch::empty_like(x);
+  auto y = apply ? torch::empty_like(x) : Tensor();
   auto fopt = x.options().dtype(torch::kFloat32);
   auto mean = torch::empty({C}, fopt), invstd = torch::empty({C}, fopt);
   auto coef = torch::empty({2 * C}, fopt);
@@ -426,7 +427,7 @@ std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optiona
   psamd::BnFwdArgs a;
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.res = (res.has_value() && res->defined()) ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr;
-  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.y = apply ? reinterpret_cast<uint16_t*>(y.data_ptr()) : nullptr;
   a.gamma = opt_ptr<const float>(gamma);
   a.beta = opt_ptr<const float>(beta);
   a.rmean = opt_ptr<float>(rmean);
@@ -444,17 +445,79 @@ std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optiona
   a.eps = static_cast<float>(eps);
   a.momentum = static_cast<float>(momentum);
   psamd::launch_bn_fwd(a, cur_stream(x));
-  return {y, mean, invstd};
+  return {y, mean, invstd, coef};
 }
 
-std::vector<Tensor> bn_act_bwd(Tensor dy, Tensor y, Tensor x, c10::optional<Tensor> gamma, Tensor mean,
-                               Tensor invstd, int64_t act, bool want_dres, bool affine) {
-  check_gpu(dy, "dy");
-  check_gpu(y, "y");
+std::vector<Tensor> bn_act_fwd(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
+                               c10::optional<Tensor> beta, c10::optional<Tensor> rmean, c10::optional<Tensor> rvar,
+                               bool training, double momentum, double eps, int64_t act) {
+  return bn_fwd_impl(x, res, gamma, beta, rmean, rvar, training, momentum, eps, act, true);
+}
+
+// batch statistics + running-stat update + [scale | shift] only; the apply is fused into a consumer
+std::vector<Tensor> bn_stats(Tensor x, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
+                             c10::optional<Tensor> rmean, c10::optional<Tensor> rvar, bool training, double momentum,
+                             double eps) {
+  auto r = bn_fwd_impl(x, c10::nullopt, gamma, beta, rmean, rvar, training, momentum, eps, 0, false);
+  return {r[1], r[2], r[3]};
+}
+
+// ------------------------------------------------------------------------------ NHWC max pool
+// x: [N, H, W, C] bf16 contiguous; coef: optional [scale | shift] (fused BN-apply + ReLU prologue)
+std::vector<Tensor> maxpool_nhwc_fwd(Tensor x, c10::optional<Tensor> coef, int64_t k, int64_t s, int64_t p) {
   check_gpu(x, "x");
-  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && y.sizes() == x.sizes(), "dy/y/x [R, C]");
-  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && y.scalar_type() == torch::kBFloat16 &&
-                  x.scalar_type() == torch::kBFloat16, "bf16 tensors");
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() == torch::kBFloat16 && x.is_contiguous(), "x: [N,H,W,C] bf16");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && k <= 15 && s >= 1 && p >= 0 && p < k, "unsupported pool geometry");
+  const bool bn = coef.has_value() && coef->defined();
+  if (bn) {
+    check_f32(*coef, "coef");
+    TORCH_CHECK(coef->numel() == 2 * C, "coef = [scale | shift]");
+  }
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "empty output");
+  const c10::DeviceGuard guard(x.device());
+  auto y = torch::empty({N, OH, OW, C}, x.options());
+  auto idx = torch::empty({N, OH, OW, C}, x.options().dtype(torch::kUInt8));
+  psamd::launch_maxpool_nhwc_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), bn ? coef->data_ptr<float>() : nullptr,
+                                 reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H, W, C, OH,
+                                 OW, k, s, p, cur_stream(x));
+  return {y, idx};
+}
+
+Tensor maxpool_nhwc_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  check_gpu(dy, "dy");
+  TORCH_CHECK(dy.dim() == 4 && dy.scalar_type() == torch::kBFloat16 && dy.is_contiguous(), "dy: [N,OH,OW,C] bf16");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == torch::kUInt8 && idx.is_contiguous(), "idx like dy");
+  const int64_t N = dy.size(0), OH = dy.size(1), OW = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(C % 8 == 0 && OH == (H + 2 * p - k) / s + 1 && OW == (W + 2 * p - k) / s + 1, "pool geometry");
+  const c10::DeviceGuard guard(dy.device());
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  psamd::launch_maxpool_nhwc_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                                 reinterpret_cast<uint16_t*>(dx.data_ptr()), N, H, W, C, OH, OW, k, s, p,
+                                 cur_stream(dy));
+  return dx;
+}
+
+std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::optional<Tensor> gamma, Tensor mean,
+                               Tensor invstd, int64_t act, bool want_dres, bool affine,
+                               c10::optional<Tensor> mask_coef) {
+  check_gpu(dy, "dy");
+  check_gpu(x, "x");
+  const bool has_y = y.has_value() && y->defined();
+  const bool has_mc = mask_coef.has_value() && mask_coef->defined();
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes(), "dy/x [R, C]");
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && x.scalar_type() == torch::kBFloat16, "bf16 tensors");
+  if (has_y) {
+    check_gpu(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes() && y->scalar_type() == torch::kBFloat16, "y like x");
+  }
+  if (has_mc) {
+    check_f32(*mask_coef, "mask_coef");
+    TORCH_CHECK(mask_coef->numel() == 2 * x.size(1), "mask_coef = [scale | shift]");
+    TORCH_CHECK(!want_dres, "recomputed relu mask is only valid without a residual");
+  }
+  TORCH_CHECK(act == 0 || has_y || has_mc, "relu backward needs y or mask_coef");
   const int64_t R = x.size(0), C = x.size(1);
   TORCH_CHECK(C % 8 == 0, "C % 8");
   check_f32(mean, "mean");
@@ -471,7 +534,8 @@ std::vector<Tensor> bn_act_bwd(Tensor dy, Tensor y, Tensor x, c10::optional<Tens
   auto ws = torch::empty({2 * G * C + 3 * C}, fopt);
   psamd::BnBwdArgs a;
   a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());
-  a.y = reinterpret_cast<const uint16_t*>(y.data_ptr());
+  a.y = has_y ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr;
+  a.mask_coef = has_mc ? mask_coef->data_ptr<float>() : nullptr;
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   a.gamma = opt_ptr<const float>(gamma);
   a.mean = mean.data_ptr<float>();
@@ -554,7 +618,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt);
   m.def("act_bwd", &act_bwd);
   m.def("bn_act_fwd", &bn_act_fwd);
-  m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("bn_stats", &bn_stats);
+  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd);
+  m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
+  m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
+        py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),
+        py::arg("mask_coef") = py::none());
   m.attr("ONEBIT_CHUNK") = psamd::kOnebitChunk;
   m.attr("ARCH") = "gfx950";
 }

@@ -127,9 +127,15 @@ struct BnFwdArgs {
 };
 void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s);
 
+void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W,
+                             int C, int OH, int OW, int k, int s, int p, hipStream_t st);
+void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
+                             int OW, int k, int s, int p, hipStream_t st);
+
 struct BnBwdArgs {
   const uint16_t* dy;
-  const uint16_t* y;
+  const uint16_t* y;          // nullable when mask_coef is given (relu, no residual)
+  const float* mask_coef;     // nullable: forward [scale | shift], relu mask recomputed from x
   const uint16_t* x;
   const float* gamma;
   const float* mean;

@@ -40,11 +40,23 @@ int bn_red_blocks(int64_t R) {
 }
 
 // ------------------------------------------------------------------------------ stats
-// partial_s[g, c] = sum_{rows of block g} x[r, c]; partial_q likewise for x^2
+// Welford per thread over its rows, Chan-merged across the block: partial_mean[g, c] and
+// partial_m2[g, c] for block g (its row count follows from the geometry).  Numerically
+// robust when |mean| >> std, unlike E[x^2] - E[x]^2 (measured: stem-BN gradients).
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
+  if (nb == 0.f) return;
+  const float nn = n + nb;
+  const float d = mb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t R, int C,
-                                                               float* __restrict__ ps, float* __restrict__ pq) {
-  __shared__ float lds_s[256 * 8];
-  __shared__ float lds_q[256 * 8];
+                                                               float* __restrict__ pm, float* __restrict__ pv) {
+  __shared__ float lds_m[256 * 8];
+  __shared__ float lds_v[256 * 8];
+  __shared__ float lds_n[256];
   const RedGeom gm = red_geom(C);
   const int t = threadIdx.x;
   const int cg = t % gm.tpr + blockIdx.y * 256;  // channel group (8 channels)
@@ -54,39 +66,46 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* _
   const int64_t rows_per_block = (R + G - 1) / G;
   const int64_t rb = blockIdx.x * rows_per_block;
   const int64_t re = (rb + rows_per_block < R) ? rb + rows_per_block : R;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mean[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float n = 0.f;
   if (cg < ngroups) {
     for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
       float v[8];
       load8(x, r * C + cg * 8, v);
+      n += 1.f;
+      const float inv = 1.f / n;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        s[j] += v[j];
-        q[j] += v[j] * v[j];
+        const float d = v[j] - mean[j];
+        mean[j] += d * inv;
+        m2[j] += d * (v[j] - mean[j]);
       }
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    lds_s[t * 8 + j] = s[j];
-    lds_q[t * 8 + j] = q[j];
+    lds_m[t * 8 + j] = mean[j];
+    lds_v[t * 8 + j] = m2[j];
   }
+  lds_n[t] = n;
   __syncthreads();
   if (r0 == 0 && cg < ngroups) {
     for (int k = 1; k < gm.rows_it; ++k) {
-      const int src = (k * gm.tpr + t) * 8;
+      const int src = k * gm.tpr + t;
+      const float nb = lds_n[src];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        s[j] += lds_s[src + j];
-        q[j] += lds_q[src + j];
+        float nn = n;
+        chan_merge(nn, mean[j], m2[j], nb, lds_m[src * 8 + j], lds_v[src * 8 + j]);
       }
+      n += nb;
     }
-    float* os = ps + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
-    float* oq = pq + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
-    *reinterpret_cast<f32x4*>(os) = f32x4{s[0], s[1], s[2], s[3]};
-    *reinterpret_cast<f32x4*>(os + 4) = f32x4{s[4], s[5], s[6], s[7]};
-    *reinterpret_cast<f32x4*>(oq) = f32x4{q[0], q[1], q[2], q[3]};
-    *reinterpret_cast<f32x4*>(oq + 4) = f32x4{q[4], q[5], q[6], q[7]};
+    float* om = pm + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    float* ov = pv + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    *reinterpret_cast<f32x4*>(om) = f32x4{mean[0], mean[1], mean[2], mean[3]};
+    *reinterpret_cast<f32x4*>(om + 4) = f32x4{mean[4], mean[5], mean[6], mean[7]};
+    *reinterpret_cast<f32x4*>(ov) = f32x4{m2[0], m2[1], m2[2], m2[3]};
+    *reinterpret_cast<f32x4*>(ov + 4) = f32x4{m2[4], m2[5], m2[6], m2[7]};
   }
 }
 
@@ -132,23 +151,76 @@ __device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const
   }
 }
 
+// Chan-merge the [G, C] (mean, M2) partials of one 8-channel group per block.  Thread t
+// merges blocks g = t, t+256, ... in order, then a fixed LDS tree merges the 256 thread
+// results (deterministic).
+__device__ __forceinline__ void merge_partials8(const float* __restrict__ pm, const float* __restrict__ pv, int G,
+                                                int C, int64_t R, int cg, float* lds_m, float* lds_v, float* lds_n,
+                                                float& out_mean, float& out_var) {
+  const int64_t rpb = (R + G - 1) / G;
+  float mean[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float n = 0.f;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    const int64_t rb = g * rpb;
+    const int64_t re = rb + rpb < R ? rb + rpb : R;
+    const float nb = re > rb ? static_cast<float>(re - rb) : 0.f;
+    float u[8], v[8];
+    load8(pm, static_cast<int64_t>(g) * C + cg * 8, u);
+    load8(pv, static_cast<int64_t>(g) * C + cg * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float nn = n;
+      chan_merge(nn, mean[j], m2[j], nb, u[j], v[j]);
+    }
+    n += nb;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lds_m[threadIdx.x * 8 + j] = mean[j];
+    lds_v[threadIdx.x * 8 + j] = m2[j];
+  }
+  lds_n[threadIdx.x] = n;
+  __syncthreads();
+  // fixed-shape tree over the block (deterministic): stride 128, 64, ..., 1
+  for (int stride = blockDim.x >> 1; stride > 0; stride >>= 1) {
+    if (threadIdx.x < stride) {
+      const int o = threadIdx.x + stride;
+      const float nb = lds_n[o];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float nn = n;
+        chan_merge(nn, mean[j], m2[j], nb, lds_m[o * 8 + j], lds_v[o * 8 + j]);
+        lds_m[threadIdx.x * 8 + j] = mean[j];
+        lds_v[threadIdx.x * 8 + j] = m2[j];
+      }
+      n += nb;
+      lds_n[threadIdx.x] = n;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 8) {
+    const float nn = lds_n[0];
+    out_mean = lds_m[threadIdx.x];
+    out_var = nn > 0.f ? lds_v[threadIdx.x] / nn : 0.f;
+  }
+}
+
 // per channel: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; running stats.
 // grid = C / 8 blocks of 256 threads.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pm, const float* __restrict__ pv,
                                                           int G, int C, int64_t R, float eps, float momentum,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out, float* __restrict__ scale,
                                                           float* __restrict__ shift) {
-  __shared__ float lds[64];
-  float s = 0.f, q = 0.f;
-  sum_partials8(ps, pq, G, C, blockIdx.x, lds, s, q);
+  __shared__ float lds_m[256 * 8];
+  __shared__ float lds_v[256 * 8];
+  __shared__ float lds_n[256];
+  float mean = 0.f, var = 0.f;
+  merge_partials8(pm, pv, G, C, R, blockIdx.x, lds_m, lds_v, lds_n, mean, var);
   if (threadIdx.x >= 8) return;
   const int c = blockIdx.x * 8 + threadIdx.x;
-  const float inv_r = 1.f / static_cast<float>(R);
-  const float mean = s * inv_r;
-  float var = q * inv_r - mean * mean;
   if (var < 0.f) var = 0.f;
   const float invstd = rsqrtf(var + eps);
   const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
@@ -204,11 +276,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 }
 
 // ------------------------------------------------------------------------------ backward
-// partial_dz[g,c] = sum dz ; partial_dzx[g,c] = sum dz * (x - mean) * invstd ; dz = dy * act'(y)
+// partial_dz[g,c] = sum dz ; partial_dzx[g,c] = sum dz * (x - mean) * invstd ; dz = dy * act'(.)
+// ACT: 0 identity, 1 relu mask from the saved output y, 2 relu mask recomputed from x with the
+// forward's scale/shift (mc = [scale | shift]) -- no residual, so y > 0 <=> x*scale+shift > 0;
+// saves one tensor read in both backward passes.
 template <int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                             const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ mc,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int64_t R, int C,
                                                             float* __restrict__ pd, float* __restrict__ px) {
@@ -225,9 +301,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   const int64_t re = (rb + rows_per_block < R) ? rb + rows_per_block : R;
   float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (cg < ngroups) {
-    float mu[8], is[8];
+    float mu[8], is[8], sc[8], sh[8];
     load8(mean, cg * 8, mu);
     load8(invstd, cg * 8, is);
+    if constexpr (ACT == 2) {
+      load8(mc, cg * 8, sc);
+      load8(mc + C, cg * 8, sh);
+    }
     for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
       float g[8], xv[8];
       load8(dy, r * C + cg * 8, g);
@@ -237,6 +317,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         load8(y, r * C + cg * 8, yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      } else if constexpr (ACT == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = xv[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -299,6 +382,7 @@ template <int ACT, bool DRES>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ y,
                                                            const uint16_t* __restrict__ x,
+                                                           const float* __restrict__ mc,
                                                            const float* __restrict__ ca,
                                                            const float* __restrict__ cb,
                                                            const float* __restrict__ cc, uint16_t* __restrict__ dx,
@@ -315,6 +399,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
       load8(y, v * 8, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    } else if constexpr (ACT == 2) {
+      float sc[8], sh[8];
+      load8(mc, c, sc);
+      load8(mc + C, c, sh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = xv[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
     }
     load8(ca, c, A);
     load8(cb, c, B);
@@ -341,6 +431,7 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(cblocks), dim3(256), 0, s, C, a.eps, a.gamma, a.beta, a.rmean,
                        a.rvar, a.scale, a.shift);
   }
+  if (!a.y) return;  // statistics / coefficients only (the apply is fused into a consumer)
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
 #define PSAMD_BN_APPLY(RES, ACT)                                                                                 \
@@ -361,25 +452,28 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   const int64_t R = a.R;
   const int G = a.G;
   const int ctiles = (C / 8 + 255) / 256;
-  if (a.act == 1)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mean, a.invstd,
-                       R, C, a.ws, a.ws + G * C);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<0>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mean, a.invstd,
-                       R, C, a.ws, a.ws + G * C);
+  const int act = (a.act == 1 && a.mask_coef && !a.dres) ? 2 : a.act;
+#define PSAMD_BN_RED(ACT)                                                                                       \
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel<ACT>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mask_coef, \
+                     a.mean, a.invstd, R, C, a.ws, a.ws + G * C)
+  if (act == 2) PSAMD_BN_RED(2);
+  else if (act == 1) PSAMD_BN_RED(1);
+  else PSAMD_BN_RED(0);
+#undef PSAMD_BN_RED
   float* coef = a.ws + 2 * G * C;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, G, C, R,
                      a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
 #define PSAMD_BN_BWD(ACT, DRES)                                                                                    \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x, coef, coef + C, \
-                     coef + 2 * C, a.dx, a.dres, nvec, C)
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x, a.mask_coef, \
+                     coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C)
   if (a.dres) {
-    if (a.act == 1) PSAMD_BN_BWD(1, true);
+    if (act == 1) PSAMD_BN_BWD(1, true);
     else PSAMD_BN_BWD(0, true);
   } else {
-    if (a.act == 1) PSAMD_BN_BWD(1, false);
+    if (act == 2) PSAMD_BN_BWD(2, false);
+    else if (act == 1) PSAMD_BN_BWD(1, false);
     else PSAMD_BN_BWD(0, false);
   }
 #undef PSAMD_BN_BWD

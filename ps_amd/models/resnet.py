@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.pool import MaxPool2d, bn_relu_maxpool
 
 
 class Bottleneck(nn.Module):
@@ -57,7 +58,7 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(64) if fused_bn else nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = (MaxPool2d if fused_bn else nn.MaxPool2d)(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0])
         self.layer2 = self._make_layer(128, layers[1], stride=2)
         self.layer3 = self._make_layer(256, layers[2], stride=2)
@@ -87,8 +88,10 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.bn1(self.conv1(x))
-        x = self.maxpool(x if self.fused_bn else self.relu(x))
+        if self.fused_bn:  # stem BN + ReLU fused into the pool: the BN output never hits HBM
+            x = bn_relu_maxpool(self.conv1(x), self.bn1, 3, 2, 1)
+        else:
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

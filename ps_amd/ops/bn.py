@@ -37,19 +37,23 @@ class _BnActFn(torch.autograd.Function):
         shape = x.shape
         x2 = _as_rows(x)
         r2 = _as_rows(res) if res is not None else None
-        y2, mean, invstd = native().bn_act_fwd(x2, r2, gamma, beta, rmean, rvar, bool(training), float(momentum),
-                                              float(eps), int(act))
-        ctx.save_for_backward(x2, y2, gamma, mean, invstd)
+        y2, mean, invstd, coef = native().bn_act_fwd(x2, r2, gamma, beta, rmean, rvar, bool(training),
+                                                    float(momentum), float(eps), int(act))
+        if act and res is None:
+            # relu mask recomputed from x * scale + shift in backward: y is not re-read
+            ctx.save_for_backward(x2, None, gamma, mean, invstd, coef)
+        else:
+            ctx.save_for_backward(x2, y2 if act else None, gamma, mean, invstd, None)
         ctx.act, ctx.has_res, ctx.shape = act, res is not None, shape
         ctx.affine = gamma is not None
         return _from_rows(y2, shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, y2, gamma, mean, invstd = ctx.saved_tensors
+        x2, y2, gamma, mean, invstd, coef = ctx.saved_tensors
         dy2 = _as_rows(dy)
         dx2, dres2, dg, db = native().bn_act_bwd(dy2, y2, x2, gamma, mean, invstd, int(ctx.act), ctx.has_res,
-                                                 ctx.affine)
+                                                 ctx.affine, coef)
         dx = _from_rows(dx2, ctx.shape)
         dres = _from_rows(dres2, ctx.shape) if ctx.has_res else None
         return dx, dres, (dg if ctx.affine else None), (db if ctx.affine else None), None, None, None, None, None, \

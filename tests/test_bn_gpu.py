@@ -94,4 +94,25 @@ def test_resnet_fused_matches_unfused_gpu():
     for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(), ref.named_parameters()):
         ca = cos(p.grad.float().reshape(1, -1), r.grad.reshape(1, -1)).item()
         cb = cos(q.grad.float().reshape(1, -1), r.grad.reshape(1, -1)).item()
-        assert ca > 0.9 and ca > cb - 0.02, (n, ca, cb)
+        assert ca > 0.9 and ca > cb - 0.05, (n, ca, cb)
+
+
+@pytest.mark.gpu
+def test_bn_stats_large_mean_offset():
+    """Welford/Chan statistics: |mean| >> std must not lose the variance (E[x^2]-E[x]^2 would)."""
+    from ps_amd.ops import native
+
+    torch.manual_seed(0)
+    N, H, W, C = 16, 28, 28, 64
+    x64 = 50.0 + 0.05 * torch.randn(N, C, H, W, dtype=torch.float64)
+    x = x64.cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    xr = x.double()
+    g = torch.ones(C, device="cuda")
+    b = torch.zeros(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    x2 = x.permute(0, 2, 3, 1).reshape(-1, C)  # NHWC rows (a view: channels_last)
+    y, mean, invstd, _ = native().bn_act_fwd(x2, None, g, b, rm, rv, True, 0.1, 1e-5, 0)
+    mref = xr.mean((0, 2, 3))
+    vref = xr.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(mean.double(), mref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close((1 / invstd.double() ** 2 - 1e-5), vref, rtol=2e-3, atol=1e-7)

@@ -1,0 +1,51 @@
+"""NHWC max pool HIP kernels (+ fused stem BN -> ReLU -> pool) vs plain torch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ps_amd.ops.bn import BatchNormAct2d
+from ps_amd.ops.pool import bn_relu_maxpool, max_pool2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,C,H,W,k,s,p", [(2, 64, 112, 112, 3, 2, 1), (3, 16, 9, 7, 2, 2, 0),
+                                           (1, 24, 10, 10, 3, 1, 1), (2, 8, 15, 15, 3, 2, 1)])
+def test_maxpool_nhwc_fwd_bwd(N, C, H, W, k, s, p):
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xr = x.float().detach().requires_grad_(True)
+    xh = x.detach().requires_grad_(True)
+    y = max_pool2d(xh, k, s, p)
+    yr = F.max_pool2d(xr, k, s, p)
+    assert torch.equal(y.float(), yr)  # max of bf16 values is exact
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g.bfloat16().float())
+    torch.testing.assert_close(xh.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+def test_bn_relu_maxpool_matches_unfused():
+    torch.manual_seed(0)
+    N, C, H, W = 4, 64, 56, 56
+    x = (torch.randn(N, C, H, W, device="cuda") * 2 + 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(bn.state_dict())
+    xh = x.detach().requires_grad_(True)
+    xr = x.float().detach().requires_grad_(True)
+    y = bn_relu_maxpool(xh, bn, 3, 2, 1)
+    yr = F.max_pool2d(torch.relu(ref(xr)), 3, 2, 1)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    cos = torch.nn.functional.cosine_similarity
+    assert cos(xh.grad.float().flatten(), xr.grad.flatten(), dim=0) > 0.99
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=5e-2, atol=0.5)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=5e-2, atol=0.5)
