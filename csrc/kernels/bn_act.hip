@@ -33,30 +33,21 @@ __host__ __device__ inline RedGeom red_geom(int C) {
 }
 
 int bn_red_blocks(int64_t R) {
-  int64_t g = (R + 63) / 64;  // >= 64 rows per block keeps the [G, C] partials <= 1/16 of the data
+  int64_t g = (R + 127) / 128;  // >= 128 rows per block keeps the [G, C] partials <= 1/32 of the data
   if (g < 1) g = 1;
-  if (g > 1024) g = 1024;
+  if (g > 2048) g = 2048;  // 8 blocks per CU: enough loads in flight to stream at the HBM rate
   return static_cast<int>(g);
 }
 
 // ------------------------------------------------------------------------------ stats
-// Welford per thread over its rows, Chan-merged across the block: partial_mean[g, c] and
-// partial_m2[g, c] for block g (its row count follows from the geometry).  Numerically
-// robust when |mean| >> std, unlike E[x^2] - E[x]^2 (measured: stem-BN gradients).
-__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
-  if (nb == 0.f) return;
-  const float nn = n + nb;
-  const float d = mb - mean;
-  mean += d * (nb / nn);
-  m2 += m2b + d * d * (n * nb / nn);
-  n = nn;
-}
-
+// Shifted sums per block: partial_s1[g, c] = sum (x - K_c), partial_s2[g, c] = sum (x - K_c)^2
+// with the shift K_c = x[0, c] (a sample of the channel, so |mean - K| ~ std): robust when
+// |mean| >> std, unlike raw E[x^2] - E[x]^2, and -- unlike Welford -- no division or serial
+// dependency per row, so the pass streams at the HBM rate (4 rows' loads in flight/thread).
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t R, int C,
-                                                               float* __restrict__ pm, float* __restrict__ pv) {
-  __shared__ float lds_m[256 * 8];
-  __shared__ float lds_v[256 * 8];
-  __shared__ float lds_n[256];
+                                                               float* __restrict__ ps, float* __restrict__ pq) {
+  __shared__ float lds_s[256 * 8];
+  __shared__ float lds_q[256 * 8];
   const RedGeom gm = red_geom(C);
   const int t = threadIdx.x;
   const int cg = t % gm.tpr + blockIdx.y * 256;  // channel group (8 channels)
@@ -66,46 +57,54 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* _
   const int64_t rows_per_block = (R + G - 1) / G;
   const int64_t rb = blockIdx.x * rows_per_block;
   const int64_t re = (rb + rows_per_block < R) ? rb + rows_per_block : R;
-  float mean[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float n = 0.f;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (cg < ngroups) {
-    for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
-      float v[8];
-      load8(x, r * C + cg * 8, v);
-      n += 1.f;
-      const float inv = 1.f / n;
+    float K[8];
+    load8(x, cg * 8, K);
+    auto upd = [&](const float (&v)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = v[j] - mean[j];
-        mean[j] += d * inv;
-        m2[j] += d * (v[j] - mean[j]);
+        const float d = v[j] - K[j];
+        s1[j] += d;
+        s2[j] += d * d;
       }
+    };
+    const int64_t step = gm.rows_it;
+    int64_t r = rb + r0;
+    for (; r + 3 * step < re; r += 4 * step) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8(x, (r + u * step) * C + cg * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) upd(v[u]);
+    }
+    for (; r < re; r += step) {
+      float v[8];
+      load8(x, r * C + cg * 8, v);
+      upd(v);
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    lds_m[t * 8 + j] = mean[j];
-    lds_v[t * 8 + j] = m2[j];
+    lds_s[t * 8 + j] = s1[j];
+    lds_q[t * 8 + j] = s2[j];
   }
-  lds_n[t] = n;
   __syncthreads();
   if (r0 == 0 && cg < ngroups) {
     for (int k = 1; k < gm.rows_it; ++k) {
-      const int src = k * gm.tpr + t;
-      const float nb = lds_n[src];
+      const int src = (k * gm.tpr + t) * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float nn = n;
-        chan_merge(nn, mean[j], m2[j], nb, lds_m[src * 8 + j], lds_v[src * 8 + j]);
+        s1[j] += lds_s[src + j];
+        s2[j] += lds_q[src + j];
       }
-      n += nb;
     }
-    float* om = pm + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
-    float* ov = pv + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
-    *reinterpret_cast<f32x4*>(om) = f32x4{mean[0], mean[1], mean[2], mean[3]};
-    *reinterpret_cast<f32x4*>(om + 4) = f32x4{mean[4], mean[5], mean[6], mean[7]};
-    *reinterpret_cast<f32x4*>(ov) = f32x4{m2[0], m2[1], m2[2], m2[3]};
-    *reinterpret_cast<f32x4*>(ov + 4) = f32x4{m2[4], m2[5], m2[6], m2[7]};
+    float* o1 = ps + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    float* o2 = pq + blockIdx.x * static_cast<int64_t>(C) + cg * 8;
+    *reinterpret_cast<f32x4*>(o1) = f32x4{s1[0], s1[1], s1[2], s1[3]};
+    *reinterpret_cast<f32x4*>(o1 + 4) = f32x4{s1[4], s1[5], s1[6], s1[7]};
+    *reinterpret_cast<f32x4*>(o2) = f32x4{s2[0], s2[1], s2[2], s2[3]};
+    *reinterpret_cast<f32x4*>(o2 + 4) = f32x4{s2[4], s2[5], s2[6], s2[7]};
   }
 }
 
@@ -151,76 +150,24 @@ __device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const
   }
 }
 
-// Chan-merge the [G, C] (mean, M2) partials of one 8-channel group per block.  Thread t
-// merges blocks g = t, t+256, ... in order, then a fixed LDS tree merges the 256 thread
-// results (deterministic).
-__device__ __forceinline__ void merge_partials8(const float* __restrict__ pm, const float* __restrict__ pv, int G,
-                                                int C, int64_t R, int cg, float* lds_m, float* lds_v, float* lds_n,
-                                                float& out_mean, float& out_var) {
-  const int64_t rpb = (R + G - 1) / G;
-  float mean[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float n = 0.f;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    const int64_t rb = g * rpb;
-    const int64_t re = rb + rpb < R ? rb + rpb : R;
-    const float nb = re > rb ? static_cast<float>(re - rb) : 0.f;
-    float u[8], v[8];
-    load8(pm, static_cast<int64_t>(g) * C + cg * 8, u);
-    load8(pv, static_cast<int64_t>(g) * C + cg * 8, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float nn = n;
-      chan_merge(nn, mean[j], m2[j], nb, u[j], v[j]);
-    }
-    n += nb;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    lds_m[threadIdx.x * 8 + j] = mean[j];
-    lds_v[threadIdx.x * 8 + j] = m2[j];
-  }
-  lds_n[threadIdx.x] = n;
-  __syncthreads();
-  // fixed-shape tree over the block (deterministic): stride 128, 64, ..., 1
-  for (int stride = blockDim.x >> 1; stride > 0; stride >>= 1) {
-    if (threadIdx.x < stride) {
-      const int o = threadIdx.x + stride;
-      const float nb = lds_n[o];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float nn = n;
-        chan_merge(nn, mean[j], m2[j], nb, lds_m[o * 8 + j], lds_v[o * 8 + j]);
-        lds_m[threadIdx.x * 8 + j] = mean[j];
-        lds_v[threadIdx.x * 8 + j] = m2[j];
-      }
-      n += nb;
-      lds_n[threadIdx.x] = n;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x < 8) {
-    const float nn = lds_n[0];
-    out_mean = lds_m[threadIdx.x];
-    out_var = nn > 0.f ? lds_v[threadIdx.x] / nn : 0.f;
-  }
-}
-
 // per channel: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; running stats.
 // grid = C / 8 blocks of 256 threads.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ pm, const float* __restrict__ pv,
-                                                          int G, int C, int64_t R, float eps, float momentum,
-                                                          const float* __restrict__ gamma,
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
+                                                          const uint16_t* __restrict__ x, int G, int C, int64_t R,
+                                                          float eps, float momentum, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out, float* __restrict__ scale,
                                                           float* __restrict__ shift) {
-  __shared__ float lds_m[256 * 8];
-  __shared__ float lds_v[256 * 8];
-  __shared__ float lds_n[256];
-  float mean = 0.f, var = 0.f;
-  merge_partials8(pm, pv, G, C, R, blockIdx.x, lds_m, lds_v, lds_n, mean, var);
+  __shared__ float lds[64];
+  float s1 = 0.f, s2 = 0.f;
+  sum_partials8(ps, pq, G, C, blockIdx.x, lds, s1, s2);
   if (threadIdx.x >= 8) return;
   const int c = blockIdx.x * 8 + threadIdx.x;
+  const float inv_n = 1.f / static_cast<float>(R);
+  const float dm = s1 * inv_n;  // mean - K
+  const float mean = bf16_to_f32(x[c]) + dm;
+  float var = s2 * inv_n - dm * dm;
   if (var < 0.f) var = 0.f;
   const float invstd = rsqrtf(var + eps);
   const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
@@ -249,21 +196,29 @@ __global__ __launch_bounds__(256) void bn_eval_coef_kernel(int C, float eps, con
   shift[c] = be - rmean[c] * ga * invstd;
 }
 
-// y = act(x * scale_c + shift_c [+ res])
-template <bool RES, int ACT>
+// y = act(x * scale_c + shift_c [+ res]).  FIXED_C: the grid stride is a multiple of C/8, so
+// each thread's channel group never changes -- coefficients are loaded once and the 64-bit
+// modulo leaves the loop.  Two vectors per thread per iteration keep enough loads in flight.
+template <bool RES, int ACT, bool FIXED_C>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, uint16_t* __restrict__ y,
                                                        int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int cvec = C / 8;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c = static_cast<int>(v % cvec) * 8;
-    float a[8], b[8], sc[8], sh[8];
-    load8(x, v * 8, a);
+  const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  float sc[8], sh[8];
+  if constexpr (FIXED_C) {
+    const int c = static_cast<int>(v0 % cvec) * 8;
     load8(scale, c, sc);
     load8(shift, c, sh);
-    if constexpr (RES) load8(res, v * 8, b);
+  }
+  auto one = [&](int64_t v, float (&a)[8], const float (&b)[8]) {
+    if constexpr (!FIXED_C) {
+      const int c = static_cast<int>(v % cvec) * 8;
+      load8(scale, c, sc);
+      load8(shift, c, sh);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = a[j] * sc[j] + sh[j];
@@ -272,6 +227,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       a[j] = o;
     }
     store8(y, v * 8, a);
+  };
+  int64_t v = v0;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float a0[8], a1[8], b0[8], b1[8];
+    load8(x, v * 8, a0);
+    load8(x, (v + stride) * 8, a1);
+    if constexpr (RES) {
+      load8(res, v * 8, b0);
+      load8(res, (v + stride) * 8, b1);
+    }
+    one(v, a0, b0);
+    one(v + stride, a1, b1);
+  }
+  if (v < nvec) {
+    float a0[8], b0[8];
+    load8(x, v * 8, a0);
+    if constexpr (RES) load8(res, v * 8, b0);
+    one(v, a0, b0);
   }
 }
 
@@ -308,13 +281,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       load8(mc, cg * 8, sc);
       load8(mc + C, cg * 8, sh);
     }
-    for (int64_t r = rb + r0; r < re; r += gm.rows_it) {
-      float g[8], xv[8];
-      load8(dy, r * C + cg * 8, g);
-      load8(x, r * C + cg * 8, xv);
+    auto acc = [&](float (&g)[8], const float (&xv)[8], const float (&yv)[8]) {
       if constexpr (ACT == 1) {
-        float yv[8];
-        load8(y, r * C + cg * 8, yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
       } else if constexpr (ACT == 2) {
@@ -326,6 +294,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
         sd[j] += g[j];
         sx[j] += g[j] * (xv[j] - mu[j]) * is[j];
       }
+    };
+    const int64_t step = gm.rows_it;
+    int64_t r = rb + r0;
+    constexpr int U = ACT == 1 ? 2 : 4;  // loads in flight per thread (2 or 3 tensors each)
+    for (; r + (U - 1) * step < re; r += U * step) {
+      float g[U][8], xv[U][8], yv[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t o = (r + u * step) * C + cg * 8;
+        load8(dy, o, g[u]);
+        load8(x, o, xv[u]);
+        if constexpr (ACT == 1) load8(y, o, yv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc(g[u], xv[u], yv[u]);
+    }
+    for (; r < re; r += step) {
+      float g[8], xv[8], yv[8];
+      const int64_t o = r * C + cg * 8;
+      load8(dy, o, g);
+      load8(x, o, xv);
+      if constexpr (ACT == 1) load8(y, o, yv);
+      acc(g, xv, yv);
     }
   }
 #pragma unroll
@@ -378,7 +369,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   cc[c] = -k * md + k * is * mx * mean[c];
 }
 
-template <int ACT, bool DRES>
+// dz = dy * act'(.) [dres = dz]; dx = A dz + B x + Cc.  FIXED_C as in bn_apply_kernel.
+template <int ACT, bool DRES, bool FIXED_C>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ y,
                                                            const uint16_t* __restrict__ x,
@@ -389,30 +381,52 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            uint16_t* __restrict__ dres, int64_t nvec, int C) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int cvec = C / 8;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c = static_cast<int>(v % cvec) * 8;
-    float g[8], xv[8], A[8], B[8], Cc[8];
-    load8(dy, v * 8, g);
-    load8(x, v * 8, xv);
-    if constexpr (ACT == 1) {
-      float yv[8];
-      load8(y, v * 8, yv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
-    } else if constexpr (ACT == 2) {
-      float sc[8], sh[8];
-      load8(mc, c, sc);
-      load8(mc + C, c, sh);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = xv[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
-    }
+  const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  float A[8], B[8], Cc[8], sc[8], sh[8];
+  auto coefs = [&](int c) {
     load8(ca, c, A);
     load8(cb, c, B);
     load8(cc, c, Cc);
+    if constexpr (ACT == 2) {
+      load8(mc, c, sc);
+      load8(mc + C, c, sh);
+    }
+  };
+  if constexpr (FIXED_C) coefs(static_cast<int>(v0 % cvec) * 8);
+  auto one = [&](int64_t v, float (&g)[8], float (&xv)[8], const float (&yv)[8]) {
+    if constexpr (!FIXED_C) coefs(static_cast<int>(v % cvec) * 8);
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    } else if constexpr (ACT == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = xv[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
+    }
     if constexpr (DRES) store8(dres, v * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = A[j] * g[j] + B[j] * xv[j] + Cc[j];
     store8(dx, v * 8, xv);
+  };
+  int64_t v = v0;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
+    load8(dy, v * 8, g0);
+    load8(dy, (v + stride) * 8, g1);
+    load8(x, v * 8, x0);
+    load8(x, (v + stride) * 8, x1);
+    if constexpr (ACT == 1) {
+      load8(y, v * 8, y0);
+      load8(y, (v + stride) * 8, y1);
+    }
+    one(v, g0, x0, y0);
+    one(v + stride, g1, x1, y1);
+  }
+  if (v < nvec) {
+    float g0[8], x0[8], y0[8];
+    load8(dy, v * 8, g0);
+    load8(x, v * 8, x0);
+    if constexpr (ACT == 1) load8(y, v * 8, y0);
+    one(v, g0, x0, y0);
   }
 }
 
@@ -425,7 +439,7 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
     const int G = a.G;
     const int ctiles = (C / 8 + 255) / 256;
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(G, ctiles), dim3(256), 0, s, a.x, R, C, a.ws, a.ws + G * C);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, G, C, R, a.eps,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, a.x, G, C, R, a.eps,
                        a.momentum, a.gamma, a.beta, a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(cblocks), dim3(256), 0, s, C, a.eps, a.gamma, a.beta, a.rmean,
@@ -434,15 +448,20 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
   if (!a.y) return;  // statistics / coefficients only (the apply is fused into a consumer)
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
-#define PSAMD_BN_APPLY(RES, ACT)                                                                                 \
-  hipLaunchKernelGGL((bn_apply_kernel<RES, ACT>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale, a.shift, a.y, \
-                     nvec, C)
+  const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
+#define PSAMD_BN_APPLY(RES, ACT)                                                                              \
+  if (fixed)                                                                                                  \
+    hipLaunchKernelGGL((bn_apply_kernel<RES, ACT, true>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale,    \
+                       a.shift, a.y, nvec, C);                                                                \
+  else                                                                                                        \
+    hipLaunchKernelGGL((bn_apply_kernel<RES, ACT, false>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale,   \
+                       a.shift, a.y, nvec, C)
   if (a.res) {
-    if (a.act == 1) PSAMD_BN_APPLY(true, 1);
-    else PSAMD_BN_APPLY(true, 0);
+    if (a.act == 1) { PSAMD_BN_APPLY(true, 1); }
+    else { PSAMD_BN_APPLY(true, 0); }
   } else {
-    if (a.act == 1) PSAMD_BN_APPLY(false, 1);
-    else PSAMD_BN_APPLY(false, 0);
+    if (a.act == 1) { PSAMD_BN_APPLY(false, 1); }
+    else { PSAMD_BN_APPLY(false, 0); }
   }
 #undef PSAMD_BN_APPLY
 }
@@ -465,16 +484,21 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
                      a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
-#define PSAMD_BN_BWD(ACT, DRES)                                                                                    \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x, a.mask_coef, \
-                     coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C)
+  const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
+#define PSAMD_BN_BWD(ACT, DRES)                                                                                 \
+  if (fixed)                                                                                                    \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES, true>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x,      \
+                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C);                       \
+  else                                                                                                          \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES, false>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x,     \
+                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C)
   if (a.dres) {
-    if (act == 1) PSAMD_BN_BWD(1, true);
-    else PSAMD_BN_BWD(0, true);
+    if (act == 1) { PSAMD_BN_BWD(1, true); }
+    else { PSAMD_BN_BWD(0, true); }
   } else {
-    if (act == 2) PSAMD_BN_BWD(2, false);
-    else if (act == 1) PSAMD_BN_BWD(1, false);
-    else PSAMD_BN_BWD(0, false);
+    if (act == 2) { PSAMD_BN_BWD(2, false); }
+    else if (act == 1) { PSAMD_BN_BWD(1, false); }
+    else { PSAMD_BN_BWD(0, false); }
   }
 #undef PSAMD_BN_BWD
 }

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.conv import Conv1x1
 from ..ops.pool import MaxPool2d, bn_relu_maxpool
 
 
@@ -27,11 +28,12 @@ class Bottleneck(nn.Module):
         width = planes
         self.fused_bn = fused_bn
         BN = BatchNormAct2d if fused_bn else nn.BatchNorm2d
-        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        C1 = Conv1x1 if fused_bn else (lambda i, o: nn.Conv2d(i, o, 1, bias=False))
+        self.conv1 = C1(inplanes, width)
         self.bn1 = BN(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BN(width)
-        self.conv3 = nn.Conv2d(width, planes * 4, 1, bias=False)
+        self.conv3 = C1(width, planes * 4)
         self.bn3 = BN(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample

@@ -49,3 +49,24 @@ def test_bn_relu_maxpool_matches_unfused():
     assert cos(xh.grad.float().flatten(), xr.grad.flatten(), dim=0) > 0.99
     torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=5e-2, atol=0.5)
     torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=5e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("ci,co,h", [(256, 64, 14), (1024, 256, 7), (64, 256, 14), (2048, 512, 7)])
+def test_conv1x1_routed_matches_conv2d(ci, co, h):
+    from ps_amd.ops.conv import Conv1x1
+
+    torch.manual_seed(0)
+    m = Conv1x1(ci, co).cuda().bfloat16().to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(ci, co, 1, bias=False).cuda()
+    ref.weight.data.copy_(m.weight.float())
+    x = torch.randn(4, ci, h, h, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xh = x.detach().requires_grad_(True)
+    xr = x.float().detach().requires_grad_(True)
+    y, yr = m(xh), ref(xr)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g.bfloat16().float())
+    torch.testing.assert_close(xh.grad.float(), xr.grad, rtol=2e-2, atol=5e-2)
+    cos = torch.nn.functional.cosine_similarity
+    assert cos(m.weight.grad.float().flatten(), ref.weight.grad.flatten(), dim=0) > 0.999
