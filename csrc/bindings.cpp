@@ -462,6 +462,79 @@ std::vector<Tensor> bn_stats(Tensor x, c10::optional<Tensor> gamma, c10::optiona
   return {r[1], r[2], r[3]};
 }
 
+// ------------------------------------------------------------------------------ ResNet stem conv
+static void check_stem(const Tensor& x) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 4 && (x.size(3) == 3 || x.size(3) == 4) && x.scalar_type() == torch::kBFloat16 &&
+                  x.is_contiguous(), "x: [N, H, W, 3 or 4] bf16 contiguous");
+}
+
+// returns [z, part]; with kshift (running mean, [64] fp32) the BN partial sums of z are
+// produced in the conv epilogue: part [2, blocks, 64] (else an empty tensor)
+std::vector<Tensor> stem_conv_fwd(Tensor x, Tensor wp, c10::optional<Tensor> kshift) {
+  check_stem(x);
+  check_gpu(wp, "wp");
+  TORCH_CHECK(wp.scalar_type() == torch::kBFloat16 && wp.numel() == 64 * 224 && wp.is_contiguous(), "wp [64,224]");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(OW <= 128, "stem kernel supports OW <= 128");
+  const bool stats = kshift.has_value() && kshift->defined();
+  if (stats) {
+    check_f32(*kshift, "kshift");
+    TORCH_CHECK(kshift->numel() == 64, "kshift [64]");
+  }
+  const c10::DeviceGuard guard(x.device());
+  auto z = torch::empty({N, OH, OW, 64}, x.options());
+  const int nblk = psamd::stem_fwd_blocks(static_cast<int>(N));
+  auto part = stats ? torch::empty({2, nblk, 64}, x.options().dtype(torch::kFloat32)) : Tensor();
+  psamd::launch_stem_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), static_cast<int>(x.size(3)),
+                              reinterpret_cast<const uint16_t*>(wp.data_ptr()), reinterpret_cast<uint16_t*>(z.data_ptr()),
+                              N, H, W, OH, OW, stats ? kshift->data_ptr<float>() : nullptr,
+                              stats ? part.data_ptr<float>() : nullptr, cur_stream(x));
+  return {z, part};
+}
+
+// BN statistics from producer partial sums: part [2, G, C] about kshift over R rows.
+// Returns [mean, invstd, coef = scale | shift]; updates running stats when given.
+std::vector<Tensor> bn_finalize_sums(Tensor part, Tensor kshift, int64_t R, c10::optional<Tensor> gamma,
+                                     c10::optional<Tensor> beta, c10::optional<Tensor> rmean,
+                                     c10::optional<Tensor> rvar, double momentum, double eps) {
+  check_f32(part, "part");
+  check_f32(kshift, "kshift");
+  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.is_contiguous(), "part [2, G, C]");
+  const int64_t G = part.size(1), C = part.size(2);
+  TORCH_CHECK(C % 8 == 0 && kshift.numel() == C, "C % 8, kshift [C]");
+  const c10::DeviceGuard guard(part.device());
+  auto fopt = part.options();
+  auto mean = torch::empty({C}, fopt), invstd = torch::empty({C}, fopt), coef = torch::empty({2 * C}, fopt);
+  psamd::launch_bn_finalize_sums(part.data_ptr<float>(), part.data_ptr<float>() + G * C, kshift.data_ptr<float>(),
+                                 static_cast<int>(G), static_cast<int>(C), R, static_cast<float>(eps),
+                                 static_cast<float>(momentum), opt_ptr<const float>(gamma), opt_ptr<const float>(beta),
+                                 opt_ptr<float>(rmean), opt_ptr<float>(rvar), mean.data_ptr<float>(),
+                                 invstd.data_ptr<float>(), coef.data_ptr<float>(), coef.data_ptr<float>() + C,
+                                 cur_stream(part));
+  return {mean, invstd, coef};
+}
+
+Tensor stem_conv_wrw(Tensor x, Tensor dz) {
+  check_stem(x);
+  check_gpu(dz, "dz");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dz.dim() == 4 && dz.size(0) == N && dz.size(1) == OH && dz.size(2) == OW && dz.size(3) == 64 &&
+                  dz.scalar_type() == torch::kBFloat16 && dz.is_contiguous(), "dz: [N, OH, OW, 64] bf16 contiguous");
+  TORCH_CHECK(OW <= 128, "stem kernel supports OW <= 128");
+  const c10::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(torch::kFloat32);
+  const int nblk = psamd::stem_wrw_blocks(N, OH);
+  auto ws = torch::empty({(nblk + 32) * 64 * 224}, fopt);
+  auto dwp = torch::empty({64, 224}, fopt);
+  psamd::launch_stem_conv_wrw(reinterpret_cast<const uint16_t*>(x.data_ptr()), static_cast<int>(x.size(3)),
+                              reinterpret_cast<const uint16_t*>(dz.data_ptr()), ws.data_ptr<float>(),
+                              dwp.data_ptr<float>(), N, H, W, OH, OW, cur_stream(x));
+  return dwp;
+}
+
 // ------------------------------------------------------------------------------ NHWC max pool
 // x: [N, H, W, C] bf16 contiguous; coef: optional [scale | shift] (fused BN-apply + ReLU prologue)
 std::vector<Tensor> maxpool_nhwc_fwd(Tensor x, c10::optional<Tensor> coef, int64_t k, int64_t s, int64_t p) {
@@ -620,6 +693,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_stats", &bn_stats);
   m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd);
+  m.def("stem_conv_fwd", &stem_conv_fwd, py::arg("x"), py::arg("wp"), py::arg("kshift") = py::none());
+  m.def("bn_finalize_sums", &bn_finalize_sums);
+  m.def("stem_conv_wrw", &stem_conv_wrw);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),

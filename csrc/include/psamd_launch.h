@@ -132,6 +132,22 @@ void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, 
 void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                              int OW, int k, int s, int p, hipStream_t st);
 
+// ---------------------------------------------------------------- stem.hip (ResNet 7x7/2 stem, MFMA)
+// x: [N, H, W, cin] bf16, cin 3 or 4 (channel 3 meets zero weights); wp: [64][224] packed
+// bf16 (k' = kh*32 + kw*4 + c); z: [N, OH, OW, 64] bf16; OW <= 128.
+// kshift/part optional: per-block BN partial sums of z about kshift -> part[2][blocks][64]
+void launch_stem_conv_fwd(const uint16_t* x, int cin, const uint16_t* wp, uint16_t* z, int N, int H, int W, int OH,
+                          int OW, const float* kshift, float* part, hipStream_t s);
+int stem_fwd_blocks(int N);
+int stem_wrw_blocks(int N, int OH);
+// BN finalize from producer-fused partial sums ps/pq: [G][C] of sum(x - k), sum((x - k)^2)
+void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
+                             float eps, float momentum, const float* gamma, const float* beta, float* rmean,
+                             float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
+// ws: (stem_wrw_blocks + 32) * 64 * 224 floats; dwp: [64][224] fp32 packed weight gradient
+void launch_stem_conv_wrw(const uint16_t* x, int cin, const uint16_t* dz, float* ws, float* dwp, int N, int H, int W,
+                          int OH, int OW, hipStream_t s);
+
 struct BnBwdArgs {
   const uint16_t* dy;
   const uint16_t* y;          // nullable when mask_coef is given (relu, no residual)

@@ -152,8 +152,11 @@ __device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const
 
 // per channel: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; running stats.
 // grid = C / 8 blocks of 256 threads.
+// kshift: the shift the partial sums were taken about -- x[0, c] when null (bn_stats_partial),
+// else an explicit per-channel array (producer-fused statistics, e.g. the stem convolution).
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
-                                                          const uint16_t* __restrict__ x, int G, int C, int64_t R,
+                                                          const uint16_t* __restrict__ x,
+                                                          const float* __restrict__ kshift, int G, int C, int64_t R,
                                                           float eps, float momentum, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ rmean,
                                                           float* __restrict__ rvar, float* __restrict__ mean_out,
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   const int c = blockIdx.x * 8 + threadIdx.x;
   const float inv_n = 1.f / static_cast<float>(R);
   const float dm = s1 * inv_n;  // mean - K
-  const float mean = bf16_to_f32(x[c]) + dm;
+  const float mean = (kshift ? kshift[c] : bf16_to_f32(x[c])) + dm;
   float var = s2 * inv_n - dm * dm;
   if (var < 0.f) var = 0.f;
   const float invstd = rsqrtf(var + eps);
@@ -439,7 +442,8 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
     const int G = a.G;
     const int ctiles = (C / 8 + 255) / 256;
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(G, ctiles), dim3(256), 0, s, a.x, R, C, a.ws, a.ws + G * C);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, a.x, G, C, R, a.eps,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, a.x, nullptr, G, C, R,
+                       a.eps,
                        a.momentum, a.gamma, a.beta, a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(cblocks), dim3(256), 0, s, C, a.eps, a.gamma, a.beta, a.rmean,
@@ -464,6 +468,13 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
     else { PSAMD_BN_APPLY(false, 0); }
   }
 #undef PSAMD_BN_APPLY
+}
+
+void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
+                             float eps, float momentum, const float* gamma, const float* beta, float* rmean,
+                             float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, ps, pq, nullptr, kshift, G, C, R, eps,
+                     momentum, gamma, beta, rmean, rvar, mean, invstd, scale, shift);
 }
 
 void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {

@@ -1,0 +1,341 @@
+// ResNet stem convolution (7x7, stride 2, pad 3, 64 output channels) on NHWC bf16 input with
+// 3 or 4 channels (staged into LDS as 4-channel 8-B pixels), as MFMA implicit GEMMs.  MIOpen reaches ~140-170 TF/s on this layer (C_in = 3
+// gives it no K to tile: scripts/probe_convs.py); the whole layer is HBM-bound (output
+// 822 MB at batch 512), so the goal is to stream at the memory rate.
+//
+// Layout trick: with 4 input channels one input pixel is 8 B, so the 7 (kw) x 4 (c) patch
+// segment of an output pixel for one kernel row kh is 56 contiguous bytes at an 8-B aligned
+// LDS offset.  Packing K as k' = kh*32 + kw*4 + c (kw = 7 and c = 3 slots carry zero weight)
+// makes every MFMA A fragment (8 consecutive k') ONE aligned 16-B ds_read_b128 of the staged
+// input rows: no im2col buffer exists anywhere.
+//
+//   forward      z[p, co]   = sum_k' patch[p, k'] wp[co, k']       (M = pixels, N = 64, K = 224)
+//   weight grad  dwp[co, k'] = sum_p dz[p, co] patch[p, k']        (M = 64, N = 224, K = pixels)
+//
+// The weight-gradient kernel reads both operands transposed out of row-major LDS tiles with
+// ds_read_b64_tr_b16 (gfx950 hardware transpose read), accumulates a per-block fp32 partial,
+// and a two-level fixed-order reduction produces dW (deterministic, no atomics).
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+
+namespace {
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kRS = 1056;   // LDS input-row stride (elements): covers (2*127 + 8) * 4 for OW <= 128
+constexpr int kSlots = 16;  // input-row ring: rows 2oh-3 .. 2oh+5 (9) never collide mod 16
+constexpr int kOutLd = 72;  // LDS output-tile row stride (elements), 144 B: conflict-light C stores
+constexpr int kDzLd = 68;   // LDS dz-tile row stride (elements), 136 B (8-B aligned rows for tr reads)
+constexpr int kKp = 224;    // packed K (7 kh x 32)
+constexpr int kUnits = kRS / 4;  // 8-B pixel units per LDS input row
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(s16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// One input pixel (n, ih, iw = u - 3) as an 8-B unit of 4 channels, zero outside the image.
+// cin = 4: one 8-B load; cin = 3 (plain NHWC RGB): three 2-B loads, channel 3 = 0 -- so the
+// network input needs no padding copy.
+__device__ __forceinline__ uint2 load_unit(const uint16_t* __restrict__ x, int n, int ih, int u, int H, int W,
+                                           int cin) {
+  const int iw = u - 3;
+  if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+    const int64_t pix = (static_cast<int64_t>(n) * H + ih) * W + iw;
+    if (cin == 4) return *reinterpret_cast<const uint2*>(x + pix * 4);
+    const uint16_t* q = x + pix * 3;
+    return make_uint2(q[0] | (uint32_t(q[1]) << 16), q[2]);
+  }
+  return make_uint2(0u, 0u);
+}
+
+// Register prefetch of the two input rows a block needs next (rows ih0, ih0 + 1): 2 * kUnits
+// units over 256 threads = 3 loads per thread, all issued before any is consumed.
+struct RowPrefetch {
+  uint2 v[3];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ x, int n, int ih0, int H, int W, int cin) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = threadIdx.x + k * 256;
+      v[k] = make_uint2(0u, 0u);
+      if (i < 2 * kUnits) v[k] = load_unit(x, n, ih0 + (i >= kUnits), i % kUnits, H, W, cin);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* lds_in, int ih0) const {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < 2 * kUnits) {
+        const int ih = ih0 + (i >= kUnits);
+        *reinterpret_cast<uint2*>(lds_in + (ih & (kSlots - 1)) * kRS + (i % kUnits) * 4) = v[k];
+      }
+    }
+  }
+};
+
+// Prologue: input rows 2*oh - 3 .. 2*oh + 3 into their ring slots (loads batched 8 per thread).
+__device__ __forceinline__ void stage_window(const uint16_t* __restrict__ x, uint16_t* lds_in, int n, int oh, int H,
+                                             int W, int cin) {
+  uint2 v[8];
+  const int ih0 = 2 * oh - 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = threadIdx.x + k * 256;
+    v[k] = make_uint2(0u, 0u);
+    if (i < 7 * kUnits) v[k] = load_unit(x, n, ih0 + i / kUnits, i % kUnits, H, W, cin);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = threadIdx.x + k * 256;
+    if (i < 7 * kUnits) {
+      const int ih = ih0 + i / kUnits;
+      *reinterpret_cast<uint2*>(lds_in + (ih & (kSlots - 1)) * kRS + (i % kUnits) * 4) = v[k];
+    }
+  }
+}
+}  // namespace
+
+// grid = N * splits blocks; block b: image b / splits, output rows [chunk*rpb, +rpb).
+// wp: [64][224] packed bf16.  Input rows slide through an LDS ring (2 new rows per output row,
+// prefetched into registers while the current row computes).
+__global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ wp,
+                                                            uint16_t* __restrict__ z, int N, int H, int W, int OH,
+                                                            int OW, int splits, int rpb, int cin,
+                                                            const float* __restrict__ kshift,
+                                                            float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 128 * kOutLd];
+  __shared__ float lds_red[2 * 256];
+  uint16_t* lds_in = lds;
+  uint16_t* lds_out = lds + kSlots * kRS;
+  const int n = blockIdx.x / splits, chunk = blockIdx.x - n * splits;
+  const int oh0 = chunk * rpb, oh1 = min(OH, oh0 + rpb);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  // fused BN statistics: thread t owns channel t & 63, output pixels (t >> 6) + 4i of each row
+  const int sc = threadIdx.x & 63, sq = threadIdx.x >> 6;
+  const float ks = part ? kshift[sc] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  // B fragments for all 4 N-tiles x 7 k-steps (held for the whole block)
+  bf16x8_t bw[4][7];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+      bw[nt][kh] = *reinterpret_cast<const bf16x8_t*>(wp + (16 * nt + fr) * kKp + kh * 32 + 8 * g);
+  if (oh0 < oh1) stage_window(x, lds_in, n, oh0, H, W, cin);  // block-uniform
+  __syncthreads();
+  const int mtiles = (OW + 15) / 16;
+  for (int oh = oh0; oh < oh1; ++oh) {
+    RowPrefetch pf;
+    const bool more = oh + 1 < oh1;
+    if (more) pf.load(x, n, 2 * oh + 4, H, W, cin);
+    for (int mi = wave; mi < mtiles; mi += 4) {
+      f32x4v acc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      const int ow = 16 * mi + fr;  // >= OW rows read finite staged data and are never stored
+#pragma unroll
+      for (int kh = 0; kh < 7; ++kh) {
+        const int slot = (2 * oh - 3 + kh) & (kSlots - 1);
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(lds_in + slot * kRS + 8 * ow + 8 * g);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[nt][kh], acc[nt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds_out[(16 * mi + 4 * g + r) * kOutLd + 16 * nt + fr] = f32_to_bf16(acc[nt][r]);
+    }
+    __syncthreads();
+    // the output row is OW * 64 contiguous bf16 in NHWC: 16-B chunks
+    uint16_t* zo = z + (static_cast<int64_t>(n) * OH + oh) * OW * 64;
+    for (int c = threadIdx.x; c < OW * 8; c += blockDim.x) {
+      const int row = c >> 3, ch = c & 7;
+      *reinterpret_cast<u16x8*>(zo + row * 64 + ch * 8) =
+          *reinterpret_cast<const u16x8*>(lds_out + row * kOutLd + ch * 8);
+    }
+    if (part) {  // statistics of the bf16 values the next layer reads
+      for (int px = sq; px < OW; px += 4) {
+        const float d = bf16_to_f32(lds_out[px * kOutLd + sc]) - ks;
+        s1 += d;
+        s2 += d * d;
+      }
+    }
+    if (more) pf.store(lds_in, 2 * oh + 4);  // slots of rows 2oh+4, 2oh+5: not read by row oh
+    __syncthreads();
+  }
+  if (part) {  // fixed-order combine of the 4 pixel phases -> part[0 | 1][block][channel]
+    lds_red[threadIdx.x] = s1;
+    lds_red[256 + threadIdx.x] = s2;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const float a = (lds_red[sc] + lds_red[64 + sc]) + (lds_red[128 + sc] + lds_red[192 + sc]);
+      const float b = (lds_red[256 + sc] + lds_red[320 + sc]) + (lds_red[384 + sc] + lds_red[448 + sc]);
+      part[static_cast<int64_t>(blockIdx.x) * 64 + sc] = a;
+      part[(static_cast<int64_t>(gridDim.x) + blockIdx.x) * 64 + sc] = b;
+    }
+  }
+}
+
+// dz row -> LDS [128 pixels][kDzLd] (pixels >= OW zero): 4 x 16-B loads per thread.
+struct DzPrefetch {
+  u16x8 v[4];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ dzr, int OW) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = threadIdx.x + k * 256, pix = c >> 3, ch = c & 7;
+      v[k] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (pix < OW) v[k] = *reinterpret_cast<const u16x8*>(dzr + pix * 64 + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* lds_dz) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = threadIdx.x + k * 256, pix = c >> 3, ch = c & 7;
+      uint16_t* d = lds_dz + pix * kDzLd + ch * 8;  // 136-B rows: 8-B aligned stores
+      const u16x8 u = v[k];
+      *reinterpret_cast<uint2*>(d) = make_uint2(u[0] | (uint32_t(u[1]) << 16), u[2] | (uint32_t(u[3]) << 16));
+      *reinterpret_cast<uint2*>(d + 4) = make_uint2(u[4] | (uint32_t(u[5]) << 16), u[6] | (uint32_t(u[7]) << 16));
+    }
+  }
+};
+
+// grid = N * splits blocks (as the forward); each accumulates its output rows into
+// part[b][64][224] (fp32).
+__global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ dz,
+                                                            float* __restrict__ part, int N, int H, int W, int OH,
+                                                            int OW, int splits, int rpb, int cin) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 2 * 128 * kDzLd];
+  uint16_t* lds_in = lds;
+  const int n = blockIdx.x / splits, chunk = blockIdx.x - n * splits;
+  const int oh0 = chunk * rpb, oh1 = min(OH, oh0 + rpb);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  // this wave's N-tiles (16 packed-k' columns each): w, w+4, w+8, w+12 (< 14)
+  const int nnt = wave < 2 ? 4 : 3;
+  f32x4v acc[4][4];  // [mt][j]
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[mt][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  if (oh0 < oh1) {  // block-uniform
+    stage_window(x, lds_in, n, oh0, H, W, cin);
+    {
+      DzPrefetch d0;
+      d0.load(dz + (static_cast<int64_t>(n) * OH + oh0) * OW * 64, OW);
+      d0.store(lds + kSlots * kRS);
+    }
+    __syncthreads();
+    for (int oh = oh0; oh < oh1; ++oh) {
+      const bool more = oh + 1 < oh1;
+      RowPrefetch pf;
+      DzPrefetch pd;
+      if (more) {
+        pf.load(x, n, 2 * oh + 4, H, W, cin);
+        pd.load(dz + (static_cast<int64_t>(n) * OH + oh + 1) * OW * 64, OW);
+      }
+      const uint16_t* lds_dz = lds + kSlots * kRS + ((oh - oh0) & 1) * 128 * kDzLd;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int pix0 = 32 * s + 8 * g + q;  // tr-read row of this lane (and +4 for the second half)
+        bf16x8_t a[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(lds_dz + pix0 * kDzLd + 16 * mt + 4 * p));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4*)(lds_dz + (pix0 + 4) * kDzLd + 16 * mt + 4 * p));
+          a[mt] = as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j < nnt) {  // wave-uniform
+            const int kp = 16 * (wave + 4 * j) + 4 * p;  // packed k' of this lane's 4 columns
+            const int kh = kp >> 5, kw = (kp & 31) >> 2;
+            const uint16_t* base = lds_in + ((2 * oh - 3 + kh) & (kSlots - 1)) * kRS + kw * 4;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 8 * pix0));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 8 * (pix0 + 4)));
+            const bf16x8_t b = as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+              acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b, acc[mt][j], 0, 0, 0);
+          }
+        }
+      }
+      if (more) {
+        pf.store(lds_in, 2 * oh + 4);
+        pd.store(lds + kSlots * kRS + ((oh + 1 - oh0) & 1) * 128 * kDzLd);
+      }
+      __syncthreads();
+    }
+  }
+  // C layout: row (co) = 16*mt + 4*g + r, col (k') = 16*nt + (lane & 15)
+  float* pb = part + static_cast<int64_t>(blockIdx.x) * 64 * kKp;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < nnt) {
+      const int col = 16 * (wave + 4 * j) + i16;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[(16 * mt + 4 * g + r) * kKp + col] = acc[mt][j][r];
+    }
+  }
+}
+
+// out[e] = sum_{b in group y} part[b][e]; fixed order.  grid (ceil(E/256), groups)
+__global__ __launch_bounds__(256) void stem_wrw_reduce_kernel(const float* __restrict__ part, int nblk, int per,
+                                                              float* __restrict__ out) {
+  constexpr int E = 64 * kKp;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = b0;
+  for (; b + 3 < b1; b += 4) {
+    s0 += part[static_cast<int64_t>(b) * E + e];
+    s1 += part[static_cast<int64_t>(b + 1) * E + e];
+    s2 += part[static_cast<int64_t>(b + 2) * E + e];
+    s3 += part[static_cast<int64_t>(b + 3) * E + e];
+  }
+  for (; b < b1; ++b) s0 += part[static_cast<int64_t>(b) * E + e];
+  out[static_cast<int64_t>(blockIdx.y) * E + e] = (s0 + s1) + (s2 + s3);
+}
+
+namespace {
+constexpr int kFwdSplits = 4;  // blocks per image (forward): N*4 blocks, ~28 rows each at OH = 112
+constexpr int kWrwSplits = 2;  // blocks per image (weight grad): fewer fp32 partials to reduce
+}  // namespace
+
+int stem_fwd_blocks(int N) { return N * kFwdSplits; }
+
+void launch_stem_conv_fwd(const uint16_t* x, int cin, const uint16_t* wp, uint16_t* z, int N, int H, int W, int OH,
+                          int OW, const float* kshift, float* part, hipStream_t s) {
+  if (N <= 0 || OH <= 0) return;
+  const int rpb = (OH + kFwdSplits - 1) / kFwdSplits;
+  hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(N * kFwdSplits), dim3(256), 0, s, x, wp, z, N, H, W, OH, OW,
+                     kFwdSplits, rpb, cin, kshift, part);
+}
+
+int stem_wrw_blocks(int N, int OH) { return N * kWrwSplits; }
+
+// ws: [nblk * 64 * 224 + 32 * 64 * 224] floats; dwp: [64 * 224] floats
+void launch_stem_conv_wrw(const uint16_t* x, int cin, const uint16_t* dz, float* ws, float* dwp, int N, int H, int W,
+                          int OH, int OW, hipStream_t s) {
+  if (N <= 0 || OH <= 0) return;
+  const int nblk = stem_wrw_blocks(N, OH);
+  const int rpb = (OH + kWrwSplits - 1) / kWrwSplits;
+  hipLaunchKernelGGL(stem_conv_wrw_kernel, dim3(nblk), dim3(256), 0, s, x, dz, ws, N, H, W, OH, OW, kWrwSplits, rpb, cin);
+  constexpr int E = 64 * kKp;
+  const int groups = 32;
+  const int per = (nblk + groups - 1) / groups;
+  float* mid = ws + static_cast<int64_t>(nblk) * E;
+  hipLaunchKernelGGL(stem_wrw_reduce_kernel, dim3(E / 256, groups), dim3(256), 0, s, ws, nblk, per, mid);
+  hipLaunchKernelGGL(stem_wrw_reduce_kernel, dim3(E / 256, 1), dim3(256), 0, s, mid, groups, groups, dwp);
+}
+
+}  // namespace psamd

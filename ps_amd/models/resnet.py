@@ -15,8 +15,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1
-from ..ops.pool import MaxPool2d, bn_relu_maxpool
+from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
+from ..ops.pool import MaxPool2d
 
 
 class Bottleneck(nn.Module):
@@ -57,7 +57,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.fused_bn = fused_bn
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.conv1 = StemConv(3) if fused_bn else nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(64) if fused_bn else nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = (MaxPool2d if fused_bn else nn.MaxPool2d)(3, stride=2, padding=1)
@@ -91,7 +91,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         if self.fused_bn:  # stem BN + ReLU fused into the pool: the BN output never hits HBM
-            x = bn_relu_maxpool(self.conv1(x), self.bn1, 3, 2, 1)
+            x = stem_bn_relu_maxpool(x, self.conv1, self.bn1)
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

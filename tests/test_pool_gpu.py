@@ -70,3 +70,54 @@ def test_conv1x1_routed_matches_conv2d(ci, co, h):
     torch.testing.assert_close(xh.grad.float(), xr.grad, rtol=2e-2, atol=5e-2)
     cos = torch.nn.functional.cosine_similarity
     assert cos(m.weight.grad.float().flatten(), ref.weight.grad.flatten(), dim=0) > 0.999
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 30, 46), (1, 17, 9), (2, 256, 256)])
+@pytest.mark.parametrize("cin", [3, 4])
+def test_stem_conv_fwd_wgrad(N, H, W, cin):
+    from ps_amd.ops.conv import StemConv
+
+    torch.manual_seed(0)
+    m = StemConv(cin).cuda().bfloat16().to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(cin, 64, 7, 2, 3, bias=False).cuda()
+    ref.weight.data.copy_(m.weight.float())
+    x = torch.randn(N, cin, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = m(x)
+    yr = ref(x.float())
+    assert y.shape == yr.shape
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    g = torch.randn_like(yr).bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, rtol=2e-2, atol=2e-2 * ref.weight.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("N,H", [(4, 64), (2, 224)])
+def test_stem_fused_block_matches_unfused(N, H):
+    from ps_amd.ops.conv import StemConv, stem_bn_relu_maxpool
+
+    torch.manual_seed(0)
+    conv = StemConv(3).cuda().bfloat16().to(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)  # the partial-sum shift; must not affect the result
+    rconv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda()
+    rconv.weight.data.copy_(conv.weight.float())
+    rbn = torch.nn.BatchNorm2d(64).cuda()
+    rbn.load_state_dict({k: v for k, v in bn.state_dict().items()})
+    x = (torch.randn(N, 3, H, H, device="cuda") + 3.0).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = stem_bn_relu_maxpool(x, conv, bn)
+    yr = F.max_pool2d(torch.relu(rbn(rconv(x.float()))), 3, 2, 1)
+    rel = ((y.float() - yr).norm() / yr.norm()).item()
+    assert rel < 1e-2, rel
+    torch.testing.assert_close(bn.running_mean, rbn.running_mean, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.running_var, rbn.running_var, rtol=1e-2, atol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    cos = torch.nn.functional.cosine_similarity
+    for a, b in ((conv.weight.grad, rconv.weight.grad), (bn.weight.grad, rbn.weight.grad),
+                 (bn.bias.grad, rbn.bias.grad)):
+        assert cos(a.float().flatten(), b.flatten(), dim=0) > 0.99
