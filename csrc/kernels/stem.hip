@@ -28,154 +28,228 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kRS = 1056;   // LDS input-row stride (elements): covers (2*127 + 8) * 4 for OW <= 128
 constexpr int kSlots = 16;  // input-row ring: rows 2oh-3 .. 2oh+5 (9) never collide mod 16
-constexpr int kOutLd = 72;  // LDS output-tile row stride (elements), 144 B: conflict-light C stores
 constexpr int kDzLd = 68;   // LDS dz-tile row stride (elements), 136 B (8-B aligned rows for tr reads)
 constexpr int kKp = 224;    // packed K (7 kh x 32)
 constexpr int kUnits = kRS / 4;  // 8-B pixel units per LDS input row
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(s16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
-// One input pixel (n, ih, iw = u - 3) as an 8-B unit of 4 channels, zero outside the image.
-// cin = 4: one 8-B load; cin = 3 (plain NHWC RGB): three 2-B loads, channel 3 = 0 -- so the
-// network input needs no padding copy.
-__device__ __forceinline__ uint2 load_unit(const uint16_t* __restrict__ x, int n, int ih, int u, int H, int W,
-                                           int cin) {
-  const int iw = u - 3;
-  if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-    const int64_t pix = (static_cast<int64_t>(n) * H + ih) * W + iw;
-    if (cin == 4) return *reinterpret_cast<const uint2*>(x + pix * 4);
-    const uint16_t* q = x + pix * 3;
-    return make_uint2(q[0] | (uint32_t(q[1]) << 16), q[2]);
-  }
-  return make_uint2(0u, 0u);
+// Workgroup barrier for LDS hand-offs only: __syncthreads()'s release fence also drains vmcnt,
+// i.e. waits for every outstanding global STORE of the wave (CDNA4 counts stores in vmcnt) --
+// a per-row stall of the output stream in the forward kernel.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-// Register prefetch of the two input rows a block needs next (rows ih0, ih0 + 1): 2 * kUnits
-// units over 256 threads = 3 loads per thread, all issued before any is consumed.
+// Input pixel PAIRS (iw0 = 2j - 4, iw0 + 1) of row ih as two 8-B units of 4 channels (zero
+// outside the image): LDS units u = iw + 3, so pair j covers units 2j - 1 and 2j.
+// cin = 4: one 16-B load; cin = 3 (plain NHWC RGB, no padding copy): one 12-B load when the
+// pair is 4-B aligned, else 2-B loads.
+constexpr int kPairs = kUnits / 2 + 1;
+
+__device__ __forceinline__ uint4 load_pair(const uint16_t* __restrict__ x, int n, int ih, int j, int H, int W,
+                                           int cin) {
+  const int iw0 = 2 * j - 4;
+  if ((W & 1) == 0) {
+    // even W: a pair is wholly inside or outside the image, and 3-channel pairs are 4-B aligned.
+    // Branch-free (clamped address + select), so unrolled loads stay in flight together instead
+    // of draining vmcnt at every divergent join.
+    const bool ok = ih >= 0 && ih < H && iw0 >= 0 && iw0 < W;
+    const int64_t pix = ok ? (static_cast<int64_t>(n) * H + ih) * W + iw0 : 0;
+    if (cin == 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + pix * 4);
+      return ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint3 d = *reinterpret_cast<const uint3*>(x + pix * 3);  // c0 c1 | c2 c0' | c1' c2'
+    return ok ? make_uint4(d.x, d.y & 0xffffu, (d.y >> 16) | (d.z << 16), d.z >> 16) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);  // odd W: guarded per-pixel path
+  if (ih < 0 || ih >= H || iw0 + 1 < 0 || iw0 >= W) return r;
+  const int64_t pix = (static_cast<int64_t>(n) * H + ih) * W + iw0;
+  if (cin == 4) {
+    if (iw0 >= 0) {
+      const uint2 a = *reinterpret_cast<const uint2*>(x + pix * 4);
+      r.x = a.x, r.y = a.y;
+    }
+    if (iw0 + 1 < W) {
+      const uint2 b = *reinterpret_cast<const uint2*>(x + (pix + 1) * 4);
+      r.z = b.x, r.w = b.y;
+    }
+    return r;
+  }
+  const uint16_t* q = x + pix * 3;
+  if (iw0 >= 0) r.x = q[0] | (uint32_t(q[1]) << 16), r.y = q[2];
+  if (iw0 + 1 < W) r.z = q[3] | (uint32_t(q[4]) << 16), r.w = q[5];
+  return r;
+}
+
+__device__ __forceinline__ void store_pair(uint16_t* lds_in, int ih, int j, uint4 v) {
+  uint16_t* row = lds_in + (ih & (kSlots - 1)) * kRS;
+  const int u0 = 2 * j - 1;
+  if (u0 >= 0) *reinterpret_cast<uint2*>(row + u0 * 4) = make_uint2(v.x, v.y);
+  if (u0 + 1 < kUnits) *reinterpret_cast<uint2*>(row + (u0 + 1) * 4) = make_uint2(v.z, v.w);
+}
+
+// Register prefetch of the two input rows a block needs next (rows ih0, ih0 + 1): 2 * kPairs
+// pairs over NT threads (lane index t), all loads issued before any is consumed.
+template <int NT>
 struct RowPrefetch {
-  uint2 v[3];
-  __device__ __forceinline__ void load(const uint16_t* __restrict__ x, int n, int ih0, int H, int W, int cin) {
+  static constexpr int kIt = (2 * kPairs + NT - 1) / NT;
+  uint4 v[kIt];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ x, int t, int n, int ih0, int H, int W, int cin) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int i = threadIdx.x + k * 256;
-      v[k] = make_uint2(0u, 0u);
-      if (i < 2 * kUnits) v[k] = load_unit(x, n, ih0 + (i >= kUnits), i % kUnits, H, W, cin);
+    for (int k = 0; k < kIt; ++k) {
+      const int i = t + k * NT;
+      v[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < 2 * kPairs) v[k] = load_pair(x, n, ih0 + (i >= kPairs), i % kPairs, H, W, cin);
     }
   }
-  __device__ __forceinline__ void store(uint16_t* lds_in, int ih0) const {
+  __device__ __forceinline__ void store(uint16_t* lds_in, int t, int ih0) const {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int i = threadIdx.x + k * 256;
-      if (i < 2 * kUnits) {
-        const int ih = ih0 + (i >= kUnits);
-        *reinterpret_cast<uint2*>(lds_in + (ih & (kSlots - 1)) * kRS + (i % kUnits) * 4) = v[k];
-      }
+    for (int k = 0; k < kIt; ++k) {
+      const int i = t + k * NT;
+      if (i < 2 * kPairs) store_pair(lds_in, ih0 + (i >= kPairs), i % kPairs, v[k]);
     }
   }
 };
 
-// Prologue: input rows 2*oh - 3 .. 2*oh + 3 into their ring slots (loads batched 8 per thread).
+// Prologue: input rows 2*oh - 3 .. 2*oh + 3 into their ring slots (loads batched per thread).
 __device__ __forceinline__ void stage_window(const uint16_t* __restrict__ x, uint16_t* lds_in, int n, int oh, int H,
                                              int W, int cin) {
-  uint2 v[8];
+  constexpr int kIt = (7 * kPairs + 255) / 256;  // blockDim >= 256
+  uint4 v[kIt];
   const int ih0 = 2 * oh - 3;
+  const int nt = blockDim.x;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = threadIdx.x + k * 256;
-    v[k] = make_uint2(0u, 0u);
-    if (i < 7 * kUnits) v[k] = load_unit(x, n, ih0 + i / kUnits, i % kUnits, H, W, cin);
+  for (int k = 0; k < kIt; ++k) {
+    const int i = threadIdx.x + k * nt;
+    v[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < 7 * kPairs) v[k] = load_pair(x, n, ih0 + i / kPairs, i % kPairs, H, W, cin);
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = threadIdx.x + k * 256;
-    if (i < 7 * kUnits) {
-      const int ih = ih0 + i / kUnits;
-      *reinterpret_cast<uint2*>(lds_in + (ih & (kSlots - 1)) * kRS + (i % kUnits) * 4) = v[k];
-    }
+  for (int k = 0; k < kIt; ++k) {
+    const int i = threadIdx.x + k * nt;
+    if (i < 7 * kPairs) store_pair(lds_in, ih0 + i / kPairs, i % kPairs, v[k]);
   }
 }
 }  // namespace
 
-// grid = N * splits blocks; block b: image b / splits, output rows [chunk*rpb, +rpb).
-// wp: [64][224] packed bf16.  Input rows slide through an LDS ring (2 new rows per output row,
-// prefetched into registers while the current row computes).
+// grid = N * splits blocks of 256 threads; block b: image b / splits, output rows
+// [chunk*rpb, +rpb).  wp: [64][224] packed bf16.  Input rows slide through an LDS ring (2 new
+// rows per output row).  Per row: issue the next row's input loads, run all MFMAs into
+// registers, publish the prefetched rows to LDS, THEN issue this row's output stores and pass
+// an LDS-only barrier -- CDNA4's vmcnt counts stores too, so waiting for the prefetch before
+// the stores are issued keeps the output stream from being drained every row.
 __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ wp,
                                                             uint16_t* __restrict__ z, int N, int H, int W, int OH,
                                                             int OW, int splits, int rpb, int cin,
                                                             const float* __restrict__ kshift,
                                                             float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 128 * kOutLd];
-  __shared__ float lds_red[2 * 256];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 1024];
   uint16_t* lds_in = lds;
-  uint16_t* lds_out = lds + kSlots * kRS;
+  uint16_t* lds_red = lds + kSlots * kRS;  // 512 floats for the statistics combine
   const int n = blockIdx.x / splits, chunk = blockIdx.x - n * splits;
   const int oh0 = chunk * rpb, oh1 = min(OH, oh0 + rpb);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  // fused BN statistics: thread t owns channel t & 63, output pixels (t >> 6) + 4i of each row
-  const int sc = threadIdx.x & 63, sq = threadIdx.x >> 6;
-  const float ks = part ? kshift[sc] : 0.f;
-  float s1 = 0.f, s2 = 0.f;
-  // B fragments for all 4 N-tiles x 7 k-steps (held for the whole block)
-  bf16x8_t bw[4][7];
+  // 2 x 2 wave grid: wave (wm, wn) computes M-tiles wm, wm+2, wm+4, wm+6 and N-tiles 2wn, 2wn+1
+  const int wm = wave & 1, wn = wave >> 1;
+  // fused BN statistics from the accumulators: the lane keeps channels 32*wn + 16*j + 4*g + r of
+  // its pixels; combined across the 16 pixel lanes and the 2 M-waves at the end
+  float s1[2][4], s2[2][4], ks[2][4];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[j][r] = s2[j][r] = 0.f;
+      ks[j][r] = part ? kshift[32 * wn + 16 * j + 4 * g + r] : 0.f;
+    }
+  bf16x8_t bw[2][7];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int kh = 0; kh < 7; ++kh)
-      bw[nt][kh] = *reinterpret_cast<const bf16x8_t*>(wp + (16 * nt + fr) * kKp + kh * 32 + 8 * g);
+      bw[j][kh] = *reinterpret_cast<const bf16x8_t*>(wp + (32 * wn + 16 * j + fr) * kKp + kh * 32 + 8 * g);
   if (oh0 < oh1) stage_window(x, lds_in, n, oh0, H, W, cin);  // block-uniform
   __syncthreads();
-  const int mtiles = (OW + 15) / 16;
+  const int mtiles = (OW + 15) / 16;  // <= 8
   for (int oh = oh0; oh < oh1; ++oh) {
-    RowPrefetch pf;
+    RowPrefetch<256> pf;
     const bool more = oh + 1 < oh1;
-    if (more) pf.load(x, n, 2 * oh + 4, H, W, cin);
-    for (int mi = wave; mi < mtiles; mi += 4) {
-      f32x4v acc[4];
+    if (more) pf.load(x, threadIdx.x, n, 2 * oh + 4, H, W, cin);
+    f32x4v acc[4][2];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      const int ow = 16 * mi + fr;  // >= OW rows read finite staged data and are never stored
+    for (int t = 0; t < 4; ++t) {
+      acc[t][0] = acc[t][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      const int mi = wm + 2 * t;
+      if (mi < mtiles) {  // wave-uniform
+        const int ow = 16 * mi + fr;  // pixels >= OW read finite staged data and are never stored
 #pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        const int slot = (2 * oh - 3 + kh) & (kSlots - 1);
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(lds_in + slot * kRS + 8 * ow + 8 * g);
+        for (int kh = 0; kh < 7; ++kh) {
+          const int slot = (2 * oh - 3 + kh) & (kSlots - 1);
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(lds_in + slot * kRS + 8 * ow + 8 * g);
+          // D[co][pixel] = W . patch^T: the lane ends up with 4 consecutive channels of one pixel
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[nt][kh], acc[nt], 0, 0, 0);
+          for (int j = 0; j < 2; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], a, acc[t][j], 0, 0, 0);
+        }
       }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) lds_out[(16 * mi + 4 * g + r) * kOutLd + 16 * nt + fr] = f32_to_bf16(acc[nt][r]);
     }
-    __syncthreads();
-    // the output row is OW * 64 contiguous bf16 in NHWC: 16-B chunks
+    if (more) pf.store(lds_in, threadIdx.x, 2 * oh + 4);  // ring slots not read by rows oh-1, oh
     uint16_t* zo = z + (static_cast<int64_t>(n) * OH + oh) * OW * 64;
-    for (int c = threadIdx.x; c < OW * 8; c += blockDim.x) {
-      const int row = c >> 3, ch = c & 7;
-      *reinterpret_cast<u16x8*>(zo + row * 64 + ch * 8) =
-          *reinterpret_cast<const u16x8*>(lds_out + row * kOutLd + ch * 8);
-    }
-    if (part) {  // statistics of the bf16 values the next layer reads
-      for (int px = sq; px < OW; px += 4) {
-        const float d = bf16_to_f32(lds_out[px * kOutLd + sc]) - ks;
-        s1 += d;
-        s2 += d * d;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ow = 16 * (wm + 2 * t) + fr;
+      if (ow < OW) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          // C layout: row (channel) = 16*nt + 4*g + r, col (pixel) = fr -> one 8-B store per tile
+          uint16_t h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = f32_to_bf16(acc[t][j][r]);
+            if (part) {  // statistics of the bf16 values stored
+              const float d = bf16_to_f32(h[r]) - ks[j][r];
+              s1[j][r] += d;
+              s2[j][r] += d * d;
+            }
+          }
+          *reinterpret_cast<uint2*>(zo + ow * 64 + 32 * wn + 16 * j + 4 * g) =
+              make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+        }
       }
     }
-    if (more) pf.store(lds_in, 2 * oh + 4);  // slots of rows 2oh+4, 2oh+5: not read by row oh
-    __syncthreads();
+    lds_barrier();
   }
-  if (part) {  // fixed-order combine of the 4 pixel phases -> part[0 | 1][block][channel]
-    lds_red[threadIdx.x] = s1;
-    lds_red[256 + threadIdx.x] = s2;
+  if (part) {  // fixed-order combine: the 16 pixel lanes (xor shuffles), then the 2 M-waves
+    float* red = reinterpret_cast<float*>(lds_red);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          s1[j][r] += __shfl_xor(s1[j][r], off, 64);
+          s2[j][r] += __shfl_xor(s2[j][r], off, 64);
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 32 * wn + 16 * j + 4 * g + r;
+          red[wm * 64 + c] = s1[j][r];
+          red[128 + wm * 64 + c] = s2[j][r];
+        }
+    }
     __syncthreads();
     if (threadIdx.x < 64) {
-      const float a = (lds_red[sc] + lds_red[64 + sc]) + (lds_red[128 + sc] + lds_red[192 + sc]);
-      const float b = (lds_red[256 + sc] + lds_red[320 + sc]) + (lds_red[384 + sc] + lds_red[448 + sc]);
-      part[static_cast<int64_t>(blockIdx.x) * 64 + sc] = a;
-      part[(static_cast<int64_t>(gridDim.x) + blockIdx.x) * 64 + sc] = b;
+      const int c = threadIdx.x;
+      part[static_cast<int64_t>(blockIdx.x) * 64 + c] = red[c] + red[64 + c];
+      part[(static_cast<int64_t>(gridDim.x) + blockIdx.x) * 64 + c] = red[128 + c] + red[192 + c];
     }
   }
 }
@@ -232,10 +306,10 @@ __global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __re
     __syncthreads();
     for (int oh = oh0; oh < oh1; ++oh) {
       const bool more = oh + 1 < oh1;
-      RowPrefetch pf;
+      RowPrefetch<256> pf;
       DzPrefetch pd;
       if (more) {
-        pf.load(x, n, 2 * oh + 4, H, W, cin);
+        pf.load(x, threadIdx.x, n, 2 * oh + 4, H, W, cin);
         pd.load(dz + (static_cast<int64_t>(n) * OH + oh + 1) * OW * 64, OW);
       }
       const uint16_t* lds_dz = lds + kSlots * kRS + ((oh - oh0) & 1) * 128 * kDzLd;
@@ -267,7 +341,7 @@ __global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __re
         }
       }
       if (more) {
-        pf.store(lds_in, 2 * oh + 4);
+        pf.store(lds_in, threadIdx.x, 2 * oh + 4);
         pd.store(lds + kSlots * kRS + ((oh + 1 - oh0) & 1) * 128 * kDzLd);
       }
       __syncthreads();
