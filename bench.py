@@ -176,7 +176,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,  # the reference publishes no throughput number
-            "dtype": "bf16" if args.config != "dlrm" else "fp32",
+            "dtype": "bf16",
             "data": "synthetic (GPU-resident batches of the named shape); random-init weights",
             "config": cfg,
         }

@@ -462,6 +462,44 @@ std::vector<Tensor> bn_stats(Tensor x, c10::optional<Tensor> gamma, c10::optiona
   return {r[1], r[2], r[3]};
 }
 
+// ------------------------------------------------------------------------------ DLRM interaction
+static void check_interact(const Tensor& x, const Tensor& e) {
+  check_gpu(x, "x");
+  check_gpu(e, "e");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && e.scalar_type() == torch::kBFloat16, "bf16 x/e");
+  TORCH_CHECK(x.dim() == 2 && e.dim() == 3 && e.size(0) == x.size(0) && e.size(2) == x.size(1), "x [B,D], e [B,T,D]");
+  TORCH_CHECK(x.is_contiguous() && e.is_contiguous(), "contiguous x/e");
+  TORCH_CHECK(e.size(1) + 1 <= 32 && x.size(1) % 32 == 0 && x.size(1) <= 224, "n = T+1 <= 32, D % 32 == 0, D <= 224");
+}
+
+Tensor dlrm_interact_fwd(Tensor x, Tensor e) {
+  check_interact(x, e);
+  const int64_t B = x.size(0), D = x.size(1), T = e.size(1), n = T + 1;
+  const c10::DeviceGuard guard(x.device());
+  auto out = torch::empty({B, D + n * (n - 1) / 2}, x.options());
+  psamd::launch_dlrm_interact_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(e.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(out.data_ptr()), B, T, D, cur_stream(x));
+  return out;
+}
+
+std::vector<Tensor> dlrm_interact_bwd(Tensor x, Tensor e, Tensor dout) {
+  check_interact(x, e);
+  const int64_t B = x.size(0), D = x.size(1), T = e.size(1), n = T + 1;
+  check_gpu(dout, "dout");
+  TORCH_CHECK(dout.scalar_type() == torch::kBFloat16 && dout.is_contiguous() && dout.dim() == 2 &&
+                  dout.size(0) == B && dout.size(1) == D + n * (n - 1) / 2, "dout [B, D + n(n-1)/2] bf16");
+  const c10::DeviceGuard guard(x.device());
+  auto dx = torch::empty_like(x);
+  auto de = torch::empty_like(e);
+  psamd::launch_dlrm_interact_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(e.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(dout.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(dx.data_ptr()), reinterpret_cast<uint16_t*>(de.data_ptr()),
+                                  B, T, D, cur_stream(x));
+  return {dx, de};
+}
+
 // ------------------------------------------------------------------------------ ResNet stem conv
 static void check_stem(const Tensor& x) {
   check_gpu(x, "x");
@@ -696,6 +734,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_fwd", &stem_conv_fwd, py::arg("x"), py::arg("wp"), py::arg("kshift") = py::none());
   m.def("bn_finalize_sums", &bn_finalize_sums);
   m.def("stem_conv_wrw", &stem_conv_wrw);
+  m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
+  m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),

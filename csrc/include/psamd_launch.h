@@ -176,5 +176,10 @@ void launch_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int6
                          int64_t ldc, int M, int N, int K, float alpha, int accumulate, const float* bias, int act,
                          hipStream_t s);
 void launch_act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t n, int act, hipStream_t s);
+// DLRM dot interaction: out [B, D + n(n-1)/2] = [x | triu(z z^T)], z = [x; e[b]] (n = T+1 <= 32, D % 32 == 0)
+void launch_dlrm_interact_fwd(const uint16_t* x, const uint16_t* e, uint16_t* out, int B, int T, int D,
+                              hipStream_t s);
+void launch_dlrm_interact_bwd(const uint16_t* x, const uint16_t* e, const uint16_t* dout, uint16_t* dx, uint16_t* de,
+                              int B, int T, int D, hipStream_t s);
 
 }  // namespace psamd

@@ -172,4 +172,120 @@ void launch_act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, int64_t
   hipLaunchKernelGGL(act_bwd_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, s, dy, y, dz, n, act);
 }
 
+
+
+// ------------------------------------------------------------------------------ DLRM interaction
+// out[b] = [ x[b] | triu_{i<j}( z_i . z_j ) ] with z = [x[b]; e[b, 0..T)] (n = T + 1 <= 32
+// vectors of D bf16), i.e. torch.cat + bmm + triu gather + cat in ONE pass: one wave per sample,
+// Z = z z^T on v_mfma_f32_32x32x16_bf16 (the A and B fragments of z z^T are the same registers),
+// only the n(n-1)/2 upper-triangle dots are written.  Backward: dz = (G + G^T) z, G the
+// scattered triangle gradient, as a second 32x32 MFMA product per sample; dx adds the
+// pass-through gradient.  SURVEY K16 (dense.hip, "DLRM interaction").
+namespace {
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int tri_index(int i, int j, int n) { return i * (2 * n - i - 1) / 2 + (j - i - 1); }
+}  // namespace
+
+__global__ __launch_bounds__(256) void dlrm_interact_fwd_kernel(const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ e,
+                                                                uint16_t* __restrict__ out, int B, int T, int D) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // wave-uniform; no block barriers below
+  const int n = T + 1, P = n * (n - 1) / 2;
+  const int r = lane & 31, h = lane >> 5;
+  const uint16_t* row = r == 0 ? x + static_cast<int64_t>(b) * D
+                               : e + (static_cast<int64_t>(b) * T + (r - 1)) * D;
+  f32x16v acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (int k0 = 0; k0 < D; k0 += 16) {
+    bf16x8_t f = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < n) f = *reinterpret_cast<const bf16x8_t*>(row + k0 + 8 * h);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, f, acc, 0, 0, 0);
+  }
+  uint16_t* o = out + static_cast<int64_t>(b) * (D + P);
+  for (int c = lane; c < D / 8; c += 64)  // dense pass-through
+    *reinterpret_cast<u16x8*>(o + 8 * c) = *reinterpret_cast<const u16x8*>(x + static_cast<int64_t>(b) * D + 8 * c);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = (q & 3) + 8 * (q >> 2) + 4 * h, j = r;  // C layout of 32x32x16
+    if (i < j && j < n) o[D + tri_index(i, j, n)] = f32_to_bf16(acc[q]);
+  }
+}
+
+// 4 waves (samples) per block; LDS z tile per wave: [32][D + 8] bf16
+__global__ __launch_bounds__(256) void dlrm_interact_bwd_kernel(const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ e,
+                                                                const uint16_t* __restrict__ dout,
+                                                                uint16_t* __restrict__ dx, uint16_t* __restrict__ de,
+                                                                int B, int T, int D) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t zl[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + w;
+  const bool live = b < B;  // dead waves still pass the barrier
+  const int n = T + 1, P = n * (n - 1) / 2, ld = D + 8;
+  uint16_t* z = zl + w * 32 * ld;
+  if (live) {
+    for (int c = lane; c < 32 * (D / 8); c += 64) {
+      const int rr = c / (D / 8), k = (c % (D / 8)) * 8;
+      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (rr == 0) v = *reinterpret_cast<const u16x8*>(x + static_cast<int64_t>(b) * D + k);
+      else if (rr < n) v = *reinterpret_cast<const u16x8*>(e + (static_cast<int64_t>(b) * T + (rr - 1)) * D + k);
+      *reinterpret_cast<u16x8*>(z + rr * ld + k) = v;
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const int r = lane & 31, h = lane >> 5;
+  const uint16_t* gi = dout + static_cast<int64_t>(b) * (D + P) + D;
+  // G fragments (A operand): lane holds Gs[i = r][j = 16 s + 8 h + t], Gs symmetric, zero diagonal
+  bf16x8_t ga[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int i = r, j = 16 * s + 8 * h + t;
+      uint16_t v = 0;
+      if (i < n && j < n && i != j) v = gi[i < j ? tri_index(i, j, n) : tri_index(j, i, n)];
+      ga[s][t] = static_cast<short>(v);
+    }
+  for (int c0 = 0; c0 < D; c0 += 32) {
+    f32x16v acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t bz;  // B operand: lane holds z[j = 16 s + 8 h + t][c0 + r]
+#pragma unroll
+      for (int t = 0; t < 8; ++t) bz[t] = static_cast<short>(z[(16 * s + 8 * h + t) * ld + c0 + r]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], bz, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = (q & 3) + 8 * (q >> 2) + 4 * h, col = c0 + r;
+      if (i == 0) {
+        const float pass = bf16_to_f32(dout[static_cast<int64_t>(b) * (D + P) + col]);
+        dx[static_cast<int64_t>(b) * D + col] = f32_to_bf16(acc[q] + pass);
+      } else if (i < n) {
+        de[(static_cast<int64_t>(b) * T + (i - 1)) * D + col] = f32_to_bf16(acc[q]);
+      }
+    }
+  }
+}
+
+void launch_dlrm_interact_fwd(const uint16_t* x, const uint16_t* e, uint16_t* out, int B, int T, int D,
+                              hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(dlrm_interact_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, x, e, out, B, T, D);
+}
+
+void launch_dlrm_interact_bwd(const uint16_t* x, const uint16_t* e, const uint16_t* dout, uint16_t* dx, uint16_t* de,
+                              int B, int T, int D, hipStream_t s) {
+  if (B <= 0) return;
+  const size_t lds = static_cast<size_t>(4) * 32 * (D + 8) * sizeof(uint16_t);
+  hipLaunchKernelGGL(dlrm_interact_bwd_kernel, dim3((B + 3) / 4), dim3(256), lds, s, x, e, dout, dx, de, B, T, D);
+}
+
 }  // namespace psamd

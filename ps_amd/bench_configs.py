@@ -92,6 +92,10 @@ def setup_dlrm(args, tp, dev) -> Bench:
     rows = [args.dlrm_rows] * 26
     model = DLRM(table_rows=rows, transport=tp, device=dev,
                  sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True)).to(dev)
+    # bf16 compute for the MLPs + interaction (fp32 master weights live in the PS shards);
+    # embedding tables and their Adagrad state stay fp32, rows are cast inside the gather
+    model.bottom.to(torch.bfloat16)
+    model.top.to(torch.bfloat16)
     ps = ColocatedPS(model, AdagradUpdater(0.01, 1e-8), tp, bucket_mb=args.bucket_mb,
                      last_bucket_mb=args.last_bucket_mb)
     B = args.batch_per_gpu

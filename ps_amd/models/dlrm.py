@@ -23,6 +23,7 @@ import torch.nn.functional as F
 from ..parallel.sparse_table import ShardedSparseTable, SparseTable
 from ..parallel.transport import Transport
 from ..parallel.updaters import AdagradUpdater, Updater
+from ..ops.dense import dlrm_interact
 from .layers import SparseLayerMixin
 
 
@@ -56,12 +57,12 @@ class MultiTableEmbedding(SparseLayerMixin, nn.Module):
         else:
             self.table = SparseTable("emb", dim, total, upd, init=(-bound, bound), seed=seed, device=device)
         self._pending = []
+        self.out_dtype = None  # compute dtype of the looked-up rows (tables stay fp32)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         """ids [B, T] (per-table row ids) -> [B, T, dim]."""
         gids = ids + self.offsets.to(ids.device)[None, :]
-        leaf, inv = self._pull_leaf(self.table, gids)
-        return leaf[inv]
+        return self._lookup(self.table, gids, self.out_dtype)
 
 
 class DLRM(nn.Module):
@@ -79,12 +80,11 @@ class DLRM(nn.Module):
         self.register_buffer("iu1", iu[1], persistent=False)
 
     def forward(self, dense: torch.Tensor, sparse: torch.Tensor) -> torch.Tensor:
-        x = self.bottom(dense)  # [B, dim]
-        e = self.emb(sparse).to(x.dtype)  # [B, T, dim]
-        z = torch.cat([x.unsqueeze(1), e], dim=1)  # [B, T+1, dim]
-        dots = torch.bmm(z, z.transpose(1, 2))  # [B, T+1, T+1]
-        inter = dots[:, self.iu0, self.iu1]
-        return self.top(torch.cat([x, inter], dim=1)).squeeze(1)
+        x = self.bottom(dense.to(self.bottom[0].weight.dtype))  # [B, dim]
+        self.emb.out_dtype = x.dtype
+        e = self.emb(sparse)  # [B, T, dim] in the compute dtype (cast fused into the gather)
+        # [x | triu(z z^T)], z = [x; e]: one fused MFMA kernel on GPU bf16 (ops/dense.py)
+        return self.top(dlrm_interact(x, e)).squeeze(1)
 
     def push_sparse(self) -> int:
         return self.emb.push_sparse()

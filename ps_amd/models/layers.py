@@ -103,6 +103,22 @@ class SparseLayerMixin:
         self._pending.append((table, uniq, leaf, counts, ids.shape[0]))
         return leaf, inv.view(ids.shape)
 
+    def _lookup(self, table, ids: torch.Tensor, out_dtype=None) -> torch.Tensor:
+        """rows of ``ids`` ([..., dim], autograd to the pulled leaf).  GPU: one sort for the
+        dedupe, HIP gather with the dtype cast fused, segment-sum backward (ops/sparse.py)."""
+        if not ids.is_cuda:
+            leaf, inv = self._pull_leaf(table, ids)
+            out = leaf[inv]
+            return out if out_dtype is None else out.to(out_dtype)
+        from ..ops.sparse import gather_unique, unique_with_segments
+
+        uniq, inv, counts, perm, seg_off = unique_with_segments(ids)
+        rows = table.pull(uniq)
+        leaf = rows.detach().clone().requires_grad_(self.training and torch.is_grad_enabled())
+        self._pending.append((table, uniq, leaf, counts, ids.shape[0]))
+        out = gather_unique(leaf, inv, perm, seg_off, out_dtype)
+        return out.view(*ids.shape, leaf.shape[1])
+
     def push_sparse(self) -> int:
         """Push gradients of the rows touched since the last call; returns rows pushed."""
         n = 0

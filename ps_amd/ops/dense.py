@@ -66,3 +66,36 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act:
         return _LinearAct.apply(x.to(torch.bfloat16), w, b, int(act))
     z = F.linear(x.to(w.dtype), w, b)
     return _act_ref(z, act)
+
+
+# ------------------------------------------------------------------------------ DLRM interaction
+def _interact_ref(x: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
+    z = torch.cat([x.unsqueeze(1), e], dim=1)
+    n = z.shape[1]
+    iu = torch.triu_indices(n, n, offset=1, device=z.device)
+    dots = torch.bmm(z, z.transpose(1, 2))
+    return torch.cat([x, dots[:, iu[0], iu[1]]], dim=1)
+
+
+class _Interact(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, e):
+        x, e = x.contiguous(), e.contiguous()
+        ctx.save_for_backward(x, e)
+        return native().dlrm_interact_fwd(x, e)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, e = ctx.saved_tensors
+        dx, de = native().dlrm_interact_bwd(x, e, dout.contiguous().to(torch.bfloat16))
+        return dx, de
+
+
+def dlrm_interact(x: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
+    """[x | triu_{i<j}(z_i . z_j)] with z = [x; e] (DLRM dot interaction, torch.triu_indices order).
+    x [B, D], e [B, T, D]; bf16 GPU tensors with T + 1 <= 32 and D % 32 == 0 run the MFMA kernel
+    (csrc/kernels/dense.hip), anything else the torch composition."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and e.dtype == torch.bfloat16 and e.shape[1] + 1 <= 32
+            and x.shape[1] % 32 == 0 and x.shape[1] <= 224):
+        return _Interact.apply(x, e)
+    return _interact_ref(x, e)

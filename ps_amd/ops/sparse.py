@@ -110,3 +110,46 @@ def lazy_init_rows(table: torch.Tensor, rows: torch.Tensor, flags: torch.Tensor,
         g = torch.Generator().manual_seed((int(seed) * 1000003 + r + row_base) & 0x7FFFFFFFFFFFFFFF)
         table[r] = lo + (hi - lo) * torch.rand(table.shape[1], generator=g)
         flags[r] = 1
+
+
+class _GatherUnique(torch.autograd.Function):
+    """out[k] = leaf[inv[k]] (cast to out_dtype); backward = deterministic segment sum of the
+    output gradient per unique row (sorted-order perm + seg_off), no atomics, no sort."""
+
+    @staticmethod
+    def forward(ctx, leaf, inv, perm, seg_off, out_dtype):
+        out = torch.empty(inv.numel(), leaf.shape[1], dtype=out_dtype, device=leaf.device)
+        native().gather_rows(leaf, inv, out, 0, ACT_NONE)
+        ctx.save_for_backward(perm, seg_off)
+        ctx.nrows, ctx.ldtype = leaf.shape[0], leaf.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        perm, seg_off = ctx.saved_tensors
+        dleaf = torch.empty(ctx.nrows, dout.shape[1], dtype=ctx.ldtype, device=dout.device)
+        native().segment_reduce_rows(dout.contiguous(), perm, seg_off, dleaf, False)
+        return dleaf, None, None, None, None
+
+
+def unique_with_segments(ids: torch.Tensor):
+    """(uniq, inv, counts, perm, seg_off) of a flat id vector: perm lists positions in sorted-id
+    order (stable), seg_off[u]..seg_off[u+1] the occurrences of uniq[u] within perm."""
+    ids = ids.reshape(-1)
+    srt, perm = torch.sort(ids, stable=True)
+    uniq, inv_sorted, counts = torch.unique_consecutive(srt, return_inverse=True, return_counts=True)
+    inv = torch.empty_like(inv_sorted)
+    inv[perm] = inv_sorted
+    seg_off = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=ids.device)
+    torch.cumsum(counts, 0, out=seg_off[1:])
+    return uniq, inv, counts, perm, seg_off
+
+
+def gather_unique(leaf: torch.Tensor, inv: torch.Tensor, perm: torch.Tensor, seg_off: torch.Tensor,
+                  out_dtype=None) -> torch.Tensor:
+    """leaf[inv] (optionally cast) with a segment-sum backward; GPU path = HIP gather_rows /
+    segment_reduce_rows, CPU = torch indexing."""
+    out_dtype = out_dtype or leaf.dtype
+    if use_native(leaf, inv):
+        return _GatherUnique.apply(leaf, inv.reshape(-1), perm, seg_off, out_dtype)
+    return leaf[inv.reshape(-1)].to(out_dtype)

@@ -299,3 +299,25 @@ def test_mfma_gemm_asymmetric_identity():
     b = torch.arange(n * n, dtype=torch.float32).view(n, n).remainder(97).bfloat16().cuda()
     c = D.gemm_nt(eye, b, out_dtype=torch.float32)  # I @ B^T = B^T
     torch.testing.assert_close(c, b.float().t())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,D", [(37, 26, 128), (8, 3, 64), (5, 31, 32)])
+def test_dlrm_interact_fwd_bwd(B, T, D):
+    from ps_amd.ops.dense import _interact_ref, dlrm_interact
+
+    torch.manual_seed(0)
+    x = torch.randn(B, D, device="cuda").bfloat16().requires_grad_(True)
+    e = torch.randn(B, T, D, device="cuda").bfloat16().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    er = e.detach().float().requires_grad_(True)
+    y = dlrm_interact(x, e)
+    yr = _interact_ref(xr, er)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2 * (D ** 0.5) / 4)
+    g = torch.randn_like(yr).bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+    cos = torch.nn.functional.cosine_similarity
+    assert cos(x.grad.float().flatten(), xr.grad.flatten(), dim=0) > 0.999
+    assert cos(e.grad.float().flatten(), er.grad.flatten(), dim=0) > 0.999
+    torch.testing.assert_close(e.grad.float(), er.grad, rtol=3e-2, atol=0.15 * (D ** 0.5) / 4)
