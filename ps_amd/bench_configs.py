@@ -70,10 +70,10 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
     ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
                      staleness=stale, clip_norm=None)
     B, S = args.batch_per_gpu, args.seq_len
-    ids, labels = mlm_batch(B, S, seed=tp.rank, device=dev)
+    ids, labels, positions = mlm_batch(B, S, seed=tp.rank, device=dev, with_positions=True)
 
     def step():
-        loss = model(ids, labels)
+        loss = model(ids, labels, positions)  # LM head on the masked positions only (BERT format)
         loss.backward()
         ps.finish_step()
         return loss

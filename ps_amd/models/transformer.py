@@ -79,30 +79,44 @@ class BertForMLM(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
-    def forward(self, ids, labels=None):
+    def forward(self, ids, labels=None, positions=None):
+        """``positions`` [B, P] (the masked-LM positions of the original BERT pretraining input
+        format, ``masked_lm_positions``): the LM head runs only on those B*P rows -- the vocab
+        projection and its softmax are 1/(S/P) of the dense-head cost.  Without positions the
+        head runs on every token (labels -100 are ignored)."""
         b, s = ids.shape
         pos = torch.arange(s, device=ids.device)
         x = self.word(ids) + self.pos(pos)[None] + self.tok_type.weight[0]
         x = F.dropout(self.ln(x), self.c.dropout, self.training)
         for layer in self.layers:
             x = layer(x)
+        if positions is not None:
+            flat = (positions + torch.arange(b, device=ids.device)[:, None] * s).reshape(-1)
+            x = x.reshape(b * s, -1).index_select(0, flat)
+            if labels is not None:
+                labels = labels.reshape(-1).index_select(0, flat)
         h = self.head_ln(F.gelu(self.head_dense(x)))
         logits = h @ self.word.weight.t() + self.head_bias
         if labels is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, self.c.vocab), labels.view(-1), ignore_index=-100)
+        return F.cross_entropy(logits.float().view(-1, self.c.vocab), labels.reshape(-1), ignore_index=-100)
 
 
-def mlm_batch(batch: int, seq: int, vocab: int = 30522, mask_prob: float = 0.15, seed: int = 0, device=None):
+def mlm_batch(batch: int, seq: int, vocab: int = 30522, mask_prob: float = 0.15, seed: int = 0, device=None,
+              with_positions: bool = False):
+    """Synthetic MLM batch in the BERT pretraining format: exactly round(mask_prob * seq)
+    masked positions per sequence (create_pretraining_data's num_to_predict), replaced by
+    [MASK]; labels -100 elsewhere.  ``with_positions`` also returns masked_lm_positions [B, P]."""
     g = torch.Generator().manual_seed(seed)
     ids = torch.randint(min(1000, vocab // 2), vocab, (batch, seq), generator=g)
+    npred = max(1, int(round(mask_prob * seq)))
+    positions = torch.rand(batch, seq, generator=g).argsort(dim=1)[:, :npred].sort(dim=1).values
     labels = torch.full_like(ids, -100)
-    m = torch.rand(batch, seq, generator=g) < mask_prob
-    labels[m] = ids[m]
-    ids = ids.masked_fill(m, 103)  # [MASK]
+    labels.scatter_(1, positions, ids.gather(1, positions))
+    ids = ids.scatter(1, positions, 103)  # [MASK]
     if device is not None:
-        ids, labels = ids.to(device), labels.to(device)
-    return ids, labels
+        ids, labels, positions = ids.to(device), labels.to(device), positions.to(device)
+    return (ids, labels, positions) if with_positions else (ids, labels)
 
 
 # ----------------------------------------------------------------------------------- Llama

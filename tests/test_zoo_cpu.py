@@ -35,6 +35,24 @@ def test_bert_tiny_ssp_learns():
     assert losses[-1] < losses[0] - 1.0
 
 
+def test_bert_masked_positions_head_matches_dense_head():
+    """The sparse-prediction head (masked_lm_positions) computes the same loss and gradients
+    as the dense head with ignore_index -- it only skips the unmasked rows."""
+    from ps_amd.models.transformer import BertConfig, BertForMLM, mlm_batch
+
+    torch.manual_seed(0)
+    m = BertForMLM(BertConfig(vocab=300, hidden=32, layers=2, heads=4, ffn=64, max_pos=32, dropout=0.0))
+    ids, labels, pos = mlm_batch(8, 20, vocab=300, seed=1, with_positions=True)
+    assert pos.shape == (8, 3) and bool((labels != -100).sum(1).eq(3).all())
+    l_dense = m(ids, labels)
+    g_dense = torch.autograd.grad(l_dense, list(m.parameters()))
+    l_sparse = m(ids, labels, pos)
+    g_sparse = torch.autograd.grad(l_sparse, list(m.parameters()))
+    torch.testing.assert_close(l_sparse, l_dense)
+    for a, b in zip(g_sparse, g_dense):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
 def _llama_body(tp):
     from ps_amd.models.transformer import LlamaConfig, LlamaForCausalLM
     from ps_amd.parallel.colocated import ColocatedPS
