@@ -68,12 +68,15 @@ void PSServer::stop() {
     std::lock_guard<std::mutex> g(barrier_mu_);
     barrier_cv_.notify_all();
   }
+  // wake the acceptor, join it, and only then close/reset the fd: closing it while the
+  // acceptor still polls it raced on listen_fd_ and could hand a reused fd number to poll()
+  // (found by the TSan build, scripts/tsan_native.sh)
+  if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  if (accept_thread_.joinable()) accept_thread_.join();
   if (listen_fd_ >= 0) {
-    ::shutdown(listen_fd_, SHUT_RDWR);
     ::close(listen_fd_);
     listen_fd_ = -1;
   }
-  if (accept_thread_.joinable()) accept_thread_.join();
   std::vector<std::thread> ts;
   {
     std::lock_guard<std::mutex> g(conn_mu_);
@@ -444,8 +447,10 @@ uint16_t PSClient::call(Op op, const Writer& req, std::vector<uint8_t>* resp) {
   uint16_t status;
   if (!recv_all(fd_, &magic, 4) || magic != kMagic || !recv_all(fd_, &status, 2) || !recv_all(fd_, &len, 4))
     throw std::runtime_error("PS connection lost (recv)");
-  resp->resize(len);
-  if (len && !recv_all(fd_, resp->data(), len)) throw std::runtime_error("PS connection lost (payload)");
+  std::vector<uint8_t> discard;
+  std::vector<uint8_t>* dst = resp ? resp : &discard;  // null resp: payload read and dropped
+  dst->resize(len);
+  if (len && !recv_all(fd_, dst->data(), len)) throw std::runtime_error("PS connection lost (payload)");
   bytes_sent_ += h.buf.size() + req.buf.size();
   bytes_recv_ += 10 + len;
   return status;

@@ -103,3 +103,26 @@ def test_trace_ranges_noop_safe():
             pass
     st.step_done()
     assert "push" in st.summary()
+
+
+def test_native_ps_server_threadsanitizer(tmp_path):
+    """SURVEY §5.2 c: the native PS server under ThreadSanitizer -- W concurrent clients x R BSP
+    rounds (exact result check) + an SSP clock-bound phase; any TSan report fails the test."""
+    import os
+    import shutil
+    import subprocess
+
+    import pytest
+
+    cxx = os.environ.get("CXX", "/opt/rocm/lib/llvm/bin/clang++")
+    if not (os.path.exists(cxx) or shutil.which(cxx)):
+        pytest.skip("no clang++ with a TSan runtime")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "ps_stress_tsan")
+    subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                    f"-I{root}/csrc/runtime", f"{root}/csrc/runtime/ps_server.cpp",
+                    f"{root}/csrc/runtime/tests/ps_stress.cpp", "-o", exe], check=True, timeout=300)
+    r = subprocess.run([exe, "4", "10", "8"], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "TSAN_OPTIONS": "halt_on_error=1"})
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "ps_stress ok" in out and "ThreadSanitizer" not in out, out[-3000:]
