@@ -148,3 +148,134 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(**kw)
     return Transport()
+
+
+# ------------------------------------------------------------------------------ loopback
+class LoopbackHub:
+    """Rendezvous of ``world`` in-process ranks (threads): every collective is one exchange
+    of per-rank payloads behind a pair of barriers.  The SURVEY §7.6 "fake backend": PS and
+    consistency logic run deterministically in one process, reductions in rank order."""
+
+    def __init__(self, world: int, timeout_s: float = 120.0):
+        import threading
+
+        self.world = world
+        self.slots: List[object] = [None] * world
+        self.bar = threading.Barrier(world, timeout=timeout_s)
+
+    def exchange(self, rank: int, obj):
+        self.slots[rank] = obj
+        self.bar.wait()
+        got = list(self.slots)
+        self.bar.wait()  # nobody overwrites a slot before every rank has read it
+        return got
+
+    def abort(self):
+        self.bar.abort()
+
+
+class LoopbackTransport(Transport):
+    """Transport over a LoopbackHub (same API as the RCCL/gloo Transport)."""
+
+    def __init__(self, hub: LoopbackHub, rank: int, check_order: bool = False):
+        self.group = None
+        self.initialized = True
+        self.hub = hub
+        self.world = hub.world
+        self.rank = rank
+        self.backend = "loopback"
+        self.check_order = check_order
+        self._h = hashlib.sha1()
+        self.n_ops = 0
+        self.bytes_sent = 0
+
+    def _sum(self, parts):
+        acc = parts[0].clone()
+        for p in parts[1:]:
+            acc += p
+        return acc
+
+    def verify_order(self) -> bool:
+        got = self.hub.exchange(self.rank, self.order_digest())
+        if any(g != got[0] for g in got):
+            raise RuntimeError("collective order mismatch across ranks (loopback)")
+        return True
+
+    def reduce_scatter(self, out, inp, average: bool = False):
+        self._note("rs", inp)
+        parts = self.hub.exchange(self.rank, inp.detach().clone())
+        total = self._sum(parts).view(self.world, -1)[self.rank]
+        out.copy_(total.view_as(out))
+        if average:
+            out.div_(self.world)
+        return out
+
+    def all_gather(self, out, inp):
+        self._note("ag", out)
+        parts = self.hub.exchange(self.rank, inp.detach().clone().reshape(-1))
+        out.copy_(torch.cat(parts).view_as(out))
+        return out
+
+    def all_reduce(self, t, op=None):
+        self._note("ar", t)
+        parts = self.hub.exchange(self.rank, t.detach().clone())
+        if op is not None and op == dist.ReduceOp.MAX:
+            r = parts[0].clone()
+            for p in parts[1:]:
+                r = torch.maximum(r, p)
+        else:
+            r = self._sum(parts)
+        t.copy_(r)
+        return t
+
+    def broadcast(self, t, src: int = 0):
+        self._note("bc", t)
+        parts = self.hub.exchange(self.rank, t.detach().clone())
+        t.copy_(parts[src])
+        return t
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        self._note("a2a", inp)
+        w = self.world
+        if in_splits is None:
+            in_splits = [inp.shape[0] // w] * w
+        parts = self.hub.exchange(self.rank, (inp.detach().clone(), list(in_splits)))
+        chunks = []
+        for src in range(w):
+            t, sp = parts[src]
+            off = sum(sp[:self.rank])
+            chunks.append(t[off:off + sp[self.rank]])
+        out.copy_(torch.cat(chunks).view_as(out))
+        return out
+
+    def all_gather_object(self, obj):
+        return self.hub.exchange(self.rank, obj)
+
+    def barrier(self):
+        self.hub.exchange(self.rank, None)
+
+
+def run_loopback(fn, world: int, *args, timeout_s: float = 120.0):
+    """Run ``fn(transport, *args)`` on ``world`` threads joined by a LoopbackHub; returns the
+    per-rank results (re-raises the first rank failure)."""
+    import threading
+
+    hub = LoopbackHub(world, timeout_s)
+    res: List[object] = [None] * world
+    err: List[BaseException] = []
+
+    def body(r):
+        try:
+            res[r] = fn(LoopbackTransport(hub, r), *args)
+        except BaseException as e:  # noqa: BLE001 -- surfaced below
+            err.append(e)
+            hub.abort()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if err:
+        raise err[0]
+    return res
