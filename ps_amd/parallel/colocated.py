@@ -146,6 +146,11 @@ class ColocatedPS:
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
         self.round_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
+        # fault injection (PS_AMD_FAULT / HIPPS_FAULT): kill at a step, delay pushes
+        from ..utils.fault import FaultInjector
+
+        fi = FaultInjector(rank=self.rank)
+        self.fault = fi if fi.spec else None
         self._bind(self.wslot, self.gslot)
         self._hooks = [p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
 
@@ -176,6 +181,8 @@ class ColocatedPS:
         if self.launched[b]:
             return
         self.launched[b] = True
+        if self.fault is not None:
+            self.fault.before_push()
         if self.gpu:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
@@ -248,6 +255,8 @@ class ColocatedPS:
     def finish_step(self) -> None:
         """End of a worker step: flush buckets that did not fire, run the round's remaining
         phases, advance the PS clock and bind the weights the next forward may use."""
+        if self.fault is not None:
+            self.fault.at_step(self.round)
         for b in range(len(self.reg.buckets)):
             if not self.launched[b]:
                 self._launch(b)

@@ -54,6 +54,7 @@ class KVStore:
         self._lock = threading.RLock()
         self.clock = 0
         self.round = 0
+        self._fault = None  # lazily built FaultInjector (PS_AMD_FAULT); False = none configured
 
     @property
     def distributed(self) -> bool:
@@ -142,8 +143,19 @@ class KVStore:
         groups: Dict[str, Dict[str, torch.Tensor]] = {}
         for k, g in avg.items():
             groups.setdefault(resolve_updater(k, umap).name, {})[k] = g
+        if self._fault is None:
+            from ..utils.fault import FaultInjector
+
+            fi = FaultInjector(rank=self.worker_id)
+            self._fault = fi if fi.spec else False
         for spec, grads in groups.items():
+            if self._fault:
+                self._fault.before_push()
+                if self.consistency == "asp" and self._fault.drop():  # lost push (ASP only)
+                    continue
             self.client.push(grads, spec)
+        if self._fault:
+            self._fault.at_step(self.round)
         self.round += 1
         self.clock += 1
         if self.consistency == "bsp":

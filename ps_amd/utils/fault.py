@@ -35,7 +35,8 @@ def parse_fault(spec: str) -> Dict[str, Dict[str, str]]:
 
 class FaultInjector:
     def __init__(self, spec: Optional[str] = None, rank: int = 0, seed: int = 0):
-        self.spec = parse_fault(spec if spec is not None else os.environ.get("PS_AMD_FAULT", ""))
+        env = os.environ.get("PS_AMD_FAULT") or os.environ.get("HIPPS_FAULT", "")  # SURVEY §5.3 spelling
+        self.spec = parse_fault(spec if spec is not None else env)
         self.rank = rank
         self.rng = random.Random(seed + rank)
 

@@ -126,3 +126,25 @@ def test_native_ps_server_threadsanitizer(tmp_path):
                        env={**os.environ, "TSAN_OPTIONS": "halt_on_error=1"})
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "ps_stress ok" in out and "ThreadSanitizer" not in out, out[-3000:]
+
+
+def test_fault_kill_at_step_exits_the_rank():
+    """PS_AMD_FAULT=kill:rank=0:step=2 ends the process hard at the start of PS round 2."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, torch, torch.nn.functional as F\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from ps_amd.parallel.colocated import ColocatedPS\n"
+        "from ps_amd.parallel.updaters import SimpleUpdater\n"
+        "m = torch.nn.Linear(4, 2); ps = ColocatedPS(m, SimpleUpdater(0.1))\n"
+        "for i in range(5):\n"
+        "    F.mse_loss(m(torch.ones(3, 4)), torch.zeros(3, 2)).backward(); ps.finish_step()\n"
+        "    print('step', i, flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "PS_AMD_FAULT": "kill:rank=0:step=2"})
+    assert r.returncode == 17, r.stderr[-2000:]
+    assert r.stdout.split() == ["step", "0", "step", "1"]
