@@ -55,6 +55,9 @@ def parse():
                          "ResNet-50: 32.7 vs 31.6 ms, profiles/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--timing", type=int, default=0,
+                    help="after the timed region: N more steps with per-phase device timing "
+                         "(fwd+bwd / push / serve / pull / exposed comm) printed to stderr")
     return ap.parse_args()
 
 
@@ -151,6 +154,17 @@ def main():
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
     value = bench.samples_per_step * world * args.steps / elapsed
+    if args.timing and getattr(bench.engine, "timing_summary", None) is not None:
+        eng = bench.engine
+        eng.timing = True
+        eng._mark("step0")
+        for _ in range(args.timing):
+            step()
+        torch.cuda.synchronize()
+        tsum = eng.timing_summary()
+        if rank == 0:
+            print("[bench-timing] " + json.dumps({k: round(v, 3) for k, v in tsum.items()}), file=sys.stderr,
+                  flush=True)
     if args.profile_steps and rank == 0:
         from torch.profiler import ProfilerActivity, profile
 

@@ -50,7 +50,7 @@ class ColocatedPS:
     def __init__(self, model: torch.nn.Module, updaters: Union[Updater, Dict[str, Updater]],
                  transport: Optional[Transport] = None, *, bucket_mb: float = 32.0, last_bucket_mb: float = 4.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
-                 average: bool = True, broadcast_init: bool = True, overlap: bool = True):
+                 average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -151,7 +151,17 @@ class ColocatedPS:
 
         fi = FaultInjector(rank=self.rank)
         self.fault = fi if fi.spec else None
+        # per-step phase timing: device events on the comm stream around push /
+        # serve / pull of every bucket, plus backward-end vs round-end for the exposed tail
+        import os as _os
+
+        self.timing = timing or _os.environ.get("PS_AMD_TIMING", "0") == "1"
+        self._marks: List[tuple] = []  # (name, event or perf_counter) of the current step
+        self._tsum: Dict[str, float] = {}
+        self._tsteps = 0
+        self._prev_marks: List[tuple] = []
         self._bind(self.wslot, self.gslot)
+        self._mark("step0")
         self._hooks = [p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
 
     # ------------------------------------------------------------------ views
@@ -188,13 +198,68 @@ class ColocatedPS:
             ev.record(torch.cuda.current_stream(self.device))
             self.comm.wait_event(ev)
             with torch.cuda.stream(self.comm):
+                self._mark("push0")
                 self._push(b)
+                self._mark("push1")
                 if self.clip_norm is None:
                     self._serve_pull(b)
         else:
+            self._mark("push0")
             self._push(b)
+            self._mark("push1")
             if self.clip_norm is None:
                 self._serve_pull(b)
+
+    # ------------------------------------------------------------------ timing
+    def _mark(self, name: str) -> None:
+        if not self.timing:
+            return
+        if self.gpu:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # current stream (comm inside _launch, compute in finish_step)
+            self._marks.append((name, ev))
+        else:
+            self._marks.append((name, time.perf_counter()))
+
+    def _close_timing(self) -> None:
+        """Fold the finished step's marks into the running sums (synchronizes on them)."""
+        if not self._marks:
+            return
+        def ms(a, b):
+            return a.elapsed_time(b) if self.gpu else (b - a) * 1e3
+        if self.gpu:
+            self._marks[-1][1].synchronize()
+        acc = {"push_ms": 0.0, "serve_ms": 0.0, "pull_ms": 0.0}
+        last = {}
+        for name, t in self._marks:
+            if name == "push1":
+                acc["push_ms"] += ms(last["push0"], t)
+            elif name == "serve1":
+                acc["serve_ms"] += ms(last.get("push1", last.get("serve0")), t)
+            elif name == "pull1":
+                acc["pull_ms"] += ms(last["serve1"], t)
+            last[name] = t
+        if "bwd_end" in last and "round_end" in last:
+            acc["exposed_comm_ms"] = max(0.0, ms(last["bwd_end"], last["round_end"]))
+        if "step0" in last and "bwd_end" in last:
+            acc["fwd_bwd_ms"] = ms(last["step0"], last["bwd_end"])
+        for k, v in acc.items():
+            self._tsum[k] = self._tsum.get(k, 0.0) + v
+        self._tsteps += 1
+        self._marks = []
+
+    def timing_summary(self, reset: bool = True) -> Dict[str, float]:
+        """Mean per-step phase times (ms) since the last reset: fwd_bwd, push (reduce-scatter),
+        serve (owner optimizer), pull (all-gather) summed over buckets, and the exposed tail of
+        the round after backward.  Enable with ``timing=True`` or PS_AMD_TIMING=1."""
+        if self._prev_marks:  # the last completed step (the current one is still open)
+            cur, self._marks = self._marks, self._prev_marks
+            self._close_timing()
+            self._marks, self._prev_marks = cur, []
+        out = {k: v / max(1, self._tsteps) for k, v in self._tsum.items()}
+        if reset:
+            self._tsum, self._tsteps = {}, 0
+        return out
 
     def _push(self, b: int) -> None:
         bk = self.reg.buckets[b]
@@ -235,10 +300,13 @@ class ColocatedPS:
         g = self._grad_shard(b)
         gscale = 1.0 / self.world if self.average else 1.0
         gst = self._factor if self.clip_norm is not None else None
+        self._mark("serve0")
         for (u, a, z), st in zip(self.segs[b], self.states[b]):
             u.step_flat(self.master[b][a:z], st, g[a:z], wout=own[a:z], gscale=gscale, gscale_t=gst,
                         step=self.round + 1)
+        self._mark("serve1")
         self.t.all_gather(wfull[bk.start:bk.start + bk.size], own)
+        self._mark("pull1")
 
     def _clip_and_serve(self) -> None:
         self._sq.zero_()
@@ -257,6 +325,8 @@ class ColocatedPS:
         phases, advance the PS clock and bind the weights the next forward may use."""
         if self.fault is not None:
             self.fault.at_step(self.round)
+        if self.timing:
+            self._mark("bwd_end")
         for b in range(len(self.reg.buckets)):
             if not self.launched[b]:
                 self._launch(b)
@@ -270,6 +340,12 @@ class ColocatedPS:
             ev = torch.cuda.Event()
             ev.record(self.comm)
             self.round_events.append(ev)
+        if self.timing:
+            if self.gpu:
+                with torch.cuda.stream(self.comm):
+                    self._mark("round_end")
+            else:
+                self._mark("round_end")
         r = self.round
         self.round += 1
         self.stats["rounds"] += 1
@@ -288,6 +364,19 @@ class ColocatedPS:
         self.pending = [len(b.keys) for b in self.reg.buckets]
         self.launched = [False] * len(self.reg.buckets)
         self._bind(self.wslot, self.gslot)
+        if self.timing:
+            self._close_timing_deferred()
+
+    def _close_timing_deferred(self) -> None:
+        # keep one step in flight: fold the PREVIOUS step's marks (already complete or nearly)
+        # so timing adds no per-step host sync to the critical path
+        prev = self._prev_marks
+        cur, self._marks = self._marks, []
+        if prev:
+            self._marks = prev
+            self._close_timing()
+        self._prev_marks = cur
+        self._mark("step0")
 
     def synchronize(self) -> None:
         """Drain every in-flight round (checkpoint / eval boundary)."""
