@@ -179,6 +179,7 @@ def main():
         cfg = dict(bench.config)
         cfg["hip_graph"] = bool(use_graph)
         cfg["final_loss"] = round(float(loss.item()), 4)
+        cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         rec = {
             "metric": bench.metric,
             "value": round(value, 2),

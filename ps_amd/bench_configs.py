@@ -121,7 +121,11 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
     cfg = LlamaConfig.tiny() if args.tiny else LlamaConfig.llama3_8b()
     torch.manual_seed(0)
     with torch.device(dev):
-        model = LlamaForCausalLM(cfg, checkpointing=True).to(torch.bfloat16)
+        # no activation checkpointing: bs 1 x 4096 activations (~26 GB) + weights/grads (32 GB) +
+        # fp32 master/Adam state (96 GB, 1/W of it per rank) fit the 288 GB HBM -- recomputing
+        # the forward would cost ~25 % of the step
+        model = LlamaForCausalLM(cfg, checkpointing=bool(int(os.environ.get("PS_AMD_LLAMA_CKPT", "0")))).to(
+            torch.bfloat16)
     upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
                      compress="onebit" if tp.world > 1 else None)

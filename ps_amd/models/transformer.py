@@ -168,18 +168,20 @@ def apply_rope(x, cos, sin):
 
 
 class LlamaBlock(nn.Module):
+    """Pre-norm decoder block.  Q/K/V and gate/up projections are single fused GEMMs
+    (``wqkv`` [(H + 2 KV) * hd, D], ``w13`` [2 F, D] -- same parameter count as separate
+    matrices, one hipBLASLt launch each); attention uses SDPA with native GQA (no K/V
+    replication)."""
+
     def __init__(self, c: LlamaConfig):
         super().__init__()
         self.c = c
         hd = c.hidden // c.heads
         self.attn_norm = RMSNorm(c.hidden, c.eps)
-        self.wq = nn.Linear(c.hidden, c.heads * hd, bias=False)
-        self.wk = nn.Linear(c.hidden, c.kv_heads * hd, bias=False)
-        self.wv = nn.Linear(c.hidden, c.kv_heads * hd, bias=False)
+        self.wqkv = nn.Linear(c.hidden, (c.heads + 2 * c.kv_heads) * hd, bias=False)
         self.wo = nn.Linear(c.heads * hd, c.hidden, bias=False)
         self.mlp_norm = RMSNorm(c.hidden, c.eps)
-        self.w1 = nn.Linear(c.hidden, c.ffn, bias=False)
-        self.w3 = nn.Linear(c.hidden, c.ffn, bias=False)
+        self.w13 = nn.Linear(c.hidden, 2 * c.ffn, bias=False)
         self.w2 = nn.Linear(c.ffn, c.hidden, bias=False)
 
     def forward(self, x, cos, sin):
@@ -187,17 +189,14 @@ class LlamaBlock(nn.Module):
         c = self.c
         hd = c.hidden // c.heads
         h = self.attn_norm(x)
-        q = self.wq(h).view(b, s, c.heads, hd).transpose(1, 2)
-        k = self.wk(h).view(b, s, c.kv_heads, hd).transpose(1, 2)
-        v = self.wv(h).view(b, s, c.kv_heads, hd).transpose(1, 2)
+        qkv = self.wqkv(h).view(b, s, c.heads + 2 * c.kv_heads, hd).transpose(1, 2)
+        q, k, v = qkv.split([c.heads, c.kv_heads, c.kv_heads], dim=1)
         q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
-        rep = c.heads // c.kv_heads
-        k = k.repeat_interleave(rep, dim=1)
-        v = v.repeat_interleave(rep, dim=1)
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        a = F.scaled_dot_product_attention(q, k, v.contiguous(), is_causal=True, enable_gqa=True)
         x = x + self.wo(a.transpose(1, 2).reshape(b, s, -1))
         h = self.mlp_norm(x)
-        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+        g, u = self.w13(h).chunk(2, dim=-1)
+        return x + self.w2(F.silu(g) * u)
 
 
 class LlamaForCausalLM(nn.Module):
