@@ -462,6 +462,155 @@ std::vector<Tensor> bn_stats(Tensor x, c10::optional<Tensor> gamma, c10::optiona
   return {r[1], r[2], r[3]};
 }
 
+// ------------------------------------------------------------------------------ transformer row kernels
+static void check_rows(const Tensor& t, const char* n) {
+  check_gpu(t, n);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), n, ": bf16 contiguous");
+}
+static void check_dim(int64_t D) { TORCH_CHECK(D % 8 == 0 && D <= 4096, "row length must be a multiple of 8, <= 4096"); }
+static const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+static uint16_t* u16m(Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+// x [R, D] (+ r) -> [s (or empty), y, rstd]
+std::vector<Tensor> rmsnorm_fwd(Tensor x, c10::optional<Tensor> r, Tensor w, double eps) {
+  check_rows(x, "x");
+  const int64_t D = x.size(-1), R = x.numel() / D;
+  check_dim(D);
+  check_gpu(w, "w");
+  TORCH_CHECK(w.numel() == D && w.is_contiguous() && (w.scalar_type() == torch::kBFloat16 || w.scalar_type() == torch::kFloat32), "w [D]");
+  const bool res = r.has_value() && r->defined();
+  if (res) {
+    check_rows(*r, "r");
+    TORCH_CHECK(r->sizes() == x.sizes(), "r like x");
+  }
+  const c10::DeviceGuard guard(x.device());
+  auto y = torch::empty_like(x);
+  auto s = res ? torch::empty_like(x) : Tensor();
+  auto rstd = torch::empty({R}, x.options().dtype(torch::kFloat32));
+  psamd::launch_rmsnorm_fwd(u16(x), res ? u16(*r) : nullptr, w.data_ptr(), w.scalar_type() == torch::kBFloat16,
+                            res ? u16m(s) : nullptr, u16m(y), rstd.data_ptr<float>(), R, D, static_cast<float>(eps),
+                            cur_stream(x));
+  return {s, y, rstd};
+}
+
+// -> [dx, dw (fp32)]; ds_in: extra gradient of s (residual stream) added into dx
+std::vector<Tensor> rmsnorm_bwd(Tensor dy, Tensor s, Tensor w, Tensor rstd, c10::optional<Tensor> ds_in) {
+  check_rows(dy, "dy");
+  check_rows(s, "s");
+  TORCH_CHECK(dy.sizes() == s.sizes(), "dy like s");
+  const int64_t D = s.size(-1), R = s.numel() / D;
+  check_dim(D);
+  check_f32(rstd, "rstd");
+  const bool add = ds_in.has_value() && ds_in->defined();
+  if (add) {
+    check_rows(*ds_in, "ds_in");
+    TORCH_CHECK(ds_in->sizes() == s.sizes(), "ds_in like s");
+  }
+  const c10::DeviceGuard guard(s.device());
+  auto dx = torch::empty_like(s);
+  auto fopt = s.options().dtype(torch::kFloat32);
+  auto wpart = torch::empty({psamd::rmsnorm_bwd_parts(static_cast<int>(R)), D}, fopt);
+  auto dw = torch::empty({D}, fopt);
+  psamd::launch_rmsnorm_bwd(u16(dy), u16(s), w.data_ptr(), w.scalar_type() == torch::kBFloat16, rstd.data_ptr<float>(),
+                            add ? u16(*ds_in) : nullptr, u16m(dx), wpart.data_ptr<float>(), dw.data_ptr<float>(), R, D,
+                            cur_stream(s));
+  return {dx, dw};
+}
+
+// s = x + dropout_p(o); y = LN(s) -> [s, y, mean, rstd]
+std::vector<Tensor> layernorm_fwd(Tensor x, Tensor o, Tensor gamma, Tensor beta, double eps, double p, int64_t seed) {
+  check_rows(x, "x");
+  check_rows(o, "o");
+  TORCH_CHECK(o.sizes() == x.sizes(), "o like x");
+  const int64_t D = x.size(-1), R = x.numel() / D;
+  check_dim(D);
+  check_gpu(gamma, "gamma");
+  check_gpu(beta, "beta");
+  const bool wb = gamma.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(gamma.numel() == D && beta.numel() == D && beta.scalar_type() == gamma.scalar_type() &&
+                  (wb || gamma.scalar_type() == torch::kFloat32), "gamma/beta [D], fp32 or bf16");
+  const c10::DeviceGuard guard(x.device());
+  auto s = torch::empty_like(x), y = torch::empty_like(x);
+  auto fopt = x.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({R}, fopt), rstd = torch::empty({R}, fopt);
+  psamd::launch_layernorm_fwd(u16(x), u16(o), gamma.data_ptr(), beta.data_ptr(), wb, u16m(s), u16m(y),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), R, D, static_cast<float>(eps),
+                              static_cast<float>(p), static_cast<uint64_t>(seed), cur_stream(x));
+  return {s, y, mean, rstd};
+}
+
+// -> [dx (residual input), do (dropout input), dgamma, dbeta]
+std::vector<Tensor> layernorm_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, double p, int64_t seed) {
+  check_rows(dy, "dy");
+  check_rows(s, "s");
+  TORCH_CHECK(dy.sizes() == s.sizes(), "dy like s");
+  const int64_t D = s.size(-1), R = s.numel() / D;
+  check_dim(D);
+  const c10::DeviceGuard guard(s.device());
+  auto dx = torch::empty_like(s), dout = torch::empty_like(s);
+  auto fopt = s.options().dtype(torch::kFloat32);
+  const int parts = psamd::layernorm_bwd_parts(static_cast<int>(R));
+  auto part = torch::empty({2, parts, D}, fopt);
+  auto dg = torch::empty({D}, fopt), db = torch::empty({D}, fopt);
+  psamd::launch_layernorm_bwd(u16(dy), u16(s), gamma.data_ptr(), gamma.scalar_type() == torch::kBFloat16,
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                              u16m(dx), u16m(dout), part.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(),
+                              R, D, static_cast<float>(p), static_cast<uint64_t>(seed), cur_stream(s));
+  return {dx, dout, dg, db};
+}
+
+Tensor swiglu_fwd(Tensor gu) {
+  check_rows(gu, "gu");
+  const int64_t F2 = gu.size(-1), R = gu.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0, "2F % 16");
+  const c10::DeviceGuard guard(gu.device());
+  auto shape = gu.sizes().vec();
+  shape.back() = F2 / 2;
+  auto h = torch::empty(shape, gu.options());
+  psamd::launch_swiglu_fwd(u16(gu), u16m(h), R, static_cast<int>(F2 / 2), cur_stream(gu));
+  return h;
+}
+
+Tensor swiglu_bwd(Tensor dh, Tensor gu) {
+  check_rows(dh, "dh");
+  check_rows(gu, "gu");
+  const int64_t F2 = gu.size(-1), R = gu.numel() / F2;
+  TORCH_CHECK(dh.numel() == R * (F2 / 2), "dh [.., F]");
+  const c10::DeviceGuard guard(gu.device());
+  auto dgu = torch::empty_like(gu);
+  psamd::launch_swiglu_bwd(u16(dh), u16(gu), u16m(dgu), R, static_cast<int>(F2 / 2), cur_stream(gu));
+  return dgu;
+}
+
+// qkv [B, S, H + 2KV, hd] -> [q [B,H,S,hd], k [B,KV,S,hd], v [B,KV,S,hd]]; cs [S, hd/2, 2] fp32
+std::vector<Tensor> rope_split_fwd(Tensor qkv, Tensor cs, int64_t H, int64_t KV) {
+  check_rows(qkv, "qkv");
+  check_f32(cs, "cs");
+  TORCH_CHECK(qkv.dim() == 4 && qkv.size(2) == H + 2 * KV, "qkv [B, S, H+2KV, hd]");
+  const int64_t B = qkv.size(0), S = qkv.size(1), hd = qkv.size(3);
+  TORCH_CHECK(hd % 16 == 0 && cs.numel() == S * hd, "hd % 16, cs [S, hd/2, 2]");
+  const c10::DeviceGuard guard(qkv.device());
+  auto q = torch::empty({B, H, S, hd}, qkv.options());
+  auto k = torch::empty({B, KV, S, hd}, qkv.options());
+  auto v = torch::empty({B, KV, S, hd}, qkv.options());
+  psamd::launch_rope_split_fwd(u16(qkv), cs.data_ptr<float>(), u16m(q), u16m(k), u16m(v), B, S, H, KV, hd,
+                               cur_stream(qkv));
+  return {q, k, v};
+}
+
+Tensor rope_split_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cs) {
+  check_rows(dq, "dq");
+  check_rows(dk, "dk");
+  check_rows(dv, "dv");
+  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), hd = dq.size(3), KV = dk.size(1);
+  TORCH_CHECK(dk.sizes() == dv.sizes() && dk.size(0) == B && dk.size(2) == S && dk.size(3) == hd, "dk/dv [B,KV,S,hd]");
+  const c10::DeviceGuard guard(dq.device());
+  auto dqkv = torch::empty({B, S, H + 2 * KV, hd}, dq.options());
+  psamd::launch_rope_split_bwd(u16(dq), u16(dk), u16(dv), cs.data_ptr<float>(), u16m(dqkv), B, S, H, KV, hd,
+                               cur_stream(dq));
+  return dqkv;
+}
+
 // ------------------------------------------------------------------------------ DLRM interaction
 static void check_interact(const Tensor& x, const Tensor& e) {
   check_gpu(x, "x");
@@ -735,6 +884,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize_sums", &bn_finalize_sums);
   m.def("stem_conv_wrw", &stem_conv_wrw);
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_split_fwd", &rope_split_fwd);
+  m.def("rope_split_bwd", &rope_split_bwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),

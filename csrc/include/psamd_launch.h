@@ -148,6 +148,26 @@ void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshi
 void launch_stem_conv_wrw(const uint16_t* x, int cin, const uint16_t* dz, float* ws, float* dwp, int N, int H, int W,
                           int OH, int OW, hipStream_t s);
 
+// ---------------------------------------------------------------- transformer.hip (row / elementwise)
+void launch_rmsnorm_fwd(const uint16_t* x, const uint16_t* r, const void* w, bool w_bf16, uint16_t* s, uint16_t* y,
+                        float* rstd, int R, int D, float eps, hipStream_t st);
+int rmsnorm_bwd_parts(int R);
+void launch_rmsnorm_bwd(const uint16_t* dy, const uint16_t* s, const void* w, bool w_bf16, const float* rstd,
+                        const uint16_t* ds_in, uint16_t* dx, float* wpart, float* dw, int R, int D, hipStream_t st);
+void launch_layernorm_fwd(const uint16_t* x, const uint16_t* o, const void* gamma, const void* beta, bool w_bf16,
+                          uint16_t* s, uint16_t* y, float* mean, float* rstd, int R, int D, float eps, float p,
+                          uint64_t seed, hipStream_t st);
+int layernorm_bwd_parts(int R);
+void launch_layernorm_bwd(const uint16_t* dy, const uint16_t* s, const void* gamma, bool w_bf16, const float* mean,
+                          const float* rstd, uint16_t* dx, uint16_t* dout, float* part, float* dgamma, float* dbeta,
+                          int R, int D, float p, uint64_t seed, hipStream_t st);
+void launch_swiglu_fwd(const uint16_t* gu, uint16_t* h, int64_t R, int F, hipStream_t st);
+void launch_swiglu_bwd(const uint16_t* dh, const uint16_t* gu, uint16_t* dgu, int64_t R, int F, hipStream_t st);
+void launch_rope_split_fwd(const uint16_t* qkv, const float* cs, uint16_t* q, uint16_t* k, uint16_t* v, int B, int S,
+                           int H, int KV, int hd, hipStream_t st);
+void launch_rope_split_bwd(const uint16_t* dq, const uint16_t* dk, const uint16_t* dv, const float* cs,
+                           uint16_t* dqkv, int B, int S, int H, int KV, int hd, hipStream_t st);
+
 struct BnBwdArgs {
   const uint16_t* dy;
   const uint16_t* y;          // nullable when mask_coef is given (relu, no residual)

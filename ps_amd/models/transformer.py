@@ -18,6 +18,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
+from ..ops.transformer import layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
+
 
 # ------------------------------------------------------------------------------------ BERT
 @dataclass
@@ -51,9 +53,10 @@ class BertLayer(nn.Module):
         p = self.c.dropout if self.training else 0.0
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
         a = a.transpose(1, 2).reshape(b, s, h)
-        x = self.ln1(x + F.dropout(self.proj(a), p, self.training))
+        # post-LN epilogues: LN(x + dropout(sublayer)) as one fused HIP pass each way
+        x = layer_norm_residual(x, self.proj(a), self.ln1.weight, self.ln1.bias, self.c.eps, p, self.training)
         f = self.fc2(F.gelu(self.fc1(x)))
-        return self.ln2(x + F.dropout(f, p, self.training))
+        return layer_norm_residual(x, f, self.ln2.weight, self.ln2.bias, self.c.eps, p, self.training)
 
 
 class BertForMLM(nn.Module):
@@ -148,23 +151,7 @@ class RMSNorm(nn.Module):
         self.eps = eps
 
     def forward(self, x):
-        xf = x.float()
-        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).to(x.dtype) * self.weight
-
-
-def rope_cache(seq: int, dim: int, theta: float, device):
-    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, device=device).float() / dim))
-    t = torch.arange(seq, device=device).float()
-    f = torch.outer(t, inv)
-    return torch.cos(f), torch.sin(f)
-
-
-def apply_rope(x, cos, sin):
-    # x [b, h, s, d]; rotate halves (Llama/HF convention)
-    d = x.shape[-1]
-    x1, x2 = x[..., : d // 2], x[..., d // 2:]
-    c, s = cos[None, None].to(x.dtype), sin[None, None].to(x.dtype)
-    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+        return rms_norm(x, self.weight, self.eps)  # fused HIP kernel on GPU bf16 (ops/transformer.py)
 
 
 class LlamaBlock(nn.Module):
@@ -184,19 +171,23 @@ class LlamaBlock(nn.Module):
         self.w13 = nn.Linear(c.hidden, 2 * c.ffn, bias=False)
         self.w2 = nn.Linear(c.ffn, c.hidden, bias=False)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, r, cs):
+        """Residual stream = x + r (r: the previous block's pending MLP output, None for the
+        first block) -- the add is fused into this block's first RMSNorm, and this block's
+        MLP output is returned pending for the next one."""
         b, s, _ = x.shape
         c = self.c
         hd = c.hidden // c.heads
-        h = self.attn_norm(x)
-        qkv = self.wqkv(h).view(b, s, c.heads + 2 * c.kv_heads, hd).transpose(1, 2)
-        q, k, v = qkv.split([c.heads, c.kv_heads, c.kv_heads], dim=1)
-        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
-        a = F.scaled_dot_product_attention(q, k, v.contiguous(), is_causal=True, enable_gqa=True)
-        x = x + self.wo(a.transpose(1, 2).reshape(b, s, -1))
-        h = self.mlp_norm(x)
-        g, u = self.w13(h).chunk(2, dim=-1)
-        return x + self.w2(F.silu(g) * u)
+        if r is None:
+            h = self.attn_norm(x)
+        else:
+            x, h = rms_norm(x, self.attn_norm.weight, c.eps, residual=r)
+        qkv = self.wqkv(h).view(b, s, c.heads + 2 * c.kv_heads, hd)
+        q, k, v = rope_split(qkv, cs, c.heads, c.kv_heads)  # RoPE + split + transpose, one pass
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
+        o = self.wo(a.transpose(1, 2).reshape(b, s, -1))
+        x, h = rms_norm(x, self.mlp_norm.weight, c.eps, residual=o)
+        return x, self.w2(swiglu(self.w13(h)))
 
 
 class LlamaForCausalLM(nn.Module):
@@ -214,14 +205,15 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, ids, labels=None):
         s = ids.shape[1]
-        cos, sin = rope_cache(s, self.c.hidden // self.c.heads, self.c.rope_theta, ids.device)
-        x = self.embed(ids)
+        cs = rope_table(s, self.c.hidden // self.c.heads, self.c.rope_theta, ids.device)
+        x, r = self.embed(ids), None
         for layer in self.layers:
             if self.checkpointing and self.training:
-                x = checkpoint(layer, x, cos, sin, use_reentrant=False)
+                x, r = checkpoint(layer, x, r, cs, use_reentrant=False)
             else:
-                x = layer(x, cos, sin)
-        logits = self.lm_head(self.norm(x))
+                x, r = layer(x, r, cs)
+        _, h = rms_norm(x, self.norm.weight, self.c.eps, residual=r)
+        logits = self.lm_head(h)
         if labels is None:
             return logits
         return F.cross_entropy(logits[:, :-1].float().reshape(-1, self.c.vocab), labels[:, 1:].reshape(-1))

@@ -1,0 +1,166 @@
+"""Fused transformer row / elementwise ops (csrc/kernels/transformer.hip) with autograd.
+
+  rms_norm(x, w, eps, residual=None)         -> y  |  (s = x + residual, y = RMSNorm(s))
+  layer_norm_residual(x, o, g, b, eps, p)    -> LN(x + dropout_p(o))        (BERT post-LN)
+  swiglu(gu)                                  -> silu(gu[..., :F]) * gu[..., F:]
+  rope_split(qkv, cs, H, KV)                  -> q, k, v  (RoPE + head split + transpose)
+
+GPU bf16 tensors (row length <= 4096, multiple of 8) take the HIP kernels; everything else
+runs the plain torch composition, which is also the numerics oracle in the GPU tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import native
+
+
+def _hip(*ts) -> bool:
+    return all(t is not None and t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def _seed() -> int:
+    # host RNG (no device sync); deterministic under torch.manual_seed
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+# ------------------------------------------------------------------------------ RMSNorm
+def _rms_ref(x, w, eps):
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * w
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        x = x.contiguous()
+        _, y, rstd = native().rmsnorm_fwd(x, None, w.contiguous(), float(eps))
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = native().rmsnorm_bwd(dy.contiguous(), x, w, rstd, None)
+        return dx, dw.to(w.dtype), None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """s = x + r (the residual stream, returned) and y = RMSNorm(s) in one pass; backward
+    folds the stream gradient ds into the norm backward (one pass, dx = dr)."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, eps):
+        s, y, rstd = native().rmsnorm_fwd(x.contiguous(), r.contiguous(), w.contiguous(), float(eps))
+        ctx.save_for_backward(s, w, rstd)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, w, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dsum, dw = native().rmsnorm_bwd(dy.contiguous(), s, w, rstd,
+                                        ds.contiguous() if ds is not None else None)
+        return dsum, dsum, dw.to(w.dtype), None
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None):
+    D = x.shape[-1]
+    ok = _hip(x) and D % 8 == 0 and D <= 4096 and w.is_cuda and w.dtype in (torch.bfloat16, torch.float32)
+    if residual is None:
+        return _RMSNorm.apply(x, w, eps) if ok else _rms_ref(x, w, eps)
+    if ok and _hip(residual):
+        return _AddRMSNorm.apply(x, residual, w, eps)
+    s = x + residual
+    return s, _rms_ref(s, w, eps)
+
+
+# ------------------------------------------------------------------------------ LayerNorm
+class _LNResidual(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, o, gamma, beta, eps, p):
+        seed = _seed()
+        s, y, mean, rstd = native().layernorm_fwd(x.contiguous(), o.contiguous(), gamma.contiguous(),
+                                                  beta.contiguous(), float(eps), float(p), seed)
+        ctx.save_for_backward(s, gamma, mean, rstd)
+        ctx.p, ctx.seed = float(p), seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, gamma, mean, rstd = ctx.saved_tensors
+        dx, do, dg, db = native().layernorm_bwd(dy.contiguous(), s, gamma, mean, rstd, ctx.p, ctx.seed)
+        return dx, do, dg.to(gamma.dtype), db.to(gamma.dtype), None, None
+
+
+def layer_norm_residual(x: torch.Tensor, o: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                        p: float = 0.0, training: bool = True) -> torch.Tensor:
+    """LayerNorm(x + dropout_p(o)) -- the BERT sublayer epilogue in one pass each way."""
+    p = float(p) if training else 0.0
+    D = x.shape[-1]
+    if _hip(x, o) and D % 8 == 0 and D <= 4096 and gamma.dtype in (torch.bfloat16, torch.float32):
+        return _LNResidual.apply(x, o, gamma, beta, eps, p)
+    return F.layer_norm(x + F.dropout(o, p, training), (D,), gamma, beta, eps)
+
+
+# ------------------------------------------------------------------------------ SwiGLU
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return native().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return native().swiglu_bwd(dh.contiguous(), gu)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if _hip(gu) and gu.shape[-1] % 16 == 0:
+        return _SwiGLU.apply(gu)
+    g, u = gu.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+# ------------------------------------------------------------------------------ RoPE
+def rope_table(seq: int, hd: int, theta: float, device) -> torch.Tensor:
+    """[S, hd/2, 2] fp32 (cos, sin) -- rotate-halves convention (Llama / HF)."""
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, device=device).float() / hd))
+    f = torch.outer(torch.arange(seq, device=device).float(), inv)
+    return torch.stack([torch.cos(f), torch.sin(f)], dim=-1).contiguous()
+
+
+def _rope_ref(x, cs):
+    d = x.shape[-1]
+    c, s = cs[..., 0][None, None].to(x.dtype), cs[..., 1][None, None].to(x.dtype)
+    x1, x2 = x[..., : d // 2], x[..., d // 2:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+class _RopeSplit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cs, H, KV):
+        q, k, v = native().rope_split_fwd(qkv.contiguous(), cs, int(H), int(KV))
+        ctx.save_for_backward(cs)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        (cs,) = ctx.saved_tensors
+        dq = dq if dq is not None else None
+        return native().rope_split_bwd(dq.contiguous(), dk.contiguous(), dv.contiguous(), cs), None, None, None
+
+
+def rope_split(qkv: torch.Tensor, cs: torch.Tensor, H: int, KV: int):
+    """qkv [B, S, H + 2 KV, hd] -> q [B, H, S, hd], k/v [B, KV, S, hd] with RoPE on q and k."""
+    if _hip(qkv) and qkv.shape[-1] % 16 == 0:
+        return _RopeSplit.apply(qkv, cs, H, KV)
+    x = qkv.transpose(1, 2)
+    q, k, v = x.split([H, KV, KV], dim=1)
+    return _rope_ref(q, cs), _rope_ref(k, cs), v
