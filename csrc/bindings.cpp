@@ -846,10 +846,159 @@ Tensor act_bwd(Tensor dy, Tensor y, int64_t act) {
   return dz;
 }
 
+// ------------------------------------------------------------------------------ implicit-GEMM convs (convgemm.hip)
+static const float* f32_opt(const c10::optional<Tensor>& t, int64_t n, const char* name) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  check_f32(*t, name);
+  TORCH_CHECK(t->numel() == n, name, ": expected ", n, " elements, got ", t->numel());
+  return t->data_ptr<float>();
+}
+
+// geo = [H, W, OH, OW, ks, stride, pad] of a [images*H*W, C] NHWC row tensor -> (geometry, images)
+static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::vector<int64_t>& geo) {
+  TORCH_CHECK(geo.size() == 7, "geo = [H, W, OH, OW, ks, stride, pad]");
+  const int64_t H = geo[0], W = geo[1], OH = geo[2], OW = geo[3], ks = geo[4], st = geo[5], pd = geo[6];
+  TORCH_CHECK(H > 0 && W > 0 && ks >= 1 && ks <= 7 && st >= 1 && st <= 4 && pd >= 0 && pd < ks, "conv geometry");
+  TORCH_CHECK(OH == (H + 2 * pd - ks) / st + 1 && OW == (W + 2 * pd - ks) / st + 1, "output map size");
+  const int64_t C = a.size(1);
+  TORCH_CHECK(C % 64 == 0, "input channels must be a multiple of 64");
+  TORCH_CHECK(a.size(0) % (H * W) == 0, "rows of the input must be images * H * W");
+  psamd::ConvGeo g{static_cast<int>(H), static_cast<int>(W), static_cast<int>(OH), static_cast<int>(OW),
+                   static_cast<int>(C), static_cast<int>(ks), static_cast<int>(st), static_cast<int>(pd)};
+  return {g, a.size(0) / (H * W)};
+}
+
+// c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> [c, BN partials [2, G, N] (epi 1/3)]
+std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10::optional<Tensor> pro, int64_t epi,
+                              c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
+                              c10::optional<Tensor> mean, c10::optional<Tensor> invstd) {
+  check_rows(a, "a");
+  check_rows(b, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
+  const auto gi = conv_geo(a, geo);
+  const psamd::ConvGeo g = gi.first;
+  const int64_t N = b.size(0), K = b.size(1);
+  TORCH_CHECK(K == static_cast<int64_t>(g.ks) * g.ks * g.C, "b must be [N, ks*ks*C]");
+  TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "epi in 0..4");
+  const int64_t M = gi.second * g.OH * g.OW;
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "pixel count");
+  const uint16_t* auxp = nullptr;
+  if (epi >= 2) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "epi ", epi, " needs aux");
+    check_rows(*aux, "aux");
+    const int64_t want = epi == 4 ? gi.second * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) * N : M * N;
+    TORCH_CHECK(aux->numel() == want, "aux has ", aux->numel(), " elements, expected ", want);
+    auxp = u16(*aux);
+  }
+  if (epi == 3) TORCH_CHECK(mc.has_value() && mean.has_value() && invstd.has_value(), "epi 3 needs mc, mean, invstd");
+  const c10::DeviceGuard guard(a.device());
+  auto c = torch::empty({M, N}, a.options());
+  auto fopt = a.options().dtype(torch::kFloat32);
+  const int G = psamd::conv_fwd_groups(static_cast<int>(M), static_cast<int>(N));
+  const bool sums = epi == 1 || epi == 3;
+  Tensor part = sums ? torch::empty({2, G, N}, fopt) : Tensor();
+  psamd::ConvGemmArgs p{};
+  p.a = u16(a);
+  p.b = u16(b);
+  p.c = u16m(c);
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.g = g;
+  p.pro = f32_opt(pro, 2 * g.C, "pro");
+  p.epi = static_cast<int>(epi);
+  p.aux = auxp;
+  p.kshift = f32_opt(kshift, N, "kshift");
+  p.mc = f32_opt(mc, 2 * N, "mc");
+  p.mean = f32_opt(mean, N, "mean");
+  p.invstd = f32_opt(invstd, N, "invstd");
+  p.part = sums ? part.data_ptr<float>() : nullptr;
+  psamd::launch_conv_fwd(p, cur_stream(a));
+  return {c, part};
+}
+
+// dW [N, ks*ks*C] (bf16) = sum_m dz[m, :]^T f(x[src(m, k)])
+Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<Tensor> pro) {
+  check_rows(dz, "dz");
+  check_rows(x, "x");
+  TORCH_CHECK(dz.dim() == 2 && x.dim() == 2, "dz [M, N], x [rows, C]");
+  const auto gi = conv_geo(x, geo);
+  const psamd::ConvGeo g = gi.first;
+  const int64_t M = dz.size(0), N = dz.size(1), K = static_cast<int64_t>(g.ks) * g.ks * g.C;
+  TORCH_CHECK(M == gi.second * g.OH * g.OW, "dz rows must be images * OH * OW");
+  TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
+  const c10::DeviceGuard guard(dz.device());
+  auto ws = torch::empty({psamd::conv_wgrad_ws(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), g.C)},
+                         dz.options().dtype(torch::kFloat32));
+  auto dw = torch::empty({N, K}, dz.options());
+  psamd::ConvWgradArgs p{};
+  p.dz = u16(dz);
+  p.x = u16(x);
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.g = g;
+  p.pro = f32_opt(pro, 2 * g.C, "pro");
+  p.ws = ws.data_ptr<float>();
+  p.dw = u16m(dw);
+  psamd::launch_conv_wgrad(p, cur_stream(dz));
+  return dw;
+}
+
+// y = act(x * scale + shift [+ res [* rscale + rshift]]) from precomputed coefficients [scale | shift]
+Tensor bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> res, c10::optional<Tensor> rcoef, int64_t act) {
+  check_rows(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "x [R, C], C % 8");
+  const int64_t R = x.size(0), C = x.size(1);
+  check_f32(coef, "coef");
+  TORCH_CHECK(coef.numel() == 2 * C, "coef = [scale | shift]");
+  const bool hr = res.has_value() && res->defined();
+  if (hr) {
+    check_rows(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res like x");
+  }
+  const float* rc = f32_opt(rcoef, 2 * C, "rcoef");
+  TORCH_CHECK(!rc || hr, "rcoef needs res");
+  const c10::DeviceGuard guard(x.device());
+  auto y = torch::empty_like(x);
+  psamd::launch_bn_apply_coef(u16(x), hr ? u16(*res) : nullptr, coef.data_ptr<float>(), rc, u16m(y), R,
+                              static_cast<int>(C), static_cast<int>(act), cur_stream(x));
+  return y;
+}
+
+// BN backward from producer partial sums part [2, G, C] (conv_gemm epi 3); g = masked gradient
+std::vector<Tensor> bn_bwd_partials(Tensor g, Tensor x, Tensor part, c10::optional<Tensor> gamma, Tensor mean,
+                                    Tensor invstd) {
+  check_rows(g, "g");
+  check_rows(x, "x");
+  TORCH_CHECK(x.dim() == 2 && g.sizes() == x.sizes() && x.size(1) % 8 == 0, "g/x [R, C], C % 8");
+  const int64_t R = x.size(0), C = x.size(1);
+  check_f32(part, "part");
+  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.size(2) == C, "part [2, G, C]");
+  const int G = static_cast<int>(part.size(1));
+  const c10::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(torch::kFloat32);
+  auto dx = torch::empty_like(x);
+  auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt), coef = torch::empty({3 * C}, fopt);
+  psamd::launch_bn_bwd_partials(part.data_ptr<float>(), part.data_ptr<float>() + G * C, G, u16(g), u16(x),
+                                f32_opt(gamma, C, "gamma"), f32_opt(mean, C, "mean"), f32_opt(invstd, C, "invstd"),
+                                dg.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), u16m(dx), R,
+                                static_cast<int>(C), cur_stream(x));
+  return {dx, dg, db};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "ps_amd HIP kernels for MI355X (gfx950)";
+  m.def("conv_gemm", &conv_gemm, py::arg("a"), py::arg("b"), py::arg("geo"), py::arg("pro") = py::none(),
+        py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
+  m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
+        py::arg("rcoef") = py::none(), py::arg("act") = 1);
+  m.def("bn_bwd_partials", &bn_bwd_partials);
   m.def("fused_opt", &fused_opt);
   m.def("sparse_opt", &sparse_opt);
   m.def("sumsq", &sumsq);

@@ -202,4 +202,49 @@ void launch_dlrm_interact_fwd(const uint16_t* x, const uint16_t* e, uint16_t* ou
 void launch_dlrm_interact_bwd(const uint16_t* x, const uint16_t* e, const uint16_t* dout, uint16_t* dx, uint16_t* de,
                               int B, int T, int D, hipStream_t s);
 
+// ---------------------------------------------------------------- convgemm.hip (MFMA implicit-GEMM convs)
+// NHWC conv geometry of the A operand: input map H x W x C, output map OH x OW, square kernel
+// ks with stride / pad.  Reduction index k = (kh * ks + kw) * C + c (channels_last weight order).
+struct ConvGeo {
+  int H, W, OH, OW, C, ks, stride, pad;
+};
+struct ConvGemmArgs {
+  const uint16_t* a;    // [images, H, W, C] bf16
+  const uint16_t* b;    // [N, K] bf16, K = ks * ks * C
+  uint16_t* c;          // [M, N] bf16, M = images * OH * OW
+  int M, N, K;
+  ConvGeo g;
+  const float* pro;     // [scale | shift] (2C): A := relu(A * scale + shift) while staging; nullable
+  int epi;              // 0 store, 1 + BN partial sums, 2 + residual, 3 ReLU mask + BN-backward sums,
+                        // 4 + residual of the (OH+1)/2 x (OW+1)/2 map at even (h, w)
+  const uint16_t* aux;  // epi 2/4: residual rows; epi 3: BN input z [M, N]
+  const float* kshift;  // epi 1: shift of the partial sums [N] (nullable = 0)
+  const float* mc;      // epi 3: [scale | shift] (2N) of that BN (ReLU mask)
+  const float* mean;    // epi 3: [N]
+  const float* invstd;  // epi 3: [N]
+  float* part;          // epi 1/3: [2][conv_fwd_groups(M, N)][N] block partial sums
+};
+int conv_mtiles(int M);
+int conv_fwd_groups(int M, int N);
+void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
+
+struct ConvWgradArgs {
+  const uint16_t* dz;   // [M, N] output gradient rows
+  const uint16_t* x;    // [images, H, W, C] input map
+  int M, N, K;          // K = ks * ks * C
+  ConvGeo g;
+  const float* pro;     // [scale | shift] (2C) applied to x while staging; nullable
+  float* ws;            // conv_wgrad_ws(M, N, K, C) floats
+  uint16_t* dw;         // [N, K] bf16
+};
+int64_t conv_wgrad_ws(int M, int N, int K, int C);
+void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
+// BN helpers for the fused bottleneck (bn_act.hip): y = act(x*scale + shift [+ res [* rscale + rshift]])
+void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* coef, const float* rcoef, uint16_t* y,
+                          int64_t R, int C, int act, hipStream_t s);
+// BN backward from producer partial sums pd/px [G][C] (g = already-masked output gradient)
+void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
+                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                            float* coef, uint16_t* dx, int64_t R, int C, hipStream_t s);
+
 }  // namespace psamd

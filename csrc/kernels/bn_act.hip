@@ -514,4 +514,86 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
 #undef PSAMD_BN_BWD
 }
 
+// ------------------------------------------------------------------------------ fused-bottleneck helpers
+// y = act(x * scale + shift + res * rscale + rshift): the bottleneck output when the identity
+// branch is a downsample conv whose BN is applied in the same pass (its output never hits HBM).
+template <int ACT, bool FIXED_C>
+__global__ __launch_bounds__(256) void bn_apply_dual_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ r,
+                                                            const float* __restrict__ coef,
+                                                            const float* __restrict__ rcoef, uint16_t* __restrict__ y,
+                                                            int64_t nvec, int C) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int cvec = C / 8;
+  const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  float sc[8], sh[8], rs[8], rh[8];
+  auto coefs = [&](int c) {
+    load8(coef, c, sc);
+    load8(coef + C, c, sh);
+    load8(rcoef, c, rs);
+    load8(rcoef + C, c, rh);
+  };
+  if constexpr (FIXED_C) coefs(static_cast<int>(v0 % cvec) * 8);
+  for (int64_t v = v0; v < nvec; v += stride) {
+    if constexpr (!FIXED_C) coefs(static_cast<int>(v % cvec) * 8);
+    float a[8], b[8];
+    load8(x, v * 8, a);
+    load8(r, v * 8, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = a[j] * sc[j] + sh[j] + (b[j] * rs[j] + rh[j]);
+      if constexpr (ACT == 1) o = o > 0.f ? o : 0.f;
+      a[j] = o;
+    }
+    store8(y, v * 8, a);
+  }
+}
+
+void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* coef, const float* rcoef, uint16_t* y,
+                          int64_t R, int C, int act, hipStream_t s) {
+  const int64_t nvec = R * C / 8;
+  if (nvec <= 0) return;
+  const int grid = stream_grid(nvec, 256);
+  const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
+#define PSAMD_APPLY(K, ...)                                                                              \
+  if (fixed) hipLaunchKernelGGL((K<__VA_ARGS__, true>), dim3(grid), dim3(256), 0, s, ARGS);            \
+  else hipLaunchKernelGGL((K<__VA_ARGS__, false>), dim3(grid), dim3(256), 0, s, ARGS)
+  if (rcoef) {
+#define ARGS x, res, coef, rcoef, y, nvec, C
+    if (act == 1) { PSAMD_APPLY(bn_apply_dual_kernel, 1); }
+    else { PSAMD_APPLY(bn_apply_dual_kernel, 0); }
+#undef ARGS
+  } else {
+#define ARGS x, res, coef, coef + C, y, nvec, C
+    if (res) {
+      if (act == 1) { PSAMD_APPLY(bn_apply_kernel, true, 1); }
+      else { PSAMD_APPLY(bn_apply_kernel, true, 0); }
+    } else {
+      if (act == 1) { PSAMD_APPLY(bn_apply_kernel, false, 1); }
+      else { PSAMD_APPLY(bn_apply_kernel, false, 0); }
+    }
+#undef ARGS
+  }
+#undef PSAMD_APPLY
+}
+
+void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
+                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                            float* coef, uint16_t* dx, int64_t R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, s, pd, px, G, C, R, gamma, mean, invstd,
+                     dgamma, dbeta, coef, coef + C, coef + 2 * C);
+  const int64_t nvec = R * C / 8;
+  if (nvec <= 0) return;
+  const int grid = stream_grid(nvec, 256);
+  const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
+  const uint16_t* none = nullptr;
+  const float* nomc = nullptr;
+  uint16_t* nodres = nullptr;
+  if (fixed)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false, true>), dim3(grid), dim3(256), 0, s, g, none, x, nomc, coef,
+                       coef + C, coef + 2 * C, dx, nodres, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false, false>), dim3(grid), dim3(256), 0, s, g, none, x, nomc, coef,
+                       coef + C, coef + 2 * C, dx, nodres, nvec, C);
+}
+
 }  // namespace psamd

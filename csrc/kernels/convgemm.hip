@@ -1,0 +1,584 @@
+// Convolutions of NHWC (channels_last) bf16 activations as implicit MFMA GEMMs, with the
+// neighbouring BatchNorm passes folded into their prologues / epilogues -- the ResNet-50
+// bottleneck (im2col + conv GEMM + weight gradient, MI355X-native).
+//
+// Output pixel m = (i, oh, ow) reads input pixel (i, oh*s - p + kh, ow*s - p + kw) for tap
+// (kh, kw); the reduction index is k = (kh*ks + kw)*C + c, so the channels_last weight
+// [N][ks][ks][C] is already the K-contiguous B operand and no im2col buffer exists: the
+// staging loads gather A rows tap by tap (C % 64 == 0: a 64-deep stage never straddles taps).
+//
+// At ResNet-50 widths most 1x1 layers are HBM-bound (2MKN FLOPs against 2M(K+N) bytes), so the
+// lever is the number of passes over the activations.  Each GEMM folds adjacent BN work in:
+//
+//   conv_fwd    C[m, n] = sum_k f(A[src(m, k)]) B[n, k]   (forward; the data gradient is the
+//               same GEMM on the transposed / flipped weight)
+//     prologue  f(a) = relu(a * scale_c + shift_c): the previous BN + ReLU applied while A is
+//               staged -- that BN's output is never written (taps outside the map stay 0)
+//     epilogue  1: per-channel partial sums of C about a shift (the next BN's statistics)
+//               2: + residual rows (block-input gradient = conv1 data grad + identity grad)
+//               3: ReLU mask from z*scale + shift and that BN's backward sums sum(g),
+//                  sum(g * xhat) -- its reduce pass
+//               4: + a stride-2 map's rows at even (h, w) (downsample data gradient)
+//   conv_wgrad  dW[n, k] = sum_m dZ[m, n] f(A[src(m, k)]), split over m; both operands are read
+//               transposed from row-major LDS tiles (ds_read_b64_tr_b16); fp32 per-split slabs,
+//               fixed-order reduction (deterministic, no atomics).
+//
+// MFMA v_mfma_f32_32x32x16_bf16 with the weight tile as the A operand, so every lane's
+// accumulator holds 4 consecutive output channels of one pixel; the tile goes through LDS and
+// leaves as 16-byte row pieces, which is also where the epilogue statistics are taken (on the
+// bf16-rounded values the next BN reads).  The forward grid is persistent (2 blocks per CU, a
+// fixed channel tile per block), so the statistics accumulate in registers across pixel tiles
+// and the BN finalize kernels sum only [2][blocks][N] partials in fixed order.
+#include <algorithm>
+
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kBM = 128;  // output pixels per tile (conv_fwd)
+constexpr int kBK = 64;   // reduction depth per LDS stage: 8 x 16-B chunks per row
+constexpr int kWM = 64;   // pixels per LDS stage (conv_wgrad)
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(s16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+// LDS hand-off barrier that waits for this wave's LDS traffic only; __syncthreads() would also
+// drain the prefetched stage's global loads.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Bijective XCD-aware remap (blocks b and b + 8 share an XCD): consecutive logical ids run on
+// one XCD, so the channel tiles of one pixel tile share its A rows through that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// Source of output pixel m: image (-1 past M) and the input coordinates of tap (0, 0).
+struct PixSrc {
+  int img, ih0, iw0;
+};
+
+__device__ __forceinline__ PixSrc pix_src(int m, int M, const ConvGeo& g) {
+  PixSrc s{-1, 0, 0};
+  if (m < M) {
+    const int ohw = g.OH * g.OW;
+    s.img = m / ohw;
+    const int r = m - s.img * ohw, oh = r / g.OW;
+    s.ih0 = oh * g.stride - g.pad;
+    s.iw0 = (r - oh * g.OW) * g.stride - g.pad;
+  }
+  return s;
+}
+
+// Element offset of channel c of tap (kh, kw) of pixel s, or -1 outside the map / past M.
+__device__ __forceinline__ int64_t tap_off(const PixSrc& s, int kh, int kw, int c, const ConvGeo& g) {
+  const int ih = s.ih0 + kh, iw = s.iw0 + kw;
+  if (s.img < 0 || static_cast<unsigned>(ih) >= static_cast<unsigned>(g.H) ||
+      static_cast<unsigned>(iw) >= static_cast<unsigned>(g.W))
+    return -1;
+  return ((static_cast<int64_t>(s.img) * g.H + ih) * g.W + iw) * g.C + c;
+}
+
+// [rows][64] tiles read as ds_read_b128 fragments: 16-B chunk c of row r is stored at chunk
+// c ^ ((r >> 1) & 7), so every 16-lane group of a fragment read (rows {0-3,12-15,20-27} or
+// {4-11,16-19,28-31} of a 32-row block, one chunk) hits 16 distinct bank slots.
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// [64][RL] tiles read transposed (ds_read_b64_tr_b16): a 32-lane half reads rows r0..r0+3 x 64
+// contiguous bytes; the chunk XOR gives each of the 4 rows its own quarter of the bank row.
+template <int RL>
+__device__ __forceinline__ int tr_off(int r, int col) {
+  const int c = col >> 3;
+  const int pc = RL == 128 ? (c ^ ((r & 3) << 2)) : (c ^ (((r >> 1) & 1) << 2));
+  return r * RL + pc * 8 + (col & 7);
+}
+
+// 32x32x16 MFMA operand from a [64][RL] tile read transposed: lane l receives
+// T[16 s + 8 (l >> 5) + j][c0 + (l & 31)], j = 0..7 (two 4-row transposed reads; lane 4q + p of
+// each 16-lane group addresses row q, columns 4p..4p+3 of its block).
+template <int RL>
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* T, int s, int c0, int lane) {
+  const int gi = lane >> 4, i16 = lane & 15;
+  const int r = 16 * s + 8 * (gi >> 1) + (i16 >> 2);
+  const int col = c0 + 16 * (gi & 1) + 4 * (i16 & 3);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(T + tr_off<RL>(r, col)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(T + tr_off<RL>(r + 4, col)));
+  return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+}
+
+__device__ __forceinline__ u16x8 bn_relu8(u16x8 v, const float (&sc)[8], const float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float f = bf16_to_f32(v[j]) * sc[j] + sh[j];
+    v[j] = f32_to_bf16(f > 0.f ? f : 0.f);
+  }
+  return v;
+}
+
+constexpr u16x8 kZero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ conv_fwd
+// Persistent grid of nN * GM blocks of 256 threads (4 waves: 2 pixel halves x 2 channel halves):
+// block (n-tile nt, group mg) computes pixel tiles mg, mg + GM, ... of channel tile nt (a fixed
+// channel tile, so the epilogue statistics stay in registers across tiles and the partials are
+// [2][GM][N]).  Tile 128 pixels x BN channels; K in 64-deep stages through two LDS buffers, the
+// next stage's -- or, after the last stage, the next tile's first stage's -- global loads in
+// flight under the current MFMAs and the epilogue.
+template <int BN, bool PRO, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
+  constexpr int TN = BN / 64;              // 32-channel MFMA blocks per wave
+  constexpr int BCH = BN / 32;             // B-tile chunks per thread per stage
+  constexpr int STAGE = (kBM + BN) * kBK;  // bf16 per LDS stage
+  constexpr int CS = BN + 8;               // output tile row stride (bf16): 16-B aligned rows
+  constexpr int STAGE_BYTES = 2 * STAGE * 2;
+  constexpr int EPI_BYTES = kBM * CS * 2 + 8 * BN * 4;
+  constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_BYTES / 2];
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nN = p.N / BN, mtiles = (p.M + kBM - 1) / kBM;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int mg = L / nN, n0 = (L - mg * nN) * BN;
+
+  // staging: thread t moves 16-B chunk (t & 7) of tile rows (t >> 3) + 32 i
+  const int srow = t >> 3, sc = t & 7;
+  PixSrc src[4];
+  auto set_tile = [&](int mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) src[i] = pix_src(mt * kBM + srow + 32 * i, p.M, g);
+  };
+  const uint16_t* bptr = p.b + static_cast<int64_t>(n0 + srow) * p.K + sc * 8;
+  u16x8 ra[4], rb[BCH];
+  unsigned ok = 0;
+  float psc[8], psh[8];
+  auto gload = [&](int k0) {
+    const int tap = k0 / g.C, cc = k0 - tap * g.C;
+    const int kh = tap / g.ks, kw = tap - kh * g.ks;
+    ok = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = tap_off(src[i], kh, kw, cc + sc * 8, g);
+      ok |= (o >= 0 ? 1u : 0u) << i;
+      // out-of-map taps / rows past M read element 0 (in bounds) and are zeroed in LDS
+      ra[i] = *reinterpret_cast<const u16x8*>(p.a + (o >= 0 ? o : 0));
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      rb[i] = *reinterpret_cast<const u16x8*>(bptr + static_cast<int64_t>(32 * i) * p.K + k0);
+    if constexpr (PRO) {
+      load8(p.pro, cc + sc * 8, psc);
+      load8(p.pro + g.C, cc + sc * 8, psh);
+    }
+  };
+  auto swrite = [&](int buf) {
+    uint16_t* As = lds + buf * STAGE;
+    uint16_t* Bs = As + kBM * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u16x8 v = ra[i];
+      if constexpr (PRO) v = bn_relu8(v, psc, psh);
+      if (!((ok >> i) & 1u)) v = kZero8;
+      const int r = srow + 32 * i;
+      *reinterpret_cast<u16x8*>(As + r * kBK + swz(r, sc) * 8) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int r = srow + 32 * i;
+      *reinterpret_cast<u16x8*>(Bs + r * kBK + swz(r, sc) * 8) = rb[i];
+    }
+  };
+
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (BN / 2);
+  const int fr = lane & 31, fh = lane >> 5;
+  // output pass: thread t owns channels [8 cg, 8 cg + 8) of tile rows r0, r0 + RPP, ...
+  constexpr int CPR = BN / 8, RPP = 256 / CPR;
+  const int cg = t % CPR, r0 = t / CPR, nc = n0 + cg * 8;
+  float s1[8], s2[8], e0[8], e1[8], e2[8], e3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = e0[j] = e1[j] = e2[j] = e3[j] = 0.f;
+  if constexpr (EPI == 1) {
+    if (p.kshift) load8(p.kshift, nc, e0);
+  } else if constexpr (EPI == 3) {
+    load8(p.mc, nc, e0);
+    load8(p.mc + p.N, nc, e1);
+    load8(p.mean, nc, e2);
+    load8(p.invstd, nc, e3);
+  }
+  const int nk = p.K / kBK;
+  uint16_t* Cs = lds;
+
+  if (mg < mtiles) {  // block-uniform
+    set_tile(mg);
+    gload(0);
+    swrite(0);
+    lds_barrier();
+  }
+  for (int mt = mg; mt < mtiles; mt += GM) {
+    const bool next_tile = mt + GM < mtiles;
+    f32x16 acc[TN][2];
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        gload((kt + 1) * kBK);
+      } else if (next_tile) {  // the next tile's first stage, in flight under MFMAs + epilogue
+        set_tile(mt + GM);
+        gload(0);
+      }
+      const uint16_t* As = lds + (kt & 1) * STAGE;
+      const uint16_t* Bs = As + kBM * kBK;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ch = 2 * s + fh;  // this lane's chunk: k = 16 s + 8 fh + j
+        bf16x8_t xa[2], wb[TN];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r = wm + 32 * j + fr;
+          xa[j] = *reinterpret_cast<const bf16x8_t*>(As + r * kBK + swz(r, ch) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          const int r = wn + 32 * i + fr;
+          wb[i] = *reinterpret_cast<const bf16x8_t*>(Bs + r * kBK + swz(r, ch) * 8);
+        }
+        // D[n][m] = sum_k W[n][k] A[m][k]: the weight rows are the MFMA A operand
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[i], xa[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) swrite((kt + 1) & 1);
+      lds_barrier();
+    }
+
+    // accumulators -> bf16 output tile [128][CS]: register q of lane l is channel
+    // (q & 3) + 8 (q >> 2) + 4 (l >> 5), pixel l & 31 -> 4 consecutive channels per 8-B store
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int nl = wn + 32 * i + 8 * q4 + 4 * fh, ml = wm + 32 * j + fr;
+          const u16x4 v = {f32_to_bf16(acc[i][j][4 * q4]), f32_to_bf16(acc[i][j][4 * q4 + 1]),
+                           f32_to_bf16(acc[i][j][4 * q4 + 2]), f32_to_bf16(acc[i][j][4 * q4 + 3])};
+          *reinterpret_cast<u16x4*>(Cs + ml * CS + nl) = v;
+        }
+    lds_barrier();
+    const int m0 = mt * kBM;
+    for (int rr = r0; rr < kBM; rr += RPP) {
+      const int m = m0 + rr;
+      if (m >= p.M) break;
+      u16x8 v = *reinterpret_cast<const u16x8*>(Cs + rr * CS + cg * 8);
+      const int64_t o = static_cast<int64_t>(m) * p.N + nc;
+      if constexpr (EPI == 2 || EPI == 4) {
+        int64_t ro = o;
+        if constexpr (EPI == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
+          const int ohw = g.OH * g.OW;
+          const int i = m / ohw, r = m - i * ohw, h = r / g.OW, w = r - h * g.OW;
+          const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
+          ro = ((h | w) & 1) ? -1 : ((static_cast<int64_t>(i) * RH + (h >> 1)) * RW + (w >> 1)) * p.N + nc;
+        }
+        if (ro >= 0) {
+          const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + ro);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
+        }
+      } else if constexpr (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf16_to_f32(v[j]) - e0[j];
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      } else if constexpr (EPI == 3) {
+        const u16x8 z8 = *reinterpret_cast<const u16x8*>(p.aux + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = bf16_to_f32(z8[j]);
+          const bool on = z * e0[j] + e1[j] > 0.f;
+          const float gv = on ? bf16_to_f32(v[j]) : 0.f;
+          s1[j] += gv;
+          s2[j] += gv * ((z - e2[j]) * e3[j]);
+          if (!on) v[j] = 0;
+        }
+      }
+      *reinterpret_cast<u16x8*>(p.c + o) = v;
+    }
+    if (next_tile) {
+      lds_barrier();  // every wave is done reading the output tile
+      swrite(0);
+      lds_barrier();
+    }
+  }
+  if constexpr (EPI == 1 || EPI == 3) {
+    // threads with equal cg: lanes l ^ CPR, l ^ 2 CPR, ... of a wave, then the 4 waves via LDS
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], off, 64);
+        s2[j] += __shfl_xor(s2[j], off, 64);
+      }
+    float* red = reinterpret_cast<float*>(lds + kBM * CS);
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave * BN + cg * 8 + j] = s1[j];
+        red[(4 + wave) * BN + cg * 8 + j] = s2[j];
+      }
+    }
+    lds_barrier();
+    for (int c = t; c < BN; c += 256) {
+      p.part[mg * static_cast<int64_t>(p.N) + n0 + c] = (red[c] + red[BN + c]) + (red[2 * BN + c] + red[3 * BN + c]);
+      p.part[(static_cast<int64_t>(GM) + mg) * p.N + n0 + c] =
+          (red[4 * BN + c] + red[5 * BN + c]) + (red[6 * BN + c] + red[7 * BN + c]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ conv_wgrad
+// dW tile [n0, n0 + 64 TNO) x [k0, k0 + 64 TKO) over pixels [mb, me): grid = tiles * nsplit
+// blocks; logical id -> tile = id % tiles, split = id / tiles, so blocks on one XCD share a
+// pixel range (dZ / A rows through L2).  4 waves as 2 x 2; 64-pixel stages, two LDS buffers.
+template <int TNO, int TKO, bool PRO>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs p, int rows_per_split) {
+  constexpr int BNO = 64 * TNO, BKO = 64 * TKO;
+  constexpr int STAGE = kWM * (BNO + BKO);
+  constexpr int GCPR = BNO / 8, XCPR = BKO / 8;                 // 16-B chunks per tile row
+  constexpr int GIT = kWM * GCPR / 256, XIT = kWM * XCPR / 256;  // chunks per thread per stage
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE];
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ntk = p.K / BKO, tiles = (p.N / BNO) * ntk;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, tile = L - split * tiles;
+  const int tn = tile / ntk;
+  const int n0 = tn * BNO, k0 = (tile - tn * ntk) * BKO;
+  const int tap = k0 / g.C, cc0 = k0 - tap * g.C, kh = tap / g.ks, kw = tap - kh * g.ks;
+  const int mb = split * rows_per_split;
+  const int me = min(p.M, mb + rows_per_split);
+  const int xc = t % XCPR;  // this thread's A chunk column (fixed: 256 % XCPR == 0)
+  float psc[8], psh[8];
+  if constexpr (PRO) {
+    load8(p.pro, cc0 + xc * 8, psc);
+    load8(p.pro + g.C, cc0 + xc * 8, psh);
+  }
+  u16x8 rg[GIT], rx[XIT];
+  unsigned xok = 0;
+  auto gload = [&](int mc) {
+#pragma unroll
+    for (int i = 0; i < GIT; ++i) {
+      const int id = t + 256 * i, r = id / GCPR, c = id % GCPR;
+      const int m = mc + r < me ? mc + r : mb;
+      rg[i] = *reinterpret_cast<const u16x8*>(p.dz + static_cast<int64_t>(m) * p.N + n0 + c * 8);
+    }
+    xok = 0;
+#pragma unroll
+    for (int i = 0; i < XIT; ++i) {
+      const int r = (t + 256 * i) / XCPR;
+      const PixSrc s = pix_src(mc + r < me ? mc + r : p.M, p.M, g);
+      const int64_t o = tap_off(s, kh, kw, cc0 + xc * 8, g);
+      xok |= (o >= 0 ? 1u : 0u) << i;
+      rx[i] = *reinterpret_cast<const u16x8*>(p.x + (o >= 0 ? o : 0));
+    }
+  };
+  auto swrite = [&](int buf, int mc) {
+    uint16_t* Gs = lds + buf * STAGE;
+    uint16_t* Xs = Gs + kWM * BNO;
+#pragma unroll
+    for (int i = 0; i < GIT; ++i) {
+      const int id = t + 256 * i, r = id / GCPR, c = id % GCPR;
+      *reinterpret_cast<u16x8*>(Gs + tr_off<BNO>(r, c * 8)) = mc + r < me ? rg[i] : kZero8;
+    }
+#pragma unroll
+    for (int i = 0; i < XIT; ++i) {
+      const int r = (t + 256 * i) / XCPR;
+      u16x8 v = rx[i];
+      if constexpr (PRO) v = bn_relu8(v, psc, psh);
+      if (!((xok >> i) & 1u)) v = kZero8;
+      *reinterpret_cast<u16x8*>(Xs + tr_off<BKO>(r, xc * 8)) = v;
+    }
+  };
+
+  const int wn = (wave >> 1) * (BNO / 2), wk = (wave & 1) * (BKO / 2);
+  f32x16 acc[TNO][TKO];
+#pragma unroll
+  for (int i = 0; i < TNO; ++i)
+#pragma unroll
+    for (int j = 0; j < TKO; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int nch = me > mb ? (me - mb + kWM - 1) / kWM : 0;  // block-uniform
+  if (nch > 0) {
+    gload(mb);
+    swrite(0, mb);
+    lds_barrier();
+    for (int ci = 0; ci < nch; ++ci) {
+      const bool more = ci + 1 < nch;
+      const int mc = mb + kWM * ci;
+      if (more) gload(mc + kWM);
+      const uint16_t* Gs = lds + (ci & 1) * STAGE;
+      const uint16_t* Xs = Gs + kWM * BNO;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8_t ga[TNO], xb[TKO];
+#pragma unroll
+        for (int i = 0; i < TNO; ++i) ga[i] = tr_frag<BNO>(Gs, s, wn + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < TKO; ++j) xb[j] = tr_frag<BKO>(Xs, s, wk + 32 * j, lane);
+#pragma unroll
+        for (int i = 0; i < TNO; ++i)
+#pragma unroll
+          for (int j = 0; j < TKO; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) swrite((ci + 1) & 1, mc + kWM);
+      lds_barrier();
+    }
+  }
+  // fp32 slab of this split; register q of lane l: n = .. + (q & 3) + 8 (q >> 2) + 4 (l >> 5),
+  // k = .. + (l & 31) -> two 128-B row segments per store instruction
+  float* sl = p.ws + static_cast<int64_t>(split) * p.N * p.K;
+  const int h = lane >> 5, kl = lane & 31;
+#pragma unroll
+  for (int i = 0; i < TNO; ++i)
+#pragma unroll
+    for (int j = 0; j < TKO; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int n = n0 + wn + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+        sl[static_cast<int64_t>(n) * p.K + k0 + wk + 32 * j + kl] = acc[i][j][q];
+      }
+}
+
+// out[y][e] = sum_{b in [y*per, y*per + per)} in[b][e] in fixed order (bf16 or fp32 out)
+template <bool BF16>
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int nslab, int per, int64_t E,
+                                                          void* __restrict__ out) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= E) return;
+  const int b0 = blockIdx.y * per, b1 = min(nslab, b0 + per);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int b = b0;
+  for (; b + 3 < b1; b += 4) {
+    a0 += in[b * E + e];
+    a1 += in[(b + 1) * E + e];
+    a2 += in[(b + 2) * E + e];
+    a3 += in[(b + 3) * E + e];
+  }
+  for (; b < b1; ++b) a0 += in[b * E + e];
+  const float v = (a0 + a1) + (a2 + a3);
+  if constexpr (BF16) static_cast<uint16_t*>(out)[blockIdx.y * E + e] = f32_to_bf16(v);
+  else static_cast<float*>(out)[blockIdx.y * E + e] = v;
+}
+
+// ------------------------------------------------------------------------------ launchers
+int conv_mtiles(int M) { return (M + kBM - 1) / kBM; }
+
+// pixel-tile groups of the persistent forward grid: nN * GM blocks = 2 resident blocks per CU
+int conv_fwd_groups(int M, int N) {
+  const int nN = N / (N % 128 == 0 ? 128 : 64);
+  return std::max(1, std::min(conv_mtiles(M), 512 / nN));
+}
+
+void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
+  if (a.M <= 0) return;
+  const bool wide = a.N % 128 == 0;
+  const int GM = conv_fwd_groups(a.M, a.N);
+  const int nblk = GM * (a.N / (wide ? 128 : 64));
+#define PSAMD_CF(BN, PRO, EPI) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, PRO, EPI>), dim3(nblk), dim3(256), 0, s, a, GM)
+#define PSAMD_CFE(BN, PRO)               \
+  switch (a.epi) {                       \
+    case 1: PSAMD_CF(BN, PRO, 1); break; \
+    case 2: PSAMD_CF(BN, PRO, 2); break; \
+    case 3: PSAMD_CF(BN, PRO, 3); break; \
+    case 4: PSAMD_CF(BN, PRO, 4); break; \
+    default: PSAMD_CF(BN, PRO, 0); break; \
+  }
+  if (wide) {
+    if (a.pro) { PSAMD_CFE(128, true) } else { PSAMD_CFE(128, false) }
+  } else {
+    if (a.pro) { PSAMD_CFE(64, true) } else { PSAMD_CFE(64, false) }
+  }
+#undef PSAMD_CFE
+#undef PSAMD_CF
+}
+
+namespace {
+struct WPlan {
+  int tno, tko, tiles, nsplit, rows, groups;
+};
+
+// tile widths 128 where the channel counts allow (a k-tile must not straddle taps), splits so
+// that ~512 blocks run, >= 4 stages per split; > 16 slabs reduce in two fixed-order levels
+WPlan wplan(int M, int N, int K, int C) {
+  WPlan w;
+  w.tno = N % 128 == 0 ? 2 : 1;
+  w.tko = C % 128 == 0 ? 2 : 1;
+  w.tiles = (N / (64 * w.tno)) * (K / (64 * w.tko));
+  const int chunks = (M + kWM - 1) / kWM;
+  int ns = (512 + w.tiles - 1) / w.tiles;
+  ns = std::max(1, std::min(ns, chunks / 4));
+  w.rows = ((chunks + ns - 1) / ns) * kWM;
+  w.nsplit = (M + w.rows - 1) / w.rows;
+  w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;
+  return w;
+}
+}  // namespace
+
+int64_t conv_wgrad_ws(int M, int N, int K, int C) {
+  const WPlan w = wplan(M, N, K, C);
+  return static_cast<int64_t>(w.nsplit + w.groups) * N * K;
+}
+
+void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
+  if (a.M <= 0) return;
+  const WPlan w = wplan(a.M, a.N, a.K, a.g.C);
+  const int nblk = w.tiles * w.nsplit;
+#define PSAMD_CW(TN, TK, PRO) \
+  hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO>), dim3(nblk), dim3(256), 0, s, a, w.rows)
+#define PSAMD_CWP(TN, TK) \
+  if (a.pro) { PSAMD_CW(TN, TK, true); } else { PSAMD_CW(TN, TK, false); }
+  if (w.tno == 2) {
+    if (w.tko == 2) { PSAMD_CWP(2, 2) } else { PSAMD_CWP(2, 1) }
+  } else {
+    if (w.tko == 2) { PSAMD_CWP(1, 2) } else { PSAMD_CWP(1, 1) }
+  }
+#undef PSAMD_CWP
+#undef PSAMD_CW
+  const int64_t E = static_cast<int64_t>(a.N) * a.K;
+  const unsigned eb = static_cast<unsigned>((E + 255) / 256);
+  void* dw = a.dw;
+  if (w.groups) {
+    float* mid = a.ws + static_cast<int64_t>(w.nsplit) * E;
+    void* midv = mid;
+    hipLaunchKernelGGL(slab_reduce_kernel<false>, dim3(eb, w.groups), dim3(256), 0, s, a.ws, w.nsplit, 16, E, midv);
+    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, mid, w.groups, w.groups, E, dw);
+  } else {
+    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, a.ws, w.nsplit, w.nsplit, E, dw);
+  }
+}
+
+}  // namespace psamd

@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
+from ..ops.convgemm import fused_block_ok, fused_bottleneck
 from ..ops.pool import MaxPool2d
 
 
@@ -37,8 +38,13 @@ class Bottleneck(nn.Module):
         self.bn3 = BN(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        # whole-block fused path (implicit-GEMM 1x1 convs with the BN passes folded in,
+        # ops/convgemm.py) for GPU bf16 training; the module path below otherwise
+        self.fuse_block = fused_bn
 
     def forward(self, x):
+        if self.fuse_block and fused_block_ok(self, x):
+            return fused_bottleneck(self, x)
         identity = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
             # BN + ReLU fused; bn3 fuses the residual add and the final ReLU (ops/bn.py)

@@ -1,0 +1,191 @@
+"""Implicit-GEMM convolutions with fused BatchNorm for the ResNet-50 bottleneck
+(csrc/kernels/convgemm.hip).
+
+A bottleneck block -- conv1x1 -> BN -> ReLU -> conv3x3 -> BN -> ReLU -> conv1x1 -> BN (+ identity
+or downsample conv1x1 -> BN) -> ReLU -- runs as ONE autograd Function whose 1x1 layers are our
+MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
+
+  forward   z1 = conv1(x)            + bn1 statistics        (GEMM epilogue)
+            y1 = relu(bn1(z1))                               (one apply pass)
+            z2 = conv2(y1) [MIOpen]    bn2 statistics        (one pass)
+            z3 = conv3(relu(bn2(z2))) + bn3 statistics       (bn2 + ReLU in the GEMM prologue:
+                                                              bn2's output is never written)
+            zd = downsample(x)       + bn_d statistics       (stride-2 rows gathered in-kernel)
+            out = relu(bn3(z3) + x  or  bn_d(zd))            (one pass)
+  backward  bn3 backward; its masked gradient is also the identity-branch gradient
+            conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
+            with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
+            conv2 backward [MIOpen], bn1 backward
+            conv1 data grad + identity / downsample gradient (GEMM epilogue), weight grads.
+
+Per block that removes the statistics passes of bn1 / bn3 / bn_d, bn2's output write + re-read,
+bn2's backward reduce pass and the residual-gradient add, and replaces MIOpen's 1x1 solvers (and
+their zero-fill / cast side kernels).  Anything else -- CPU tensors, eval mode, fp32, channel
+counts that are not multiples of 64 -- runs the module-by-module path, which is also the numerics
+oracle in tests/test_convgemm_gpu.py.  ``PS_AMD_FUSED_BLOCK=0`` disables the fused path.
+"""
+from __future__ import annotations
+
+import os
+from typing import List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ._ext import native
+
+
+def rows(x: torch.Tensor) -> torch.Tensor:
+    """NCHW channels_last tensor -> its [N*H*W, C] row view (a copy only if not channels_last)."""
+    n, c, h, w = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def image(y2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    """[N*H*W, C] rows -> NCHW channels_last view."""
+    return y2.view(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def geo(h: int, w: int, ks: int = 1, stride: int = 1, pad: int = 0) -> List[int]:
+    """Geometry vector [H, W, OH, OW, ks, stride, pad] of a square-kernel NHWC convolution."""
+    return [h, w, (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1, ks, stride, pad]
+
+
+def conv_gemm(a, b, g, pro=None, epi=0, aux=None, kshift=None, mc=None, mean=None, invstd=None):
+    """c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> (c, folded BN partials [2, G, N] or None).
+
+    a: [images*H*W, C] bf16 rows; b: [N, ks*ks*C] (channels_last weight order); g: ``geo(...)``;
+    pro: [scale | shift] applied with ReLU to ``a`` while staging; epi: 0 store, 1 + BN statistics
+    (about ``kshift``), 2 + ``aux`` rows, 3 ReLU mask from ``aux`` * mc + shift and BN-backward sums,
+    4 + ``aux`` of the stride-2 map at even (h, w)."""
+    return native().conv_gemm(a, b, g, pro, epi, aux, kshift, mc, mean, invstd)
+
+
+def conv_wgrad(dz, x, g, pro=None):
+    """dW [N, ks*ks*C] bf16 = sum_m dz[m]^T f(x[src(m, k)])."""
+    return native().conv_wgrad(dz, x, g, pro)
+
+
+def _momentum(bn: nn.BatchNorm2d) -> float:
+    return float(bn.momentum if bn.momentum is not None else 0.1)
+
+
+def _finalize(part, kshift, nrows, bn):
+    return native().bn_finalize_sums(part, kshift, nrows, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     _momentum(bn), float(bn.eps))
+
+
+def _mat(w: torch.Tensor) -> torch.Tensor:
+    """1x1 conv weight [N, C, 1, 1] -> [N, C] view."""
+    return w.reshape(w.shape[0], w.shape[1])
+
+
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, blk):
+        nat = native()
+        n, cin, h, w = x.shape
+        s = blk.conv2.stride[0]
+        oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+        gi, go = geo(h, w), geo(oh, ow)
+        x2 = rows(x)
+        bn1, bn2, bn3 = blk.bn1, blk.bn2, blk.bn3
+        k1 = bn1.running_mean.clone()  # shift of the statistics sums (~ the batch mean)
+        z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
+        m1, i1, cf1 = _finalize(p1, k1, n * h * w, bn1)
+        y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)
+        z2 = F.conv2d(image(y1, n, h, w), w2, None, s, 1)
+        z2r = rows(z2)
+        m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
+                                   float(bn2.eps))
+        k3 = bn3.running_mean.clone()
+        z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
+        m3, i3, cf3 = _finalize(p3, k3, n * oh * ow, bn3)
+        if wd is not None:
+            bnd = blk.downsample[1]
+            kd = bnd.running_mean.clone()
+            zd, pd = nat.conv_gemm(x2, _mat(wd), geo(h, w, 1, s), None, 1, None, kd)
+            md, idd, cfd = _finalize(pd, kd, n * oh * ow, bnd)
+            out = nat.bn_apply_coef(z3, cf3, zd, cfd, 1)
+        else:
+            zd = md = idd = None
+            out = nat.bn_apply_coef(z3, cf3, x2, None, 1)
+        ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, out, zd,
+                              m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd)
+        ctx.dims = (n, h, w, s, oh, ow)
+        return image(out, n, oh, ow)
+
+    @staticmethod
+    def backward(ctx, dout):
+        nat = native()
+        (x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, out, zd,
+         m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd) = ctx.saved_tensors
+        n, h, w, s, oh, ow = ctx.dims
+        gi, go = geo(h, w), geo(oh, ow)
+        # bn3 (ReLU mask from the block output); gr, the masked gradient, is the identity gradient
+        dz3, gr, dg3, db3 = nat.bn_act_bwd(rows(dout), out, z3, g3, m3, i3, 1, True, True, None)
+        # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
+        # relu(bn2(z2)) recomputed in the prologue
+        gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t().contiguous(), go, None, 3, z2r, None, cf2, m2, i2)
+        dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
+        dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
+        dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
+                                                          [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                          [True, True, False])
+        dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
+        w1t = _mat(w1).t().contiguous()
+        dwd = dgd = dbd = None
+        if wd is not None:
+            dzd, _, dgd, dbd = nat.bn_act_bwd(gr, None, zd, gd, md, idd, 0, False, True, None)
+            dwd = nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)).view_as(wd)
+            t = nat.conv_gemm(dzd, _mat(wd).t().contiguous(), go)[0]
+            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 4 if s == 2 else 2, t)[0]
+        else:
+            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 2, gr)[0]
+        dw1 = nat.conv_wgrad(dz1, x2, gi)
+        return (image(dx2, n, h, w), dw1.view_as(w1), dg1, db1, dw2, dg2, db2, dw3.view_as(w3), dg3, db3,
+                dwd, dgd, dbd, None)
+
+
+def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
+    """True when ``blk`` (models.resnet.Bottleneck) can run the fused path on ``x``."""
+    if os.environ.get("PS_AMD_FUSED_BLOCK", "1") == "0" or not getattr(blk, "fuse_block", False):
+        return False
+    if not (blk.training and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    ds = blk.downsample
+    bns = [blk.bn1, blk.bn2, blk.bn3] + ([ds[1]] if ds is not None else [])
+    for bn in bns:
+        if not (bn.track_running_stats and bn.affine and bn.weight.dtype == torch.float32
+                and bn.running_mean is not None and bn.running_mean.dtype == torch.float32):
+            return False
+    c1, c2, c3 = blk.conv1, blk.conv2, blk.conv3
+    convs = [c1, c2, c3] + ([ds[0]] if ds is not None else [])
+    if any(not isinstance(c, nn.Conv2d) or c.weight.dtype != torch.bfloat16 or c.bias is not None or c.groups != 1
+           for c in convs):
+        return False
+    if c1.kernel_size != (1, 1) or c1.stride != (1, 1) or c3.kernel_size != (1, 1) or c3.stride != (1, 1):
+        return False
+    if (c2.kernel_size != (3, 3) or c2.padding != (1, 1) or c2.dilation != (1, 1)
+            or c2.stride[0] != c2.stride[1] or c2.stride[0] not in (1, 2)):
+        return False
+    if ds is not None:
+        if len(ds) != 2 or ds[0].kernel_size != (1, 1) or ds[0].stride != c2.stride or ds[0].padding != (0, 0):
+            return False
+        if getattr(ds[1], "act", "none") != "none":
+            return False
+    elif c2.stride != (1, 1) or x.shape[1] != c3.out_channels:
+        return False
+    return all(c % 64 == 0 for c in (x.shape[1], c1.out_channels, c3.out_channels))
+
+
+def fused_bottleneck(blk: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    ds = blk.downsample
+    for bn in [blk.bn1, blk.bn2, blk.bn3] + ([ds[1]] if ds is not None else []):
+        bn.num_batches_tracked.add_(1)
+    wd, gd, bd = (ds[0].weight, ds[1].weight, ds[1].bias) if ds is not None else (None, None, None)
+    return _BottleneckFn.apply(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                               blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk)

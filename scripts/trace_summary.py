@@ -16,6 +16,8 @@ def family(name: str) -> str:
         n = n[5:]
     rules = [
         (r"naive_conv", "miopen naive conv (find)"),
+        (r"psamd::conv_fwd_kernel", "ps_amd implicit-GEMM conv (fwd / dgrad)"),
+        (r"psamd::conv_wgrad_kernel", "ps_amd implicit-GEMM conv (wgrad)"),
         (r"igemm_fwd|conv_fwd|grouped_conv_fwd", "conv fwd"),
         (r"igemm_bwd|bwd_data", "conv bwd-data"),
         (r"igemm_wrw|bwd_weight|wrw", "conv bwd-weight"),

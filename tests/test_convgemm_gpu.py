@@ -1,0 +1,208 @@
+"""Implicit-GEMM convolution kernels (csrc/kernels/convgemm.hip) vs plain-torch fp32 references
+of the same op, and the fused ResNet bottleneck vs the module-by-module path.
+
+Pixel counts are not multiples of the 128-row tile, both 64- and 128-channel tile widths are
+used, stride-2 gathers run on odd map sizes, and the 3x3 geometry (padding taps) is checked
+against F.conv2d."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ps_amd.ops import native
+from ps_amd.ops.convgemm import geo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(t):
+    return t.bfloat16().to(DEV).contiguous()
+
+
+def _close(out, ref, tol=1e-2, amax=0.05):
+    out = out.float().cpu()
+    ref = ref.float().cpu()
+    err = ((out - ref).norm() / ref.norm().clamp_min(1e-12)).item()
+    assert err < tol, f"relative error {err:.3g}"
+    assert (out - ref).abs().max().item() <= amax * ref.abs().max().item() + 1e-3
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def _coef(k, g):
+    return torch.cat([torch.rand(k, generator=g) + 0.5, torch.randn(k, generator=g) * 0.5])
+
+
+def _bn_relu(a, coef):
+    k = a.shape[-1]
+    return torch.relu(a * coef[:k] + coef[k:]).bfloat16().float()
+
+
+def _rnd(*shape, g, scale=1.0):
+    return (torch.randn(*shape, generator=g) * scale).bfloat16().float()
+
+
+SHAPES = [(300, 64, 64), (1000, 128, 256), (128, 256, 128), (4099, 512, 64), (517, 1024, 128)]
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv1x1_forward_with_bn_statistics(M, K, N, pro):
+    g = _gen(M * 7 + K + N)
+    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    coef = _coef(K, g) if pro else None
+    ref = (_bn_relu(a, coef) if pro else a) @ b.t()
+    kshift = torch.randn(N, generator=g) * 0.1
+    c, part = native().conv_gemm(_bf(a), _bf(b), [M, 1, M, 1, 1, 1, 0], coef.to(DEV) if pro else None, 1, None,
+                                 kshift.to(DEV))
+    _close(c, ref)
+    cb = c.float().cpu() - kshift
+    torch.testing.assert_close(part[0].sum(0).cpu(), cb.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), (cb * cb).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES[:3])
+def test_conv1x1_residual_epilogue(M, K, N):
+    g = _gen(M + 1)
+    a, b, r = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5), _rnd(M, N, g=g)
+    c, _ = native().conv_gemm(_bf(a), _bf(b), [M, 1, M, 1, 1, 1, 0], None, 2, _bf(r))
+    _close(c, a @ b.t() + r)
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES[:4])
+def test_conv1x1_bn_backward_epilogue(M, K, N):
+    g = _gen(M + 2)
+    a, b, z = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5), _rnd(M, N, g=g)
+    mc = _coef(N, g)
+    mean, invstd = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+    c, part = native().conv_gemm(_bf(a), _bf(b), [M, 1, M, 1, 1, 1, 0], None, 3, _bf(z), None, mc.to(DEV),
+                                 mean.to(DEV), invstd.to(DEV))
+    mask = (z * mc[:N] + mc[N:]) > 0
+    _close(c, (a @ b.t()) * mask)
+    cg = c.float().cpu()
+    torch.testing.assert_close(part[0].sum(0).cpu(), cg.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), (cg * ((z - mean) * invstd)).sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_conv1x1_stride2_gather_and_strided_residual():
+    n, h, w, K, N = 3, 13, 11, 128, 64
+    g = _gen(3)
+    a, b = _rnd(n * h * w, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    gg = geo(h, w, 1, 2)
+    oh, ow = gg[2], gg[3]
+    c, _ = native().conv_gemm(_bf(a), _bf(b), gg)
+    _close(c, a.view(n, h, w, K)[:, ::2, ::2].reshape(-1, K) @ b.t())
+    # data gradient of a stride-2 downsample added into the full-resolution map (epilogue 4)
+    a2, b2 = _rnd(n * h * w, 64, g=g), _rnd(K, 64, g=g, scale=0.125)
+    t = _rnd(n * oh * ow, K, g=g)
+    c2, _ = native().conv_gemm(_bf(a2), _bf(b2), geo(h, w), None, 4, _bf(t))
+    ref = a2 @ b2.t()
+    ref.view(n, h, w, K)[:, ::2, ::2] += t.view(n, oh, ow, K)
+    _close(c2, ref)
+
+
+@pytest.mark.parametrize("cin,cout,hw,stride", [(64, 64, 14, 1), (128, 128, 9, 2), (64, 128, 7, 1)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv3x3_implicit_gemm_forward_and_wgrad(cin, cout, hw, stride, pro):
+    n = 3
+    g = _gen(cin + cout + hw + stride)
+    x = _rnd(n, hw, hw, cin, g=g)
+    wt = _rnd(cout, cin, 3, 3, g=g, scale=(9 * cin) ** -0.5)
+    coef = _coef(cin, g) if pro else None
+    xin = _bn_relu(x, coef) if pro else x
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), wt, None, stride, 1).permute(0, 2, 3, 1).reshape(-1, cout)
+    gg = geo(hw, hw, 3, stride, 1)
+    wmat = wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin)  # channels_last weight order
+    c, _ = native().conv_gemm(_bf(x.reshape(-1, cin)), _bf(wmat), gg, coef.to(DEV) if pro else None)
+    _close(c, ref)
+    dz = _rnd(n * gg[2] * gg[3], cout, g=g)
+    wv = wt.clone().requires_grad_()
+    yr = F.conv2d(xin.permute(0, 3, 1, 2), wv, None, stride, 1)
+    dw_ref = torch.autograd.grad(yr, wv, dz.view(n, gg[2], gg[3], cout).permute(0, 3, 1, 2))[0]
+    dw = native().conv_wgrad(_bf(dz), _bf(x.reshape(-1, cin)), gg, coef.to(DEV) if pro else None)
+    _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, 9 * cin))
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 64, 64), (5000, 256, 64), (1000, 128, 512), (777, 512, 128)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv1x1_weight_grad(M, N, K, pro):
+    g = _gen(M + N + K)
+    dz, x = _rnd(M, N, g=g), _rnd(M, K, g=g)
+    coef = _coef(K, g) if pro else None
+    ref = dz.t() @ (_bn_relu(x, coef) if pro else x)
+    dw = native().conv_wgrad(_bf(dz), _bf(x), [M, 1, M, 1, 1, 1, 0], coef.to(DEV) if pro else None)
+    _close(dw, ref)
+
+
+def test_conv1x1_weight_grad_stride2():
+    n, h, w = 4, 14, 13
+    gg = geo(h, w, 1, 2)
+    g = _gen(11)
+    dz, x = _rnd(n * gg[2] * gg[3], 256, g=g), _rnd(n * h * w, 128, g=g)
+    dw = native().conv_wgrad(_bf(dz), _bf(x), gg)
+    _close(dw, dz.t() @ x.view(n, h, w, 128)[:, ::2, ::2].reshape(-1, 128))
+
+
+def test_bn_apply_coef_and_backward_from_partials():
+    from ps_amd.ops.bn import bn_act  # noqa: F401  (module import check)
+
+    g = _gen(5)
+    R, C = 999, 192
+    x, r = _rnd(R, C, g=g), _rnd(R, C, g=g)
+    cf, rcf = _coef(C, g), _coef(C, g)
+    y = native().bn_apply_coef(_bf(x), cf.to(DEV), _bf(r), rcf.to(DEV), 1)
+    _close(y, torch.relu(x * cf[:C] + cf[C:] + r * rcf[:C] + rcf[C:]))
+    y0 = native().bn_apply_coef(_bf(x), cf.to(DEV), None, None, 0)
+    _close(y0, x * cf[:C] + cf[C:])
+    # backward from partial sums == backward with its own reduce pass
+    gr = _rnd(R, C, g=g)
+    gamma, mean, invstd = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1, torch.rand(C) + 0.5
+    xhat = (x - mean) * invstd
+    part = torch.stack([gr.sum(0, keepdim=True), (gr * xhat).sum(0, keepdim=True)])
+    dx, dg, db = native().bn_bwd_partials(_bf(gr), _bf(x), part.to(DEV).contiguous(), gamma.to(DEV), mean.to(DEV),
+                                          invstd.to(DEV))
+    ref_dx = gamma * invstd * (gr - gr.mean(0) - xhat * (gr * xhat).mean(0))
+    _close(dx, ref_dx)
+    torch.testing.assert_close(db.cpu(), gr.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dg.cpu(), (gr * xhat).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("inplanes,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2)])
+def test_fused_bottleneck_matches_module_path(inplanes, planes, stride):
+    import torch.nn as nn
+
+    from ps_amd.models.resnet import Bottleneck, prepare_for_mi355x
+    from ps_amd.ops.bn import BatchNormAct2d
+    from ps_amd.ops.convgemm import fused_block_ok
+
+    torch.manual_seed(0)
+    ds = None
+    if stride != 1 or inplanes != planes * 4:
+        ds = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False),
+                           BatchNormAct2d(planes * 4, act="none"))
+    a = Bottleneck(inplanes, planes, stride, ds)
+    for m in a.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    b = copy.deepcopy(a)
+    b.fuse_block = False
+    a, b = prepare_for_mi355x(a.cuda()), prepare_for_mi355x(b.cuda())
+    x = torch.randn(4, inplanes, 15, 15, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    assert fused_block_ok(a, x) and not fused_block_ok(b, x)
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    ya, yb = a(xa), b(xb)
+    _close(ya.detach(), yb.detach(), tol=2e-2, amax=0.1)
+    gout = torch.randn_like(ya)
+    ya.backward(gout)
+    yb.backward(gout)
+    _close(xa.grad, xb.grad, tol=3e-2, amax=0.25)  # bf16 ReLU-mask flips near 0 differ per path
+    for (name, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert p.grad is not None, name
+        _close(p.grad, q.grad, tol=3e-2, amax=0.25)
+    for (name, t), (_, u) in zip(a.named_buffers(), b.named_buffers()):
+        torch.testing.assert_close(t.float(), u.float(), rtol=2e-3, atol=2e-3, msg=name)
