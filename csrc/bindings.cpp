@@ -761,7 +761,7 @@ Tensor maxpool_nhwc_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, 
 
 std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::optional<Tensor> gamma, Tensor mean,
                                Tensor invstd, int64_t act, bool want_dres, bool affine,
-                               c10::optional<Tensor> mask_coef) {
+                               c10::optional<Tensor> mask_coef, c10::optional<Tensor> mbits) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   const bool has_y = y.has_value() && y->defined();
@@ -777,7 +777,12 @@ std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10
     TORCH_CHECK(mask_coef->numel() == 2 * x.size(1), "mask_coef = [scale | shift]");
     TORCH_CHECK(!want_dres, "recomputed relu mask is only valid without a residual");
   }
-  TORCH_CHECK(act == 0 || has_y || has_mc, "relu backward needs y or mask_coef");
+  const bool has_mb = mbits.has_value() && mbits->defined();
+  if (has_mb) {
+    check_gpu(*mbits, "mbits");
+    TORCH_CHECK(mbits->scalar_type() == torch::kUInt8 && mbits->numel() * 8 == x.numel(), "mbits: uint8 [R*C/8]");
+  }
+  TORCH_CHECK(act == 0 || has_y || has_mc || has_mb, "relu backward needs y, mask_coef or mbits");
   const int64_t R = x.size(0), C = x.size(1);
   TORCH_CHECK(C % 8 == 0, "C % 8");
   check_f32(mean, "mean");
@@ -804,6 +809,7 @@ std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10
   a.dbeta = affine ? dbeta.data_ptr<float>() : nullptr;
   a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
   a.dres = want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr;
+  a.mbits = has_mb ? mbits->data_ptr<uint8_t>() : nullptr;
   a.ws = ws.data_ptr<float>();
   a.R = R;
   a.C = static_cast<int>(C);
@@ -871,7 +877,7 @@ static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::v
 // c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> [c, BN partials [2, G, N] (epi 1/3)]
 std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10::optional<Tensor> pro, int64_t epi,
                               c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
-                              c10::optional<Tensor> mean, c10::optional<Tensor> invstd) {
+                              c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits) {
   check_rows(a, "a");
   check_rows(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
@@ -880,7 +886,7 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   const int64_t N = b.size(0), K = b.size(1);
   TORCH_CHECK(K == static_cast<int64_t>(g.ks) * g.ks * g.C, "b must be [N, ks*ks*C]");
   TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
-  TORCH_CHECK(epi >= 0 && epi <= 4, "epi in 0..4");
+  TORCH_CHECK(epi >= 0 && epi <= 5, "epi in 0..5");
   const int64_t M = gi.second * g.OH * g.OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "pixel count");
   const uint16_t* auxp = nullptr;
@@ -892,10 +898,18 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     auxp = u16(*aux);
   }
   if (epi == 3) TORCH_CHECK(mc.has_value() && mean.has_value() && invstd.has_value(), "epi 3 needs mc, mean, invstd");
+  const uint8_t* bitsp = nullptr;
+  if (epi == 5) {
+    TORCH_CHECK(bits.has_value() && bits->defined(), "epi 5 needs bits");
+    check_gpu(*bits, "bits");
+    TORCH_CHECK(bits->scalar_type() == torch::kUInt8 && bits->numel() * 8 == M * N, "bits: uint8 [M * N / 8]");
+    bitsp = bits->data_ptr<uint8_t>();
+  }
+  TORCH_CHECK(!(pro.has_value() && pro->defined()) || epi <= 1, "the BN prologue combines with epilogue 0 or 1 only");
   const c10::DeviceGuard guard(a.device());
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
-  const int G = psamd::conv_fwd_groups(static_cast<int>(M), static_cast<int>(N));
+  const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K)).gm;
   const bool sums = epi == 1 || epi == 3;
   Tensor part = sums ? torch::empty({2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};
@@ -909,6 +923,7 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   p.pro = f32_opt(pro, 2 * g.C, "pro");
   p.epi = static_cast<int>(epi);
   p.aux = auxp;
+  p.bits = bitsp;
   p.kshift = f32_opt(kshift, N, "kshift");
   p.mc = f32_opt(mc, 2 * N, "mc");
   p.mean = f32_opt(mean, N, "mean");
@@ -947,7 +962,9 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
 }
 
 // y = act(x * scale + shift [+ res [* rscale + rshift]]) from precomputed coefficients [scale | shift]
-Tensor bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> res, c10::optional<Tensor> rcoef, int64_t act) {
+// -> [y, ReLU mask bits (uint8 [R*C/8], with want_mask) or empty]
+std::vector<Tensor> bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> res, c10::optional<Tensor> rcoef,
+                                  int64_t act, bool want_mask) {
   check_rows(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "x [R, C], C % 8");
   const int64_t R = x.size(0), C = x.size(1);
@@ -962,9 +979,11 @@ Tensor bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> res, c10::opti
   TORCH_CHECK(!rc || hr, "rcoef needs res");
   const c10::DeviceGuard guard(x.device());
   auto y = torch::empty_like(x);
-  psamd::launch_bn_apply_coef(u16(x), hr ? u16(*res) : nullptr, coef.data_ptr<float>(), rc, u16m(y), R,
-                              static_cast<int>(C), static_cast<int>(act), cur_stream(x));
-  return y;
+  Tensor mb = want_mask ? torch::empty({R * C / 8}, x.options().dtype(torch::kUInt8)) : Tensor();
+  psamd::launch_bn_apply_coef(u16(x), hr ? u16(*res) : nullptr, coef.data_ptr<float>(), rc, u16m(y),
+                              want_mask ? mb.data_ptr<uint8_t>() : nullptr, R, static_cast<int>(C),
+                              static_cast<int>(act), cur_stream(x));
+  return {y, mb};
 }
 
 // BN backward from producer partial sums part [2, G, C] (conv_gemm epi 3); g = masked gradient
@@ -994,10 +1013,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "ps_amd HIP kernels for MI355X (gfx950)";
   m.def("conv_gemm", &conv_gemm, py::arg("a"), py::arg("b"), py::arg("geo"), py::arg("pro") = py::none(),
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
-        py::arg("mean") = py::none(), py::arg("invstd") = py::none());
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
-        py::arg("rcoef") = py::none(), py::arg("act") = 1);
+        py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);
   m.def("bn_bwd_partials", &bn_bwd_partials);
   m.def("fused_opt", &fused_opt);
   m.def("sparse_opt", &sparse_opt);
@@ -1045,7 +1064,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),
-        py::arg("mask_coef") = py::none());
+        py::arg("mask_coef") = py::none(), py::arg("mbits") = py::none());
   m.attr("ONEBIT_CHUNK") = psamd::kOnebitChunk;
   m.attr("ARCH") = "gfx950";
 }

@@ -180,6 +180,7 @@ struct BnBwdArgs {
   float* dbeta;   // nullable
   uint16_t* dx;
   uint16_t* dres;  // nullable: gradient of the fused residual input (= dz)
+  const uint8_t* mbits;  // nullable: ReLU mask bits of the forward output (1 bit / element)
   float* ws;       // [2, G, C] partials + [3, C] coefficients
   int64_t R;
   int C;
@@ -216,16 +217,20 @@ struct ConvGemmArgs {
   ConvGeo g;
   const float* pro;     // [scale | shift] (2C): A := relu(A * scale + shift) while staging; nullable
   int epi;              // 0 store, 1 + BN partial sums, 2 + residual, 3 ReLU mask + BN-backward sums,
-                        // 4 + residual of the (OH+1)/2 x (OW+1)/2 map at even (h, w)
-  const uint16_t* aux;  // epi 2/4: residual rows; epi 3: BN input z [M, N]
+                        // 4 + residual of the (OH+1)/2 x (OW+1)/2 map at even (h, w),
+                        // 5 + residual masked by bits (aux * relu'(forward output))
+  const uint16_t* aux;  // epi 2/4/5: residual rows; epi 3: BN input z [M, N]
+  const uint8_t* bits;  // epi 5: ReLU mask bits of aux's elements
   const float* kshift;  // epi 1: shift of the partial sums [N] (nullable = 0)
   const float* mc;      // epi 3: [scale | shift] (2N) of that BN (ReLU mask)
   const float* mean;    // epi 3: [N]
   const float* invstd;  // epi 3: [N]
-  float* part;          // epi 1/3: [2][conv_fwd_groups(M, N)][N] block partial sums
+  float* part;          // epi 1/3: [2][conv_fwd_plan(M, N, K).gm][N] block partial sums
 };
-int conv_mtiles(int M);
-int conv_fwd_groups(int M, int N);
+struct ConvFwdPlan {
+  int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
+};
+ConvFwdPlan conv_fwd_plan(int M, int N, int K);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 
 struct ConvWgradArgs {
@@ -240,8 +245,9 @@ struct ConvWgradArgs {
 int64_t conv_wgrad_ws(int M, int N, int K, int C);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
 // BN helpers for the fused bottleneck (bn_act.hip): y = act(x*scale + shift [+ res [* rscale + rshift]])
+// mbits (nullable): also write the ReLU mask of y, 1 bit per element
 void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* coef, const float* rcoef, uint16_t* y,
-                          int64_t R, int C, int act, hipStream_t s);
+                          uint8_t* mbits, int64_t R, int C, int act, hipStream_t s);
 // BN backward from producer partial sums pd/px [G][C] (g = already-masked output gradient)
 void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,

@@ -202,11 +202,13 @@ __global__ __launch_bounds__(256) void bn_eval_coef_kernel(int C, float eps, con
 // y = act(x * scale_c + shift_c [+ res]).  FIXED_C: the grid stride is a multiple of C/8, so
 // each thread's channel group never changes -- coefficients are loaded once and the 64-bit
 // modulo leaves the loop.  Two vectors per thread per iteration keep enough loads in flight.
-template <bool RES, int ACT, bool FIXED_C>
+// MASK: also store the ReLU mask of y as one bit per element (byte v <-> elements 8v..8v+7):
+// the backward then reads 1/16 of the bytes it would read from y.
+template <bool RES, int ACT, bool FIXED_C, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, uint16_t* __restrict__ y,
-                                                       int64_t nvec, int C) {
+                                                       int64_t nvec, int C, uint8_t* __restrict__ mb) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int cvec = C / 8;
   const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -230,6 +232,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
       a[j] = o;
     }
     store8(y, v * 8, a);
+    if constexpr (MASK) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (a[j] > 0.f ? 1u : 0u) << j;
+      mb[v] = static_cast<uint8_t>(bits);
+    }
   };
   int64_t v = v0;
   for (; v + stride < nvec; v += 2 * stride) {
@@ -256,6 +264,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 // ACT: 0 identity, 1 relu mask from the saved output y, 2 relu mask recomputed from x with the
 // forward's scale/shift (mc = [scale | shift]) -- no residual, so y > 0 <=> x*scale+shift > 0;
 // saves one tensor read in both backward passes.
+// ACT 3: relu mask from the bit mask written by the forward apply (MASK)
 template <int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                             const uint16_t* __restrict__ y,
@@ -263,7 +272,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
                                                             const float* __restrict__ mc,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int64_t R, int C,
-                                                            float* __restrict__ pd, float* __restrict__ px) {
+                                                            float* __restrict__ pd, float* __restrict__ px,
+                                                            const uint8_t* __restrict__ mb) {
   __shared__ float lds_d[256 * 8];
   __shared__ float lds_x[256 * 8];
   const RedGeom gm = red_geom(C);
@@ -284,8 +294,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       load8(mc, cg * 8, sc);
       load8(mc + C, cg * 8, sh);
     }
-    auto acc = [&](float (&g)[8], const float (&xv)[8], const float (&yv)[8]) {
-      if constexpr (ACT == 1) {
+    auto acc = [&](float (&g)[8], const float (&xv)[8], const float (&yv)[8], unsigned bits) {
+      if constexpr (ACT == 3) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (bits >> j) & 1u ? g[j] : 0.f;
+      } else if constexpr (ACT == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
       } else if constexpr (ACT == 2) {
@@ -303,15 +316,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     constexpr int U = ACT == 1 ? 2 : 4;  // loads in flight per thread (2 or 3 tensors each)
     for (; r + (U - 1) * step < re; r += U * step) {
       float g[U][8], xv[U][8], yv[U][8];
+      unsigned bits[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t o = (r + u * step) * C + cg * 8;
         load8(dy, o, g[u]);
         load8(x, o, xv[u]);
         if constexpr (ACT == 1) load8(y, o, yv[u]);
+        if constexpr (ACT == 3) bits[u] = mb[o >> 3];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc(g[u], xv[u], yv[u]);
+      for (int u = 0; u < U; ++u) acc(g[u], xv[u], yv[u], ACT == 3 ? bits[u] : 0u);
     }
     for (; r < re; r += step) {
       float g[8], xv[8], yv[8];
@@ -319,7 +334,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       load8(dy, o, g);
       load8(x, o, xv);
       if constexpr (ACT == 1) load8(y, o, yv);
-      acc(g, xv, yv);
+      acc(g, xv, yv, ACT == 3 ? static_cast<unsigned>(mb[o >> 3]) : 0u);
     }
   }
 #pragma unroll
@@ -381,7 +396,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
                                                            const float* __restrict__ ca,
                                                            const float* __restrict__ cb,
                                                            const float* __restrict__ cc, uint16_t* __restrict__ dx,
-                                                           uint16_t* __restrict__ dres, int64_t nvec, int C) {
+                                                           uint16_t* __restrict__ dres, int64_t nvec, int C,
+                                                           const uint8_t* __restrict__ mb) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int cvec = C / 8;
   const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -398,7 +414,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   if constexpr (FIXED_C) coefs(static_cast<int>(v0 % cvec) * 8);
   auto one = [&](int64_t v, float (&g)[8], float (&xv)[8], const float (&yv)[8]) {
     if constexpr (!FIXED_C) coefs(static_cast<int>(v % cvec) * 8);
-    if constexpr (ACT == 1) {
+    if constexpr (ACT == 3) {
+      const unsigned bits = mb[v];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (bits >> j) & 1u ? g[j] : 0.f;
+    } else if constexpr (ACT == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
     } else if constexpr (ACT == 2) {
@@ -453,13 +473,14 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
+  uint8_t* nomask = nullptr;
 #define PSAMD_BN_APPLY(RES, ACT)                                                                              \
   if (fixed)                                                                                                  \
     hipLaunchKernelGGL((bn_apply_kernel<RES, ACT, true>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale,    \
-                       a.shift, a.y, nvec, C);                                                                \
+                       a.shift, a.y, nvec, C, nomask);                                                        \
   else                                                                                                        \
     hipLaunchKernelGGL((bn_apply_kernel<RES, ACT, false>), dim3(grid), dim3(256), 0, s, a.x, a.res, a.scale,   \
-                       a.shift, a.y, nvec, C)
+                       a.shift, a.y, nvec, C, nomask)
   if (a.res) {
     if (a.act == 1) { PSAMD_BN_APPLY(true, 1); }
     else { PSAMD_BN_APPLY(true, 0); }
@@ -482,11 +503,12 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   const int64_t R = a.R;
   const int G = a.G;
   const int ctiles = (C / 8 + 255) / 256;
-  const int act = (a.act == 1 && a.mask_coef && !a.dres) ? 2 : a.act;
+  const int act = a.mbits ? 3 : ((a.act == 1 && a.mask_coef && !a.dres) ? 2 : a.act);
 #define PSAMD_BN_RED(ACT)                                                                                       \
   hipLaunchKernelGGL(bn_bwd_reduce_kernel<ACT>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mask_coef, \
-                     a.mean, a.invstd, R, C, a.ws, a.ws + G * C)
-  if (act == 2) PSAMD_BN_RED(2);
+                     a.mean, a.invstd, R, C, a.ws, a.ws + G * C, a.mbits)
+  if (act == 3) PSAMD_BN_RED(3);
+  else if (act == 2) PSAMD_BN_RED(2);
   else if (act == 1) PSAMD_BN_RED(1);
   else PSAMD_BN_RED(0);
 #undef PSAMD_BN_RED
@@ -499,11 +521,14 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
 #define PSAMD_BN_BWD(ACT, DRES)                                                                                 \
   if (fixed)                                                                                                    \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES, true>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x,      \
-                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C);                       \
+                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C, a.mbits);              \
   else                                                                                                          \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<ACT, DRES, false>), dim3(grid), dim3(256), 0, s, a.dy, a.y, a.x,     \
-                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C)
-  if (a.dres) {
+                       a.mask_coef, coef, coef + C, coef + 2 * C, a.dx, a.dres, nvec, C, a.mbits)
+  if (act == 3) {
+    if (a.dres) { PSAMD_BN_BWD(3, true); }
+    else { PSAMD_BN_BWD(3, false); }
+  } else if (a.dres) {
     if (act == 1) { PSAMD_BN_BWD(1, true); }
     else { PSAMD_BN_BWD(0, true); }
   } else {
@@ -517,11 +542,11 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------ fused-bottleneck helpers
 // y = act(x * scale + shift + res * rscale + rshift): the bottleneck output when the identity
 // branch is a downsample conv whose BN is applied in the same pass (its output never hits HBM).
-template <int ACT, bool FIXED_C>
+template <int ACT, bool FIXED_C, bool MASK>
 __global__ __launch_bounds__(256) void bn_apply_dual_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ r,
                                                             const float* __restrict__ coef,
                                                             const float* __restrict__ rcoef, uint16_t* __restrict__ y,
-                                                            int64_t nvec, int C) {
+                                                            int64_t nvec, int C, uint8_t* __restrict__ mb) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int cvec = C / 8;
   const int64_t v0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -545,35 +570,49 @@ __global__ __launch_bounds__(256) void bn_apply_dual_kernel(const uint16_t* __re
       a[j] = o;
     }
     store8(y, v * 8, a);
+    if constexpr (MASK) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (a[j] > 0.f ? 1u : 0u) << j;
+      mb[v] = static_cast<uint8_t>(bits);
+    }
   }
 }
 
 void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* coef, const float* rcoef, uint16_t* y,
-                          int64_t R, int C, int act, hipStream_t s) {
+                          uint8_t* mbits, int64_t R, int C, int act, hipStream_t s) {
   const int64_t nvec = R * C / 8;
   if (nvec <= 0) return;
   const int grid = stream_grid(nvec, 256);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
-#define PSAMD_APPLY(K, ...)                                                                              \
-  if (fixed) hipLaunchKernelGGL((K<__VA_ARGS__, true>), dim3(grid), dim3(256), 0, s, ARGS);            \
-  else hipLaunchKernelGGL((K<__VA_ARGS__, false>), dim3(grid), dim3(256), 0, s, ARGS)
+  const bool mask = mbits != nullptr;
+#define PSAMD_LAUNCH(K, ...) hipLaunchKernelGGL((K<__VA_ARGS__>), dim3(grid), dim3(256), 0, s, ARGS)
+#define PSAMD_FM(K, ...)                                                            \
+  if (fixed) {                                                                      \
+    if (mask) { PSAMD_LAUNCH(K, __VA_ARGS__, true, true); }                         \
+    else { PSAMD_LAUNCH(K, __VA_ARGS__, true, false); }                             \
+  } else {                                                                          \
+    if (mask) { PSAMD_LAUNCH(K, __VA_ARGS__, false, true); }                        \
+    else { PSAMD_LAUNCH(K, __VA_ARGS__, false, false); }                            \
+  }
   if (rcoef) {
-#define ARGS x, res, coef, rcoef, y, nvec, C
-    if (act == 1) { PSAMD_APPLY(bn_apply_dual_kernel, 1); }
-    else { PSAMD_APPLY(bn_apply_dual_kernel, 0); }
+#define ARGS x, res, coef, rcoef, y, nvec, C, mbits
+    if (act == 1) { PSAMD_FM(bn_apply_dual_kernel, 1) }
+    else { PSAMD_FM(bn_apply_dual_kernel, 0) }
 #undef ARGS
   } else {
-#define ARGS x, res, coef, coef + C, y, nvec, C
+#define ARGS x, res, coef, coef + C, y, nvec, C, mbits
     if (res) {
-      if (act == 1) { PSAMD_APPLY(bn_apply_kernel, true, 1); }
-      else { PSAMD_APPLY(bn_apply_kernel, true, 0); }
+      if (act == 1) { PSAMD_FM(bn_apply_kernel, true, 1) }
+      else { PSAMD_FM(bn_apply_kernel, true, 0) }
     } else {
-      if (act == 1) { PSAMD_APPLY(bn_apply_kernel, false, 1); }
-      else { PSAMD_APPLY(bn_apply_kernel, false, 0); }
+      if (act == 1) { PSAMD_FM(bn_apply_kernel, false, 1) }
+      else { PSAMD_FM(bn_apply_kernel, false, 0) }
     }
 #undef ARGS
   }
-#undef PSAMD_APPLY
+#undef PSAMD_FM
+#undef PSAMD_LAUNCH
 }
 
 void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
@@ -588,12 +627,13 @@ void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint1
   const uint16_t* none = nullptr;
   const float* nomc = nullptr;
   uint16_t* nodres = nullptr;
+  const uint8_t* nobits = nullptr;
   if (fixed)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false, true>), dim3(grid), dim3(256), 0, s, g, none, x, nomc, coef,
-                       coef + C, coef + 2 * C, dx, nodres, nvec, C);
+                       coef + C, coef + 2 * C, dx, nodres, nvec, C, nobits);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false, false>), dim3(grid), dim3(256), 0, s, g, none, x, nomc, coef,
-                       coef + C, coef + 2 * C, dx, nodres, nvec, C);
+                       coef + C, coef + 2 * C, dx, nodres, nvec, C, nobits);
 }
 
 }  // namespace psamd

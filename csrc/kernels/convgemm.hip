@@ -19,6 +19,7 @@
 //               3: ReLU mask from z*scale + shift and that BN's backward sums sum(g),
 //                  sum(g * xhat) -- its reduce pass
 //               4: + a stride-2 map's rows at even (h, w) (downsample data gradient)
+//               5: + residual rows masked by forward ReLU bits (identity gradient, never stored)
 //   conv_wgrad  dW[n, k] = sum_m dZ[m, n] f(A[src(m, k)]), split over m; both operands are read
 //               transposed from row-major LDS tiles (ds_read_b64_tr_b16); fp32 per-split slabs,
 //               fixed-order reduction (deterministic, no atomics).
@@ -133,76 +134,155 @@ constexpr u16x8 kZero8 = {0, 0, 0, 0, 0, 0, 0, 0};
 // Persistent grid of nN * GM blocks of 256 threads (4 waves: 2 pixel halves x 2 channel halves):
 // block (n-tile nt, group mg) computes pixel tiles mg, mg + GM, ... of channel tile nt (a fixed
 // channel tile, so the epilogue statistics stay in registers across tiles and the partials are
-// [2][GM][N]).  Tile 128 pixels x BN channels; K in 64-deep stages through two LDS buffers, the
-// next stage's -- or, after the last stage, the next tile's first stage's -- global loads in
-// flight under the current MFMAs and the epilogue.
-template <int BN, bool PRO, int EPI>
+// [2][GM][N]).  Tile 128 pixels x BN channels; K in 64-deep stages.  The block walks one linear
+// sequence of (tile, stage) steps through two LDS buffers and two register stage sets: the loads
+// of step q + 2 are issued before the MFMAs of step q, so two steps of work -- and at tile ends
+// the epilogue -- cover their latency (the HBM-bound 1x1 layers have a single stage per tile).
+template <int AR, int BCH>
+struct StageRegs {
+  u16x8 a[AR];
+  u16x8 b[BCH];
+  unsigned ok;  // valid-row bits of a[]
+  int cc;       // channel offset of the stage inside its tap (prologue coefficients)
+};
+
+template <int BM, int BN, bool PRO, int EPI, bool KS1>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr int TN = BN / 64;              // 32-channel MFMA blocks per wave
+  constexpr int TM = BM / 64;              // 32-pixel MFMA blocks per wave
+  constexpr int AR = BM / 32;              // A-tile chunks per thread per stage
   constexpr int BCH = BN / 32;             // B-tile chunks per thread per stage
-  constexpr int STAGE = (kBM + BN) * kBK;  // bf16 per LDS stage
+  constexpr int STAGE = (BM + BN) * kBK;  // bf16 per LDS stage
   constexpr int CS = BN + 8;               // output tile row stride (bf16): 16-B aligned rows
   constexpr int STAGE_BYTES = 2 * STAGE * 2;
-  constexpr int EPI_BYTES = kBM * CS * 2 + 8 * BN * 4;
+  constexpr int EPI_BYTES = BM * CS * 2 + 8 * BN * 4;
   constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_BYTES / 2];
 
   const ConvGeo& g = p.g;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int nN = p.N / BN, mtiles = (p.M + kBM - 1) / kBM;
+  const int nN = p.N / BN, mtiles = (p.M + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int mg = L / nN, n0 = (L - mg * nN) * BN;
+  const int nk = p.K / kBK;
+  const int my_tiles = mg < mtiles ? (mtiles - mg + GM - 1) / GM : 0;
+  const int nq = my_tiles * nk;  // block-uniform
 
   // staging: thread t moves 16-B chunk (t & 7) of tile rows (t >> 3) + 32 i
   const int srow = t >> 3, sc = t & 7;
-  PixSrc src[4];
-  auto set_tile = [&](int mt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) src[i] = pix_src(mt * kBM + srow + 32 * i, p.M, g);
-  };
   const uint16_t* bptr = p.b + static_cast<int64_t>(n0 + srow) * p.K + sc * 8;
-  u16x8 ra[4], rb[BCH];
-  unsigned ok = 0;
-  float psc[8], psh[8];
-  auto gload = [&](int k0) {
-    const int tap = k0 / g.C, cc = k0 - tap * g.C;
-    const int kh = tap / g.ks, kw = tap - kh * g.ks;
-    ok = 0;
+  StageRegs<AR, BCH> S0, S1;
+  // producer cursor (runs two steps ahead of the MFMAs): tile iteration pti, stage pkt and its
+  // tap (pkh, pkw) / channel offset pcc, advanced incrementally (no divisions per stage);
+  // per-tile row sources: offset of tap (0, 0) channel 0, its input coordinates, row valid
+  int pti = 0, pkt = 0, pkh = 0, pkw = 0, pcc = 0;
+  int64_t rbase[AR];
+  int rih[AR], riw[AR];
+  unsigned rok = 0;
+  auto set_rows = [&](int mt) {
+    rok = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t o = tap_off(src[i], kh, kw, cc + sc * 8, g);
-      ok |= (o >= 0 ? 1u : 0u) << i;
-      // out-of-map taps / rows past M read element 0 (in bounds) and are zeroed in LDS
-      ra[i] = *reinterpret_cast<const u16x8*>(p.a + (o >= 0 ? o : 0));
+    for (int i = 0; i < AR; ++i) {
+      const PixSrc ps = pix_src(mt * BM + srow + 32 * i, p.M, g);
+      rok |= (ps.img >= 0 ? 1u : 0u) << i;
+      rih[i] = ps.ih0;
+      riw[i] = ps.iw0;
+      rbase[i] = ((static_cast<int64_t>(ps.img > 0 ? ps.img : 0) * g.H + ps.ih0) * g.W + ps.iw0) * g.C + sc * 8;
     }
+  };
+  auto gload = [&](StageRegs<AR, BCH>& R) {
+    R.cc = pcc;
+    R.ok = 0;
+    const int64_t toff = KS1 ? pcc : static_cast<int64_t>(pkh * g.W + pkw) * g.C + pcc;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      bool v = (rok >> i) & 1u;
+      if constexpr (!KS1) {
+        v = v && static_cast<unsigned>(rih[i] + pkh) < static_cast<unsigned>(g.H) &&
+            static_cast<unsigned>(riw[i] + pkw) < static_cast<unsigned>(g.W);
+      }
+      R.ok |= (v ? 1u : 0u) << i;
+      // out-of-map taps / rows past M read element 0 (in bounds) and are zeroed in LDS
+      R.a[i] = *reinterpret_cast<const u16x8*>(p.a + (v ? rbase[i] + toff : 0));
+    }
+    const int k0 = pkt * kBK;
 #pragma unroll
     for (int i = 0; i < BCH; ++i)
-      rb[i] = *reinterpret_cast<const u16x8*>(bptr + static_cast<int64_t>(32 * i) * p.K + k0);
-    if constexpr (PRO) {
-      load8(p.pro, cc + sc * 8, psc);
-      load8(p.pro + g.C, cc + sc * 8, psh);
+      R.b[i] = *reinterpret_cast<const u16x8*>(bptr + static_cast<int64_t>(32 * i) * p.K + k0);
+    // advance the cursor
+    pcc += kBK;
+    if (pcc == g.C) {
+      pcc = 0;
+      if (++pkw == g.ks) {
+        pkw = 0;
+        ++pkh;
+      }
+    }
+    if (++pkt == nk) {
+      pkt = pkh = pkw = pcc = 0;
+      if (++pti < my_tiles) set_rows(mg + pti * GM);
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](const StageRegs<AR, BCH>& R, int buf) {
     uint16_t* As = lds + buf * STAGE;
-    uint16_t* Bs = As + kBM * kBK;
+    uint16_t* Bs = As + BM * kBK;
+    float psc[8], psh[8];
+    if constexpr (PRO) {  // [scale | shift] of 8 channels: L1-resident
+      load8(p.pro, R.cc + sc * 8, psc);
+      load8(p.pro + g.C, R.cc + sc * 8, psh);
+    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      u16x8 v = ra[i];
+    for (int i = 0; i < AR; ++i) {
+      u16x8 v = R.a[i];
       if constexpr (PRO) v = bn_relu8(v, psc, psh);
-      if (!((ok >> i) & 1u)) v = kZero8;
+      if (!((R.ok >> i) & 1u)) v = kZero8;
       const int r = srow + 32 * i;
       *reinterpret_cast<u16x8*>(As + r * kBK + swz(r, sc) * 8) = v;
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int r = srow + 32 * i;
-      *reinterpret_cast<u16x8*>(Bs + r * kBK + swz(r, sc) * 8) = rb[i];
+      *reinterpret_cast<u16x8*>(Bs + r * kBK + swz(r, sc) * 8) = R.b[i];
     }
   };
 
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (BN / 2);
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
   const int fr = lane & 31, fh = lane >> 5;
+  f32x16 acc[TN][TM];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  };
+  auto compute = [&](int buf) {
+    const uint16_t* As = lds + buf * STAGE;
+    const uint16_t* Bs = As + BM * kBK;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ch = 2 * s + fh;  // this lane's chunk: k = 16 s + 8 fh + j
+      bf16x8_t xa[TM], wb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm + 32 * j + fr;
+        xa[j] = *reinterpret_cast<const bf16x8_t*>(As + r * kBK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn + 32 * i + fr;
+        wb[i] = *reinterpret_cast<const bf16x8_t*>(Bs + r * kBK + swz(r, ch) * 8);
+      }
+      // D[n][m] = sum_k W[n][k] A[m][k]: the weight rows are the MFMA A operand
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[i], xa[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
   // output pass: thread t owns channels [8 cg, 8 cg + 8) of tile rows r0, r0 + RPP, ...
   constexpr int CPR = BN / 8, RPP = 256 / CPR;
   const int cg = t % CPR, r0 = t / CPR, nc = n0 + cg * 8;
@@ -217,65 +297,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     load8(p.mean, nc, e2);
     load8(p.invstd, nc, e3);
   }
-  const int nk = p.K / kBK;
   uint16_t* Cs = lds;
-
-  if (mg < mtiles) {  // block-uniform
-    set_tile(mg);
-    gload(0);
-    swrite(0);
-    lds_barrier();
-  }
-  for (int mt = mg; mt < mtiles; mt += GM) {
-    const bool next_tile = mt + GM < mtiles;
-    f32x16 acc[TN][2];
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool more = kt + 1 < nk;
-      if (more) {
-        gload((kt + 1) * kBK);
-      } else if (next_tile) {  // the next tile's first stage, in flight under MFMAs + epilogue
-        set_tile(mt + GM);
-        gload(0);
-      }
-      const uint16_t* As = lds + (kt & 1) * STAGE;
-      const uint16_t* Bs = As + kBM * kBK;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int ch = 2 * s + fh;  // this lane's chunk: k = 16 s + 8 fh + j
-        bf16x8_t xa[2], wb[TN];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r = wm + 32 * j + fr;
-          xa[j] = *reinterpret_cast<const bf16x8_t*>(As + r * kBK + swz(r, ch) * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < TN; ++i) {
-          const int r = wn + 32 * i + fr;
-          wb[i] = *reinterpret_cast<const bf16x8_t*>(Bs + r * kBK + swz(r, ch) * 8);
-        }
-        // D[n][m] = sum_k W[n][k] A[m][k]: the weight rows are the MFMA A operand
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[i], xa[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) swrite((kt + 1) & 1);
-      lds_barrier();
-    }
-
-    // accumulators -> bf16 output tile [128][CS]: register q of lane l is channel
+  auto epilogue = [&](int mt) {
+    // accumulators -> bf16 output tile [BM][CS]: register q of lane l is channel
     // (q & 3) + 8 (q >> 2) + 4 (l >> 5), pixel l & 31 -> 4 consecutive channels per 8-B store
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TM; ++j)
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
           const int nl = wn + 32 * i + 8 * q4 + 4 * fh, ml = wm + 32 * j + fr;
@@ -284,13 +313,19 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
           *reinterpret_cast<u16x4*>(Cs + ml * CS + nl) = v;
         }
     lds_barrier();
-    const int m0 = mt * kBM;
-    for (int rr = r0; rr < kBM; rr += RPP) {
+    const int m0 = mt * BM;
+    for (int rr = r0; rr < BM; rr += RPP) {
       const int m = m0 + rr;
       if (m >= p.M) break;
       u16x8 v = *reinterpret_cast<const u16x8*>(Cs + rr * CS + cg * 8);
       const int64_t o = static_cast<int64_t>(m) * p.N + nc;
-      if constexpr (EPI == 2 || EPI == 4) {
+      if constexpr (EPI == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
+        const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + o);
+        const unsigned bits = p.bits[o >> 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((bits >> j) & 1u) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
+      } else if constexpr (EPI == 2 || EPI == 4) {
         int64_t ro = o;
         if constexpr (EPI == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
           const int ohw = g.OH * g.OW;
@@ -324,12 +359,38 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       }
       *reinterpret_cast<u16x8*>(p.c + o) = v;
     }
-    if (next_tile) {
-      lds_barrier();  // every wave is done reading the output tile
-      swrite(0);
-      lds_barrier();
+  };
+
+  // one step of the (tile, stage) sequence; SF: the free register set (held step q), SN: step q + 1
+  int ckt = 0, cti = 0;  // consumer cursor
+  auto step = [&](StageRegs<AR, BCH>& SF, const StageRegs<AR, BCH>& SN, int q) {
+    if (q + 2 < nq) gload(SF);
+    compute(q & 1);
+    if (++ckt == nk) {  // tile done
+      lds_barrier();    // all waves are done with the stage buffers (the output tile overlaps)
+      epilogue(mg + cti * GM);
+      zero_acc();
+      ckt = 0;
+      ++cti;
+      lds_barrier();    // output tile read back before step q + 1 is staged over it
     }
+    if (q + 1 < nq) swrite(SN, (q + 1) & 1);
+    lds_barrier();
+  };
+
+  zero_acc();
+  if (nq > 0) {
+    set_rows(mg);
+    gload(S0);
+    swrite(S0, 0);
+    if (nq > 1) gload(S1);
+    lds_barrier();
   }
+  for (int q = 0; q < nq; q += 2) {
+    step(S0, S1, q);
+    if (q + 1 < nq) step(S1, S0, q + 1);
+  }
+
   if constexpr (EPI == 1 || EPI == 3) {
     // threads with equal cg: lanes l ^ CPR, l ^ 2 CPR, ... of a wave, then the 4 waves via LDS
 #pragma unroll
@@ -339,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         s1[j] += __shfl_xor(s1[j], off, 64);
         s2[j] += __shfl_xor(s2[j], off, 64);
       }
-    float* red = reinterpret_cast<float*>(lds + kBM * CS);
+    float* red = reinterpret_cast<float*>(lds + BM * CS);
     if (lane < CPR) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -494,36 +555,50 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------------------ launchers
-int conv_mtiles(int M) { return (M + kBM - 1) / kBM; }
-
-// pixel-tile groups of the persistent forward grid: nN * GM blocks = 2 resident blocks per CU
-int conv_fwd_groups(int M, int N) {
-  const int nN = N / (N % 128 == 0 ? 128 : 64);
-  return std::max(1, std::min(conv_mtiles(M), 512 / nN));
+// Forward tile plan.  HBM-bound shallow-K layers (<= 2 stages) run a persistent grid of 2 blocks
+// per CU (cross-tile prefetch, statistics kept in registers); deeper K runs one block per tile
+// so the hardware balances the tail.
+ConvFwdPlan conv_fwd_plan(int M, int N, int K) {
+  ConvFwdPlan pl;
+  pl.bn = N % 128 == 0 ? 128 : 64;
+  const int nN = N / pl.bn;
+  pl.bm = 128;  // (64-pixel tiles measured slower on every ResNet-50 shape: scripts/probe_convgemm.py)
+  pl.gm = K / kBK > 2 ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
+  return pl;
 }
 
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
-  const bool wide = a.N % 128 == 0;
-  const int GM = conv_fwd_groups(a.M, a.N);
-  const int nblk = GM * (a.N / (wide ? 128 : 64));
-#define PSAMD_CF(BN, PRO, EPI) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, PRO, EPI>), dim3(nblk), dim3(256), 0, s, a, GM)
+  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K);
+  const int GM = pl.gm;
+  const int nblk = GM * (a.N / pl.bn);
+  const bool ks1 = a.g.ks == 1;
+#define PSAMD_CF2(BM, BN, PRO, EPI)                                                                              \
+  if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true>), dim3(nblk), dim3(256), 0, s, a, GM);  \
+  else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false>), dim3(nblk), dim3(256), 0, s, a, GM)
+#define PSAMD_CF(BN, PRO, EPI) PSAMD_CF2(128, BN, PRO, EPI)
 #define PSAMD_CFE(BN, PRO)               \
   switch (a.epi) {                       \
     case 1: PSAMD_CF(BN, PRO, 1); break; \
     case 2: PSAMD_CF(BN, PRO, 2); break; \
     case 3: PSAMD_CF(BN, PRO, 3); break; \
     case 4: PSAMD_CF(BN, PRO, 4); break; \
+    case 5: PSAMD_CF(BN, PRO, 5); break; \
     default: PSAMD_CF(BN, PRO, 0); break; \
   }
-  if (wide) {
-    if (a.pro) { PSAMD_CFE(128, true) } else { PSAMD_CFE(128, false) }
+  // the BN prologue only appears on forward convolutions (epilogue 0 / 1)
+  if (pl.bn == 128) {
+    if (a.pro) {
+      if (a.epi == 1) { PSAMD_CF(128, true, 1); } else { PSAMD_CF(128, true, 0); }
+    } else { PSAMD_CFE(128, false) }
   } else {
-    if (a.pro) { PSAMD_CFE(64, true) } else { PSAMD_CFE(64, false) }
+    if (a.pro) {
+      if (a.epi == 1) { PSAMD_CF(64, true, 1); } else { PSAMD_CF(64, true, 0); }
+    } else { PSAMD_CFE(64, false) }
   }
 #undef PSAMD_CFE
 #undef PSAMD_CF
+#undef PSAMD_CF2
 }
 
 namespace {

@@ -12,11 +12,13 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
                                                               bn2's output is never written)
             zd = downsample(x)       + bn_d statistics       (stride-2 rows gathered in-kernel)
             out = relu(bn3(z3) + x  or  bn_d(zd))            (one pass)
-  backward  bn3 backward; its masked gradient is also the identity-branch gradient
+  backward  bn3 backward (ReLU mask from 1-bit-per-element output bits); the masked gradient is
+            also the identity-branch gradient, recomputed from (dout, bits) where consumed
             conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
             with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
             conv2 backward [MIOpen], bn1 backward
-            conv1 data grad + identity / downsample gradient (GEMM epilogue), weight grads.
+            conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
+            epilogue), weight grads.
 
 Per block that removes the statistics passes of bn1 / bn3 / bn_d, bn2's output write + re-read,
 bn2's backward reduce pass and the residual-gradient add, and replaces MIOpen's 1x1 solvers (and
@@ -54,14 +56,14 @@ def geo(h: int, w: int, ks: int = 1, stride: int = 1, pad: int = 0) -> List[int]
     return [h, w, (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1, ks, stride, pad]
 
 
-def conv_gemm(a, b, g, pro=None, epi=0, aux=None, kshift=None, mc=None, mean=None, invstd=None):
+def conv_gemm(a, b, g, pro=None, epi=0, aux=None, kshift=None, mc=None, mean=None, invstd=None, bits=None):
     """c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> (c, folded BN partials [2, G, N] or None).
 
     a: [images*H*W, C] bf16 rows; b: [N, ks*ks*C] (channels_last weight order); g: ``geo(...)``;
     pro: [scale | shift] applied with ReLU to ``a`` while staging; epi: 0 store, 1 + BN statistics
     (about ``kshift``), 2 + ``aux`` rows, 3 ReLU mask from ``aux`` * mc + shift and BN-backward sums,
-    4 + ``aux`` of the stride-2 map at even (h, w)."""
-    return native().conv_gemm(a, b, g, pro, epi, aux, kshift, mc, mean, invstd)
+    4 + ``aux`` of the stride-2 map at even (h, w), 5 + ``aux`` masked by ReLU ``bits``."""
+    return native().conv_gemm(a, b, g, pro, epi, aux, kshift, mc, mean, invstd, bits)
 
 
 def conv_wgrad(dz, x, g, pro=None):
@@ -96,7 +98,7 @@ class _BottleneckFn(torch.autograd.Function):
         k1 = bn1.running_mean.clone()  # shift of the statistics sums (~ the batch mean)
         z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
         m1, i1, cf1 = _finalize(p1, k1, n * h * w, bn1)
-        y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)
+        y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)[0]
         z2 = F.conv2d(image(y1, n, h, w), w2, None, s, 1)
         z2r = rows(z2)
         m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
@@ -109,11 +111,13 @@ class _BottleneckFn(torch.autograd.Function):
             kd = bnd.running_mean.clone()
             zd, pd = nat.conv_gemm(x2, _mat(wd), geo(h, w, 1, s), None, 1, None, kd)
             md, idd, cfd = _finalize(pd, kd, n * oh * ow, bnd)
-            out = nat.bn_apply_coef(z3, cf3, zd, cfd, 1)
+            out, obits = nat.bn_apply_coef(z3, cf3, zd, cfd, 1, True)
         else:
             zd = md = idd = None
-            out = nat.bn_apply_coef(z3, cf3, x2, None, 1)
-        ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, out, zd,
+            out, obits = nat.bn_apply_coef(z3, cf3, x2, None, 1, True)
+        # the block output's ReLU mask is kept as 1 bit per element (the output itself is the
+        # next block's input; the backward reads 1/16 of its bytes)
+        ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, obits, zd,
                               m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd)
         ctx.dims = (n, h, w, s, oh, ow)
         return image(out, n, oh, ow)
@@ -121,12 +125,14 @@ class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         nat = native()
-        (x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, out, zd,
+        (x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, obits, zd,
          m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd) = ctx.saved_tensors
         n, h, w, s, oh, ow = ctx.dims
         gi, go = geo(h, w), geo(oh, ow)
-        # bn3 (ReLU mask from the block output); gr, the masked gradient, is the identity gradient
-        dz3, gr, dg3, db3 = nat.bn_act_bwd(rows(dout), out, z3, g3, m3, i3, 1, True, True, None)
+        d2 = rows(dout)
+        # bn3 with the ReLU mask from the output bits; the masked gradient dout * relu' is also
+        # the identity-branch gradient -- recomputed where needed from (dout, bits), never stored
+        dz3, _, dg3, db3 = nat.bn_act_bwd(d2, None, z3, g3, m3, i3, 3, False, True, None, obits)
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
         gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t().contiguous(), go, None, 3, z2r, None, cf2, m2, i2)
@@ -139,12 +145,12 @@ class _BottleneckFn(torch.autograd.Function):
         w1t = _mat(w1).t().contiguous()
         dwd = dgd = dbd = None
         if wd is not None:
-            dzd, _, dgd, dbd = nat.bn_act_bwd(gr, None, zd, gd, md, idd, 0, False, True, None)
+            dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
             dwd = nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)).view_as(wd)
             t = nat.conv_gemm(dzd, _mat(wd).t().contiguous(), go)[0]
             dx2 = nat.conv_gemm(dz1, w1t, gi, None, 4 if s == 2 else 2, t)[0]
         else:
-            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 2, gr)[0]
+            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 5, d2, bits=obits)[0]
         dw1 = nat.conv_wgrad(dz1, x2, gi)
         return (image(dx2, n, h, w), dw1.view_as(w1), dg1, db1, dw2, dg2, db2, dw3.view_as(w3), dg3, db3,
                 dwd, dgd, dbd, None)

@@ -71,6 +71,11 @@ def test_conv1x1_residual_epilogue(M, K, N):
     a, b, r = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5), _rnd(M, N, g=g)
     c, _ = native().conv_gemm(_bf(a), _bf(b), [M, 1, M, 1, 1, 1, 0], None, 2, _bf(r))
     _close(c, a @ b.t() + r)
+    # epilogue 5: residual masked by ReLU bits
+    keep = torch.rand(M, N, generator=g) > 0.5
+    bits = (keep.view(-1, 8).int() << torch.arange(8)).sum(1).to(torch.uint8)
+    c5, _ = native().conv_gemm(_bf(a), _bf(b), [M, 1, M, 1, 1, 1, 0], None, 5, _bf(r), bits=bits.to(DEV))
+    _close(c5, a @ b.t() + r * keep)
 
 
 @pytest.mark.parametrize("M,K,N", SHAPES[:4])
@@ -154,10 +159,21 @@ def test_bn_apply_coef_and_backward_from_partials():
     R, C = 999, 192
     x, r = _rnd(R, C, g=g), _rnd(R, C, g=g)
     cf, rcf = _coef(C, g), _coef(C, g)
-    y = native().bn_apply_coef(_bf(x), cf.to(DEV), _bf(r), rcf.to(DEV), 1)
+    y, bits = native().bn_apply_coef(_bf(x), cf.to(DEV), _bf(r), rcf.to(DEV), 1, True)
     _close(y, torch.relu(x * cf[:C] + cf[C:] + r * rcf[:C] + rcf[C:]))
-    y0 = native().bn_apply_coef(_bf(x), cf.to(DEV), None, None, 0)
+    # 1 bit per element: bit j of byte v is y[8 v + j] > 0
+    unpacked = ((bits.cpu()[:, None].int() >> torch.arange(8)) & 1).reshape(R, C).bool()
+    assert torch.equal(unpacked, y.cpu().float() > 0)
+    y0 = native().bn_apply_coef(_bf(x), cf.to(DEV), None, None, 0)[0]
     _close(y0, x * cf[:C] + cf[C:])
+    # BN backward with the ReLU mask from the bits == with the mask from y
+    dy = _rnd(R, C, g=g)
+    gam = torch.rand(C, generator=g) + 0.5
+    mu, istd = torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g) + 0.5
+    ref = native().bn_act_bwd(_bf(dy), y, _bf(x), gam.to(DEV), mu.to(DEV), istd.to(DEV), 1, True, True, None)
+    got = native().bn_act_bwd(_bf(dy), None, _bf(x), gam.to(DEV), mu.to(DEV), istd.to(DEV), 3, True, True, None, bits)
+    for u, v in zip(ref, got):
+        torch.testing.assert_close(u.float(), v.float(), rtol=0, atol=0)
     # backward from partial sums == backward with its own reduce pass
     gr = _rnd(R, C, g=g)
     gamma, mean, invstd = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1, torch.rand(C) + 0.5
