@@ -422,7 +422,7 @@ static std::vector<Tensor> bn_fwd_impl(Tensor x, c10::optional<Tensor> res, c10:
   auto fopt = x.options().dtype(torch::kFloat32);
   auto mean = torch::empty({C}, fopt), invstd = torch::empty({C}, fopt);
   auto coef = torch::empty({2 * C}, fopt);
-  const int G = psamd::bn_red_blocks(R);
+  const int G = psamd::bn_red_blocks(R, static_cast<int>(C));
   auto ws = torch::empty({training ? 2 * G * C : 1}, fopt);
   psamd::BnFwdArgs a;
   a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
@@ -795,7 +795,7 @@ std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10
   Tensor dres = want_dres ? torch::empty_like(x) : Tensor();
   Tensor dgamma = affine ? torch::empty({C}, fopt) : Tensor();
   Tensor dbeta = affine ? torch::empty({C}, fopt) : Tensor();
-  const int G = psamd::bn_red_blocks(R);
+  const int G = psamd::bn_red_blocks(R, static_cast<int>(C));
   auto ws = torch::empty({2 * G * C + 3 * C}, fopt);
   psamd::BnBwdArgs a;
   a.dy = reinterpret_cast<const uint16_t*>(dy.data_ptr());

@@ -188,7 +188,7 @@ struct BnBwdArgs {
   int act;
 };
 void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s);
-int bn_red_blocks(int64_t R);
+int bn_red_blocks(int64_t R, int C);
 
 // ---------------------------------------------------------------- dense.hip (MFMA)
 // C[M,N] (+)= act(alpha * A[M,K] . B[N,K]^T + bias[N]); A, B bf16 K-contiguous; C bf16 or fp32.

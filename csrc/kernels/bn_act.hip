@@ -13,6 +13,8 @@
 // gamma/beta/stats fp32.  Every thread moves 8 channels (16 B) per access.  Channel reductions
 // are two-level and deterministic: block partials [G, C] in fp32 (no atomics) + a finalize
 // kernel that sums them in fixed order.  act: 0 none, 1 relu.
+#include <algorithm>
+
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
@@ -32,8 +34,15 @@ __host__ __device__ inline RedGeom red_geom(int C) {
   return {p, 256 / p};
 }
 
-int bn_red_blocks(int64_t R) {
-  int64_t g = (R + 127) / 128;  // >= 128 rows per block keeps the [G, C] partials <= 1/32 of the data
+int bn_red_blocks(int64_t R, int C) {
+  // >= 128 rows per block keeps the [G, C] partials <= 1/32 of the data ...
+  int64_t g = (R + 127) / 128;
+  // ... unless that leaves the chip under-filled: wide-channel / few-row tensors (ResNet stage 3-4:
+  // 25-100K rows x 1-2K channels) need ~2048 blocks in total to keep enough loads in flight, down
+  // to 8 rows per block
+  const int ctiles = (C / 8 + 255) / 256;
+  const int64_t want = (2048 + ctiles - 1) / ctiles;
+  if (g < want) g = std::min<int64_t>(want, (R + 7) / 8);
   if (g < 1) g = 1;
   if (g > 2048) g = 2048;  // 8 blocks per CU: enough loads in flight to stream at the HBM rate
   return static_cast<int>(g);
