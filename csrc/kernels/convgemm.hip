@@ -128,7 +128,13 @@ __device__ __forceinline__ u16x8 bn_relu8(u16x8 v, const float (&sc)[8], const f
 
 constexpr u16x8 kZero8 = {0, 0, 0, 0, 0, 0, 0, 0};
 
+typedef __attribute__((address_space(1))) const void gptr_t;
+typedef __attribute__((address_space(3))) void lptr_t;
+
 }  // namespace
+
+// source of the LDS-DMA loads of out-of-map taps / rows past M
+__device__ __attribute__((aligned(16))) uint16_t kZeroPage[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
 // ------------------------------------------------------------------------------ conv_fwd
 // Persistent grid of nN * GM blocks of 256 threads (4 waves: 2 pixel halves x 2 channel halves):
@@ -146,7 +152,7 @@ struct StageRegs {
   int cc;       // channel offset of the stage inside its tap (prologue coefficients)
 };
 
-template <int BM, int BN, bool PRO, int EPI, bool KS1>
+template <int BM, int BN, bool PRO, int EPI, bool KS1, bool GLDS>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr int TN = BN / 64;              // 32-channel MFMA blocks per wave
   constexpr int TM = BM / 64;              // 32-pixel MFMA blocks per wave
@@ -379,16 +385,91 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   };
 
   zero_acc();
-  if (nq > 0) {
+  if constexpr (GLDS) {
+    // Deep-K tile, one per block: both operands go global -> LDS by LDS-DMA (global_load_lds,
+    // 16 B per lane), no staging registers and no ds_write.  One wave instruction fills 8 rows x
+    // 128 B lane-linearly, so the chunk swizzle moves to the SOURCE address (linear destination +
+    // swizzled source + swizzled read).  Out-of-map taps / rows past M load the zero page.  Two
+    // buffers: issue stage t+1, counted vmcnt for stage t, barrier, MFMAs, barrier.
+    static_assert(!PRO, "the BN prologue needs register staging");
+    constexpr int AI = BM / 32, BI = BN / 32;  // LDS-DMA instructions per wave per stage
+    const int lrow = lane >> 3, lch = lane & 7;
+    int64_t gbase[AI];
+    int gih[AI], giw[AI];
+    unsigned gok = 0;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int r = (wave * AI + i) * 8 + lrow;
+      const PixSrc ps = pix_src(mg * BM + r, p.M, g);
+      gok |= (ps.img >= 0 ? 1u : 0u) << i;
+      gih[i] = ps.ih0;
+      giw[i] = ps.iw0;
+      gbase[i] = ((static_cast<int64_t>(ps.img > 0 ? ps.img : 0) * g.H + ps.ih0) * g.W + ps.iw0) * g.C +
+                 swz(r, lch) * 8;
+    }
+    const uint16_t* gb[BI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int r = (wave * BI + i) * 8 + lrow;
+      gb[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + swz(r, lch) * 8;
+    }
+    int qkh = 0, qkw = 0, qcc = 0;
+    auto issue = [&](int kt, int buf) {
+      uint16_t* As = lds + buf * STAGE;
+      uint16_t* Bs = As + BM * kBK;
+      const int64_t toff = KS1 ? qcc : static_cast<int64_t>(qkh * g.W + qkw) * g.C + qcc;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        bool v = (gok >> i) & 1u;
+        if constexpr (!KS1) {
+          v = v && static_cast<unsigned>(gih[i] + qkh) < static_cast<unsigned>(g.H) &&
+              static_cast<unsigned>(giw[i] + qkw) < static_cast<unsigned>(g.W);
+        }
+        const uint16_t* src = v ? p.a + gbase[i] + toff : kZeroPage;
+        __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(As + (wave * AI + i) * 8 * kBK), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        __builtin_amdgcn_global_load_lds((gptr_t*)(gb[i] + kt * kBK), (lptr_t*)(Bs + (wave * BI + i) * 8 * kBK),
+                                         16, 0, 0);
+      qcc += kBK;
+      if (qcc == g.C) {
+        qcc = 0;
+        if (++qkw == g.ks) {
+          qkw = 0;
+          ++qkh;
+        }
+      }
+    };
+    if (mg < mtiles) {  // block-uniform
+      issue(0, 0);
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) {
+          issue(kt + 1, (kt + 1) & 1);
+          // this wave's stage-kt DMAs retired (the AI + BI just issued may stay in flight)
+          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();  // every wave's stage-kt DMAs landed
+        compute(kt & 1);
+        lds_barrier();  // stage kt read out before stage kt + 2 is issued into its buffer
+      }
+      epilogue(mg);
+    }
+  } else if (nq > 0) {
     set_rows(mg);
     gload(S0);
     swrite(S0, 0);
     if (nq > 1) gload(S1);
     lds_barrier();
   }
-  for (int q = 0; q < nq; q += 2) {
-    step(S0, S1, q);
-    if (q + 1 < nq) step(S1, S0, q + 1);
+  if constexpr (!GLDS) {
+    for (int q = 0; q < nq; q += 2) {
+      step(S0, S1, q);
+      if (q + 1 < nq) step(S1, S0, q + 1);
+    }
   }
 
   if constexpr (EPI == 1 || EPI == 3) {
@@ -573,9 +654,15 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   const bool ks1 = a.g.ks == 1;
-#define PSAMD_CF2(BM, BN, PRO, EPI)                                                                              \
-  if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true>), dim3(nblk), dim3(256), 0, s, a, GM);  \
-  else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false>), dim3(nblk), dim3(256), 0, s, a, GM)
+  // deep K without the BN prologue: LDS-DMA staging (one tile per block)
+  const bool glds = !a.pro && pl.gm == (a.M + 127) / 128 && a.K / kBK > 2;
+#define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \
+  if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, GL>), dim3(nblk), dim3(256), 0, s, a, GM); \
+  else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, GL>), dim3(nblk), dim3(256), 0, s, a, GM)
+#define PSAMD_CF2(BM, BN, PRO, EPI)                        \
+  if constexpr (PRO) { PSAMD_CF3(BM, BN, PRO, EPI, false); } \
+  else if (glds) { PSAMD_CF3(BM, BN, PRO, EPI, true); }       \
+  else { PSAMD_CF3(BM, BN, PRO, EPI, false); }
 #define PSAMD_CF(BN, PRO, EPI) PSAMD_CF2(128, BN, PRO, EPI)
 #define PSAMD_CFE(BN, PRO)               \
   switch (a.epi) {                       \
@@ -599,6 +686,7 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
 #undef PSAMD_CFE
 #undef PSAMD_CF
 #undef PSAMD_CF2
+#undef PSAMD_CF3
 }
 
 namespace {
