@@ -879,7 +879,6 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
                               c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
                               c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits) {
   check_rows(a, "a");
-  check_rows(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
   const psamd::ConvGeo g = gi.first;
@@ -910,6 +909,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
   const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K)).gm;
+  b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
+  check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3;
   Tensor part = sums ? torch::empty({2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};

@@ -59,7 +59,8 @@ def geo(h: int, w: int, ks: int = 1, stride: int = 1, pad: int = 0) -> List[int]
 def conv_gemm(a, b, g, pro=None, epi=0, aux=None, kshift=None, mc=None, mean=None, invstd=None, bits=None):
     """c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> (c, folded BN partials [2, G, N] or None).
 
-    a: [images*H*W, C] bf16 rows; b: [N, ks*ks*C] (channels_last weight order); g: ``geo(...)``;
+    a: [images*H*W, C] bf16 rows; b: [N, ks*ks*C] (channels_last weight order; a strided view is
+    copied contiguous once); g: ``geo(...)``;
     pro: [scale | shift] applied with ReLU to ``a`` while staging; epi: 0 store, 1 + BN statistics
     (about ``kshift``), 2 + ``aux`` rows, 3 ReLU mask from ``aux`` * mc + shift and BN-backward sums,
     4 + ``aux`` of the stride-2 map at even (h, w), 5 + ``aux`` masked by ReLU ``bits``."""
@@ -135,19 +136,19 @@ class _BottleneckFn(torch.autograd.Function):
         dz3, _, dg3, db3 = nat.bn_act_bwd(d2, None, z3, g3, m3, i3, 3, False, True, None, obits)
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
-        gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t().contiguous(), go, None, 3, z2r, None, cf2, m2, i2)
+        gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
         dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
         dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
                                                           [s, s], [1, 1], [1, 1], False, [0, 0], 1,
                                                           [True, True, False])
         dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
-        w1t = _mat(w1).t().contiguous()
+        w1t = _mat(w1).t()
         dwd = dgd = dbd = None
         if wd is not None:
             dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
             dwd = nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)).view_as(wd)
-            t = nat.conv_gemm(dzd, _mat(wd).t().contiguous(), go)[0]
+            t = nat.conv_gemm(dzd, _mat(wd).t(), go)[0]
             dx2 = nat.conv_gemm(dz1, w1t, gi, None, 4 if s == 2 else 2, t)[0]
         else:
             dx2 = nat.conv_gemm(dz1, w1t, gi, None, 5, d2, bits=obits)[0]

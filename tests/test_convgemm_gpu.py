@@ -132,6 +132,57 @@ def test_conv3x3_implicit_gemm_forward_and_wgrad(cin, cout, hw, stride, pro):
     _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, 9 * cin))
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5])
+def test_deep_k_lds_dma_path_all_epilogues(epi):
+    """K % 256 == 0, 128-channel tiles, no prologue: the LDS-DMA kernel with fragment-packed
+    weights (given here as a strided transposed view, as the block backward passes them)."""
+    n, h, w, K, N = 2, 13, 11, 512, 256
+    M = n * h * w
+    g = _gen(40 + epi)
+    a, bt = _rnd(M, K, g=g), _rnd(K, N, g=g, scale=K ** -0.5)
+    ref = a @ bt
+    args = [None] * 6
+    if epi == 1:
+        args = [None, (torch.randn(N, generator=g) * 0.1).to(DEV), None, None, None, None]
+    elif epi in (2, 5):
+        r = _rnd(M, N, g=g)
+        keep = torch.rand(M, N, generator=g) > 0.5
+        bits = (keep.view(-1, 8).int() << torch.arange(8)).sum(1).to(torch.uint8)
+        args = [_bf(r), None, None, None, None, bits.to(DEV) if epi == 5 else None]
+        ref = ref + (r * keep if epi == 5 else r)
+    elif epi == 3:
+        z = _rnd(M, N, g=g)
+        mc = _coef(N, g)
+        mean, invstd = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+        args = [_bf(z), None, mc.to(DEV), mean.to(DEV), invstd.to(DEV), None]
+        ref = ref * ((z * mc[:N] + mc[N:]) > 0)
+    elif epi == 4:
+        oh, ow = (h + 1) // 2, (w + 1) // 2
+        t = _rnd(n * oh * ow, N, g=g)
+        args = [_bf(t), None, None, None, None, None]
+        ref.view(n, h, w, N)[:, ::2, ::2] += t.view(n, oh, ow, N)
+    aux, kshift, mc, mean, invstd, bits = args
+    c, part = native().conv_gemm(_bf(a), _bf(bt).t(), geo(h, w), None, epi, aux, kshift, mc, mean, invstd, bits)
+    _close(c, ref)
+    if epi == 1:
+        cb = c.float().cpu() - kshift.cpu()
+        torch.testing.assert_close(part[0].sum(0).cpu(), cb.sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(part[1].sum(0).cpu(), (cb * cb).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv3x3_deep_k_lds_dma_path(stride):
+    """3x3, C = 256 (K = 2304): padding taps of the LDS-DMA kernel come from its zero page."""
+    n, hw, cin, cout = 2, 9, 256, 128
+    g = _gen(50 + stride)
+    x = _rnd(n, hw, hw, cin, g=g)
+    wt = _rnd(cout, cin, 3, 3, g=g, scale=(9 * cin) ** -0.5)
+    ref = F.conv2d(x.permute(0, 3, 1, 2), wt, None, stride, 1).permute(0, 2, 3, 1).reshape(-1, cout)
+    c, _ = native().conv_gemm(_bf(x.reshape(-1, cin)), _bf(wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin)),
+                              geo(hw, hw, 3, stride, 1))
+    _close(c, ref)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 64, 64), (5000, 256, 64), (1000, 128, 512), (777, 512, 128)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv1x1_weight_grad(M, N, K, pro):
