@@ -150,6 +150,7 @@ struct StageRegs {
   u16x8 b[BCH];
   unsigned ok;  // valid-row bits of a[]
   int cc;       // channel offset of the stage inside its tap (prologue coefficients)
+  bool wb;      // b[] loaded (to be staged)
 };
 
 template <int BM, int BN, bool PRO, int EPI, bool KS1, bool GLDS>
@@ -158,12 +159,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   constexpr int TM = BM / 64;              // 32-pixel MFMA blocks per wave
   constexpr int AR = BM / 32;              // A-tile chunks per thread per stage
   constexpr int BCH = BN / 32;             // B-tile chunks per thread per stage
-  constexpr int STAGE = (BM + BN) * kBK;  // bf16 per LDS stage
-  constexpr int CS = BN + 8;               // output tile row stride (bf16): 16-B aligned rows
-  constexpr int STAGE_BYTES = 2 * STAGE * 2;
-  constexpr int EPI_BYTES = BM * CS * 2 + 8 * BN * 4;
-  constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_BYTES / 2];
+  // output tile row stride (bf16): 2 dwords mod 32 banks, so the 16 rows of a ds_write_b64 lane
+  // group hit distinct bank pairs (BN + 8 made them 2-way); rows are 8-B aligned -> b64 readback
+  constexpr int CS = BN + 4;
+  // LDS: [A0 | A1] overlaid by the output tile + statistics scratch, then [B0 | B1] (never
+  // overlaid, so a resident weight tile survives the epilogues)
+  constexpr int EPI_ELEMS = BM * CS + 8 * BN * 2;
+  constexpr int B_BASE = ((2 * BM * kBK > EPI_ELEMS ? 2 * BM * kBK : EPI_ELEMS) + 7) & ~7;
+  constexpr int LDS_ELEMS = B_BASE + 2 * BN * kBK;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
   const ConvGeo& g = p.g;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -182,6 +186,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // tap (pkh, pkw) / channel offset pcc, advanced incrementally (no divisions per stage);
   // per-tile row sources: offset of tap (0, 0) channel 0, its input coordinates, row valid
   int pti = 0, pkt = 0, pkh = 0, pkw = 0, pcc = 0;
+  // with <= 2 stages per tile, buffer (q & 1) always holds the same k-stage, so its weight tile
+  // is staged by the first two steps only and stays resident
+  int lq = 0;
   int64_t rbase[AR];
   int rih[AR], riw[AR];
   unsigned rok = 0;
@@ -212,9 +219,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       R.a[i] = *reinterpret_cast<const u16x8*>(p.a + (v ? rbase[i] + toff : 0));
     }
     const int k0 = pkt * kBK;
+    R.wb = lq++ < 2 || nk > 2;
+    if (R.wb) {
 #pragma unroll
-    for (int i = 0; i < BCH; ++i)
-      R.b[i] = *reinterpret_cast<const u16x8*>(bptr + static_cast<int64_t>(32 * i) * p.K + k0);
+      for (int i = 0; i < BCH; ++i)
+        R.b[i] = *reinterpret_cast<const u16x8*>(bptr + static_cast<int64_t>(32 * i) * p.K + k0);
+    }
     // advance the cursor
     pcc += kBK;
     if (pcc == g.C) {
@@ -230,8 +240,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     }
   };
   auto swrite = [&](const StageRegs<AR, BCH>& R, int buf) {
-    uint16_t* As = lds + buf * STAGE;
-    uint16_t* Bs = As + BM * kBK;
+    uint16_t* As = lds + buf * (BM * kBK);
+    uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
     float psc[8], psh[8];
     if constexpr (PRO) {  // [scale | shift] of 8 channels: L1-resident
       load8(p.pro, R.cc + sc * 8, psc);
@@ -245,10 +255,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       const int r = srow + 32 * i;
       *reinterpret_cast<u16x8*>(As + r * kBK + swz(r, sc) * 8) = v;
     }
+    if (R.wb) {
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int r = srow + 32 * i;
-      *reinterpret_cast<u16x8*>(Bs + r * kBK + swz(r, sc) * 8) = R.b[i];
+      for (int i = 0; i < BCH; ++i) {
+        const int r = srow + 32 * i;
+        *reinterpret_cast<u16x8*>(Bs + r * kBK + swz(r, sc) * 8) = R.b[i];
+      }
     }
   };
 
@@ -264,8 +276,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
   };
   auto compute = [&](int buf) {
-    const uint16_t* As = lds + buf * STAGE;
-    const uint16_t* Bs = As + BM * kBK;
+    const uint16_t* As = lds + buf * (BM * kBK);
+    const uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int ch = 2 * s + fh;  // this lane's chunk: k = 16 s + 8 fh + j
@@ -323,7 +335,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     for (int rr = r0; rr < BM; rr += RPP) {
       const int m = m0 + rr;
       if (m >= p.M) break;
-      u16x8 v = *reinterpret_cast<const u16x8*>(Cs + rr * CS + cg * 8);
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8);
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8 + 4);
+      u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const int64_t o = static_cast<int64_t>(m) * p.N + nc;
       if constexpr (EPI == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
         const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + o);
@@ -415,8 +429,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     }
     int qkh = 0, qkw = 0, qcc = 0;
     auto issue = [&](int kt, int buf) {
-      uint16_t* As = lds + buf * STAGE;
-      uint16_t* Bs = As + BM * kBK;
+      uint16_t* As = lds + buf * (BM * kBK);
+      uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
       const int64_t toff = KS1 ? qcc : static_cast<int64_t>(qkh * g.W + qkw) * g.C + qcc;
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
