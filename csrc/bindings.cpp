@@ -682,6 +682,18 @@ std::vector<Tensor> stem_conv_fwd(Tensor x, Tensor wp, c10::optional<Tensor> ksh
 }
 
 // BN statistics from producer partial sums: part [2, G, C] about kshift over R rows.
+// [2, G, C] partials -> a [2, S, C] first-level fold when G is tall (S = partials_fold_rows(G)),
+// else the input itself
+static Tensor fold_partials(const Tensor& part, hipStream_t s) {
+  const int G = static_cast<int>(part.size(1)), C = static_cast<int>(part.size(2));
+  const int S = psamd::partials_fold_rows(G);
+  if (S == 0) return part;
+  auto f = torch::empty({2, S, C}, part.options());
+  psamd::launch_partials_fold(part.data_ptr<float>(), part.data_ptr<float>() + static_cast<int64_t>(G) * C, G, C,
+                              f.data_ptr<float>(), f.data_ptr<float>() + static_cast<int64_t>(S) * C, s);
+  return f;
+}
+
 // Returns [mean, invstd, coef = scale | shift]; updates running stats when given.
 std::vector<Tensor> bn_finalize_sums(Tensor part, Tensor kshift, int64_t R, c10::optional<Tensor> gamma,
                                      c10::optional<Tensor> beta, c10::optional<Tensor> rmean,
@@ -689,13 +701,15 @@ std::vector<Tensor> bn_finalize_sums(Tensor part, Tensor kshift, int64_t R, c10:
   check_f32(part, "part");
   check_f32(kshift, "kshift");
   TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.is_contiguous(), "part [2, G, C]");
-  const int64_t G = part.size(1), C = part.size(2);
+  const int64_t C = part.size(2);
   TORCH_CHECK(C % 8 == 0 && kshift.numel() == C, "C % 8, kshift [C]");
   const c10::DeviceGuard guard(part.device());
   auto fopt = part.options();
   auto mean = torch::empty({C}, fopt), invstd = torch::empty({C}, fopt), coef = torch::empty({2 * C}, fopt);
-  psamd::launch_bn_finalize_sums(part.data_ptr<float>(), part.data_ptr<float>() + G * C, kshift.data_ptr<float>(),
-                                 static_cast<int>(G), static_cast<int>(C), R, static_cast<float>(eps),
+  const Tensor fp = fold_partials(part, cur_stream(part));
+  const int64_t Gf = fp.size(1);
+  psamd::launch_bn_finalize_sums(fp.data_ptr<float>(), fp.data_ptr<float>() + Gf * C, kshift.data_ptr<float>(),
+                                 static_cast<int>(Gf), static_cast<int>(C), R, static_cast<float>(eps),
                                  static_cast<float>(momentum), opt_ptr<const float>(gamma), opt_ptr<const float>(beta),
                                  opt_ptr<float>(rmean), opt_ptr<float>(rvar), mean.data_ptr<float>(),
                                  invstd.data_ptr<float>(), coef.data_ptr<float>(), coef.data_ptr<float>() + C,
@@ -995,13 +1009,14 @@ std::vector<Tensor> bn_bwd_partials(Tensor g, Tensor x, Tensor part, c10::option
   TORCH_CHECK(x.dim() == 2 && g.sizes() == x.sizes() && x.size(1) % 8 == 0, "g/x [R, C], C % 8");
   const int64_t R = x.size(0), C = x.size(1);
   check_f32(part, "part");
-  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.size(2) == C, "part [2, G, C]");
-  const int G = static_cast<int>(part.size(1));
+  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.size(2) == C && part.is_contiguous(), "part [2, G, C]");
   const c10::DeviceGuard guard(x.device());
   auto fopt = x.options().dtype(torch::kFloat32);
   auto dx = torch::empty_like(x);
   auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt), coef = torch::empty({3 * C}, fopt);
-  psamd::launch_bn_bwd_partials(part.data_ptr<float>(), part.data_ptr<float>() + G * C, G, u16(g), u16(x),
+  const Tensor fp = fold_partials(part, cur_stream(x));
+  const int64_t Gf = fp.size(1);
+  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + Gf * C, static_cast<int>(Gf), u16(g), u16(x),
                                 f32_opt(gamma, C, "gamma"), f32_opt(mean, C, "mean"), f32_opt(invstd, C, "invstd"),
                                 dg.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), u16m(dx), R,
                                 static_cast<int>(C), cur_stream(x));

@@ -140,6 +140,10 @@ void launch_stem_conv_fwd(const uint16_t* x, int cin, const uint16_t* wp, uint16
                           int OW, const float* kshift, float* part, hipStream_t s);
 int stem_fwd_blocks(int N);
 int stem_wrw_blocks(int N, int OH);
+// Tall [G][C] partial pairs: rows S = partials_fold_rows(G) (0: no fold needed) of a first-level
+// fixed-order sum into op/oq [S][C]
+int partials_fold_rows(int G);
+void launch_partials_fold(const float* p, const float* q, int G, int C, float* op, float* oq, hipStream_t s);
 // BN finalize from producer-fused partial sums ps/pq: [G][C] of sum(x - k), sum((x - k)^2)
 void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,

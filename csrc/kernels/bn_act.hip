@@ -20,14 +20,18 @@
 
 namespace psamd {
 
+// channel groups (8 channels) per reduction block: wide tensors split into 256-channel tiles
+// (blockIdx.y), so ~2048 blocks stream them with [G, C] partials of ~4 MB at any C
+constexpr int kRedTpr = 32;
+
 struct RedGeom {
-  int tpr;      // threads per row = C / 8 (capped at 256 per channel tile)
+  int tpr;      // threads per row = C / 8 (capped at kRedTpr per channel tile)
   int rows_it;  // rows a block covers per iteration = 256 / tpr
 };
 
 __host__ __device__ inline RedGeom red_geom(int C) {
   int tpr = C / 8;
-  if (tpr > 256) tpr = 256;
+  if (tpr > kRedTpr) tpr = kRedTpr;
   // round up to a power of two so rows_it * tpr == 256 (idle lanes if C/8 is not one)
   int p = 1;
   while (p < tpr) p <<= 1;
@@ -40,7 +44,7 @@ int bn_red_blocks(int64_t R, int C) {
   // ... unless that leaves the chip under-filled: wide-channel / few-row tensors (ResNet stage 3-4:
   // 25-100K rows x 1-2K channels) need ~2048 blocks in total to keep enough loads in flight, down
   // to 8 rows per block
-  const int ctiles = (C / 8 + 255) / 256;
+  const int ctiles = (C / 8 + kRedTpr - 1) / kRedTpr;
   const int64_t want = (2048 + ctiles - 1) / ctiles;
   if (g < want) g = std::min<int64_t>(want, (R + 7) / 8);
   if (g < 1) g = 1;
@@ -59,7 +63,7 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* _
   __shared__ float lds_q[256 * 8];
   const RedGeom gm = red_geom(C);
   const int t = threadIdx.x;
-  const int cg = t % gm.tpr + blockIdx.y * 256;  // channel group (8 channels)
+  const int cg = t % gm.tpr + blockIdx.y * kRedTpr;  // channel group (8 channels)
   const int r0 = t / gm.tpr;
   const int ngroups = C / 8;
   const int64_t G = gridDim.x;
@@ -117,21 +121,32 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const uint16_t* _
   }
 }
 
-// Sum the [G, C] partials of one 8-channel group per block: thread t reads rows g = t, t+256, ...
-// (8 consecutive channels = 32 B per row), then an LDS tree over the 256 threads.  Fixed
+// Sum the [G, C] partials of one 8-channel group per block: thread t reads rows g = t, t + blockDim, ...
+// (8 consecutive channels = 32 B per row), then a wave + LDS tree over the block.  Fixed
 // order -> deterministic.  Returns the 8 sums in threads 0..7 (one channel each).
 __device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const float* __restrict__ q, int G, int C,
                                               int cg, float* lds, float& outp, float& outq) {
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    float u[8], v[8];
-    load8(p, static_cast<int64_t>(g) * C + cg * 8, u);
-    load8(q, static_cast<int64_t>(g) * C + cg * 8, v);
+  // 4 rows per thread in flight at once (branch-free: clamped row, zero weight past G); a rolled
+  // loop waits out one L2/HBM round trip per row (12-25 us per call at G = 2048)
+  constexpr int U = 4;
+  for (int g0 = threadIdx.x; g0 < G; g0 += U * blockDim.x) {
+    float u[U][8], v[U][8], w[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a[j] += u[j];
-      b[j] += v[j];
+    for (int i = 0; i < U; ++i) {
+      const int g = g0 + i * blockDim.x;
+      w[i] = g < G ? 1.f : 0.f;
+      const int64_t o = static_cast<int64_t>(g < G ? g : G - 1) * C + cg * 8;
+      load8(p, o, u[i]);
+      load8(q, o, v[i]);
     }
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] += w[i] * u[i][j];
+        b[j] += w[i] * v[i][j];
+      }
   }
   // wave reduce, then across the 4 waves through LDS
 #pragma unroll
@@ -159,11 +174,40 @@ __device__ __forceinline__ void sum_partials8(const float* __restrict__ p, const
   }
 }
 
+// First level for very tall partials (the per-tile partials of the non-persistent conv GEMMs,
+// G ~ 12.5K rows): block (cg, s) sums rows [s * kFoldRows, (s + 1) * kFoldRows) of channel
+// group cg into row s of [S][C] -- fixed order, so the two-level sum stays deterministic.
+constexpr int kFoldRows = 1024;
+__global__ __launch_bounds__(256) void partials_fold_kernel(const float* __restrict__ p, const float* __restrict__ q,
+                                                            int G, int C, float* __restrict__ op,
+                                                            float* __restrict__ oq) {
+  __shared__ float lds[16 * 16];
+  const int r0 = blockIdx.y * kFoldRows;
+  const int rows = G - r0 < kFoldRows ? G - r0 : kFoldRows;
+  float a = 0.f, b = 0.f;
+  sum_partials8(p + static_cast<int64_t>(r0) * C, q + static_cast<int64_t>(r0) * C, rows, C, blockIdx.x, lds, a, b);
+  if (threadIdx.x < 8) {
+    const int64_t o = static_cast<int64_t>(blockIdx.y) * C + blockIdx.x * 8 + threadIdx.x;
+    op[o] = a;
+    oq[o] = b;
+  }
+}
+
+int partials_fold_rows(int G) { return G > 2 * kFoldRows ? (G + kFoldRows - 1) / kFoldRows : 0; }
+
+void launch_partials_fold(const float* p, const float* q, int G, int C, float* op, float* oq, hipStream_t s) {
+  hipLaunchKernelGGL(partials_fold_kernel, dim3(C / 8, partials_fold_rows(G)), dim3(256), 0, s, p, q, G, C, op, oq);
+}
+
+// Threads per finalize block (one block per 8 channels): the per-tile partials of the
+// non-persistent conv GEMMs reach G ~ 12.5K rows, which 256 threads walk in 25-35 us.
+inline int fin_threads(int G) { return G >= 4096 ? 1024 : G >= 1024 ? 512 : 256; }
+
 // per channel: mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; running stats.
-// grid = C / 8 blocks of 256 threads.
+// grid = C / 8 blocks of fin_threads(G) threads.
 // kshift: the shift the partial sums were taken about -- x[0, c] when null (bn_stats_partial),
 // else an explicit per-channel array (producer-fused statistics, e.g. the stem convolution).
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
                                                           const uint16_t* __restrict__ x,
                                                           const float* __restrict__ kshift, int G, int C, int64_t R,
                                                           float eps, float momentum, const float* __restrict__ gamma,
@@ -171,7 +215,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ rvar, float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out, float* __restrict__ scale,
                                                           float* __restrict__ shift) {
-  __shared__ float lds[64];
+  __shared__ float lds[16 * 16];  // up to 16 waves
   float s1 = 0.f, s2 = 0.f;
   sum_partials8(ps, pq, G, C, blockIdx.x, lds, s1, s2);
   if (threadIdx.x >= 8) return;
@@ -287,7 +331,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   __shared__ float lds_x[256 * 8];
   const RedGeom gm = red_geom(C);
   const int t = threadIdx.x;
-  const int cg = t % gm.tpr + blockIdx.y * 256;
+  const int cg = t % gm.tpr + blockIdx.y * kRedTpr;
   const int r0 = t / gm.tpr;
   const int ngroups = C / 8;
   const int64_t G = gridDim.x;
@@ -371,7 +415,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
 }
 
 // dgamma = sum dz*xhat, dbeta = sum dz; dx = A dz + B x + Cc.  grid = C / 8 blocks.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pd,
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ pd,
                                                               const float* __restrict__ px, int G, int C, int64_t R,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
@@ -379,7 +423,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ ca, float* __restrict__ cb,
                                                               float* __restrict__ cc) {
-  __shared__ float lds[64];
+  __shared__ float lds[16 * 16];  // up to 16 waves
   float sd = 0.f, sx = 0.f;
   sum_partials8(pd, px, G, C, blockIdx.x, lds, sd, sx);
   if (threadIdx.x >= 8) return;
@@ -469,9 +513,9 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
   const int cblocks = (C + 255) / 256;
   if (a.training) {
     const int G = a.G;
-    const int ctiles = (C / 8 + 255) / 256;
+    const int ctiles = (C / 8 + kRedTpr - 1) / kRedTpr;
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(G, ctiles), dim3(256), 0, s, a.x, R, C, a.ws, a.ws + G * C);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, a.x, nullptr, G, C, R,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, a.ws, a.ws + G * C, a.x, nullptr, G, C, R,
                        a.eps,
                        a.momentum, a.gamma, a.beta, a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
   } else {
@@ -503,7 +547,7 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
 void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,
                              float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(256), 0, s, ps, pq, nullptr, kshift, G, C, R, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, ps, pq, nullptr, kshift, G, C, R, eps,
                      momentum, gamma, beta, rmean, rvar, mean, invstd, scale, shift);
 }
 
@@ -511,7 +555,7 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   const int C = a.C;
   const int64_t R = a.R;
   const int G = a.G;
-  const int ctiles = (C / 8 + 255) / 256;
+  const int ctiles = (C / 8 + kRedTpr - 1) / kRedTpr;
   const int act = a.mbits ? 3 : ((a.act == 1 && a.mask_coef && !a.dres) ? 2 : a.act);
 #define PSAMD_BN_RED(ACT)                                                                                       \
   hipLaunchKernelGGL(bn_bwd_reduce_kernel<ACT>, dim3(G, ctiles), dim3(256), 0, s, a.dy, a.y, a.x, a.mask_coef, \
@@ -522,7 +566,7 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   else PSAMD_BN_RED(0);
 #undef PSAMD_BN_RED
   float* coef = a.ws + 2 * G * C;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, s, a.ws, a.ws + G * C, G, C, R,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, a.ws, a.ws + G * C, G, C, R,
                      a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   const int grid = stream_grid(nvec, 256);
@@ -627,7 +671,7 @@ void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* c
 void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
                             float* coef, uint16_t* dx, int64_t R, int C, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, s, pd, px, G, C, R, gamma, mean, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, pd, px, G, C, R, gamma, mean, invstd,
                      dgamma, dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   if (nvec <= 0) return;

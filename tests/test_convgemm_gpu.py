@@ -273,3 +273,23 @@ def test_fused_bottleneck_matches_module_path(inplanes, planes, stride):
         _close(p.grad, q.grad, tol=3e-2, amax=0.25)
     for (name, t), (_, u) in zip(a.named_buffers(), b.named_buffers()):
         torch.testing.assert_close(t.float(), u.float(), rtol=2e-3, atol=2e-3, msg=name)
+
+
+def test_tall_partials_fold_into_bn_finalize():
+    """G > 2048 partial rows (per-tile partials of a non-persistent conv GEMM) take a first-level
+    fold (partials_fold_kernel) before the finalize kernels; sums vs fp64."""
+    G, C, R = 5000, 64, 100000
+    g = _gen(77)
+    part = torch.stack([torch.randn(G, C, generator=g), torch.rand(G, C, generator=g) * 40])
+    kshift = torch.randn(C, generator=g)
+    mean, invstd, coef = native().bn_finalize_sums(part.to(DEV), kshift.to(DEV), R, None, None, None, None, 0.1, 1e-5)
+    s1, s2 = part[0].double().sum(0), part[1].double().sum(0)
+    dm = s1 / R
+    torch.testing.assert_close(mean.cpu().double(), kshift.double() + dm, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(invstd.cpu().double(), (s2 / R - dm * dm + 1e-5).rsqrt(), rtol=1e-4, atol=1e-5)
+    x = _rnd(3000, C, g=g)
+    gr = _rnd(3000, C, g=g)
+    m, i = torch.randn(C, generator=g) * 0.1, torch.rand(C, generator=g) + 0.5
+    _, dgamma, dbeta = native().bn_bwd_partials(_bf(gr), _bf(x), part.to(DEV), None, m.to(DEV), i.to(DEV))
+    torch.testing.assert_close(dbeta.cpu().double(), s1, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dgamma.cpu().double(), s2, rtol=1e-5, atol=1e-2)
