@@ -209,9 +209,9 @@ inline int fin_threads(int G) { return G >= 4096 ? 1024 : G >= 1024 ? 512 : 256;
 // else an explicit per-channel array (producer-fused statistics, e.g. the stem convolution).
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
                                                           const uint16_t* __restrict__ x,
-                                                          const float* __restrict__ kshift, int G, int C, int64_t R,
+                                                          const float* kshift /* may alias rmean */, int G, int C, int64_t R,
                                                           float eps, float momentum, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* __restrict__ rmean,
+                                                          const float* __restrict__ beta, float* rmean,
                                                           float* __restrict__ rvar, float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out, float* __restrict__ scale,
                                                           float* __restrict__ shift) {

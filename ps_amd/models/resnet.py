@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
-from ..ops.convgemm import fused_block_ok, fused_bottleneck
+from ..ops.convgemm import deferred_bn_counters, fused_block_ok, fused_bottleneck
 from ..ops.pool import MaxPool2d
 
 
@@ -100,7 +100,8 @@ class ResNet(nn.Module):
             x = stem_bn_relu_maxpool(x, self.conv1, self.bn1)
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        with deferred_bn_counters():
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

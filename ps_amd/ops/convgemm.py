@@ -28,7 +28,9 @@ oracle in tests/test_convgemm_gpu.py.  ``PS_AMD_FUSED_BLOCK=0`` disables the fus
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from typing import List
 
 import torch
@@ -96,7 +98,9 @@ class _BottleneckFn(torch.autograd.Function):
         gi, go = geo(h, w), geo(oh, ow)
         x2 = rows(x)
         bn1, bn2, bn3 = blk.bn1, blk.bn2, blk.bn3
-        k1 = bn1.running_mean.clone()  # shift of the statistics sums (~ the batch mean)
+        # shift of the statistics sums (~ the batch mean): the running mean itself -- the finalize
+        # kernel reads channel c's shift before it updates that channel's running mean
+        k1 = bn1.running_mean
         z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
         m1, i1, cf1 = _finalize(p1, k1, n * h * w, bn1)
         y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)[0]
@@ -104,12 +108,12 @@ class _BottleneckFn(torch.autograd.Function):
         z2r = rows(z2)
         m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
                                    float(bn2.eps))
-        k3 = bn3.running_mean.clone()
+        k3 = bn3.running_mean
         z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
         m3, i3, cf3 = _finalize(p3, k3, n * oh * ow, bn3)
         if wd is not None:
             bnd = blk.downsample[1]
-            kd = bnd.running_mean.clone()
+            kd = bnd.running_mean
             zd, pd = nat.conv_gemm(x2, _mat(wd), geo(h, w, 1, s), None, 1, None, kd)
             md, idd, cfd = _finalize(pd, kd, n * oh * ow, bnd)
             out, obits = nat.bn_apply_coef(z3, cf3, zd, cfd, 1, True)
@@ -189,10 +193,31 @@ def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
     return all(c % 64 == 0 for c in (x.shape[1], c1.out_channels, c3.out_channels))
 
 
+_tls = threading.local()
+
+
+@contextlib.contextmanager
+def deferred_bn_counters():
+    """Collect the BN ``num_batches_tracked`` increments of the fused blocks run inside and apply
+    them as one multi-tensor add on exit (53 one-element kernels per ResNet-50 step otherwise)."""
+    prev = getattr(_tls, "pending", None)
+    _tls.pending = []
+    try:
+        yield
+    finally:
+        pending, _tls.pending = _tls.pending, prev
+        if pending:
+            torch._foreach_add_(pending, 1)
+
+
 def fused_bottleneck(blk: nn.Module, x: torch.Tensor) -> torch.Tensor:
     ds = blk.downsample
-    for bn in [blk.bn1, blk.bn2, blk.bn3] + ([ds[1]] if ds is not None else []):
-        bn.num_batches_tracked.add_(1)
+    counters = [bn.num_batches_tracked for bn in [blk.bn1, blk.bn2, blk.bn3] + ([ds[1]] if ds is not None else [])]
+    pending = getattr(_tls, "pending", None)
+    if pending is not None:
+        pending.extend(counters)
+    else:
+        torch._foreach_add_(counters, 1)
     wd, gd, bd = (ds[0].weight, ds[1].weight, ds[1].bias) if ds is not None else (None, None, None)
     return _BottleneckFn.apply(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
                                blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk)
