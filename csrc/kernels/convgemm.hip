@@ -117,6 +117,22 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* T, int s, int c0, in
   return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
 }
 
+// tr_frag through inline asm: the compiler cannot tell an LDS-DMA (global_load_lds) in flight to
+// the other buffer from this read and would put s_waitcnt vmcnt(0) before every ds_read_b64_tr_b16
+// (serialising the prefetch).  The caller waits lgkmcnt itself (lds_wait_frags).
+template <int RL>
+__device__ __forceinline__ bf16x8_t tr_frag_asm(const uint16_t* T, int s, int c0, int lane) {
+  const int gi = lane >> 4, i16 = lane & 15;
+  const int r = 16 * s + 8 * (gi >> 1) + (i16 >> 2);
+  const int col = c0 + 16 * (gi & 1) + 4 * (i16 & 3);
+  const unsigned a0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((const lds_s16x4*)(T + tr_off<RL>(r, col))));
+  const unsigned a1 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((const lds_s16x4*)(T + tr_off<RL>(r + 4, col))));
+  s16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+  return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+}
+
 __device__ __forceinline__ u16x8 bn_relu8(u16x8 v, const float (&sc)[8], const float (&sh)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -516,7 +532,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
 // dW tile [n0, n0 + 64 TNO) x [k0, k0 + 64 TKO) over pixels [mb, me): grid = tiles * nsplit
 // blocks; logical id -> tile = id % tiles, split = id / tiles, so blocks on one XCD share a
 // pixel range (dZ / A rows through L2).  4 waves as 2 x 2; 64-pixel stages, two LDS buffers.
-template <int TNO, int TKO, bool PRO>
+template <int TNO, int TKO, bool PRO, bool GL>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs p, int rows_per_split) {
   constexpr int BNO = 64 * TNO, BKO = 64 * TKO;
   constexpr int STAGE = kWM * (BNO + BKO);
@@ -586,7 +602,92 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
   const int nch = me > mb ? (me - mb + kWM - 1) / kWM : 0;  // block-uniform
-  if (nch > 0) {
+  auto mma = [&](int buf) {
+    const uint16_t* Gs = lds + buf * STAGE;
+    const uint16_t* Xs = Gs + kWM * BNO;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8_t ga[TNO], xb[TKO];
+#pragma unroll
+      for (int i = 0; i < TNO; ++i) ga[i] = tr_frag<BNO>(Gs, s, wn + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < TKO; ++j) xb[j] = tr_frag<BKO>(Xs, s, wk + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < TNO; ++i)
+#pragma unroll
+        for (int j = 0; j < TKO; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if constexpr (GL) {
+    // LDS-DMA staging (no prologue): one wave instruction fills 64 consecutive 16-B chunks of
+    // the [64][RL] tile, i.e. 1 KB of rows lane-linearly; the transposed-read swizzle moves to
+    // the source chunk (tr_off's XOR is an involution).  Rows past the split / out-of-map taps
+    // read the zero page.  Two buffers: issue stage ci + 1, counted vmcnt for stage ci.
+    static_assert(!PRO, "the BN prologue needs register staging");
+    constexpr int GI = GIT, XI = XIT;  // DMA instructions per wave per stage (64 chunks each)
+    auto issue = [&](int mc, int buf) {
+      uint16_t* Gs = lds + buf * STAGE;
+      uint16_t* Xs = Gs + kWM * BNO;
+#pragma unroll
+      for (int i = 0; i < GI; ++i) {
+        const int L = (wave * GI + i) * 64 + lane, r = L / GCPR, pc = L % GCPR;
+        const int lc = BNO == 128 ? (pc ^ ((r & 3) << 2)) : (pc ^ (((r >> 1) & 1) << 2));
+        const uint16_t* src = mc + r < me ? p.dz + static_cast<int64_t>(mc + r) * p.N + n0 + lc * 8 : kZeroPage;
+        __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Gs + (wave * GI + i) * 512), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int L = (wave * XI + i) * 64 + lane, r = L / XCPR, pc = L % XCPR;
+        const int lc = BKO == 128 ? (pc ^ ((r & 3) << 2)) : (pc ^ (((r >> 1) & 1) << 2));
+        const PixSrc ps = pix_src(mc + r < me ? mc + r : p.M, p.M, g);
+        const int64_t o = tap_off(ps, kh, kw, cc0 + lc * 8, g);
+        const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
+        __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
+      }
+    };
+    auto mma_gl = [&](int buf) {
+      const uint16_t* Gs = lds + buf * STAGE;
+      const uint16_t* Xs = Gs + kWM * BNO;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8_t ga[TNO], xb[TKO];
+#pragma unroll
+        for (int i = 0; i < TNO; ++i) ga[i] = tr_frag_asm<BNO>(Gs, s, wn + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < TKO; ++j) xb[j] = tr_frag_asm<BKO>(Xs, s, wk + 32 * j, lane);
+        // the reads landed; the "+v" ties keep every MFMA below the wait
+#pragma unroll
+        for (int i = 0; i < TNO; ++i) asm volatile("" : "+v"(ga[i]));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < TNO; ++i) asm volatile("" : "+v"(ga[i]));
+#pragma unroll
+        for (int j = 0; j < TKO; ++j) asm volatile("" : "+v"(xb[j]));
+#pragma unroll
+        for (int i = 0; i < TNO; ++i)
+#pragma unroll
+          for (int j = 0; j < TKO; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    if (nch > 0) {
+      issue(mb, 0);
+      for (int ci = 0; ci < nch; ++ci) {
+        if (ci + 1 < nch) {
+          issue(mb + kWM * (ci + 1), (ci + 1) & 1);
+          if constexpr (GI + XI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else if constexpr (GI + XI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();  // every wave's stage-ci DMAs landed
+        mma_gl(ci & 1);
+        lds_barrier();  // stage ci read out before stage ci + 2 is issued into its buffer
+      }
+    }
+  } else if (nch > 0) {
     gload(mb);
     swrite(0, mb);
     lds_barrier();
@@ -594,21 +695,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
       const bool more = ci + 1 < nch;
       const int mc = mb + kWM * ci;
       if (more) gload(mc + kWM);
-      const uint16_t* Gs = lds + (ci & 1) * STAGE;
-      const uint16_t* Xs = Gs + kWM * BNO;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8_t ga[TNO], xb[TKO];
-#pragma unroll
-        for (int i = 0; i < TNO; ++i) ga[i] = tr_frag<BNO>(Gs, s, wn + 32 * i, lane);
-#pragma unroll
-        for (int j = 0; j < TKO; ++j) xb[j] = tr_frag<BKO>(Xs, s, wk + 32 * j, lane);
-#pragma unroll
-        for (int i = 0; i < TNO; ++i)
-#pragma unroll
-          for (int j = 0; j < TKO; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
-      }
+      mma(ci & 1);
       if (more) swrite((ci + 1) & 1, mc + kWM);
       lds_barrier();
     }
@@ -734,10 +821,11 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const WPlan w = wplan(a.M, a.N, a.K, a.g.C);
   const int nblk = w.tiles * w.nsplit;
-#define PSAMD_CW(TN, TK, PRO) \
-  hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO>), dim3(nblk), dim3(256), 0, s, a, w.rows)
+#define PSAMD_CW(TN, TK, PRO, GL) \
+  hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO, GL>), dim3(nblk), dim3(256), 0, s, a, w.rows)
+  // without the prologue both operands are plain row slices: LDS-DMA staging
 #define PSAMD_CWP(TN, TK) \
-  if (a.pro) { PSAMD_CW(TN, TK, true); } else { PSAMD_CW(TN, TK, false); }
+  if (a.pro) { PSAMD_CW(TN, TK, true, false); } else { PSAMD_CW(TN, TK, false, true); }
   if (w.tno == 2) {
     if (w.tko == 2) { PSAMD_CWP(2, 2) } else { PSAMD_CWP(2, 1) }
   } else {
