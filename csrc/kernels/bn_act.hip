@@ -52,6 +52,16 @@ int bn_red_blocks(int64_t R, int C) {
   return static_cast<int>(g);
 }
 
+// Elementwise BN passes: ~2 vectors per thread (one trip of the 2-vector loop), not a
+// 2048-block grid-stride sweep -- the short-lived waves keep more loads in flight per CU
+// (stage-1 block output + residual + bits: 519 -> 436 us, profiles/r1_stream_probe.jsonl).
+inline int apply_grid(int64_t nvec) {
+  int64_t g = (nvec + 511) / 512;
+  if (g < 1) g = 1;
+  if (g > (int64_t(1) << 22)) g = int64_t(1) << 22;
+  return static_cast<int>(g);
+}
+
 // ------------------------------------------------------------------------------ stats
 // Shifted sums per block: partial_s1[g, c] = sum (x - K_c), partial_s2[g, c] = sum (x - K_c)^2
 // with the shift K_c = x[0, c] (a sample of the channel, so |mean - K| ~ std): robust when
@@ -524,7 +534,7 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
   }
   if (!a.y) return;  // statistics / coefficients only (the apply is fused into a consumer)
   const int64_t nvec = R * C / 8;
-  const int grid = stream_grid(nvec, 256);
+  const int grid = apply_grid(nvec);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
   uint8_t* nomask = nullptr;
 #define PSAMD_BN_APPLY(RES, ACT)                                                                              \
@@ -569,7 +579,7 @@ void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, a.ws, a.ws + G * C, G, C, R,
                      a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
-  const int grid = stream_grid(nvec, 256);
+  const int grid = apply_grid(nvec);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
 #define PSAMD_BN_BWD(ACT, DRES)                                                                                 \
   if (fixed)                                                                                                    \
@@ -636,7 +646,7 @@ void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* c
                           uint8_t* mbits, int64_t R, int C, int act, hipStream_t s) {
   const int64_t nvec = R * C / 8;
   if (nvec <= 0) return;
-  const int grid = stream_grid(nvec, 256);
+  const int grid = apply_grid(nvec);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
   const bool mask = mbits != nullptr;
 #define PSAMD_LAUNCH(K, ...) hipLaunchKernelGGL((K<__VA_ARGS__>), dim3(grid), dim3(256), 0, s, ARGS)
@@ -675,7 +685,7 @@ void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint1
                      dgamma, dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   if (nvec <= 0) return;
-  const int grid = stream_grid(nvec, 256);
+  const int grid = apply_grid(nvec);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
   const uint16_t* none = nullptr;
   const float* nomc = nullptr;
