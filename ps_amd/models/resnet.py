@@ -17,7 +17,7 @@ import torch.nn as nn
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
 from ..ops.convgemm import deferred_bn_counters, fused_block_ok, fused_bottleneck
-from ..ops.pool import MaxPool2d
+from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 class Bottleneck(nn.Module):
@@ -102,7 +102,10 @@ class ResNet(nn.Module):
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         with deferred_bn_counters():
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
+        if self.fused_bn:
+            x = global_avg_pool(x)  # NHWC gradient straight into the last block's backward
+        else:
+            x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 

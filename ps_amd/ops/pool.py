@@ -94,3 +94,27 @@ def bn_relu_maxpool(x: torch.Tensor, bn: nn.BatchNorm2d, k: int, s: int, p: int)
     if getattr(bn, "act", "relu") == "none" or type(bn) is nn.BatchNorm2d:
         y = torch.relu(y)
     return max_pool2d(y, k, s, p)
+
+
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """[N, C, H, W] channels_last -> [N, C] mean.  The backward writes the broadcast gradient
+    straight in NHWC order (one vectorised expand-copy), instead of the NCHW-shaped adaptive-pool
+    gradient plus a channels_last transpose in its consumer."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return F.adaptive_avg_pool2d(x, 1).flatten(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w = ctx.shape
+        gx = (g * (1.0 / (h * w))).to(g.dtype)[:, None, None, :].expand(n, h, w, c).contiguous()
+        return gx.permute(0, 3, 1, 2)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """AdaptiveAvgPool2d(1) + flatten; channels_last GPU tensors get the NHWC backward."""
+    if x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        return _GlobalAvgPoolNHWC.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -26,6 +26,15 @@ Consistency (SURVEY §2.3, quirks Q1-Q3 fixed):
     slowest worker by more than s -- the SSP bound, enforced by the collective itself.
   * Gradient accumulators are zeroed every round and averaged over exactly W workers.
 
+Gradient landing (no per-parameter accumulate kernels): ``p.grad`` is None when backward
+starts, so autograd's AccumulateGrad adopts each freshly computed gradient without a kernel;
+the post-accumulate hook parks it, and when a bucket's last key is ready ONE multi-tensor copy
+(``torch._foreach_copy_``) lands all of them in the flat bucket, after which ``p.grad`` is the
+bucket view.  4-D conv weights with spatial extent (3x3) are stored channels_last inside the
+flat buffers, so the replica the forward reads and the gradient MIOpen returns already have
+the layout the convolution wants -- no per-step weight / gradient transposes.  Keys that got
+no gradient in a step are zero-filled at launch.
+
 Options: global-norm clipping (two-phase: push all, norm, then serve+pull), 1-bit
 compressed push with error feedback (compress="onebit": bits all-to-all to the owners +
 owner-side unpack-reduce kernel), arbitrary per-key-prefix updaters (resolve_updater).
@@ -77,6 +86,8 @@ class ColocatedPS:
             self.reg.add(n, p.shape, p.dtype)
         self.reg.finalize()
         self.params = dict(params)
+        # keys stored channels_last in the flat buffers (element order O, kh, kw, I)
+        self.cl_keys = {n for n, p in params if _wants_channels_last(p)}
         R = self.reg
         # ---------------- replica buffers (rings of s+1 slots)
         self.wbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
@@ -86,7 +97,8 @@ class ColocatedPS:
         with torch.no_grad():
             for n, p in params:
                 ki = R.keys[n]
-                self.wbuf[ki.group][0][ki.offset:ki.offset + ki.numel].copy_(p.detach().reshape(-1))
+                src = p.detach().permute(0, 2, 3, 1) if n in self.cl_keys else p.detach()
+                self.wbuf[ki.group][0][ki.offset:ki.offset + ki.numel].view(src.shape).copy_(src)
             if broadcast_init:
                 for g in self.wbuf:
                     self.t.broadcast(self.wbuf[g][0], src=0)
@@ -143,6 +155,7 @@ class ColocatedPS:
         self.pending = [len(b.keys) for b in R.buckets]
         self.launched = [False] * len(R.buckets)
         self._key_bucket = {n: R.keys[n].bucket for n in self.params}
+        self._landing: List[Dict[str, torch.Tensor]] = [dict() for _ in R.buckets]  # parked grads
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
         self.round_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
@@ -167,12 +180,16 @@ class ColocatedPS:
     # ------------------------------------------------------------------ views
     def _view(self, buf: Dict[str, List[torch.Tensor]], slot: int, name: str) -> torch.Tensor:
         ki = self.reg.keys[name]
-        return buf[ki.group][slot][ki.offset:ki.offset + ki.numel].view(ki.shape)
+        flat = buf[ki.group][slot][ki.offset:ki.offset + ki.numel]
+        if name in self.cl_keys:
+            o, i, kh, kw = ki.shape
+            return flat.view(o, kh, kw, i).permute(0, 3, 1, 2)
+        return flat.view(ki.shape)
 
     def _bind(self, wslot: int, gslot: int) -> None:
         for n, p in self.params.items():
             p.data = self._view(self.wbuf, wslot, n)
-            p.grad = self._view(self.gbuf, gslot, n)
+            p.grad = None  # AccumulateGrad adopts the fresh gradient; _land() copies it in
 
     def weight(self, name: str) -> torch.Tensor:
         """Current replica weights of key ``name`` (the pulled version)."""
@@ -183,14 +200,35 @@ class ColocatedPS:
         if self.accumulating:
             return
         b = self._key_bucket[name]
-        self.pending[b] -= 1
+        if name not in self._landing[b]:
+            self.pending[b] -= 1
+        self._landing[b][name] = p.grad
         if self.pending[b] == 0 and self.overlap:
             self._launch(b)
+
+    def _land(self, b: int) -> None:
+        """Copy the bucket's parked gradients into its gradient slot (one multi-tensor kernel on
+        the compute stream) and rebind ``p.grad`` to the bucket views; zero keys without one."""
+        parked = self._landing[b]
+        dst, src = [], []
+        for n in self.reg.buckets[b].keys:
+            v = self._view(self.gbuf, self.gslot, n)
+            g = parked.get(n)
+            if g is None:
+                v.zero_()
+            elif g.data_ptr() != v.data_ptr():
+                dst.append(v)
+                src.append(g)
+            self.params[n].grad = v
+        if dst:
+            torch._foreach_copy_(dst, src)
+        self._landing[b] = {}
 
     def _launch(self, b: int) -> None:
         if self.launched[b]:
             return
         self.launched[b] = True
+        self._land(b)
         if self.fault is not None:
             self.fault.before_push()
         if self.gpu:
@@ -358,9 +396,8 @@ class ColocatedPS:
                 torch.cuda.current_stream(self.device).wait_event(ev)
         self.wslot = v % self.nslots
         self.gslot = self.round % self.nslots
-        g = self.gbuf
-        for grp in g:
-            g[grp][self.gslot].zero_()
+        # no zero-fill of the next gradient slot: _land() overwrites every key region (padding is
+        # never written and stays zero)
         self.pending = [len(b.keys) for b in self.reg.buckets]
         self.launched = [False] * len(self.reg.buckets)
         self._bind(self.wslot, self.gslot)
@@ -393,7 +430,9 @@ class ColocatedPS:
             "master": [m.detach().cpu() for m in self.master],
             "states": [[[s.detach().cpu() for s in st] for st in sts] for sts in self.states],
             "manifest": {k: {"shape": list(ki.shape), "dtype": str(ki.dtype), "bucket": ki.bucket,
-                             "offset": ki.offset, "group": ki.group} for k, ki in self.reg.keys.items()},
+                             "offset": ki.offset, "group": ki.group,
+                             "layout": "channels_last" if k in self.cl_keys else "contiguous"}
+                         for k, ki in self.reg.keys.items()},
             "buckets": [{"group": b.group, "start": b.start, "size": b.size} for b in self.reg.buckets],
         }
 
@@ -415,6 +454,7 @@ class ColocatedPS:
                 for slot in range(self.nslots):
                     wfull = self.wbuf[bk.group][slot]
                     wfull[lo:hi].copy_(self.master[b].to(wfull.dtype))
+                    # (flat element order, channels_last keys included, is the same on every rank)
                     self.t.all_gather(wfull[bk.start:bk.start + bk.size], wfull[lo:hi])
         self.wslot = max(0, self.round - self.staleness) % self.nslots
         self.gslot = self.round % self.nslots
@@ -426,6 +466,12 @@ class ColocatedPS:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+def _wants_channels_last(p: torch.Tensor) -> bool:
+    """Conv weight with spatial extent and >4 input channels held channels_last by the model."""
+    return (p.dim() == 4 and p.shape[2] * p.shape[3] > 1 and p.shape[1] > 4
+            and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous())
 
 
 def timed(fn):
