@@ -891,7 +891,8 @@ static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::v
 // c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> [c, BN partials [2, G, N] (epi 1/3)]
 std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10::optional<Tensor> pro, int64_t epi,
                               c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
-                              c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits) {
+                              c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits,
+                              c10::optional<Tensor> aux2, c10::optional<Tensor> bits2) {
   check_rows(a, "a");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
@@ -899,33 +900,48 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   const int64_t N = b.size(0), K = b.size(1);
   TORCH_CHECK(K == static_cast<int64_t>(g.ks) * g.ks * g.C, "b must be [N, ks*ks*C]");
   TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
-  TORCH_CHECK(epi >= 0 && epi <= 5, "epi in 0..5");
+  TORCH_CHECK(epi >= 0 && epi <= 8, "epi in 0..8");
+  const int base = epi == 6 ? 5 : epi == 7 ? 2 : epi == 8 ? 4 : static_cast<int>(epi);
+  const bool fold = epi >= 6;
   const int64_t M = gi.second * g.OH * g.OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "pixel count");
   const uint16_t* auxp = nullptr;
   if (epi >= 2) {
     TORCH_CHECK(aux.has_value() && aux->defined(), "epi ", epi, " needs aux");
     check_rows(*aux, "aux");
-    const int64_t want = epi == 4 ? gi.second * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) * N : M * N;
+    const int64_t want = base == 4 ? gi.second * ((g.OH + 1) / 2) * ((g.OW + 1) / 2) * N : M * N;
     TORCH_CHECK(aux->numel() == want, "aux has ", aux->numel(), " elements, expected ", want);
     auxp = u16(*aux);
   }
   if (epi == 3) TORCH_CHECK(mc.has_value() && mean.has_value() && invstd.has_value(), "epi 3 needs mc, mean, invstd");
   const uint8_t* bitsp = nullptr;
-  if (epi == 5) {
-    TORCH_CHECK(bits.has_value() && bits->defined(), "epi 5 needs bits");
+  if (base == 5) {
+    TORCH_CHECK(bits.has_value() && bits->defined(), "epi 5/6 needs bits");
     check_gpu(*bits, "bits");
     TORCH_CHECK(bits->scalar_type() == torch::kUInt8 && bits->numel() * 8 == M * N, "bits: uint8 [M * N / 8]");
     bitsp = bits->data_ptr<uint8_t>();
   }
   TORCH_CHECK(!(pro.has_value() && pro->defined()) || epi <= 1, "the BN prologue combines with epilogue 0 or 1 only");
+  const uint16_t* aux2p = nullptr;
+  const uint8_t* bits2p = nullptr;
+  if (fold) {
+    TORCH_CHECK(aux2.has_value() && aux2->defined() && bits2.has_value() && bits2->defined() && mean.has_value() &&
+                    invstd.has_value(),
+                "epi ", epi, " needs aux2, bits2, mean, invstd");
+    check_rows(*aux2, "aux2");
+    TORCH_CHECK(aux2->numel() == M * N, "aux2 must be [M, N]");
+    check_gpu(*bits2, "bits2");
+    TORCH_CHECK(bits2->scalar_type() == torch::kUInt8 && bits2->numel() * 8 == M * N, "bits2: uint8 [M * N / 8]");
+    aux2p = u16(*aux2);
+    bits2p = bits2->data_ptr<uint8_t>();
+  }
   const c10::DeviceGuard guard(a.device());
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
   const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K)).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
-  const bool sums = epi == 1 || epi == 3;
+  const bool sums = epi == 1 || epi == 3 || fold;
   Tensor part = sums ? torch::empty({2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};
   p.a = u16(a);
@@ -939,6 +955,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   p.epi = static_cast<int>(epi);
   p.aux = auxp;
   p.bits = bitsp;
+  p.aux2 = aux2p;
+  p.bits2 = bits2p;
   p.kshift = f32_opt(kshift, N, "kshift");
   p.mc = f32_opt(mc, 2 * N, "mc");
   p.mean = f32_opt(mean, N, "mean");
@@ -1029,7 +1047,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "ps_amd HIP kernels for MI355X (gfx950)";
   m.def("conv_gemm", &conv_gemm, py::arg("a"), py::arg("b"), py::arg("geo"), py::arg("pro") = py::none(),
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
-        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none());
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
+        py::arg("aux2") = py::none(), py::arg("bits2") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);

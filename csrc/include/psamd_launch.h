@@ -222,14 +222,18 @@ struct ConvGemmArgs {
   const float* pro;     // [scale | shift] (2C): A := relu(A * scale + shift) while staging; nullable
   int epi;              // 0 store, 1 + BN partial sums, 2 + residual, 3 ReLU mask + BN-backward sums,
                         // 4 + residual of the (OH+1)/2 x (OW+1)/2 map at even (h, w),
-                        // 5 + residual masked by bits (aux * relu'(forward output))
+                        // 5 + residual masked by bits (aux * relu'(forward output)),
+                        // 6/7/8 = 5/2/4 + the previous block's bn3 backward reduce (aux2, bits2,
+                        // mean, invstd): output masked by bits2, sums into part
   const uint16_t* aux;  // epi 2/4/5: residual rows; epi 3: BN input z [M, N]
-  const uint8_t* bits;  // epi 5: ReLU mask bits of aux's elements
+  const uint8_t* bits;  // epi 5/6: ReLU mask bits of aux's elements
+  const uint16_t* aux2; // epi 6-8: previous block's bn3 input z3 [M, N]
+  const uint8_t* bits2; // epi 6-8: ReLU mask bits of the previous block's output (= this input)
   const float* kshift;  // epi 1: shift of the partial sums [N] (nullable = 0)
   const float* mc;      // epi 3: [scale | shift] (2N) of that BN (ReLU mask)
-  const float* mean;    // epi 3: [N]
-  const float* invstd;  // epi 3: [N]
-  float* part;          // epi 1/3: [2][conv_fwd_plan(M, N, K).gm][N] block partial sums
+  const float* mean;    // epi 3/6-8: [N]
+  const float* invstd;  // epi 3/6-8: [N]
+  float* part;          // epi 1/3/6-8: [2][conv_fwd_plan(M, N, K).gm][N] block partial sums
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)

@@ -20,6 +20,9 @@
 //                  sum(g * xhat) -- its reduce pass
 //               4: + a stride-2 map's rows at even (h, w) (downsample data gradient)
 //               5: + residual rows masked by forward ReLU bits (identity gradient, never stored)
+//               6/7/8: epilogue 5/2/4, then the PREVIOUS block's bn3 backward reduce folded in:
+//                  g = v * relu'(previous block output) from its bits (stored masked) and the
+//                  sums sum(g), sum(g * (z3 - mean) * invstd) over that block's bn3 input z3
 //   conv_wgrad  dW[n, k] = sum_m dZ[m, n] f(A[src(m, k)]), split over m; both operands are read
 //               transposed from row-major LDS tiles (ds_read_b64_tr_b16); fp32 per-split slabs,
 //               fixed-order reduction (deterministic, no atomics).
@@ -171,6 +174,9 @@ struct StageRegs {
 
 template <int BM, int BN, bool PRO, int EPI, bool KS1, bool GLDS>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
+  // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce
+  constexpr bool FOLD = EPI >= 6;
+  constexpr int BASE = EPI == 6 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
   constexpr int TN = BN / 64;              // 32-channel MFMA blocks per wave
   constexpr int TM = BM / 64;              // 32-pixel MFMA blocks per wave
   constexpr int AR = BM / 32;              // A-tile chunks per thread per stage
@@ -330,6 +336,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     load8(p.mc + p.N, nc, e1);
     load8(p.mean, nc, e2);
     load8(p.invstd, nc, e3);
+  } else if constexpr (FOLD) {
+    load8(p.mean, nc, e2);
+    load8(p.invstd, nc, e3);
   }
   uint16_t* Cs = lds;
   auto epilogue = [&](int mt) {
@@ -355,15 +364,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8 + 4);
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const int64_t o = static_cast<int64_t>(m) * p.N + nc;
-      if constexpr (EPI == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
+      if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
         const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + o);
         const unsigned bits = p.bits[o >> 3];
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if ((bits >> j) & 1u) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
-      } else if constexpr (EPI == 2 || EPI == 4) {
+      } else if constexpr (BASE == 2 || BASE == 4) {
         int64_t ro = o;
-        if constexpr (EPI == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
+        if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
           const int ohw = g.OH * g.OW;
           const int i = m / ohw, r = m - i * ohw, h = r / g.OW, w = r - h * g.OW;
           const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
@@ -391,6 +400,18 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
           s1[j] += gv;
           s2[j] += gv * ((z - e2[j]) * e3[j]);
           if (!on) v[j] = 0;
+        }
+      }
+      if constexpr (FOLD) {  // previous block's bn3: ReLU mask from its output bits + reduce sums
+        const u16x8 z8 = *reinterpret_cast<const u16x8*>(p.aux2 + o);
+        const unsigned pb = p.bits2[o >> 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool on = (pb >> j) & 1u;
+          if (!on) v[j] = 0;
+          const float gv = bf16_to_f32(v[j]);
+          s1[j] += gv;
+          s2[j] += gv * ((bf16_to_f32(z8[j]) - e2[j]) * e3[j]);
         }
       }
       *reinterpret_cast<u16x8*>(p.c + o) = v;
@@ -502,7 +523,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     }
   }
 
-  if constexpr (EPI == 1 || EPI == 3) {
+  if constexpr (EPI == 1 || EPI == 3 || FOLD) {
     // threads with equal cg: lanes l ^ CPR, l ^ 2 CPR, ... of a wave, then the 4 waves via LDS
 #pragma unroll
     for (int off = CPR; off < 64; off <<= 1)
@@ -772,6 +793,9 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
     case 3: PSAMD_CF(BN, PRO, 3); break; \
     case 4: PSAMD_CF(BN, PRO, 4); break; \
     case 5: PSAMD_CF(BN, PRO, 5); break; \
+    case 6: PSAMD_CF(BN, PRO, 6); break; \
+    case 7: PSAMD_CF(BN, PRO, 7); break; \
+    case 8: PSAMD_CF(BN, PRO, 8); break; \
     default: PSAMD_CF(BN, PRO, 0); break; \
   }
   // the BN prologue only appears on forward convolutions (epilogue 0 / 1)

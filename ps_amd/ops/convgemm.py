@@ -20,6 +20,13 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
             conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
             epilogue), weight grads.
 
+Across blocks: block i's conv1 data-grad epilogue also runs block i-1's bn3 backward reduce
+(epilogues 6/7/8: mask by block i-1's output bits, sums against its z3), so block i-1's bn3
+backward is one apply pass.  The hand-off is a ``_Link`` set up in forward when block i's input
+IS block i-1's output; block i-1 uses the partials only if the gradient it receives is exactly
+the tensor block i produced (same storage, same version) -- any other consumer of the block
+output makes autograd sum into a different tensor and the plain reduce runs instead.
+
 Per block that removes the statistics passes of bn1 / bn3 / bn_d, bn2's output write + re-read,
 bn2's backward reduce pass and the residual-gradient add, and replaces MIOpen's 1x1 solvers (and
 their zero-fill / cast side kernels).  Anything else -- CPU tensors, eval mode, fp32, channel
@@ -31,6 +38,7 @@ from __future__ import annotations
 import contextlib
 import os
 import threading
+import weakref
 from typing import List
 
 import torch
@@ -88,9 +96,28 @@ def _mat(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(w.shape[0], w.shape[1])
 
 
+class _Link:
+    """bn3 backward hand-off from block i (consumer of this block's output) to this block."""
+
+    __slots__ = ("out_ref", "z3", "bits", "mean", "invstd", "part", "dx_ptr", "dx_version", "dx_keep")
+
+    def __init__(self, z3, bits, mean, invstd):
+        self.out_ref = None
+        self.z3, self.bits, self.mean, self.invstd = z3, bits, mean, invstd
+        self.part = None
+        self.dx_ptr = self.dx_version = self.dx_keep = None
+
+
+FOLD_STATS = {"used": 0}  # bn3 backward passes that took the consumer's partials (tests)
+
+
+def _fold_enabled() -> bool:
+    return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
+
+
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, blk):
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, blk, link_in):
         nat = native()
         n, cin, h, w = x.shape
         s = blk.conv2.stride[0]
@@ -125,6 +152,8 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, obits, zd,
                               m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd)
         ctx.dims = (n, h, w, s, oh, ow)
+        ctx.link_in = link_in  # block i-1's bn3: its reduce runs in our conv1 data-grad epilogue
+        ctx.link_out = _Link(z3, obits, m3, i3) if _fold_enabled() else None
         return image(out, n, oh, ow)
 
     @staticmethod
@@ -135,9 +164,18 @@ class _BottleneckFn(torch.autograd.Function):
         n, h, w, s, oh, ow = ctx.dims
         gi, go = geo(h, w), geo(oh, ow)
         d2 = rows(dout)
-        # bn3 with the ReLU mask from the output bits; the masked gradient dout * relu' is also
-        # the identity-branch gradient -- recomputed where needed from (dout, bits), never stored
-        dz3, _, dg3, db3 = nat.bn_act_bwd(d2, None, z3, g3, m3, i3, 3, False, True, None, obits)
+        lk = ctx.link_out
+        if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
+                and d2._version == lk.dx_version):
+            # the consumer block already masked dout and reduced bn3's backward sums
+            dz3, dg3, db3 = nat.bn_bwd_partials(d2, z3, lk.part, g3, m3, i3)
+            FOLD_STATS["used"] += 1
+        else:
+            # bn3 with the ReLU mask from the output bits; the masked gradient dout * relu' is
+            # also the identity-branch gradient -- recomputed where needed, never stored
+            dz3, _, dg3, db3 = nat.bn_act_bwd(d2, None, z3, g3, m3, i3, 3, False, True, None, obits)
+        if lk is not None:
+            lk.part = lk.dx_keep = None
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
         gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
@@ -149,16 +187,25 @@ class _BottleneckFn(torch.autograd.Function):
         dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
         w1t = _mat(w1).t()
         dwd = dgd = dbd = None
+        li = ctx.link_in
+        fold = li is not None and _fold_enabled()
+        fkw = dict(mean=li.mean, invstd=li.invstd, aux2=li.z3, bits2=li.bits) if fold else {}
         if wd is not None:
             dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
             dwd = nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)).view_as(wd)
             t = nat.conv_gemm(dzd, _mat(wd).t(), go)[0]
-            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 4 if s == 2 else 2, t)[0]
+            epi = 4 if s == 2 else 2
+            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
         else:
-            dx2 = nat.conv_gemm(dz1, w1t, gi, None, 5, d2, bits=obits)[0]
+            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, 6 if fold else 5, d2, bits=obits, **fkw)
+        if fold:
+            # dx_keep pins a second reference on dx2's storage, so autograd cannot sum another
+            # consumer's gradient into it in place (it would not bump the version): a summed
+            # gradient always lands in a different buffer and fails the pointer check
+            li.part, li.dx_ptr, li.dx_version, li.dx_keep = part, dx2.data_ptr(), dx2._version, dx2
         dw1 = nat.conv_wgrad(dz1, x2, gi)
         return (image(dx2, n, h, w), dw1.view_as(w1), dg1, db1, dw2, dg2, db2, dw3.view_as(w3), dg3, db3,
-                dwd, dgd, dbd, None)
+                dwd, dgd, dbd, None, None)
 
 
 def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
@@ -202,9 +249,11 @@ def deferred_bn_counters():
     them as one multi-tensor add on exit (53 one-element kernels per ResNet-50 step otherwise)."""
     prev = getattr(_tls, "pending", None)
     _tls.pending = []
+    _tls.last = None  # bn3 hand-off chain starts fresh every forward
     try:
         yield
     finally:
+        _tls.last = None
         pending, _tls.pending = _tls.pending, prev
         if pending:
             torch._foreach_add_(pending, 1)
@@ -219,5 +268,12 @@ def fused_bottleneck(blk: nn.Module, x: torch.Tensor) -> torch.Tensor:
     else:
         torch._foreach_add_(counters, 1)
     wd, gd, bd = (ds[0].weight, ds[1].weight, ds[1].bias) if ds is not None else (None, None, None)
-    return _BottleneckFn.apply(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
-                               blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk)
+    last = getattr(_tls, "last", None)
+    link_in = last if last is not None and last.out_ref is not None and last.out_ref() is x else None
+    y = _BottleneckFn.apply(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                            blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk, link_in)
+    lk = y.grad_fn.link_out if y.grad_fn is not None and hasattr(y.grad_fn, "link_out") else None
+    if lk is not None and hasattr(_tls, "pending") and _tls.pending is not None:
+        lk.out_ref = weakref.ref(y)
+        _tls.last = lk
+    return y

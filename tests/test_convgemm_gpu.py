@@ -294,3 +294,93 @@ def test_tall_partials_fold_into_bn_finalize():
     _, dgamma, dbeta = native().bn_bwd_partials(_bf(gr), _bf(x), part.to(DEV), None, m.to(DEV), i.to(DEV))
     torch.testing.assert_close(dbeta.cpu().double(), s1, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(dgamma.cpu().double(), s2, rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("epi", [6, 7, 8])
+@pytest.mark.parametrize("K", [64, 512])
+def test_fold_epilogues_previous_block_bn3_reduce(epi, K):
+    """Epilogues 6/7/8 (= 5/2/4 + the previous block's bn3 backward reduce): output masked by
+    the previous block's output bits, partial sums of g and g * (z3 - mean) * invstd."""
+    n, h, w, N = 2, 13, 11, 256
+    M = n * h * w
+    g = _gen(90 + epi + K)
+    a, bt = _rnd(M, K, g=g), _rnd(K, N, g=g, scale=K ** -0.5)
+    ref = a @ bt
+    bits = None
+    if epi == 6:
+        r = _rnd(M, N, g=g)
+        keep = torch.rand(M, N, generator=g) > 0.5
+        bits = (keep.view(-1, 8).int() << torch.arange(8)).sum(1).to(torch.uint8).to(DEV)
+        aux = r
+        ref = ref + r * keep
+    elif epi == 7:
+        aux = _rnd(M, N, g=g)
+        ref = ref + aux
+    else:
+        oh, ow = (h + 1) // 2, (w + 1) // 2
+        aux = _rnd(n * oh * ow, N, g=g)
+        ref.view(n, h, w, N)[:, ::2, ::2] += aux.view(n, oh, ow, N)
+    ref = ref.bfloat16().float()
+    z3 = _rnd(M, N, g=g)
+    keep2 = torch.rand(M, N, generator=g) > 0.4
+    bits2 = (keep2.view(-1, 8).int() << torch.arange(8)).sum(1).to(torch.uint8)
+    mean, invstd = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+    c, part = native().conv_gemm(_bf(a), _bf(bt).t(), geo(h, w), None, epi, _bf(aux), None, None, mean.to(DEV),
+                                 invstd.to(DEV), bits, _bf(z3), bits2.to(DEV))
+    gref = ref * keep2
+    _close(c, gref)
+    gc = c.float().cpu()
+    assert torch.all(gc[~keep2] == 0)
+    torch.testing.assert_close(part[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), (gc * (z3 - mean) * invstd).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("extra_consumer", [False, True])
+def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
+    """Three fused bottlenecks (downsample first) inside the ResNet forward context: block i's
+    conv1 data-grad epilogue reduces block i-1's bn3 backward.  Checked against the same fused
+    chain with the fold disabled (PS_AMD_FOLD_BN3=0: every block runs its own reduce pass).
+    With a second consumer of a block output autograd sums the gradients and that block must
+    fall back to its own reduce.  (Fused vs module path per block: the test above.)"""
+    import torch.nn as nn
+
+    from ps_amd.models.resnet import Bottleneck, prepare_for_mi355x
+    from ps_amd.ops import convgemm as cg
+    from ps_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(1)
+    ds = nn.Sequential(nn.Conv2d(128, 256, 1, stride=2, bias=False), BatchNormAct2d(256, act="none"))
+    a = nn.Sequential(Bottleneck(128, 64, 2, ds), Bottleneck(256, 64), Bottleneck(256, 64))
+    for m in a.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    a = prepare_for_mi355x(a.cuda())
+    x = torch.randn(4, 128, 17, 17, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gw = torch.randn(4, 256, 9, 9, device=DEV)
+    gw1 = torch.randn(4, 256, 9, 9, device=DEV)
+    state = copy.deepcopy(a.state_dict())
+
+    def run():
+        a.load_state_dict(state)
+        a.zero_grad()
+        xi = x.clone().requires_grad_()
+        with cg.deferred_bn_counters():
+            y1 = a[0](xi)
+            y3 = a[2](a[1](y1))
+        loss = (y3.float() * gw).sum()
+        if extra_consumer:
+            loss = loss + (y1.float() * gw1).sum()
+        loss.backward()
+        return xi.grad.clone(), {n: p.grad.clone() for n, p in a.named_parameters()}
+
+    before = cg.FOLD_STATS["used"]
+    ga, pa = run()
+    assert cg.FOLD_STATS["used"] - before == (1 if extra_consumer else 2)
+    monkeypatch.setenv("PS_AMD_FOLD_BN3", "0")
+    before = cg.FOLD_STATS["used"]
+    gb, pb = run()
+    assert cg.FOLD_STATS["used"] == before
+    _close(ga, gb, tol=1e-2, amax=0.05)
+    for n in pb:
+        _close(pa[n], pb[n], tol=1e-2, amax=0.05)
