@@ -40,11 +40,27 @@ def rel(u, v):
     return ((u - v).norm() / v.norm().clamp_min(1e-12)).item()
 
 
+c = copy.deepcopy(b).float()  # fp32 module path: the arbiter
+
+
+def run32():
+    c.zero_grad()
+    xi = x.float().clone().requires_grad_()
+    y = c[2](c[1](c[0](xi)))
+    (y * gw).sum().backward()
+    return xi.grad.clone(), {n: p.grad.float().clone() for n, p in c.named_parameters()}
+
+
+g32, p32 = run32()
 gb, pb = run(b)
+print("module-bf16 vs fp32: xgrad rel", round(rel(gb, g32), 4), "worst",
+      [(k, round(e, 4)) for e, k in sorted(((rel(pb[k], p32[k]), k) for k in p32), reverse=True)[:3]], flush=True)
 for label, env, ctx in [("fold", "1", True), ("nofold", "0", True), ("noctx", "1", False)]:
     os.environ["PS_AMD_FOLD_BN3"] = env
     u0 = cg.FOLD_STATS["used"]
     ga, pa = run(a, ctx)
     worst = sorted(((rel(pa[k], pb[k]), k) for k in pb), reverse=True)[:4]
+    print(label, "vs fp32: xgrad rel", round(rel(ga, g32), 4), "worst",
+          [(k, round(e, 4)) for e, k in sorted(((rel(pa[k], p32[k]), k) for k in p32), reverse=True)[:3]])
     print(label, "used", cg.FOLD_STATS["used"] - u0, "xgrad rel", round(rel(ga, gb), 4), "worst params",
           [(k, round(e, 4)) for e, k in worst], flush=True)
