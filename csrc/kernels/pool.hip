@@ -15,18 +15,20 @@
 
 namespace psamd {
 
-template <bool BN>
+// IDX: 32-bit index math when the element count allows it (64-bit div/mod is a long
+// instruction sequence on CDNA and dominated these HBM-light, address-heavy kernels)
+template <bool BN, typename IDX>
 __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const float* __restrict__ coef,
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
                                                                int N, int H, int W, int C, int OH, int OW, int k,
                                                                int s, int p) {
-  const int cv = C / 8;
-  const int64_t total = static_cast<int64_t>(N) * OH * OW * cv;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
+  const IDX cv = C / 8;
+  const IDX total = static_cast<IDX>(N) * OH * OW * cv;
+  const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
+  for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
     const int c8 = static_cast<int>(v % cv);
-    int64_t r = v / cv;
+    IDX r = v / cv;
     const int ow = static_cast<int>(r % OW);
     r /= OW;
     const int oh = static_cast<int>(r % OH);
@@ -68,24 +70,25 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* _
         }
       }
     }
-    store8(y, v * 8, best);
+    store8(y, static_cast<int64_t>(v) * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) packed |= static_cast<uint64_t>(bi[j]) << (8 * j);
-    *reinterpret_cast<uint64_t*>(idx + v * 8) = packed;
+    *reinterpret_cast<uint64_t*>(idx + static_cast<int64_t>(v) * 8) = packed;
   }
 }
 
+template <typename IDX>
 __global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                const uint8_t* __restrict__ idx,
                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C,
                                                                int OH, int OW, int k, int s, int p) {
-  const int cv = C / 8;
-  const int64_t total = static_cast<int64_t>(N) * H * W * cv;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
+  const IDX cv = C / 8;
+  const IDX total = static_cast<IDX>(N) * H * W * cv;
+  const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
+  for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
     const int c8 = static_cast<int>(v % cv);
-    int64_t r = v / cv;
+    IDX r = v / cv;
     const int w = static_cast<int>(r % W);
     r /= W;
     const int h = static_cast<int>(r % H);
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* _
           if (static_cast<uint8_t>(packed >> (8 * j)) == code) acc[j] += g[j];
       }
     }
-    store8(dx, v * 8, acc);
+    store8(dx, static_cast<int64_t>(v) * 8, acc);
   }
 }
 
@@ -118,20 +121,29 @@ void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, 
   const int64_t total = static_cast<int64_t>(N) * OH * OW * (C / 8);
   if (total <= 0) return;
   const int grid = stream_grid(total, 256);
-  if (coef)
-    hipLaunchKernelGGL(maxpool_nhwc_fwd_kernel<true>, dim3(grid), dim3(256), 0, st, x, coef, y, idx, N, H, W, C, OH,
-                       OW, k, s, p);
-  else
-    hipLaunchKernelGGL(maxpool_nhwc_fwd_kernel<false>, dim3(grid), dim3(256), 0, st, x, coef, y, idx, N, H, W, C,
-                       OH, OW, k, s, p);
+  const bool i32 = total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(grid) * 256;
+#define PSAMD_MPF(BN, T) \
+  hipLaunchKernelGGL((maxpool_nhwc_fwd_kernel<BN, T>), dim3(grid), dim3(256), 0, st, x, coef, y, idx, N, H, W, C, OH, \
+                     OW, k, s, p)
+  if (coef) {
+    if (i32) { PSAMD_MPF(true, uint32_t); } else { PSAMD_MPF(true, int64_t); }
+  } else {
+    if (i32) { PSAMD_MPF(false, uint32_t); } else { PSAMD_MPF(false, int64_t); }
+  }
+#undef PSAMD_MPF
 }
 
 void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                              int OW, int k, int s, int p, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(N) * H * W * (C / 8);
   if (total <= 0) return;
-  hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, st, dy, idx, dx, N, H, W,
-                     C, OH, OW, k, s, p);
+  const int grid = stream_grid(total, 256);
+  if (total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(grid) * 256)
+    hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, dy, idx, dx, N, H, W, C, OH,
+                       OW, k, s, p);
+  else
+    hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel<int64_t>, dim3(grid), dim3(256), 0, st, dy, idx, dx, N, H, W, C, OH,
+                       OW, k, s, p);
 }
 
 }  // namespace psamd
