@@ -15,6 +15,8 @@
 // kernel that sums them in fixed order.  act: 0 none, 1 relu.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
@@ -48,7 +50,11 @@ int bn_red_blocks(int64_t R, int C) {
   const int64_t want = (2048 + ctiles - 1) / ctiles;
   if (g < want) g = std::min<int64_t>(want, (R + 7) / 8);
   if (g < 1) g = 1;
-  if (g > 2048) g = 2048;  // 8 blocks per CU: enough loads in flight to stream at the HBM rate
+  static const int64_t cap = [] {
+    const char* e = std::getenv("PS_AMD_BN_RED_MAXG");  // A/B knob for the block cap
+    return static_cast<int64_t>(e ? std::atoi(e) : 2048);
+  }();
+  if (g > cap) g = cap;
   return static_cast<int>(g);
 }
 
