@@ -87,14 +87,18 @@ void fused_opt(int64_t kind, Tensor w, c10::optional<Tensor> st0, c10::optional<
 
 void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::optional<Tensor> st1, Tensor rows,
                 Tensor grad, bool rowwise, bool skip_zero, double lr, double beta1, double beta2, double eps,
-                double wd, double momentum, double bc1, double bc2, double l1, double l2, double fbeta,
-                int64_t ftrl_mode, double gscale) {
+                double wd, double momentum, double dampening, bool nesterov, bool adamw, double bc1, double bc2,
+                double l1, double l2, double fbeta, int64_t ftrl_mode, double gscale, c10::optional<Tensor> perm) {
   check_f32(table, "table");
   TORCH_CHECK(table.dim() == 2, "table must be [rows, dim]");
   check_i64(rows, "rows");
   check_gpu(grad, "grad");
   const int64_t dim = table.size(1);
   TORCH_CHECK(grad.numel() == rows.numel() * dim, "grad must be [nrows, dim]");
+  if (perm.has_value() && perm->defined()) {
+    check_i64(*perm, "perm");
+    TORCH_CHECK(perm->numel() == rows.numel(), "perm must have one entry per row entry");
+  }
   if (st0.has_value() && st0->defined()) {
     check_f32(*st0, "st0");
     const int64_t want = (kind == 2 && rowwise) ? table.size(0) : table.numel();
@@ -110,6 +114,7 @@ void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::opti
   a.st0 = opt_ptr<float>(st0);
   a.st1 = opt_ptr<float>(st1);
   a.rows = rows.data_ptr<int64_t>();
+  a.perm = opt_ptr<const int64_t>(perm);
   a.grad = grad.data_ptr();
   a.g_bf16 = dcode(grad, "grad");
   a.nrows = rows.numel();
@@ -117,6 +122,7 @@ void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::opti
   a.rowwise = rowwise;
   a.skip_zero = skip_zero;
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.wd = wd; a.momentum = momentum;
+  a.dampening = dampening; a.nesterov = nesterov; a.adamw = adamw;
   a.bc1 = bc1; a.bc2 = bc2; a.l1 = l1; a.l2 = l2; a.fbeta = fbeta; a.ftrl_mode = static_cast<int>(ftrl_mode);
   a.gscale = gscale;
   psamd::launch_sparse_opt(a, cur_stream(table));
@@ -279,16 +285,37 @@ void sparse_lr_fwd(Tensor w, Tensor ids, c10::optional<Tensor> bias, Tensor out)
                               out.data_ptr<float>(), cur_stream(w));
 }
 
-void lazy_init_rows(Tensor table, Tensor rows, Tensor flags, int64_t seed, int64_t row_base, double lo, double hi) {
+void lazy_init_rows(Tensor table, Tensor rows, Tensor flags, int64_t seed, int64_t row_base, double lo, double hi,
+                    c10::optional<Tensor> keys) {
   check_f32(table, "table");
   check_i64(rows, "rows");
   check_gpu(flags, "flags");
   TORCH_CHECK(flags.scalar_type() == torch::kUInt8 && flags.numel() == table.size(0), "flags uint8 [rows]");
+  if (keys.has_value() && keys->defined()) {
+    check_i64(*keys, "keys");
+    TORCH_CHECK(keys->numel() == rows.numel(), "keys must have one entry per row");
+  }
   const c10::DeviceGuard guard(table.device());
-  psamd::launch_lazy_init_rows(table.data_ptr<float>(), rows.data_ptr<int64_t>(), rows.numel(),
-                               static_cast<int>(table.size(1)), flags.data_ptr<uint8_t>(),
+  psamd::launch_lazy_init_rows(table.data_ptr<float>(), rows.data_ptr<int64_t>(), opt_ptr<const int64_t>(keys),
+                               rows.numel(), static_cast<int>(table.size(1)), flags.data_ptr<uint8_t>(),
                                static_cast<uint64_t>(seed), row_base, static_cast<float>(lo), static_cast<float>(hi),
                                cur_stream(table));
+}
+
+// out[i] = slot of ids[i] in the device hash map ``hkeys`` (int64 [capacity], power of two,
+// -1 = empty); insert claims a slot for a new id.  status (int32 [1]) is set on a miss/overflow.
+void hash_slots(Tensor hkeys, Tensor ids, Tensor out, bool insert, Tensor status) {
+  check_i64(hkeys, "hkeys");
+  check_i64(ids, "ids");
+  check_i64(out, "out");
+  check_gpu(status, "status");
+  TORCH_CHECK(status.scalar_type() == torch::kInt32 && status.numel() >= 1, "status int32 [1]");
+  const int64_t cap = hkeys.numel();
+  TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "hash capacity must be a power of two");
+  TORCH_CHECK(out.numel() == ids.numel(), "out must match ids");
+  const c10::DeviceGuard guard(ids.device());
+  psamd::launch_hash_slots(hkeys.data_ptr<int64_t>(), cap, ids.data_ptr<int64_t>(), ids.numel(),
+                           out.data_ptr<int64_t>(), insert, status.data_ptr<int32_t>(), cur_stream(ids));
 }
 
 // ------------------------------------------------------------------------------ reference ops
@@ -1054,7 +1081,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);
   m.def("bn_bwd_partials", &bn_bwd_partials);
   m.def("fused_opt", &fused_opt);
-  m.def("sparse_opt", &sparse_opt);
+  m.def("sparse_opt", &sparse_opt, py::arg("kind"), py::arg("table"), py::arg("st0"), py::arg("st1"),
+        py::arg("rows"), py::arg("grad"), py::arg("rowwise"), py::arg("skip_zero"), py::arg("lr"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"),
+        py::arg("nesterov"), py::arg("adamw"), py::arg("bc1"), py::arg("bc2"), py::arg("l1"), py::arg("l2"),
+        py::arg("fbeta"), py::arg("ftrl_mode"), py::arg("gscale"), py::arg("perm") = py::none());
   m.def("sumsq", &sumsq);
   m.def("clip_factor", &clip_factor);
   m.def("cast_", &cast_);
@@ -1068,7 +1099,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scatter_add_rows", &scatter_add_rows);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("sparse_lr_fwd", &sparse_lr_fwd);
-  m.def("lazy_init_rows", &lazy_init_rows);
+  m.def("lazy_init_rows", &lazy_init_rows, py::arg("table"), py::arg("rows"), py::arg("flags"), py::arg("seed"),
+        py::arg("row_base"), py::arg("lo"), py::arg("hi"), py::arg("keys") = py::none());
+  m.def("hash_slots", &hash_slots);
   m.def("softmax_temp_fwd", &softmax_temp_fwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("bce", &bce);

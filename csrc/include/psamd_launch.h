@@ -35,14 +35,16 @@ struct SparseOptArgs {
   float* table;  // [rows_total, dim] owner-local fp32 table
   float* st0;
   float* st1;
-  const int64_t* rows;  // [nrows] unique owner-local rows
+  const int64_t* rows;  // [nrows] owner-local rows: unique (perm null) or sorted with repeats
+  const int64_t* perm;  // nullable: grad row of sorted entry j is perm[j] (runs are summed)
   const void* grad;     // [nrows, dim]
   int g_bf16;
   int64_t nrows;
   int dim;
   int rowwise;  // adagrad: one accumulator per row
   int skip_zero;
-  float lr, beta1, beta2, eps, wd, momentum;
+  float lr, beta1, beta2, eps, wd, momentum, dampening;
+  int nesterov, adamw;
   float bc1, bc2, l1, l2, fbeta;
   int ftrl_mode;
   float gscale;
@@ -80,8 +82,10 @@ void launch_embedding_bag_fwd(const float* table, const int64_t* ids, int64_t ba
                               void* out, int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s);
 void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int fields, int64_t hash_size,
                           const float* bias, float* out, hipStream_t s);
-void launch_lazy_init_rows(float* table, const int64_t* rows, int64_t nrows, int dim, uint8_t* init_flags,
-                           uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s);
+void launch_lazy_init_rows(float* table, const int64_t* rows, const int64_t* keys, int64_t nrows, int dim,
+                           uint8_t* init_flags, uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s);
+void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int64_t n, int64_t* out, int insert,
+                       int32_t* status, hipStream_t s);
 
 // ---------------------------------------------------------------- ref_ops.hip
 void launch_softmax_temp_fwd(const float* x, float* y, int64_t rows, int cols, float inv_temp, float clamp_lo,

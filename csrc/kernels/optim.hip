@@ -197,13 +197,32 @@ void launch_fused_opt(const FusedOptArgs& a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------------------
 // Row-sparse variants (sparse embedding tables, K24): apply the optimizer only to the rows
-// named in `rows` (unique, owner-local row indices), with `grad` laid out [nrows, dim].
-// One wave per row when dim >= 64, otherwise several rows per wave.  Row-wise Adagrad
-// keeps ONE accumulator per row (mean of g^2 over the row), the DLRM convention.
+// named in `rows` (owner-local row indices), with `grad` laid out [n, dim].  One wave per row
+// entry.  Row-wise Adagrad keeps ONE accumulator per row (mean of g^2 over the row), the DLRM
+// convention.
+//
+// Two input forms:
+//  * perm == nullptr: `rows` are unique, grad row r belongs to rows[r].
+//  * perm != nullptr: `rows` is SORTED and may repeat (several workers pushed the same row,
+//    or several micro-batches of one round); grad row perm[j] belongs to rows[j].  The wave
+//    at the head of each run sums the run's gradient rows in order (deterministic, no atomics)
+//    and applies ONE update -- the owner-side "sum the W pushes, then step" of a BSP round
+//    without a host-side unique (which would need a device->host sync for its size).
+// Negative rows (unresolved keys) are skipped.
 // ---------------------------------------------------------------------------------------
+template <typename G>
+__device__ __forceinline__ float run_grad(const G* __restrict__ grad, const int64_t* __restrict__ perm, int64_t r,
+                                          int64_t e, int dim, int c) {
+  if (perm == nullptr) return Elem<G>::load(grad + r * dim, c);
+  float acc = 0.f;
+  for (int64_t j = r; j < e; ++j) acc += Elem<G>::load(grad + perm[j] * dim, c);
+  return acc;
+}
+
 template <int KIND, typename G>
 __global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ table, float* __restrict__ st0,
                                                           float* __restrict__ st1, const int64_t* __restrict__ rows,
+                                                          const int64_t* __restrict__ perm,
                                                           const G* __restrict__ grad, int64_t nrows, int dim,
                                                           OptParams p, int rowwise) {
   float scale = p.gscale;
@@ -213,12 +232,17 @@ __global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ tab
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * blockDim.x / 64;
   for (int64_t r = wave; r < nrows; r += nwaves) {
     const int64_t row = rows[r];
+    if (row < 0) continue;
+    int64_t e = r + 1;
+    if (perm != nullptr) {
+      if (r > 0 && rows[r - 1] == row) continue;  // not the head of its run
+      while (e < nrows && rows[e] == row) ++e;
+    }
     float* wrow = table + row * dim;
-    const G* grow = grad + r * dim;
     if (KIND == kAdagrad && rowwise) {
       float ss = 0.f;
       for (int c = lane; c < dim; c += 64) {
-        const float gv = Elem<G>::load(grow, c) * scale;
+        const float gv = run_grad(grad, perm, r, e, dim, c) * scale;
         ss += gv * gv;
       }
       ss = wave_sum(ss) / static_cast<float>(dim);
@@ -226,17 +250,17 @@ __global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ tab
       if (lane == 0) st0[row] = h;
       const float denom = sqrtf(h) + p.eps;
       for (int c = lane; c < dim; c += 64) {
-        const float gv = Elem<G>::load(grow, c) * scale;
+        const float gv = run_grad(grad, perm, r, e, dim, c) * scale;
         wrow[c] -= p.lr * gv / denom;
       }
     } else {
       // skip_zero reproduces FtrlUpdater.java:52-54 (per key == per row).
-      if (p.skip_zero && Elem<G>::load(grow, 0) == 0.f) continue;
+      if (p.skip_zero && run_grad(grad, perm, r, e, dim, 0) == 0.f) continue;
       for (int c = lane; c < dim; c += 64) {
         float wr = wrow[c];
         float a = st0 ? st0[row * dim + c] : 0.f;
         float b = st1 ? st1[row * dim + c] : 0.f;
-        opt_apply<KIND>(wr, Elem<G>::load(grow, c) * scale, a, b, p);
+        opt_apply<KIND>(wr, run_grad(grad, perm, r, e, dim, c) * scale, a, b, p);
         wrow[c] = wr;
         if (st0) st0[row * dim + c] = a;
         if (st1) st1[row * dim + c] = b;
@@ -249,18 +273,18 @@ void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
   if (a.nrows <= 0) return;
   OptParams p;
   p.lr = a.lr; p.beta1 = a.beta1; p.beta2 = a.beta2; p.eps = a.eps; p.wd = a.wd;
-  p.momentum = a.momentum; p.dampening = 0.f; p.nesterov = 0; p.adamw = 0;
+  p.momentum = a.momentum; p.dampening = a.dampening; p.nesterov = a.nesterov; p.adamw = a.adamw;
   p.bc1 = a.bc1; p.bc2 = a.bc2; p.l1 = a.l1; p.l2 = a.l2; p.fbeta = a.fbeta; p.ftrl_mode = a.ftrl_mode;
   p.skip_zero = a.skip_zero; p.gscale = a.gscale; p.gscale_ptr = nullptr;
   const int block = 256;
   const int grid = stream_grid(a.nrows * 64, block);
-#define PSAMD_SPARSE_LAUNCH(K)                                                                                 \
-  if (a.g_bf16)                                                                                                \
-    hipLaunchKernelGGL((sparse_opt_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1, \
-                       a.rows, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, p, a.rowwise);            \
-  else                                                                                                         \
-    hipLaunchKernelGGL((sparse_opt_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,    \
-                       a.rows, static_cast<const float*>(a.grad), a.nrows, a.dim, p, a.rowwise);
+#define PSAMD_SPARSE_LAUNCH(K)                                                                                  \
+  if (a.g_bf16)                                                                                                 \
+    hipLaunchKernelGGL((sparse_opt_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,  \
+                       a.rows, a.perm, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, p, a.rowwise);     \
+  else                                                                                                          \
+    hipLaunchKernelGGL((sparse_opt_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,     \
+                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, p, a.rowwise);
   switch (a.kind) {
     case kSGD: PSAMD_SPARSE_LAUNCH(kSGD); break;
     case kAdam: PSAMD_SPARSE_LAUNCH(kAdam); break;

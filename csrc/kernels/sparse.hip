@@ -16,9 +16,11 @@
 //                       -> out[b, off + f*dim : off + (f+1)*dim] with ReLU (layer/EmbeddingLayer.java:36-46)
 //  sparse_lr_fwd        z[b] = sum_f w[ids[b,f] mod H] + bias (layer/LRLayer.java:62-98 with
 //                       the hash of util/MatrixUtil.java:27-33 fused in)
-//  lazy_init_rows       deterministic first-touch row init keyed by (seed, global row) with an
+//  lazy_init_rows       deterministic first-touch row init keyed by (seed, global key) with an
 //                       "initialized" byte map; replaces the upsert(replace=false) round trip
 //                       (store/KVStore.java:86-107, net/PServer.java:143-162)
+//  hash_slots           device-resident id -> slot map (open addressing, CAS insert) for
+//                       tables keyed by unbounded ids; no host round trip per lookup
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
@@ -39,8 +41,13 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ 
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   for (int64_t r = wave; r < nrows; r += nwaves) {
-    const T* src = table + rows[r] * dim;
+    const int64_t row = rows[r];
     O* dst = out + r * out_ld + out_off;
+    if (row < 0) {  // unresolved key (map overflow): zero row, wave-uniform branch
+      for (int c = lane; c < dim; c += 64) Elem<O>::store(dst, c, 0.f);
+      continue;
+    }
+    const T* src = table + row * dim;
     for (int c = lane; c < dim; c += 64) Elem<O>::store(dst, c, apply_act(Elem<T>::load(src, c), act));
   }
 }
@@ -55,8 +62,13 @@ __global__ __launch_bounds__(256) void gather_rows_vec4_kernel(const float* __re
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const int d4 = dim >> 2;
   for (int64_t r = wave; r < nrows; r += nwaves) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(table + rows[r] * dim);
+    const int64_t row = rows[r];
     f32x4* dst = reinterpret_cast<f32x4*>(out + r * out_ld + out_off);
+    if (row < 0) {
+      for (int c = lane; c < d4; c += 64) dst[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
+    const f32x4* src = reinterpret_cast<const f32x4*>(table + row * dim);
     for (int c = lane; c < d4; c += 64) {
       f32x4 v = src[c];
       v.x = apply_act(v.x, act); v.y = apply_act(v.y, act); v.z = apply_act(v.z, act); v.w = apply_act(v.w, act);
@@ -202,35 +214,93 @@ void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int
   hipLaunchKernelGGL(sparse_lr_fwd_kernel, dim3(grid), dim3(256), 0, s, w, ids, batch, fields, hash_size, bias, out);
 }
 
-// rows: owner-local indices; row_base: global index of local row 0 (keys the RNG so the value of
-// a row does not depend on which rank owns it or when it is first touched)
+// rows: owner-local indices (negative = unresolved, skipped).  The RNG is keyed by the row's
+// GLOBAL key -- keys[r] when given (hash-mapped tables: the raw id), else row + row_base (range
+// partitioned tables: the global row) -- so a row's initial value does not depend on which rank
+// owns it, which slot it landed in, or when it is first touched (first-writer-wins for free).
 __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__ table, const int64_t* __restrict__ rows,
-                                                             int64_t nrows, int dim, uint8_t* __restrict__ flags,
-                                                             uint64_t seed, int64_t row_base, float lo, float hi) {
+                                                             const int64_t* __restrict__ keys, int64_t nrows, int dim,
+                                                             uint8_t* __restrict__ flags, uint64_t seed,
+                                                             int64_t row_base, float lo, float hi) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   for (int64_t r = wave; r < nrows; r += nwaves) {
     const int64_t row = rows[r];
-    if (flags[row]) continue;  // wave-uniform
-    const uint64_t grow = static_cast<uint64_t>(row + row_base);
+    if (row < 0 || flags[row]) continue;  // wave-uniform
+    const uint64_t grow = keys ? static_cast<uint64_t>(keys[r]) : static_cast<uint64_t>(row + row_base);
     for (int c = lane; c < dim; c += 64) {
       uint32_t rnd[4];
       Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(c), rnd);
       table[row * dim + c] = lo + (hi - lo) * Philox::u01(rnd[0]);
     }
-    // rows may repeat inside one launch only if the caller passed duplicates; flags is
+    // rows may repeat inside one launch (several workers asked for the same row); flags is
     // written after the row so a duplicate wave either re-inits identically or skips.
     if (lane == 0) flags[row] = 1;
   }
 }
 
-void launch_lazy_init_rows(float* table, const int64_t* rows, int64_t nrows, int dim, uint8_t* init_flags,
-                           uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s) {
+void launch_lazy_init_rows(float* table, const int64_t* rows, const int64_t* keys, int64_t nrows, int dim,
+                           uint8_t* init_flags, uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s) {
   if (nrows <= 0) return;
   const int grid = stream_grid(nrows * 64, 256);
-  hipLaunchKernelGGL(lazy_init_rows_kernel, dim3(grid), dim3(256), 0, s, table, rows, nrows, dim, init_flags, seed,
-                     row_base, lo, hi);
+  hipLaunchKernelGGL(lazy_init_rows_kernel, dim3(grid), dim3(256), 0, s, table, rows, keys, nrows, dim, init_flags,
+                     seed, row_base, lo, hi);
+}
+
+// ---------------------------------------------------------------------------------------
+// Device-resident id -> slot map for hash-mapped ("map" mode) sparse tables: open addressing
+// with linear probing over a power-of-two key array initialised to -1.  The slot of a key IS
+// its probe position, so creation needs no counter and no second pass: the lane whose 64-bit
+// compare-and-swap claims an empty position owns it, a lane that loses the race to the SAME
+// key (another worker asked for it in this launch) reads that key back and shares the slot.
+// This replaces the reference's upsert(replace=false) round trip for rows that do not exist
+// yet (store/KVStore.java:86-107, net/PServer.java:143-162) without a host lookup.  A key
+// that finds the table full (or is absent with insert=0) gets slot -1; ``status`` is set to 1
+// with a plain store so the host can check it at its next sync point.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix_key(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void hash_slots_kernel(unsigned long long* __restrict__ hkeys, int64_t cap_mask,
+                                                         const int64_t* __restrict__ ids, int64_t n,
+                                                         int64_t* __restrict__ out, int insert,
+                                                         int32_t* __restrict__ status) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const unsigned long long kEmpty = ~0ull;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const unsigned long long key = static_cast<unsigned long long>(ids[i]);
+    int64_t slot = -1;
+    if (ids[i] >= 0) {
+      uint64_t h = mix_key(key) & static_cast<uint64_t>(cap_mask);
+      for (int64_t probe = 0; probe <= cap_mask; ++probe) {
+        unsigned long long cur = __hip_atomic_load(&hkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) { slot = static_cast<int64_t>(h); break; }
+        if (cur == kEmpty) {
+          if (!insert) break;
+          const unsigned long long prev = atomicCAS(&hkeys[h], kEmpty, key);
+          if (prev == kEmpty || prev == key) { slot = static_cast<int64_t>(h); break; }
+        }
+        h = (h + 1) & static_cast<uint64_t>(cap_mask);
+      }
+    }
+    out[i] = slot;
+    if (slot < 0 && (insert || ids[i] < 0)) status[0] = 1;
+  }
+}
+
+void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int64_t n, int64_t* out, int insert,
+                       int32_t* status, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = stream_grid(n, 256);
+  hipLaunchKernelGGL(hash_slots_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(hkeys),
+                     capacity - 1, ids, n, out, insert, status);
 }
 
 }  // namespace psamd

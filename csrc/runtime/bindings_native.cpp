@@ -183,6 +183,53 @@ class Client {
     return rd.u64();
   }
 
+  py::array_t<float> row_pull(const std::string& table, uint32_t dim, const I64& keys, float lo, float hi,
+                              uint64_t seed) {
+    Writer w;
+    w.str(table);
+    w.u32(dim);
+    w.f32(lo);
+    w.f32(hi);
+    w.u64(seed);
+    w.u32(static_cast<uint32_t>(keys.size()));
+    w.raw(keys.data(), static_cast<size_t>(keys.size()) * 8);
+    std::vector<uint8_t> resp;
+    uint16_t st;
+    {
+      py::gil_scoped_release r;
+      st = c_.call(OP_ROW_PULL, w, &resp);
+    }
+    check(st, resp, "row_pull");
+    Reader rd(resp.data(), resp.size());
+    const uint32_t n = rd.u32();
+    py::array_t<float> out({static_cast<py::ssize_t>(n), static_cast<py::ssize_t>(dim)});
+    std::vector<float> tmp;
+    rd.vec(&tmp, static_cast<size_t>(n) * dim);
+    std::memcpy(out.mutable_data(), tmp.data(), tmp.size() * sizeof(float));
+    return out;
+  }
+
+  void row_push(const std::string& table, uint32_t dim, const I64& keys, const F32& grads, const std::string& spec,
+                int async_flag) {
+    if (static_cast<size_t>(grads.size()) != static_cast<size_t>(keys.size()) * dim)
+      throw std::runtime_error("row_push: grads must be [n, dim]");
+    Writer w;
+    w.u8(static_cast<uint8_t>(async_flag));
+    w.str(spec);
+    w.str(table);
+    w.u32(dim);
+    w.u32(static_cast<uint32_t>(keys.size()));
+    w.raw(keys.data(), static_cast<size_t>(keys.size()) * 8);
+    w.f32s(grads.data(), static_cast<size_t>(grads.size()));
+    std::vector<uint8_t> resp;
+    uint16_t st;
+    {
+      py::gil_scoped_release r;
+      st = c_.call(OP_ROW_PUSH, w, &resp);
+    }
+    check(st, resp, "row_push");
+  }
+
   void simple(Op op, const std::string& s) {
     Writer w;
     w.str(s);
@@ -274,6 +321,10 @@ PYBIND11_MODULE(_native, m) {
       .def("push", &Client::push, py::arg("keys"), py::arg("grads"), py::arg("spec"), py::arg("async_flag") = 0)
       .def("barrier", &Client::barrier, py::arg("worker") = 0)
       .def("clock", &Client::clock)
+      .def("row_pull", &Client::row_pull, py::arg("table"), py::arg("dim"), py::arg("keys"), py::arg("lo"),
+           py::arg("hi"), py::arg("seed"))
+      .def("row_push", &Client::row_push, py::arg("table"), py::arg("dim"), py::arg("keys"), py::arg("grads"),
+           py::arg("spec"), py::arg("async_flag") = 0)
       .def("register_updater", [](Client& c, const std::string& s) { c.simple(OP_REGISTER, s); })
       .def("save", [](Client& c, const std::string& p) { c.simple(OP_SAVE, p); })
       .def("load", [](Client& c, const std::string& p) { c.simple(OP_LOAD, p); })
@@ -296,7 +347,11 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("ids"), py::arg("insert") = true)
       .def("size", &IdMap::size)
-      .def("items", &IdMap::items);
+      .def("items", &IdMap::items)
+      .def("restore", [](IdMap& self, const I64& ids, const I64& slots) {
+        if (ids.size() != slots.size()) throw std::runtime_error("ids/slots length mismatch");
+        self.restore(ids.data(), slots.data(), ids.size());
+      });
 
   py::class_<BatchReader>(m, "BatchReader")
       .def(py::init<const std::string&, const std::string&, int, int, int, int, int, int, int, bool>(),

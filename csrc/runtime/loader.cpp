@@ -47,6 +47,12 @@ int64_t IdMap::size() {
   return static_cast<int64_t>(map_.size());
 }
 
+void IdMap::restore(const int64_t* ids, const int64_t* slots, int64_t n) {
+  std::lock_guard<std::mutex> g(mu_);
+  map_.clear();
+  for (int64_t i = 0; i < n; ++i) map_.emplace(ids[i], slots[i]);
+}
+
 std::vector<std::pair<int64_t, int64_t>> IdMap::items() {
   std::lock_guard<std::mutex> g(mu_);
   return std::vector<std::pair<int64_t, int64_t>>(map_.begin(), map_.end());

@@ -18,6 +18,7 @@ class IdMap {
   void lookup(const int64_t* ids, int64_t n, bool insert, int64_t* out);
   int64_t size();
   std::vector<std::pair<int64_t, int64_t>> items();
+  void restore(const int64_t* ids, const int64_t* slots, int64_t n);  // checkpoint resume
 
  private:
   int64_t capacity_;

@@ -110,6 +110,17 @@ PSServer::Stripe& PSServer::stripe(const std::string& key) {
   return stripes_[std::hash<std::string>{}(key) % kStripes];
 }
 
+RowTable& PSServer::row_table(const std::string& name, uint32_t dim) {
+  std::lock_guard<std::mutex> g(rt_mu_);
+  auto& t = row_tables_[name];
+  if (!t) {
+    t = std::make_unique<RowTable>();
+    t->dim = dim;
+  }
+  if (t->dim != dim) throw std::runtime_error("row table " + name + ": dim mismatch");
+  return *t;
+}
+
 const Updater* PSServer::updater(const std::string& spec) {
   std::lock_guard<std::mutex> g(upd_mu_);
   auto it = updaters_.find(spec);
@@ -290,6 +301,71 @@ uint16_t PSServer::handle(Op op, Reader& in, Writer& out) {
       out.u64(min_clock());
       return ST_OK;
     }
+    case OP_ROW_PULL: {
+      // str table | u32 dim | f32 lo | f32 hi | u64 seed | u32 n | i64 keys[n]  ->  f32 rows[n*dim]
+      const std::string name = in.str();
+      const uint32_t dim = in.u32();
+      const float lo = in.f32(), hi = in.f32();
+      const uint64_t seed = in.u64();
+      const uint32_t n = in.u32();
+      std::vector<int64_t> keys;
+      in.vec(&keys, n);
+      RowTable& t = row_table(name, dim);
+      std::vector<float> rows(static_cast<size_t>(n) * dim);
+      {
+        std::lock_guard<std::mutex> g(t.mu);
+        for (uint32_t i = 0; i < n; ++i) {
+          auto it = t.rows.find(keys[i]);
+          if (it == t.rows.end()) {
+            Entry e;
+            e.rows = 1;
+            e.cols = dim;
+            e.w.resize(dim, 0.f);
+            if (lo != 0.f || hi != 0.f)
+              for (uint32_t c = 0; c < dim; ++c)
+                e.w[c] = lo + (hi - lo) * philox_u01(seed, (static_cast<uint64_t>(keys[i]) << 20) ^ c);
+            it = t.rows.emplace(keys[i], std::move(e)).first;
+          }
+          std::memcpy(rows.data() + static_cast<size_t>(i) * dim, it->second.w.data(), dim * sizeof(float));
+        }
+      }
+      out.u32(n);
+      out.f32s(rows.data(), rows.size());
+      return ST_OK;
+    }
+    case OP_ROW_PUSH: {
+      // u8 async | str spec | str table | u32 dim | u32 n | i64 keys[n] | f32 grads[n*dim]
+      const uint8_t async_flag = in.u8();
+      const std::string spec = in.str();
+      const std::string name = in.str();
+      const uint32_t dim = in.u32();
+      const uint32_t n = in.u32();
+      std::vector<int64_t> keys;
+      std::vector<float> grads;
+      in.vec(&keys, n);
+      in.vec(&grads, static_cast<size_t>(n) * dim);
+      const Updater* u = updater(spec);
+      const bool apply_now = mode_ != Mode::BSP || async_flag == 2;
+      RowTable& t = row_table(name, dim);
+      std::lock_guard<std::mutex> g(t.mu);
+      for (uint32_t i = 0; i < n; ++i) {
+        auto it = t.rows.find(keys[i]);
+        if (it == t.rows.end()) throw std::runtime_error("push to a row that was never pulled: " + name);
+        Entry& e = it->second;
+        const float* gi = grads.data() + static_cast<size_t>(i) * dim;
+        if (apply_now) {
+          apply(e, name, gi, dim, u);
+        } else {
+          if (e.acc.size() != dim) e.acc.assign(dim, 0.f);
+          for (uint32_t c = 0; c < dim; ++c) e.acc[c] += gi[c];
+          e.count += 1;
+          e.pending = u;
+          t.dirty.insert(keys[i]);
+        }
+      }
+      pushes_.fetch_add(n);
+      return ST_OK;
+    }
     case OP_REGISTER: {
       updater(in.str());
       return ST_OK;
@@ -343,6 +419,24 @@ void PSServer::apply_pending() {
     }
     s.dirty.clear();
   }
+  std::lock_guard<std::mutex> g(rt_mu_);
+  for (auto& kv : row_tables_) {
+    RowTable& t = *kv.second;
+    std::lock_guard<std::mutex> lk(t.mu);
+    for (const int64_t key : t.dirty) {
+      Entry& e = t.rows[key];
+      if (e.count == 0 || e.pending == nullptr) continue;
+      // rows: the gradient of the mean loss over ALL workers' samples, i.e. sum / W even when
+      // only some workers touched the row (the reference divides by the pushes it happened to
+      // receive, store/KVStore.java:192-200 -- Q3); identical to the co-located path's 1/W
+      const float inv = 1.f / static_cast<float>(workers_);
+      for (auto& v : e.acc) v *= inv;
+      apply(e, kv.first, e.acc.data(), e.acc.size(), e.pending);
+      std::fill(e.acc.begin(), e.acc.end(), 0.f);
+      e.count = 0;
+    }
+    t.dirty.clear();
+  }
 }
 
 // checkpoint: text header + raw floats per key (weights + optimizer states + step)
@@ -363,6 +457,26 @@ void PSServer::save(const std::string& path) {
       w.u32(static_cast<uint32_t>(e.states.size()));
       for (auto& st : e.states) w.f32s(st.data(), st.size());
       ++nkeys;
+    }
+  }
+  // sparse row tables follow the dense keys: u32 ntables | per table: str name | u32 dim |
+  // u32 nrows | per row: i64 key | u64 t | f32[dim] w | u32 nstates | f32[dim] per state
+  {
+    std::lock_guard<std::mutex> g(rt_mu_);
+    w.u32(static_cast<uint32_t>(row_tables_.size()));
+    for (auto& kv : row_tables_) {
+      RowTable& t = *kv.second;
+      std::lock_guard<std::mutex> lk(t.mu);
+      w.str(kv.first);
+      w.u32(t.dim);
+      w.u32(static_cast<uint32_t>(t.rows.size()));
+      for (auto& r : t.rows) {
+        w.u64(static_cast<uint64_t>(r.first));
+        w.u64(static_cast<uint64_t>(r.second.t));
+        w.f32s(r.second.w.data(), r.second.w.size());
+        w.u32(static_cast<uint32_t>(r.second.states.size()));
+        for (auto& st : r.second.states) w.f32s(st.data(), st.size());
+      }
     }
   }
   Writer h;
@@ -404,6 +518,29 @@ void PSServer::load(const std::string& path) {
     auto& s = stripe(key);
     std::lock_guard<std::mutex> g(s.mu);
     s.map[key] = std::move(e);
+  }
+  if (r.done()) return;  // checkpoint without row tables
+  const uint32_t ntables = r.u32();
+  for (uint32_t ti = 0; ti < ntables; ++ti) {
+    const std::string name = r.str();
+    const uint32_t dim = r.u32();
+    const uint32_t nrows = r.u32();
+    RowTable& t = row_table(name, dim);
+    std::lock_guard<std::mutex> lk(t.mu);
+    t.rows.clear();
+    t.dirty.clear();
+    for (uint32_t i = 0; i < nrows; ++i) {
+      const int64_t key = static_cast<int64_t>(r.u64());
+      Entry e;
+      e.rows = 1;
+      e.cols = dim;
+      e.t = static_cast<long>(r.u64());
+      r.vec(&e.w, dim);
+      const uint32_t ns = r.u32();
+      e.states.assign(ns, std::vector<float>());
+      for (auto& st : e.states) r.vec(&st, dim);
+      t.rows.emplace(key, std::move(e));
+    }
   }
 }
 

@@ -24,6 +24,15 @@ struct Entry {
   long t = 0;                              // updates applied to this key
 };
 
+// Sparse row table (embedding / wide rows): int64 key -> dim floats, created on first pull
+// with a deterministic init keyed by (seed, key).
+struct RowTable {
+  uint32_t dim = 0;
+  std::mutex mu;
+  std::unordered_map<int64_t, Entry> rows;
+  std::unordered_set<int64_t> dirty;
+};
+
 class PSServer {
  public:
   enum class Mode { BSP, SSP, ASP };
@@ -52,6 +61,7 @@ class PSServer {
   void save(const std::string& path);
   void load(const std::string& path);
   Stripe& stripe(const std::string& key);
+  RowTable& row_table(const std::string& name, uint32_t dim);
   const Updater* updater(const std::string& spec);
 
   int port_;
@@ -68,6 +78,8 @@ class PSServer {
   std::vector<int> conn_fds_;
   std::vector<std::thread> conn_threads_;
   Stripe stripes_[kStripes];
+  std::mutex rt_mu_;
+  std::unordered_map<std::string, std::unique_ptr<RowTable>> row_tables_;
   std::mutex upd_mu_;
   std::unordered_map<std::string, std::unique_ptr<Updater>> updaters_;
   std::mutex barrier_mu_;

@@ -103,19 +103,48 @@ class AdamUpdater : public Updater {
 
 class AdagradUpdater : public Updater {
  public:
-  explicit AdagradUpdater(const std::string& s) : lr(spec_or(s, "lr", 0.01)), eps(spec_or(s, "epsilon", 1e-10)) {
+  explicit AdagradUpdater(const std::string& s)
+      : lr(spec_or(s, "lr", 0.01)), eps(spec_or(s, "epsilon", 1e-10)), rowwise(spec_or(s, "rowwise", 0.0) != 0.0) {
     spec = s;
   }
   int n_state() const override { return 1; }
   void update(float* w, const float* g, size_t n, std::vector<std::vector<float>>& st, long) const override {
     float* h = st[0].data();
+    if (rowwise) {  // one accumulator per key/row: h += mean(g^2) (the DLRM convention, optim.hip)
+      float ss = 0.f;
+      for (size_t i = 0; i < n; ++i) ss += g[i] * g[i];
+      h[0] += n ? ss / static_cast<float>(n) : 0.f;
+      const float denom = std::sqrt(h[0]) + eps;
+      for (size_t i = 0; i < n; ++i) w[i] -= lr * g[i] / denom;
+      return;
+    }
     for (size_t i = 0; i < n; ++i) {
       h[i] += g[i] * g[i];
       w[i] -= lr * g[i] / (std::sqrt(h[i]) + eps);
     }
   }
   float lr, eps;
+  bool rowwise;
 };
+
+// Philox-4x32-10, bit-identical to psamd::Philox (csrc/include/psamd_device.h) and
+// ps_amd.ops.sparse.philox_u01: server-created rows get exactly the values the HIP lazy-init
+// kernel gives the same (seed, key) on the GPU path.
+inline float philox_u01(uint64_t seed, uint64_t ctr) {
+  uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), 0u, 0u};
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c[0];
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c[2];
+    const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32), lo0 = static_cast<uint32_t>(p0);
+    const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32), lo1 = static_cast<uint32_t>(p1);
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return static_cast<float>(c[0] >> 8) * (1.0f / 16777216.0f);
+}
 
 class FtrlUpdater : public Updater {
  public:

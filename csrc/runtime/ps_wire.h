@@ -40,6 +40,8 @@ enum Op : uint8_t {
   OP_SHUTDOWN = 11,
   OP_HEARTBEAT = 12,
   OP_CLOCK = 13,
+  OP_ROW_PULL = 14,  // sparse row tables: pull (lazy deterministic create) of many int64 keys
+  OP_ROW_PUSH = 15,  // sparse row tables: push per-row gradients (BSP accumulate / apply)
 };
 
 enum Status : uint16_t { ST_OK = 200, ST_NOT_FOUND = 204, ST_BAD = 400, ST_TIMEOUT = 408, ST_ERR = 500 };
@@ -57,6 +59,7 @@ class Writer {
   void u32(uint32_t v) { raw(&v, 4); }
   void u64(uint64_t v) { raw(&v, 8); }
   void f32s(const float* p, size_t n) { raw(p, n * 4); }
+  void f32(float v) { raw(&v, 4); }
   void str(const std::string& s) {
     u32(static_cast<uint32_t>(s.size()));
     raw(s.data(), s.size());
@@ -79,6 +82,14 @@ class Reader {
   uint16_t u16() { uint16_t v; get(&v, 2); return v; }
   uint32_t u32() { uint32_t v; get(&v, 4); return v; }
   uint64_t u64() { uint64_t v; get(&v, 8); return v; }
+  float f32() { float v; get(&v, 4); return v; }
+  // n raw elements of T (int64 keys / float rows) copied out of the frame
+  template <typename T>
+  void vec(std::vector<T>* out, size_t n) {
+    if (n > (1ull << 34)) throw std::runtime_error("vector too large");
+    out->resize(n);
+    get(out->data(), n * sizeof(T));
+  }
   std::string str() {
     uint32_t n = u32();
     need(n);

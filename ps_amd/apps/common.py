@@ -45,15 +45,38 @@ def maybe_run_server(cfg: Config) -> bool:
     return True
 
 
-def make_trainer(cfg: Config, model, device=None) -> Trainer:
+def connect(cfg: Config, device=None):
+    """The parameter-server connection of this process and the matching sparse-table factory:
+
+      -Dmode=dist (TCP workers)      PSRouterClient, rows in the servers' row tables
+      torchrun (WORLD_SIZE > 1)      Transport (RCCL / gloo), rows sharded over the ranks
+      standalone                     None, rows in local tables
+
+    Models with embedding / wide rows must be built with the returned factory so that their
+    rows live on the parameter server (reference: every row is a PS key,
+    layer/EmbeddingField.java:57-104, layer/LRLayer.java:62-120)."""
+    from ..models.reference import local_table_factory, sharded_table_factory, tcp_table_factory
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if ctx.is_distributed() and world == 1:
         client = PSRouterClient(cfg.ps_addr_list)
+        return client, tcp_table_factory(client, device, seed=cfg.seed)
+    if world > 1:
+        tp = init_distributed()
+        return tp, sharded_table_factory(tp, device, seed=cfg.seed)
+    return None, local_table_factory(device, seed=cfg.seed)
+
+
+def make_trainer(cfg: Config, model, device=None, conn=None) -> Trainer:
+    """Engine for ``model`` over ``conn`` (from ``connect``; created here when omitted)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if ctx.is_distributed() and world == 1:
+        client = conn if conn is not None else PSRouterClient(cfg.ps_addr_list)
         wid = int(os.environ.get("PS_AMD_WORKER_ID", os.environ.get("RANK", "0")))
         cons = "asp" if cfg.ps_async else cfg.consistency
         engine = KVEngine(model, KVStore(client, worker_id=wid, consistency=cons))
     else:
-        tp = init_distributed() if world > 1 else None
+        tp = conn if conn is not None else (init_distributed() if world > 1 else None)
         engine = CollectiveEngine(model, tp, bucket_mb=cfg.bucket_mb, staleness=cfg.staleness,
                                   clip_norm=cfg.clip_norm or None, compress=cfg.compress or None)
     return Trainer(model, engine, n_threads=cfg.thread, device=device)

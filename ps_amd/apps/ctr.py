@@ -18,7 +18,7 @@ from ..eval.loss_surface import LossSurface
 from ..eval.metrics import AUC
 from ..models.reference import DNN, WideDeepNN
 from ..obs import metrics
-from .common import device, make_trainer, maybe_run_server, setup
+from .common import connect, device, make_trainer, maybe_run_server, setup
 
 
 def main(argv=None):
@@ -34,13 +34,15 @@ def main(argv=None):
     if maybe_run_server(cfg):
         return
     dev = device()
+    conn, tables = connect(cfg, dev)  # embedding / wide rows live on the parameter server
     gen = torch.Generator().manual_seed(cfg.seed)
     if a.wide:
-        model = WideDeepNN.build_model(23, 10, 45, [150, 10, 1], 100000, gen=gen, init_scale=a.init_scale)
+        model = WideDeepNN.build_model(23, 10, 45, [150, 10, 1], 100000, gen=gen, init_scale=a.init_scale,
+                                       table_factory=tables)
     else:
-        model = DNN.build_model(23, 10, 45, [150, 10, 1], gen=gen, init_scale=a.init_scale)
+        model = DNN.build_model(23, 10, 45, [150, 10, 1], gen=gen, init_scale=a.init_scale, table_factory=tables)
     model = model.to(dev)
-    trainer = make_trainer(cfg, model, dev)
+    trainer = make_trainer(cfg, model, dev, conn)
     w0 = {n: p.detach().clone() for n, p in model.named_parameters()}
     test = synthetic_ctr(5000, wide_k=23 if a.wide else 0, seed=10 ** 6)
     for epoch in range(a.epochs):

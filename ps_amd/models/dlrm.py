@@ -4,7 +4,8 @@ Adagrad on 8 x MI355X").
   dense [B, 13] -> bottom MLP 13-512-256-128 (ReLU)
   26 categorical ids -> 26 embedding tables (dim 128), ALL held in ONE row-sharded table
       (per-table row offsets) so a step does one id exchange + one row exchange instead of
-      26 -- the reference's one-RPC-per-row push at the other extreme
+      26 -- the reference's one-RPC-per-row push (SURVEY §2.6 C5) at the other extreme;
+      the row-gradient push leaves from a backward hook on a side stream (overlapped)
   interaction: pairwise dots of the 27 vectors (upper triangle, 351) ++ bottom output
   top MLP 479-1024-1024-512-256-1 -> sigmoid, BCE.
 
@@ -20,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..parallel.sparse_table import ShardedSparseTable, SparseTable
+from ..parallel.sparse_table import ShardedSparseTable
 from ..parallel.transport import Transport
 from ..parallel.updaters import AdagradUpdater, Updater
 from ..ops.dense import dlrm_interact
@@ -37,41 +38,34 @@ def mlp(dims: Sequence[int], last_act: bool = True) -> nn.Sequential:
 
 
 class MultiTableEmbedding(SparseLayerMixin, nn.Module):
-    """T tables of (rows_t, dim) fused into one (sharded) sparse table with row offsets."""
+    """T tables of (rows_t, dim) as the fields of ONE (sharded) sparse table: key = row offset
+    of table t + id, range-partitioned over the co-located servers; one id exchange + one row
+    exchange per step for all T tables."""
 
     def __init__(self, rows: Sequence[int], dim: int, transport: Optional[Transport] = None,
-                 updater: Optional[Updater] = None, device=None, seed: int = 0):
+                 updater: Optional[Updater] = None, device=None, seed: int = 0, overlap: bool = True):
         super().__init__()
         self.rows = list(rows)
         self.dim = dim
-        off = [0]
-        for r in self.rows[:-1]:
-            off.append(off[-1] + r)
-        self.register_buffer("offsets", torch.tensor(off, dtype=torch.int64), persistent=False)
-        total = sum(self.rows)
         bound = (1.0 / max(self.rows)) ** 0.5
         upd = updater or AdagradUpdater(0.01, 1e-8, rowwise=True)
-        if transport is not None and transport.world > 1:
-            self.table = ShardedSparseTable("emb", dim, total, transport, upd, init=(-bound, bound), seed=seed,
-                                            device=device)
-        else:
-            self.table = SparseTable("emb", dim, total, upd, init=(-bound, bound), seed=seed, device=device)
-        self._pending = []
+        self.table = ShardedSparseTable("emb", dim, self.rows, transport, upd, init=(-bound, bound), seed=seed,
+                                        device=device, fields=len(self.rows), overlap=overlap)
         self.out_dtype = None  # compute dtype of the looked-up rows (tables stay fp32)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         """ids [B, T] (per-table row ids) -> [B, T, dim]."""
-        gids = ids + self.offsets.to(ids.device)[None, :]
-        return self._lookup(self.table, gids, self.out_dtype)
+        return self._lookup(self.table, ids, self.out_dtype)
 
 
 class DLRM(nn.Module):
     def __init__(self, dense_in: int = 13, table_rows: Sequence[int] = (100000,) * 26, dim: int = 128,
                  bottom: Sequence[int] = (512, 256), top: Sequence[int] = (1024, 1024, 512, 256),
-                 transport: Optional[Transport] = None, device=None, sparse_updater: Optional[Updater] = None):
+                 transport: Optional[Transport] = None, device=None, sparse_updater: Optional[Updater] = None,
+                 overlap: bool = True):
         super().__init__()
         self.bottom = mlp([dense_in, *bottom, dim])
-        self.emb = MultiTableEmbedding(table_rows, dim, transport, sparse_updater, device)
+        self.emb = MultiTableEmbedding(table_rows, dim, transport, sparse_updater, device, overlap=overlap)
         n = len(table_rows) + 1
         self.n_inter = n * (n - 1) // 2
         self.top = mlp([self.n_inter + dim, *top, 1], last_act=False)

@@ -94,53 +94,41 @@ class FcLayer(nn.Module):
 
 
 class SparseLayerMixin:
-    """Common pull -> leaf -> push protocol for sparse-table layers."""
+    """Common lookup -> (autograd leaf) -> push protocol of sparse-table layers: every table
+    looked up in a forward keeps the routing of that pull and pushes the rows' gradients back
+    along it (parallel/sparse_table.py); ``push_sparse`` flushes what the backward hooks have
+    not already pushed."""
 
-    def _pull_leaf(self, table, ids: torch.Tensor):
-        uniq, inv, counts = torch.unique(ids.reshape(-1), return_inverse=True, return_counts=True)
-        rows = table.pull(uniq)
-        leaf = rows.detach().clone().requires_grad_(self.training and torch.is_grad_enabled())
-        self._pending.append((table, uniq, leaf, counts, ids.shape[0]))
-        return leaf, inv.view(ids.shape)
+    def _tables_used(self) -> list:
+        if not hasattr(self, "_used"):
+            self._used = []
+        return self._used
 
-    def _lookup(self, table, ids: torch.Tensor, out_dtype=None) -> torch.Tensor:
-        """rows of ``ids`` ([..., dim], autograd to the pulled leaf).  GPU: one sort for the
-        dedupe, HIP gather with the dtype cast fused, segment-sum backward (ops/sparse.py)."""
-        if not ids.is_cuda:
-            leaf, inv = self._pull_leaf(table, ids)
-            out = leaf[inv]
-            return out if out_dtype is None else out.to(out_dtype)
-        from ..ops.sparse import gather_unique, unique_with_segments
-
-        uniq, inv, counts, perm, seg_off = unique_with_segments(ids)
-        rows = table.pull(uniq)
-        leaf = rows.detach().clone().requires_grad_(self.training and torch.is_grad_enabled())
-        self._pending.append((table, uniq, leaf, counts, ids.shape[0]))
-        out = gather_unique(leaf, inv, perm, seg_off, out_dtype)
-        return out.view(*ids.shape, leaf.shape[1])
+    def _lookup(self, table, ids: torch.Tensor, out_dtype=None, grad_fn=None) -> torch.Tensor:
+        """rows of ``ids`` ([..., dim]); autograd to the pulled rows of ``table``."""
+        used = self._tables_used()
+        if not any(t is table for t in used):
+            used.append(table)
+        return table.lookup(ids, out_dtype, grad_fn)
 
     def push_sparse(self) -> int:
         """Push gradients of the rows touched since the last call; returns rows pushed."""
-        n = 0
-        for table, uniq, leaf, counts, batch in self._pending:
-            if leaf.grad is None:
-                continue
-            g = self._scale_grad(leaf.grad, counts, batch)
-            table.push(uniq, g)
-            n += uniq.numel()
-        self._pending = []
-        return n
-
-    def _scale_grad(self, g, counts, batch):
-        return g
+        return sum(t.push_pending() for t in self._tables_used())
 
     def clear(self):
-        self._pending = []
+        for t in self._tables_used():
+            t.drop_pending()
+
+
+def _reference_mean_grad(g: torch.Tensor, plan) -> torch.Tensor:
+    """EmbeddingField.java:86-104: per key, the MEAN over its occurrences of the per-sample
+    delta (no 1/N): exact grad (which carries 1/N) * N / count."""
+    return g * (plan.n / plan.counts.to(g.dtype)).unsqueeze(1)
 
 
 class EmbeddingField(SparseLayerMixin, nn.Module):
     """One categorical field: ids [N] -> act(rows) [N, dim] (layer/EmbeddingField.java:66-78).
-    Rows init U(+-4*sqrt(6/(1+dim))) on first touch (:31-38), deterministic per (seed, row)."""
+    Rows init U(+-4*sqrt(6/(1+dim))) on first touch (:31-38), deterministic per (seed, key)."""
 
     def __init__(self, name: str, dim: int, table, activation: Optional[A.Activation] = None,
                  grad_mode: str = "exact"):
@@ -148,34 +136,36 @@ class EmbeddingField(SparseLayerMixin, nn.Module):
         self.lname, self.dim, self.table = name, dim, table
         self.activation = activation
         self.grad_mode = grad_mode
-        self._pending = []
 
     def forward(self, ids):
-        leaf, inv = self._pull_leaf(self.table, ids)
-        out = leaf[inv]
+        out = self._lookup(self.table, ids, None, _reference_mean_grad if self.grad_mode == "reference" else None)
         return self.activation(out) if self.activation is not None else out
-
-    def _scale_grad(self, g, counts, batch):
-        if self.grad_mode == "reference":
-            # reference: per-key mean over occurrences of the per-sample delta (no 1/N)
-            return g * (batch / counts.to(g.dtype)).unsqueeze(1)
-        return g
 
 
 class EmbeddingLayer(SparseLayerMixin, nn.Module):
     """All categorical fields, outputs stacked into one [N, fields*dim] slice
-    (layer/EmbeddingLayer.java:25-48, build :50-57: fields ``emF<i>`` with ReLU)."""
+    (layer/EmbeddingLayer.java:25-48, build :50-57: fields ``emF<i>`` with ReLU).
 
-    def __init__(self, name: str, fields: int, dim: int, tables: List, activation: str = "relu",
+    The fields share ONE table (``table.fields == fields``; key = (field, id)), so a forward
+    pulls every field's rows in one exchange -- the reference issues one getList per field
+    (EmbeddingField.preForward, layer/EmbeddingField.java:57-64).  A list of per-field tables
+    is accepted too (looked up one by one)."""
+
+    def __init__(self, name: str, fields: int, dim: int, table, activation: str = "relu",
                  grad_mode: str = "exact"):
         super().__init__()
         self.lname, self.fields, self.dim = name, fields, dim
-        self.tables = tables
+        self.per_field = isinstance(table, (list, tuple))
+        self.tables = list(table) if self.per_field else [table]
+        if not self.per_field and getattr(table, "fields", 1) != fields:
+            raise ValueError(f"table has {table.fields} fields, layer needs {fields}")
         self.act_name = activation
+        self.act = A.get(activation)
         self.grad_mode = grad_mode
-        self.embedding_fields = nn.ModuleList([EmbeddingField(f"emF{i}", dim, tables[i], A.get(activation),
-                                                             grad_mode) for i in range(fields)])
-        self._pending = []
+
+    @property
+    def table(self):
+        return self.tables[0]
 
     @property
     def output_dims(self):
@@ -183,15 +173,13 @@ class EmbeddingLayer(SparseLayerMixin, nn.Module):
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         """ids: [N, fields] int64."""
-        outs = [f(ids[:, i]) for i, f in enumerate(self.embedding_fields)]
-        return torch.cat(outs, dim=1)
-
-    def push_sparse(self) -> int:
-        return sum(f.push_sparse() for f in self.embedding_fields)
-
-    def clear(self):
-        for f in self.embedding_fields:
-            f.clear()
+        gfn = _reference_mean_grad if self.grad_mode == "reference" else None
+        if self.per_field:
+            e = torch.stack([self._lookup(t, ids[:, i], None, gfn) for i, t in enumerate(self.tables)], dim=1)
+        else:
+            e = self._lookup(self.tables[0], ids, None, gfn)  # [N, fields, dim]
+        e = e.reshape(ids.shape[0], self.fields * self.dim)
+        return self.act(e) if self.act is not None else e
 
 
 class LRLayer(SparseLayerMixin, nn.Module):
@@ -205,20 +193,17 @@ class LRLayer(SparseLayerMixin, nn.Module):
         self.bias = nn.Parameter(torch.zeros(1))
         self.activation = activation
         self.grad_mode = grad_mode
-        self._pending = []
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        leaf, inv = self._pull_leaf(self.table, ids)
-        z = leaf[inv].reshape(ids.shape[0], -1).sum(dim=1, keepdim=True) + self.bias
+        gfn = self._reference_grad if self.grad_mode == "reference" else None
+        w = self._lookup(self.table, ids.reshape(-1), None, gfn)  # [N*k, 1]
+        z = w.reshape(ids.shape[0], -1).sum(dim=1, keepdim=True) + self.bias
         self.register_delta_hook(z)
         return self.activation(z) if self.activation is not None else z
 
-    def _scale_grad(self, g, counts, batch):
-        if self.grad_mode == "reference":
-            # every touched id gets mean(delta) (batch mean); sum over occurrences of
-            # delta/N == mean(delta) only if the id occurs in every sample -> rebuild it
-            return self._mean_delta.expand_as(g).clone()
-        return g
+    def _reference_grad(self, g, plan):
+        # every touched id gets mean(delta) (the batch mean; LRLayer.java:110-117, Q14)
+        return self._mean_delta.to(g.dtype).expand_as(g).clone()
 
     def register_delta_hook(self, z: torch.Tensor):
         if self.grad_mode == "reference" and z.requires_grad:

@@ -14,8 +14,10 @@ Interface (model/Model.java:11-17): ``train(batch) -> loss`` (forward + backward
 metrics, no optimizer step -- the PS applies it), ``predict(batch)``, ``pull_weights()``,
 ``get_updater()`` (key-prefix -> Updater).  Batches are dicts with the reference's keys:
 ``X`` numeric [N, numeric], ``E`` categorical ids [N, fields], ``W`` wide ids [N, k],
-``Y`` labels.  Sparse tables come from ``table_factory(name, dim, rows, init, id_mode)``
-so the same model runs standalone (SparseTable) or sharded (ShardedSparseTable).
+``Y`` labels.  Sparse tables come from ``table_factory(name, dim, rows, init, mode, fields)``
+so the same model runs standalone (``local_table_factory``: SparseTable), on the co-located
+PS ranks (``sharded_table_factory``: rows partitioned over the torchrun/RCCL ranks) or on
+dedicated TCP servers (``tcp_table_factory``: rows in the native server's row tables).
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ import torch.nn as nn
 from ..context import ctx
 from ..eval.metrics import AUC, SoftmaxPrecision
 from ..obs import metrics as _metrics
-from ..parallel.sparse_table import SparseTable
+from ..parallel.sparse_table import ShardedSparseTable, SparseTable, TcpSparseTable, stable_seed
 from ..parallel.updaters import AdamUpdater, FtrlUpdater, Updater
 from . import activations as A
 from . import layers as L
@@ -36,9 +38,29 @@ from .losses import CrossEntropy, Loss, SoftmaxLoss
 
 
 def local_table_factory(device=None, seed: int = 0, id_mode: str = "map"):
-    def make(name, dim, rows, init, mode=None):
-        return SparseTable(name, dim, rows, init=init, id_mode=mode or id_mode, seed=seed + hash(name) % 9973,
-                           device=device)
+    """Standalone tables (one process holds every row)."""
+    def make(name, dim, rows, init, mode=None, fields=1):
+        return SparseTable(name, dim, rows, init=init, id_mode=mode or id_mode, seed=stable_seed(name, seed),
+                           device=device, fields=fields)
+
+    return make
+
+
+def sharded_table_factory(transport, device=None, seed: int = 0, id_mode: str = "map", overlap: bool = True):
+    """Rows partitioned over the co-located servers of ``transport`` (torchrun ranks); with
+    ``overlap`` (GPU) row gradients are pushed from backward hooks on a side stream."""
+    def make(name, dim, rows, init, mode=None, fields=1):
+        return ShardedSparseTable(name, dim, rows, transport, init=init, id_mode=mode or id_mode,
+                                  seed=stable_seed(name, seed), device=device, fields=fields, overlap=overlap)
+
+    return make
+
+
+def tcp_table_factory(client, device=None, seed: int = 0, id_mode: str = "map"):
+    """Rows on the dedicated TCP parameter servers (-Dmode=dist)."""
+    def make(name, dim, rows, init, mode=None, fields=1):
+        return TcpSparseTable(name, dim, rows, client, init=init, id_mode=mode or id_mode,
+                              seed=stable_seed(name, seed), fields=fields, device=device)
 
     return make
 
@@ -101,14 +123,24 @@ class Model(nn.Module):
         return [m for m in self.modules() if isinstance(m, (L.EmbeddingLayer, L.LRLayer))]
 
     def tables(self):
+        """Sparse tables by PS key prefix: ``emF`` (all embedding fields; per-field tables are
+        ``emF<i>``) and ``wide.weights``."""
         out = {}
         for m in self.modules():
             if isinstance(m, L.EmbeddingLayer):
-                for i, t in enumerate(m.tables):
-                    out[f"emF{i}"] = t
+                if m.per_field:
+                    for i, t in enumerate(m.tables):
+                        out[f"emF{i}"] = t
+                else:
+                    out["emF"] = m.table
             elif isinstance(m, L.LRLayer):
                 out[f"{m.lname}.weights"] = m.table
         return out
+
+    def set_accumulating(self, on: bool) -> None:
+        """Micro-batch accumulation: owners keep pushed rows and step once per round."""
+        for t in self.tables().values():
+            t.accumulating = on
 
     def push_sparse(self) -> int:
         return sum(layer.push_sparse() for layer in self.sparse_layers())
@@ -124,10 +156,7 @@ def _scale_init(model: Model, scale: float) -> None:
         for p in model.parameters():
             p.mul_(scale)
     for t in model.tables().values():
-        if hasattr(t, "init"):
-            t.init = (t.init[0] * scale, t.init[1] * scale)
-        elif hasattr(t, "local"):
-            t.local.init = (t.local.init[0] * scale, t.local.init[1] * scale)
+        t.init = (t.init[0] * scale, t.init[1] * scale)
 
 
 def _bind_table_updaters(model: Model):
@@ -144,8 +173,7 @@ class DNN(Model):
         tf = table_factory or local_table_factory()
         bound = 4 * math.sqrt(6) / math.sqrt(1 + dim)
         self.embedding = L.EmbeddingLayer("embedding", fields, dim,
-                                          [tf(f"emF{i}", dim, emb_rows, (-bound, bound)) for i in range(fields)],
-                                          "relu", grad_mode)
+                                          tf("emF", dim, emb_rows, (-bound, bound), None, fields), "relu", grad_mode)
         self.concat = L.ConcatLayer("concat")
         self._set_fc(L.FcLayer.build(fields * dim + numeric, fc_dims, gen))  # keys fc0.weights, ...
         self.loss = CrossEntropy()
@@ -177,8 +205,7 @@ class WideDeepNN(Model):
         tf = table_factory or local_table_factory()
         bound = 4 * math.sqrt(6) / math.sqrt(1 + dim)
         self.embedding = L.EmbeddingLayer("embedding", fields, dim,
-                                          [tf(f"emF{i}", dim, emb_rows, (-bound, bound)) for i in range(fields)],
-                                          "relu", grad_mode)
+                                          tf("emF", dim, emb_rows, (-bound, bound), None, fields), "relu", grad_mode)
         self.concat = L.ConcatLayer("concat")
         fcs = L.FcLayer.build(fields * dim + numeric, fc_dims, gen)
         fcs[-1].set_activation(None)

@@ -95,20 +95,40 @@ def fused_opt(kind: int, w: torch.Tensor, st0: Optional[torch.Tensor], st1: Opti
 
 
 def sparse_opt(kind: int, table: torch.Tensor, st0: Optional[torch.Tensor], st1: Optional[torch.Tensor],
-               rows: torch.Tensor, grad: torch.Tensor, rowwise: bool = False, skip_zero: bool = False, **hp) -> None:
-    """Row-sparse optimizer step: apply to ``table[rows]`` with ``grad`` [len(rows), dim]."""
+               rows: torch.Tensor, grad: torch.Tensor, rowwise: bool = False, skip_zero: bool = False,
+               perm: Optional[torch.Tensor] = None, **hp) -> None:
+    """Row-sparse optimizer step on ``table[rows]``.
+
+    ``perm is None``: ``rows`` unique, ``grad`` [len(rows), dim] row-aligned.
+    ``perm`` given: ``rows`` SORTED with repeats, ``grad[perm[j]]`` belongs to ``rows[j]``; the
+    gradient rows of every run are summed and ONE update is applied per distinct row (the
+    owner-side merge of several workers' / micro-batches' pushes, no host sync).  Negative
+    rows are skipped."""
     h = _hp(hp)
     if use_native(table, grad):
         native().sparse_opt(kind, table, st0, st1, rows, grad, bool(rowwise), bool(skip_zero), h["lr"], h["beta1"],
-                            h["beta2"], h["eps"], h["wd"], h["momentum"], h["bc1"], h["bc2"], h["l1"], h["l2"],
-                            h["fbeta"], int(h["ftrl_mode"]), h["gscale"])
+                            h["beta2"], h["eps"], h["wd"], h["momentum"], h["dampening"], bool(h["nesterov"]),
+                            bool(h["adamw"]), h["bc1"], h["bc2"], h["l1"], h["l2"], h["fbeta"], int(h["ftrl_mode"]),
+                            h["gscale"], perm)
         return
     if rows.numel() == 0:
         return
-    g = grad.float().reshape(rows.numel(), table.shape[1]) * h["gscale"]
+    dim = table.shape[1]
+    g = grad.float().reshape(-1, dim)
+    if perm is not None:
+        g = g[perm]
+        head = torch.ones(rows.numel(), dtype=torch.bool)
+        head[1:] = rows[1:] != rows[:-1]
+        seg = torch.cumsum(head.long(), 0) - 1
+        nu = int(seg[-1]) + 1
+        acc = torch.zeros(nu, dim, dtype=torch.float32)
+        acc.index_add_(0, seg, g)
+        rows, g = rows[head], acc
+    g = g * h["gscale"]
+    keep = rows >= 0
     if skip_zero:
-        keep = g[:, 0] != 0
-        rows, g = rows[keep], g[keep]
+        keep &= g[:, 0] != 0
+    rows, g = rows[keep], g[keep]
     if kind == ADAGRAD and rowwise:
         ss = (g * g).mean(dim=1)
         st0[rows] += ss

@@ -99,17 +99,61 @@ def sparse_lr_fwd(w: torch.Tensor, ids: torch.Tensor, bias: torch.Tensor | None,
     return out
 
 
+_M32 = 0xFFFFFFFF
+
+
+def philox_u01(seed: int, ctr: torch.Tensor) -> torch.Tensor:
+    """uniform [0, 1) from the first word of Philox-4x32-10(seed, ctr) -- bit-identical to
+    ``Philox::gen`` + ``u01`` in csrc/include/psamd_device.h (and the host copy in the native
+    server), computed with int64 torch ops so the CPU oracle initialises rows exactly like the
+    HIP kernel."""
+    ctr = ctr.long()
+    c0, c1 = ctr & _M32, (ctr >> 32) & _M32
+    c2 = torch.zeros_like(c0)
+    c3 = torch.zeros_like(c0)
+    k0, k1 = int(seed) & _M32, (int(seed) >> 32) & _M32
+    for _ in range(10):
+        p0 = 0xD2511F53 * c0  # < 2^64: wraps in int64 with the same low bits
+        p1 = 0xCD9E8D57 * c2
+        hi0, lo0 = (p0 >> 32) & _M32, p0 & _M32
+        hi1, lo1 = (p1 >> 32) & _M32, p1 & _M32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + 0x9E3779B9) & _M32
+        k1 = (k1 + 0xBB67AE85) & _M32
+    return (c0 >> 8).float() * (1.0 / 16777216.0)
+
+
+def init_values(seed: int, keys: torch.Tensor, dim: int, lo: float, hi: float) -> torch.Tensor:
+    """Deterministic first-touch values of rows ``keys`` ([n] int64 global keys) -> [n, dim]."""
+    c = torch.arange(dim, dtype=torch.int64, device=keys.device)
+    ctr = (keys.long()[:, None] << 20) ^ c[None, :]
+    return lo + (hi - lo) * philox_u01(seed, ctr.reshape(-1)).reshape(keys.numel(), dim)
+
+
 def lazy_init_rows(table: torch.Tensor, rows: torch.Tensor, flags: torch.Tensor, seed: int, row_base: int,
-                   lo: float, hi: float) -> None:
-    """Initialise rows not yet touched (flags==0) deterministically from (seed, global row)."""
+                   lo: float, hi: float, keys: torch.Tensor | None = None) -> None:
+    """Initialise rows not yet touched (flags==0) deterministically from (seed, global key);
+    the key is ``keys[r]`` when given, else ``rows[r] + row_base``.  Negative rows skipped."""
     if use_native(table, rows):
-        native().lazy_init_rows(table, rows.contiguous(), flags, int(seed), int(row_base), float(lo), float(hi))
+        native().lazy_init_rows(table, rows.contiguous(), flags, int(seed), int(row_base), float(lo), float(hi),
+                                None if keys is None else keys.contiguous())
         return
-    new = rows[flags[rows] == 0].unique()
-    for r in new.tolist():
-        g = torch.Generator().manual_seed((int(seed) * 1000003 + r + row_base) & 0x7FFFFFFFFFFFFFFF)
-        table[r] = lo + (hi - lo) * torch.rand(table.shape[1], generator=g)
-        flags[r] = 1
+    rows = rows.long()
+    k = rows + row_base if keys is None else keys.long()
+    ok = rows >= 0
+    rows, k = rows[ok], k[ok]
+    new = flags[rows] == 0
+    rows, k = rows[new], k[new]
+    if rows.numel():
+        table[rows] = init_values(seed, k, table.shape[1], lo, hi).to(table.dtype)
+        flags[rows] = 1
+
+
+def hash_slots(hkeys: torch.Tensor, ids: torch.Tensor, insert: bool, status: torch.Tensor) -> torch.Tensor:
+    """Slots of ``ids`` in the device open-addressing map ``hkeys`` (HIP kernel, GPU only)."""
+    out = torch.empty_like(ids)
+    native().hash_slots(hkeys, ids.contiguous(), out, bool(insert), status)
+    return out
 
 
 class _GatherUnique(torch.autograd.Function):

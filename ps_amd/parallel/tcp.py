@@ -96,6 +96,18 @@ class PSClient:
     def barrier(self, worker: int = 0) -> int:
         return self._c.barrier(worker)
 
+    def row_pull(self, table: str, dim: int, keys: torch.Tensor, lo: float = 0.0, hi: float = 0.0,
+                 seed: int = 0) -> torch.Tensor:
+        """Rows of int64 ``keys`` from the server's row table (created on first pull with the
+        deterministic (seed, key) init the GPU lazy-init kernel uses)."""
+        k = keys.detach().cpu().long().contiguous().numpy()
+        return torch.from_numpy(self._c.row_pull(table, int(dim), k, float(lo), float(hi), int(seed)))
+
+    def row_push(self, table: str, dim: int, keys: torch.Tensor, grads, updater_spec: str,
+                 apply_now: bool = False) -> None:
+        k = keys.detach().cpu().long().contiguous().numpy()
+        self._c.row_push(table, int(dim), k, _np(grads).reshape(len(k), int(dim)), updater_spec, 2 if apply_now else 0)
+
     def clock(self, worker: int, c: int) -> int:
         return self._c.clock(worker, c)
 
@@ -163,6 +175,32 @@ class PSRouterClient:
     def push(self, grads: Dict[str, object], updater_spec: str, apply_now: bool = False) -> None:
         futs = [self.pool.submit(self.clients[s].push, {k: grads[k] for k in ks}, updater_spec, apply_now)
                 for s, ks in self._group(list(grads)).items()]
+        for f in futs:
+            f.result()
+
+    def _key_groups(self, keys: torch.Tensor) -> Dict[int, torch.Tensor]:
+        """Row keys -> server (the row analogue of the key router): multiplicative hash mod S."""
+        k = keys.detach().cpu().long()
+        s = torch.remainder((k * 0x9E3779B1) >> 16, len(self.clients))
+        return {int(i): torch.nonzero(s == i).reshape(-1) for i in torch.unique(s).tolist()}
+
+    def row_pull(self, table: str, dim: int, keys: torch.Tensor, lo: float = 0.0, hi: float = 0.0,
+                 seed: int = 0) -> torch.Tensor:
+        keys = keys.detach().cpu().long()
+        out = torch.empty(keys.numel(), int(dim))
+        groups = self._key_groups(keys)
+        futs = {s: self.pool.submit(self.clients[s].row_pull, table, dim, keys[pos], lo, hi, seed)
+                for s, pos in groups.items()}
+        for s, f in futs.items():
+            out[groups[s]] = f.result()
+        return out
+
+    def row_push(self, table: str, dim: int, keys: torch.Tensor, grads, updater_spec: str,
+                 apply_now: bool = False) -> None:
+        keys = keys.detach().cpu().long()
+        g = torch.as_tensor(_np(grads)).reshape(keys.numel(), int(dim))
+        futs = [self.pool.submit(self.clients[s].row_push, table, dim, keys[pos], g[pos], updater_spec, apply_now)
+                for s, pos in self._key_groups(keys).items()]
         for f in futs:
             f.result()
 

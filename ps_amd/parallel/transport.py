@@ -26,6 +26,32 @@ import torch
 import torch.distributed as dist
 
 
+_SIDE_STREAMS = {}
+
+
+def side_stream(device) -> "torch.cuda.Stream":
+    """One shared side stream per device for parameter-server traffic issued from autograd
+    hooks (sparse row pushes); collectives on it still serialise in issue order inside the
+    process group, so every rank sees the same collective sequence."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _SIDE_STREAMS[idx] = s
+    return s
+
+
+def _share(t: torch.Tensor) -> torch.Tensor:
+    """Snapshot a tensor for another (thread-)rank of the loopback hub: GPU tensors are
+    cloned on the caller's stream and that stream is drained, so the reader may use the
+    copy from any stream."""
+    c = t.detach().clone()
+    if c.is_cuda:
+        torch.cuda.current_stream(c.device).synchronize()
+    return c
+
+
 class Transport:
     def __init__(self, group=None, check_order: bool = False):
         self.group = group
@@ -203,7 +229,7 @@ class LoopbackTransport(Transport):
 
     def reduce_scatter(self, out, inp, average: bool = False):
         self._note("rs", inp)
-        parts = self.hub.exchange(self.rank, inp.detach().clone())
+        parts = self.hub.exchange(self.rank, _share(inp))
         total = self._sum(parts).view(self.world, -1)[self.rank]
         out.copy_(total.view_as(out))
         if average:
@@ -212,13 +238,13 @@ class LoopbackTransport(Transport):
 
     def all_gather(self, out, inp):
         self._note("ag", out)
-        parts = self.hub.exchange(self.rank, inp.detach().clone().reshape(-1))
+        parts = self.hub.exchange(self.rank, _share(inp).reshape(-1))
         out.copy_(torch.cat(parts).view_as(out))
         return out
 
     def all_reduce(self, t, op=None):
         self._note("ar", t)
-        parts = self.hub.exchange(self.rank, t.detach().clone())
+        parts = self.hub.exchange(self.rank, _share(t))
         if op is not None and op == dist.ReduceOp.MAX:
             r = parts[0].clone()
             for p in parts[1:]:
@@ -230,7 +256,7 @@ class LoopbackTransport(Transport):
 
     def broadcast(self, t, src: int = 0):
         self._note("bc", t)
-        parts = self.hub.exchange(self.rank, t.detach().clone())
+        parts = self.hub.exchange(self.rank, _share(t))
         t.copy_(parts[src])
         return t
 
@@ -239,7 +265,7 @@ class LoopbackTransport(Transport):
         w = self.world
         if in_splits is None:
             in_splits = [inp.shape[0] // w] * w
-        parts = self.hub.exchange(self.rank, (inp.detach().clone(), list(in_splits)))
+        parts = self.hub.exchange(self.rank, (_share(inp), list(in_splits)))
         chunks = []
         for src in range(w):
             t, sp = parts[src]

@@ -75,11 +75,14 @@ class Updater:
 
     def step_rows(self, table: torch.Tensor, states: List[torch.Tensor], rows: torch.Tensor, grad: torch.Tensor,
                   gscale: float = 1.0, step: Optional[int] = None, rowwise: bool = False,
-                  skip_zero: bool = False) -> None:
+                  skip_zero: bool = False, perm: Optional[torch.Tensor] = None) -> None:
+        """Row-sparse step; with ``perm`` the rows are sorted with repeats and each run's
+        gradient rows are summed into one update (ops/optim.py sparse_opt)."""
         st = list(states) + [None] * (2 - len(states))
         h = self.hyper(self.t + 1 if step is None else step)
         h["gscale"] = h.get("gscale", 1.0) * gscale
-        _o.sparse_opt(self.kind, table, st[0], st[1], rows, grad, rowwise=rowwise, skip_zero=skip_zero, **h)
+        _o.sparse_opt(self.kind, table, st[0], st[1], rows, grad, rowwise=rowwise, skip_zero=skip_zero, perm=perm,
+                      **h)
 
     # ---------------------------------------------------------------- reference API
     def update(self, key: str, w: torch.Tensor, dw: torch.Tensor) -> torch.Tensor:

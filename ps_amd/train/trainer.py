@@ -39,16 +39,19 @@ def _to(batch: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
 
 class CollectiveEngine:
     def __init__(self, model, transport: Optional[Transport] = None, *, bucket_mb: float = 25.0,
-                 staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None):
+                 staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
+                 overlap: bool = True):
         self.model = model
         self.t = transport or Transport()
         dense = [p for p in model.parameters() if p.requires_grad]
         self.ps = ColocatedPS(model, model.get_updater(), self.t, bucket_mb=bucket_mb, staleness=staleness,
-                              clip_norm=clip_norm, compress=compress) if dense else None
+                              clip_norm=clip_norm, compress=compress, overlap=overlap) if dense else None
 
     def accumulate(self, on: bool) -> None:
         if self.ps is not None:
             self.ps.accumulating = on
+        if hasattr(self.model, "set_accumulating"):  # sparse rows: one owner step per round
+            self.model.set_accumulating(on)
 
     def end_step(self) -> None:
         self.model.push_sparse()

@@ -36,11 +36,8 @@ class CheckpointManager:
         if ps is not None:
             state["ps"] = ps.shard_state()
         if tables:
-            state["tables"] = {}
-            for name, t in tables.items():
-                local = getattr(t, "local", t)
-                state["tables"][name] = {"table": local.table.detach().cpu(), "flags": local.flags.detach().cpu(),
-                                         "states": [s.detach().cpu() for s in local.states], "round": local.round}
+            # rows + init flags + optimizer state + the id -> slot map of this rank's shard
+            state["tables"] = {name: t.state_dict() for name, t in tables.items()}
         if extra:
             state["extra"] = extra
         path = self._path(step)
@@ -98,11 +95,5 @@ class CheckpointManager:
         if ps is not None:
             ps.load_shard_state(state["ps"])
         for name, t in (tables or {}).items():
-            s = state["tables"][name]
-            local = getattr(t, "local", t)
-            local.table.copy_(s["table"])
-            local.flags.copy_(s["flags"])
-            for dst, src in zip(local.states, s["states"]):
-                dst.copy_(src)
-            local.round = int(s["round"])
+            t.load_state_dict(state["tables"][name])
         return state

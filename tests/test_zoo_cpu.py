@@ -95,7 +95,7 @@ def _dlrm_body(tp):
         m.push_sparse()
         ps.finish_step()
         losses.append(loss.item())
-    probe = m.emb.table.pull(torch.tensor([0, 1, 2, 600, 1999]))
+    probe = m.emb.table.pull_keys(torch.tensor([0, 1, 2, 600, 1999]))
     return losses, probe
 
 
