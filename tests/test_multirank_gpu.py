@@ -185,15 +185,16 @@ def test_reference_models_sharded_rows_multirank_gpu(wide):
         torch.testing.assert_close(gpu[r][1], single[1], rtol=1e-4, atol=1e-4)
 
 
-def _dlrm_body(tp, n):
+def _dlrm_body(tp, n, inits):
     from ps_amd.models.dlrm import DLRM, dlrm_batch
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import AdagradUpdater
 
-    torch.manual_seed(0)
     rows = [700] * 4
     m = DLRM(dense_in=13, table_rows=rows, dim=16, bottom=(32,), top=(32, 16), transport=tp, device=DEV,
-             overlap=False).to(DEV)
+             overlap=False)
+    m.load_state_dict(inits, strict=False)  # dense init drawn outside the threads (shared global RNG)
+    m = m.to(DEV)
     ps = ColocatedPS(m, AdagradUpdater(0.05, 1e-8), tp, bucket_mb=0.05, overlap=False)
     dense, sparse, y = dlrm_batch(n, rows, seed=11, device=DEV)
     lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
@@ -207,8 +208,12 @@ def _dlrm_body(tp, n):
 
 
 def test_dlrm_multirank_gpu_equals_single_rank():
-    w2 = run_loopback(_dlrm_body, 2, 256)
-    w1 = run_loopback(_dlrm_body, 1, 256)[0]
+    from ps_amd.models.dlrm import DLRM
+
+    torch.manual_seed(0)
+    inits = DLRM(dense_in=13, table_rows=[700] * 4, dim=16, bottom=(32,), top=(32, 16)).state_dict()
+    w2 = run_loopback(_dlrm_body, 2, 256, inits)
+    w1 = run_loopback(_dlrm_body, 1, 256, inits)[0]
     for r in range(2):
         for k, v in w1[0].items():
             torch.testing.assert_close(w2[r][0][k], v, rtol=1e-4, atol=1e-5)
