@@ -107,8 +107,13 @@ def main():
         # launch ourselves under torchrun as a CHILD process (never exec from a GPU process)
         import subprocess
 
+        import socket
+
+        with socket.socket() as so:  # a free rendezvous port (several benches may share a node)
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-               "--master-addr=127.0.0.1", "--master-port=29533", os.path.abspath(__file__)] + sys.argv[1:]
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
     setup_miopen_db()
     if not torch.cuda.is_available():
@@ -192,7 +197,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,  # the reference publishes no throughput number
             "dtype": "bf16",
-            "data": "synthetic (GPU-resident batches of the named shape); random-init weights",
+            "data": f"synthetic: a pool of {BC.POOL if args.config != 'dlrm' else 4 * BC.POOL} distinct "
+                    f"GPU-resident batches of the named shape, cycled; random-init weights",
             "config": cfg,
         }
         line = json.dumps(rec)

@@ -129,7 +129,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> None:
     cmd = [_ninja_bin(), "-f", str(nf), f"-j{j}"]
     if verbose:
         cmd.append("-v")
-    r = subprocess.run(cmd, cwd=str(ROOT), capture_output=not verbose, text=True)
+    r = subprocess.run(cmd, cwd=str(BUILD), capture_output=not verbose, text=True)  # .ninja_log in build/
     if r.returncode != 0:
         sys.stderr.write((r.stdout or "") + (r.stderr or ""))
         raise RuntimeError("ps_amd native build failed")

@@ -21,6 +21,14 @@ import torch
 import torch.nn.functional as F
 
 
+POOL = int(os.environ.get("PS_AMD_BENCH_POOL", "8"))  # distinct GPU-resident synthetic batches cycled
+
+
+def _cycle(pool):
+    while True:
+        yield from pool
+
+
 @dataclass
 class Bench:
     step: Callable[[], torch.Tensor]
@@ -42,11 +50,13 @@ def setup_resnet50(args, tp, dev) -> Bench:
                      staleness=args.staleness)
     B, S = args.batch_per_gpu, args.image_size
     g = torch.Generator(device=dev).manual_seed(tp.rank)
-    x = torch.randn(B, 3, S, S, device=dev, generator=g).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (B,), device=dev, generator=g)
+    pool = [(torch.randn(B, 3, S, S, device=dev, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last), torch.randint(0, 1000, (B,), device=dev, generator=g))
+        for _ in range(POOL)]
+    it = _cycle(pool)
 
     def step():
+        x, y = next(it)
         loss = F.cross_entropy(model(x).float(), y)
         loss.backward()
         ps.finish_step()
@@ -70,9 +80,11 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
     ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
                      staleness=stale, clip_norm=None)
     B, S = args.batch_per_gpu, args.seq_len
-    ids, labels, positions = mlm_batch(B, S, seed=tp.rank, device=dev, with_positions=True)
+    pool = [mlm_batch(B, S, seed=tp.rank * 1000 + i, device=dev, with_positions=True) for i in range(POOL)]
+    it = _cycle(pool)
 
     def step():
+        ids, labels, positions = next(it)
         loss = model(ids, labels, positions)  # LM head on the masked positions only (BERT format)
         loss.backward()
         ps.finish_step()
@@ -90,8 +102,9 @@ def setup_dlrm(args, tp, dev) -> Bench:
 
     torch.manual_seed(0)
     rows = [args.dlrm_rows] * 26
+    overlap = os.environ.get("PS_AMD_SPARSE_OVERLAP", "1") == "1"  # A/B knob for the hook-driven push
     model = DLRM(table_rows=rows, transport=tp, device=dev,
-                 sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True)).to(dev)
+                 sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True), overlap=overlap).to(dev)
     # bf16 compute for the MLPs + interaction (fp32 master weights live in the PS shards);
     # embedding tables and their Adagrad state stay fp32, rows are cast inside the gather
     model.bottom.to(torch.bfloat16)
@@ -99,18 +112,23 @@ def setup_dlrm(args, tp, dev) -> Bench:
     ps = ColocatedPS(model, AdagradUpdater(0.01, 1e-8), tp, bucket_mb=args.bucket_mb,
                      last_bucket_mb=args.last_bucket_mb)
     B = args.batch_per_gpu
-    dense, sparse, y = dlrm_batch(B, rows, seed=tp.rank, device=dev)
+    # 4x the usual pool: every step brings new ids, so dedupe, lazy row creation and the row
+    # exchange are measured on fresh data rather than on one memorised batch
+    pool = [dlrm_batch(B, rows, seed=tp.rank * 1000 + i, device=dev) for i in range(4 * POOL)]
+    it = _cycle(pool)
 
     def step():
+        dense, sparse, y = next(it)
         loss = F.binary_cross_entropy_with_logits(model(dense, sparse).float(), y)
-        loss.backward()
-        model.push_sparse()
+        loss.backward()  # row gradients leave from the embedding leaf's hook (side stream)
+        model.push_sparse()  # flush (no-op when the hook already pushed)
         ps.finish_step()
         return loss
 
     return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",
                  {"model": "DLRM-26x128", "global_batch": B * tp.world, "seq_len": None,
-                  "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}"}, ps)
+                  "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}",
+                  "sparse_push_overlap": overlap}, ps)
 
 
 def setup_llama_onebit(args, tp, dev) -> Bench:
@@ -131,9 +149,11 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
                      compress="onebit" if tp.world > 1 else None)
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)
-    ids = torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g)
+    pool = [torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g) for _ in range(POOL)]
+    it = _cycle(pool)
 
     def step():
+        ids = next(it)
         loss = model(ids, ids)
         loss.backward()
         ps.finish_step()
