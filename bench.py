@@ -55,6 +55,9 @@ def parse():
                          "ResNet-50: 32.7 vs 31.6 ms, profiles/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--checkpoint-dir", type=str, default=os.environ.get("PS_AMD_CHECKPOINT_DIR", ""),
+                    help="after the timed region: one sharded checkpoint of every rank's server shard (timed, "
+                         "reported on stderr) -- utils/checkpoint.py")
     ap.add_argument("--timing", type=int, default=0,
                     help="after the timed region: N more steps with per-phase device timing "
                          "(fwd+bwd / push / serve / pull / exposed comm) printed to stderr")
@@ -169,6 +172,16 @@ def main():
         tsum = eng.timing_summary()
         if rank == 0:
             print("[bench-timing] " + json.dumps({k: round(v, 3) for k, v in tsum.items()}), file=sys.stderr,
+                  flush=True)
+    if args.checkpoint_dir and getattr(bench.engine, "shard_state", None) is not None:
+        from ps_amd.utils.checkpoint import CheckpointManager
+
+        tc = time.perf_counter()
+        ck = CheckpointManager(args.checkpoint_dir, rank=rank, world=world)
+        ck.save(args.warmup + args.steps, bench.engine, None, extra={"config": args.config}, blocking=True)
+        if rank == 0:
+            print(f"[bench-checkpoint] sharded save of step {args.warmup + args.steps} took "
+                  f"{time.perf_counter() - tc:.2f}s (committed={ck.latest() is not None})", file=sys.stderr,
                   flush=True)
     if args.profile_steps and rank == 0:
         from torch.profiler import ProfilerActivity, profile

@@ -29,6 +29,7 @@ def main(argv=None):
     ap.add_argument("--wide", action="store_true")
     ap.add_argument("--init-scale", type=float, default=1.0)
     ap.add_argument("--loss-surface", action="store_true")
+    ap.add_argument("--dump", default="", help="write final dense weights + probe rows (rank files) here")
     a, rest = ap.parse_known_args(argv)
     cfg = setup(rest)
     if maybe_run_server(cfg):
@@ -43,16 +44,23 @@ def main(argv=None):
         model = DNN.build_model(23, 10, 45, [150, 10, 1], gen=gen, init_scale=a.init_scale, table_factory=tables)
     model = model.to(dev)
     trainer = make_trainer(cfg, model, dev, conn)
+    start = trainer.resume()  # newest committed checkpoint of -Dcheckpoint_dir (0 = fresh start)
+    rank, world = (conn.rank, conn.world) if hasattr(conn, "world") else (0, 1)
     w0 = {n: p.detach().clone() for n, p in model.named_parameters()}
     test = synthetic_ctr(5000, wide_k=23 if a.wide else 0, seed=10 ** 6)
+    gstep = 0
     for epoch in range(a.epochs):
         if cfg.train:
-            ds = NativeBatchDataSet(cfg.train, "ctr", a.batch, dims=45, fields=23)
+            ds = NativeBatchDataSet(cfg.train, "ctr", a.batch, dims=45, fields=23, offset=rank, step=world)
             batches = iter(ds)
-        else:
-            batches = (synthetic_ctr(a.batch, wide_k=23 if a.wide else 0, seed=epoch * 100000 + i)
+        else:  # synthetic stream: global batch of step i, this rank trains its stride of it
+            batches = ({k: v[rank::world] for k, v in
+                        synthetic_ctr(a.batch, wide_k=23 if a.wide else 0, seed=epoch * 100000 + i).items()}
                        for i in range(a.steps_per_epoch))
         for b in batches:
+            gstep += 1
+            if gstep <= start:
+                continue  # already in the checkpoint
             if "W" not in b and a.wide:
                 b["W"] = b["E"] % 100000
             trainer.train([b])
@@ -62,6 +70,14 @@ def main(argv=None):
         print(f"epoch {epoch} test auc {auc:.4f}", flush=True)
         if a.loss_surface:
             LossSurface({k: v.to(dev) for k, v in test.items()}, model, w0).plot()
+    if trainer.ckpt is not None:
+        trainer.ckpt.wait()
+    if a.dump:
+        trainer.engine.synchronize()
+        probe = torch.arange(200).repeat(23, 1).t().contiguous()
+        rows = model.tables()["emF"].pull(probe.to(dev))
+        torch.save({"dense": {n: p.detach().cpu() for n, p in model.named_parameters()}, "rows": rows.cpu()},
+                   f"{a.dump}.rank{rank}")
 
 
 if __name__ == "__main__":

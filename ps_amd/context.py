@@ -57,6 +57,11 @@ class Context:
             self._step += 1
             return self._step
 
+    def set_step(self, v: int) -> None:
+        """Resume: continue the global step counter from a checkpoint."""
+        with self._lock:
+            self._step = int(v)
+
     # ------------------------------------------------------------- replica index
     @property
     def model_index(self) -> int:

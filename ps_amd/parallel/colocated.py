@@ -427,8 +427,10 @@ class ColocatedPS:
         self.synchronize()
         return {
             "rank": self.rank, "world": self.world, "round": self.round, "staleness": self.staleness,
-            "master": [m.detach().cpu() for m in self.master],
-            "states": [[[s.detach().cpu() for s in st] for st in sts] for sts in self.states],
+            # host SNAPSHOTS (to(copy=True): on a CPU run .cpu() would alias the live shard
+            # while a background checkpoint writer is still serialising it)
+            "master": [_snap(m) for m in self.master],
+            "states": [[[_snap(s) for s in st] for st in sts] for sts in self.states],
             "manifest": {k: {"shape": list(ki.shape), "dtype": str(ki.dtype), "bucket": ki.bucket,
                              "offset": ki.offset, "group": ki.group,
                              "layout": "channels_last" if k in self.cl_keys else "contiguous"}
@@ -466,6 +468,10 @@ class ColocatedPS:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+def _snap(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to("cpu", copy=True)
 
 
 def _wants_channels_last(p: torch.Tensor) -> bool:

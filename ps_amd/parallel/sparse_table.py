@@ -189,10 +189,10 @@ class RowShard:
             raise RuntimeError(f"sparse table shard full ({self.capacity} slots) or bad key")
 
     def state_dict(self) -> dict:
-        d = {"table": self.table.detach().cpu(), "flags": self.flags.detach().cpu(),
-             "states": [s.detach().cpu() for s in self.states]}
+        snap = lambda t: t.detach().to("cpu", copy=True)  # noqa: E731 -- never alias live CPU state
+        d = {"table": snap(self.table), "flags": snap(self.flags), "states": [snap(s) for s in self.states]}
         if self.hkeys is not None:
-            d["hkeys"] = self.hkeys.detach().cpu()
+            d["hkeys"] = snap(self.hkeys)
         if self.idmap is not None:
             d["idmap"] = self.idmap.items()
         return d

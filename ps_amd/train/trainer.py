@@ -15,6 +15,11 @@ ONE parameter-server round.  Engines:
 ``Trainer.train(batches)`` returns the mean loss; failures of a replica are counted as the
 reference does (loss 0 + log) only when ``tolerate_failures`` is set -- by default they
 raise.  Per-step timings (fwd+bwd, push/update, exposed wait) go to the metrics stream.
+
+Checkpoint / resume: with ``checkpoint_dir`` every ``checkpoint_every`` rounds
+each rank writes its server shard (dense master + optimizer state, sparse rows + id map) and
+the step counter (utils/checkpoint.py, committed once all ranks are on disk); ``resume()``
+restores the newest committed step.  The TCP topology asks the servers to save instead.
 """
 from __future__ import annotations
 
@@ -91,13 +96,50 @@ class KVEngine:
 
 
 class Trainer:
-    def __init__(self, model, engine=None, n_threads: int = 1, device=None, tolerate_failures: bool = False):
+    def __init__(self, model, engine=None, n_threads: int = 1, device=None, tolerate_failures: bool = False,
+                 checkpoint_dir: str = "", checkpoint_every: int = 0):
         self.model = model
         self.engine = engine or KVEngine(model)
         self.n_threads = max(1, int(n_threads))
         self.device = device
         self.tolerate_failures = tolerate_failures
         self.last_timing: Dict[str, float] = {}
+        self.ckpt = None
+        self.checkpoint_every = int(checkpoint_every)
+        if checkpoint_dir:
+            from ..utils.checkpoint import CheckpointManager
+
+            t = getattr(self.engine, "t", None)
+            rank, world = (t.rank, t.world) if t is not None else (0, 1)
+            self.ckpt = CheckpointManager(checkpoint_dir, rank=rank, world=world)
+
+    # ------------------------------------------------------------------ checkpoint
+    def _tables(self) -> dict:
+        return self.model.tables() if hasattr(self.model, "tables") else {}
+
+    def save(self, step: int, extra: Optional[dict] = None, blocking: bool = False) -> None:
+        if self.ckpt is None:
+            return
+        if isinstance(self.engine, KVEngine):
+            if self.engine.kv.client is not None and self.engine.kv.worker_id == 0:
+                import os
+
+                d = os.path.join(self.ckpt.dir, f"tcp_step{step:08d}")
+                os.makedirs(d, exist_ok=True)
+                self.engine.kv.client.save(os.path.join(d, "server"))
+            return
+        self.engine.synchronize()
+        self.ckpt.save(step, getattr(self.engine, "ps", None), self._tables(), extra={"step": step, **(extra or {})},
+                       blocking=blocking)
+
+    def resume(self) -> int:
+        """Restore the newest committed checkpoint (if any); returns the step to continue from."""
+        if self.ckpt is None or isinstance(self.engine, KVEngine) or self.ckpt.latest() is None:
+            return 0
+        st = self.ckpt.load(None, getattr(self.engine, "ps", None), self._tables())
+        step = int(st.get("extra", {}).get("step", st["step"]))
+        ctx.set_step(step)
+        return step
 
     def _dev(self, b):
         return _to(b, self.device) if self.device is not None else b
@@ -130,6 +172,8 @@ class Trainer:
         _metrics.plot("loss", loss, step)
         self.last_timing = {"fwd_bwd_ms": (t1 - t0) * 1e3, "ps_round_ms": (t2 - t1) * 1e3}
         _metrics.log_step(step=step, loss=loss, **self.last_timing)
+        if self.ckpt is not None and self.checkpoint_every and step % self.checkpoint_every == 0:
+            self.save(step)
         return loss
 
     def predict(self, batches: Sequence[Dict[str, torch.Tensor]]) -> List[torch.Tensor]:

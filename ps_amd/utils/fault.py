@@ -2,12 +2,16 @@
 hangs its barrier forever, net/PServer.java:251-258).
 
 * ``Heartbeat``: every rank bumps ``hb/<rank>`` in the c10d TCPStore every ``period`` s on
-  a daemon thread; ``Watchdog`` (rank 0) scans them and, when a rank has been silent for
+  a daemon thread; ``Watchdog`` (every rank) scans them and, when a rank has been silent for
   ``timeout`` s, records the failure and invokes ``on_failure`` (default: abort the process
-  group so every rank's pending collectives error out instead of hanging).  Recovery is
-  restart-from-checkpoint with the same world size (utils/checkpoint.py).
+  group and EXIT the process with ``EXIT_PEER_LOST`` so a rank blocked in a collective with a
+  dead peer does not hang).  ``start_failure_detection`` wires both from ``Config.heartbeat_s``.
+* Recovery = restart every rank from the last committed checkpoint with the same world size:
+  ``python -m ps_amd.launch --nproc N --max-restarts R -- <cmd>`` (ps_amd/launch.py) restarts
+  the whole job when a rank dies; apps resume from ``Config.checkpoint_dir``.
 * Fault injection from ``PS_AMD_FAULT`` (or Config.fault), e.g.
-    ``kill:rank=1:step=5``      rank 1 exits hard at step 5
+    ``kill:rank=1:step=5``      rank 1 exits hard at step 5 (first attempt only; ``attempt=k``
+                                to fire on the k-th restart -- PS_AMD_RESTART is set by launch.py)
     ``delay_push:ms=50``        sleep before every push (staleness tests)
     ``drop_push:p=0.01``        drop a fraction of ASP pushes (TCP topology only)
   ``FaultInjector.at_step(step)`` / ``before_push()`` / ``drop()`` are called by trainers.
@@ -42,7 +46,9 @@ class FaultInjector:
 
     def at_step(self, step: int) -> None:
         k = self.spec.get("kill")
-        if k and int(k.get("rank", -1)) == self.rank and int(k.get("step", -1)) == step:
+        attempt = int(os.environ.get("PS_AMD_RESTART", "0"))
+        if (k and int(k.get("rank", -1)) == self.rank and int(k.get("step", -1)) == step
+                and int(k.get("attempt", 0)) == attempt):
             os._exit(int(k.get("code", 17)))
 
     def before_push(self) -> None:
@@ -53,6 +59,9 @@ class FaultInjector:
     def drop(self) -> bool:
         d = self.spec.get("drop_push")
         return bool(d) and self.rng.random() < float(d.get("p", 0))
+
+
+EXIT_PEER_LOST = 75  # a peer rank stopped heart-beating: the job must restart from a checkpoint
 
 
 class Heartbeat:
@@ -90,13 +99,19 @@ class Watchdog:
 
     @staticmethod
     def _abort(rank: int, silent_s: float) -> None:
+        import sys
+
         import torch.distributed as dist
 
+        sys.stderr.write(f"[ps_amd watchdog] rank {rank} silent for {silent_s:.1f}s: aborting (exit "
+                         f"{EXIT_PEER_LOST})\n")
+        sys.stderr.flush()
         if dist.is_initialized():
             try:
                 dist.destroy_process_group()
             except Exception:
                 pass
+        os._exit(EXIT_PEER_LOST)
 
     def start(self) -> "Watchdog":
         self.t.start()
@@ -107,6 +122,8 @@ class Watchdog:
         out = {}
         for r in range(self.world):
             try:
+                if not self.store.check([f"hb/{r}"]):  # get() would block on a missing key
+                    continue
                 last = float(self.store.get(f"hb/{r}").decode())
             except Exception:
                 continue
@@ -124,3 +141,21 @@ class Watchdog:
 
     def stop(self):
         self._stop.set()
+
+
+def start_failure_detection(heartbeat_s: float, rank: int, world: int, store=None):
+    """Heartbeat on every rank + a watchdog on every rank (timeout = 5 periods, min 5 s) over
+    the default c10d store; returns (heartbeat, watchdog) or None when disabled / world 1."""
+    if not heartbeat_s or heartbeat_s <= 0 or world <= 1:
+        return None
+    if store is None:
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            return None
+        from torch.distributed import distributed_c10d
+
+        store = distributed_c10d._get_default_store()
+    hb = Heartbeat(store, rank, heartbeat_s).start()
+    wd = Watchdog(store, world, timeout=max(5.0, 5 * heartbeat_s), period=heartbeat_s).start()
+    return hb, wd
