@@ -219,6 +219,8 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if getattr(bench.engine, "close", None) is not None:
+        bench.engine.close()  # stops async-PS progress threads before the process tears down
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -4,6 +4,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <memory>
+#include <thread>
+
+#include "async_ctl.h"
 #include "loader.h"
 #include "ps_server.h"
 
@@ -295,6 +299,70 @@ py::object batch_to_dict(Batch& b, int dims, int fields) {
   return d;
 }
 
+// ------------------------------------------------------------------ async PS (control + CPU server)
+psasync::AsyncCtl* ctl_at(uintptr_t addr) { return reinterpret_cast<psasync::AsyncCtl*>(addr); }
+
+// Owner progress thread of the asynchronous PS for CPU (fp32) shards: the same serve_loop as
+// the GPU server (csrc/async_ps_gpu.cpp) with the CPU updaters of the TCP server.
+class CpuAsyncServer {
+ public:
+  CpuAsyncServer(uintptr_t ctl, int me, const std::string& spec, int64_t n, uintptr_t master,
+                 std::vector<uintptr_t> mbox, std::vector<uintptr_t> pub, double gscale)
+      : ctl_(ctl_at(ctl)), me_(me), n_(n), master_(reinterpret_cast<float*>(master)), gscale_(gscale) {
+    upd_ = make_updater(spec);
+    for (auto p : mbox) mbox_.push_back(reinterpret_cast<const float*>(p));
+    for (auto p : pub) pub_.push_back(reinterpret_cast<float*>(p));
+    states_.assign(static_cast<size_t>(upd_->n_state()), std::vector<float>(static_cast<size_t>(n), 0.f));
+    tmp_.resize(static_cast<size_t>(n));
+  }
+  ~CpuAsyncServer() { stop(); }
+  void start() {
+    stop_ = false;
+    th_ = std::thread([this] {
+      psasync::serve_loop(ctl_, me_, &stop_, [this](int w, int slot, int64_t step) {
+        const float* g = mbox_[static_cast<size_t>(w)];
+        for (int64_t i = 0; i < n_; ++i) tmp_[static_cast<size_t>(i)] = g[i] * static_cast<float>(gscale_);
+        upd_->update(master_, tmp_.data(), static_cast<size_t>(n_), states_, static_cast<long>(step));
+        std::memcpy(pub_[static_cast<size_t>(slot)], master_, static_cast<size_t>(n_) * sizeof(float));
+        applied_ += 1;
+      });
+    });
+  }
+  void stop() {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  int64_t applied() const { return applied_; }
+  py::list states() {
+    py::list out;
+    for (auto& v : states_) {
+      py::array_t<float> a(static_cast<py::ssize_t>(v.size()));
+      std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+      out.append(a);
+    }
+    return out;
+  }
+  void set_states(const std::vector<F32>& st) {
+    for (size_t i = 0; i < st.size() && i < states_.size(); ++i)
+      std::memcpy(states_[i].data(), st[i].data(), std::min<size_t>(states_[i].size(), st[i].size()) * 4);
+  }
+
+ private:
+  psasync::AsyncCtl* ctl_;
+  int me_;
+  int64_t n_;
+  float* master_;
+  double gscale_;
+  std::unique_ptr<Updater> upd_;
+  std::vector<const float*> mbox_;
+  std::vector<float*> pub_;
+  std::vector<std::vector<float>> states_;
+  std::vector<float> tmp_;
+  volatile bool stop_ = true;
+  std::thread th_;
+  int64_t applied_ = 0;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -333,6 +401,74 @@ PYBIND11_MODULE(_native, m) {
       .def("shutdown", &Client::shutdown)
       .def_property_readonly("bytes_sent", &Client::bytes_sent)
       .def_property_readonly("bytes_recv", &Client::bytes_recv);
+
+  // async-PS control block operations (blocking ones release the GIL); ``addr`` is the address
+  // of a psasync::AsyncCtl in shared memory (see csrc/include/async_ctl.h)
+  auto a = m.def_submodule("async_ctl", "asynchronous parameter-server control block");
+  a.attr("SIZE") = sizeof(psasync::AsyncCtl);
+  a.attr("MAX_WORLD") = psasync::kMaxW;
+  a.attr("SLOTS") = psasync::kSlots;
+  a.def("init", [](uintptr_t addr, int64_t world) {
+    if (world < 1 || world > psasync::kMaxW) throw std::runtime_error("async PS world out of range");
+    psasync::init(ctl_at(addr), world);
+  });
+  a.def("valid", [](uintptr_t addr) { return psasync::ld(&ctl_at(addr)->magic) == psasync::kMagic; });
+  a.def("wait_free", [](uintptr_t addr, int o, int w, double timeout_s) {
+    auto* c = ctl_at(addr);
+    const auto t0 = std::chrono::steady_clock::now();
+    psasync::Backoff bo;
+    while (psasync::ld(&c->ack[o][w]) < psasync::ld(&c->seq[o][w])) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        throw std::runtime_error("async PS: owner did not drain the mailbox in time (dead server?)");
+      bo();
+    }
+  }, py::call_guard<py::gil_scoped_release>());
+  a.def("bump_seq", [](uintptr_t addr, int o, int w) { return psasync::add(&ctl_at(addr)->seq[o][w], 1); });
+  a.def("bump_clock", [](uintptr_t addr, int w) { return psasync::add(&ctl_at(addr)->clock[w], 1); });
+  a.def("wait_min_ack", [](uintptr_t addr, int64_t target, double timeout_s) {
+    auto* c = ctl_at(addr);
+    const auto t0 = std::chrono::steady_clock::now();
+    psasync::Backoff bo;
+    while (psasync::min_ack(c) < target) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        throw std::runtime_error("async PS: staleness gate timed out (dead worker?)");
+      bo();
+    }
+  }, py::call_guard<py::gil_scoped_release>());
+  a.def("pin", [](uintptr_t addr, int o) { return psasync::pin(ctl_at(addr), o); },
+        py::call_guard<py::gil_scoped_release>());
+  a.def("unpin", [](uintptr_t addr, int o, int s) { psasync::unpin(ctl_at(addr), o, s); });
+  a.def("set_stop", [](uintptr_t addr, int64_t v) { psasync::st(&ctl_at(addr)->stop, v); });
+  a.def("snapshot", [](uintptr_t addr) {
+    auto* c = ctl_at(addr);
+    const int W = static_cast<int>(c->world);
+    py::dict d;
+    py::list clock, version, seq, ack;
+    for (int i = 0; i < W; ++i) {
+      clock.append(psasync::ld(&c->clock[i]));
+      version.append(psasync::ld(&c->version[i]));
+      py::list sr, ar;
+      for (int j = 0; j < W; ++j) {
+        sr.append(psasync::ld(&c->seq[i][j]));
+        ar.append(psasync::ld(&c->ack[i][j]));
+      }
+      seq.append(sr);
+      ack.append(ar);
+    }
+    d["clock"] = clock;
+    d["version"] = version;
+    d["seq"] = seq;
+    d["ack"] = ack;
+    return d;
+  });
+  py::class_<CpuAsyncServer>(m, "CpuAsyncServer")
+      .def(py::init<uintptr_t, int, const std::string&, int64_t, uintptr_t, std::vector<uintptr_t>,
+                    std::vector<uintptr_t>, double>())
+      .def("start", &CpuAsyncServer::start)
+      .def("stop", &CpuAsyncServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("applied", &CpuAsyncServer::applied)
+      .def("states", &CpuAsyncServer::states)
+      .def("set_states", &CpuAsyncServer::set_states);
 
   py::class_<IdMap>(m, "IdMap")
       .def(py::init<int64_t>())

@@ -98,9 +98,10 @@ def _write_ninja() -> Path:
         o = BUILD / (s.stem + ".hip.o")
         objs.append(o)
         lines.append(f"build {o}: hip {s}")
-    bo = BUILD / "bindings.o"
-    lines.append(f"build {bo}: bind {ROOT / 'csrc' / 'bindings.cpp'}")
-    objs.append(bo)
+    for src in sorted((ROOT / "csrc").glob("*.cpp")):  # bindings.cpp + host-side GPU runtime (async PS)
+        bo = BUILD / (src.stem + ".o")
+        lines.append(f"build {bo}: bind {src}")
+        objs.append(bo)
     out_c = PKG / f"_C{ext}"
     lines.append(f"build {out_c}: link " + " ".join(str(o) for o in objs))
     targets = [str(out_c)]

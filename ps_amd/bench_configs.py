@@ -77,8 +77,14 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
     model = BertForMLM().to(dev).to(torch.bfloat16)
     upd = AdamUpdater(1e-4, 0.9, 0.999, 1e-6, bias_correction="step", weight_decay=0.01, adamw=True)
     stale = 1 if args.staleness == 0 else args.staleness
-    ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
-                     staleness=stale, clip_norm=None)
+    use_async = os.environ.get("PS_AMD_BERT_ASYNC", "1") == "1"
+    if use_async:  # one-sided pushes into owner mailboxes + native progress threads (async_ps.py)
+        from .parallel.async_ps import AsyncPS
+
+        ps = AsyncPS(model, upd, tp, staleness=stale)
+    else:  # pipelined collective rounds (the bound enforced by the collective itself)
+        ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
+                         staleness=stale, clip_norm=None)
     B, S = args.batch_per_gpu, args.seq_len
     pool = [mlm_batch(B, S, seed=tp.rank * 1000 + i, device=dev, with_positions=True) for i in range(POOL)]
     it = _cycle(pool)
@@ -92,7 +98,8 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
 
     return Bench(step, B, "sequences/sec (whole node) BERT-base MLM async bounded-staleness s=1", "sequences/s",
                  {"model": "BERT-base", "global_batch": B * tp.world, "seq_len": S,
-                  "parallelism": f"ps-ssp{stale}-colocated-dp{tp.world}", "optimizer": upd.name}, ps)
+                  "parallelism": f"ps-ssp{stale}-{'async' if use_async else 'pipelined'}-dp{tp.world}",
+                  "optimizer": upd.name}, ps)
 
 
 def setup_dlrm(args, tp, dev) -> Bench:

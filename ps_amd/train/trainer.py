@@ -45,12 +45,24 @@ def _to(batch: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
 class CollectiveEngine:
     def __init__(self, model, transport: Optional[Transport] = None, *, bucket_mb: float = 25.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
-                 overlap: bool = True):
+                 overlap: bool = True, consistency: str = "bsp"):
+        """``consistency``: "bsp" (collective rounds; ``staleness`` > 0 pipelines them with the
+        bound enforced by the collective), "ssp" / "asp" (parallel/async_ps.py: one-sided pushes
+        into owner mailboxes, native progress threads, SSP(staleness) gate or none)."""
         self.model = model
         self.t = transport or Transport()
         dense = [p for p in model.parameters() if p.requires_grad]
-        self.ps = ColocatedPS(model, model.get_updater(), self.t, bucket_mb=bucket_mb, staleness=staleness,
-                              clip_norm=clip_norm, compress=compress, overlap=overlap) if dense else None
+        self.consistency = consistency
+        if not dense:
+            self.ps = None
+        elif consistency in ("ssp", "asp"):
+            from ..parallel.async_ps import AsyncPS
+
+            self.ps = AsyncPS(model, model.get_updater(), self.t,
+                              staleness=None if consistency == "asp" else int(staleness))
+        else:
+            self.ps = ColocatedPS(model, model.get_updater(), self.t, bucket_mb=bucket_mb, staleness=staleness,
+                                  clip_norm=clip_norm, compress=compress, overlap=overlap)
 
     def accumulate(self, on: bool) -> None:
         if self.ps is not None:

@@ -1,0 +1,101 @@
+"""Asynchronous parameter server (ASP / SSP without lockstep collectives) on CPU.
+
+Reference: async pushes are applied on arrival and the barrier returns at once
+(net/PServer.java:176-184, 242-248).  Checked: SSP(0) with SGD equals synchronous data
+parallelism exactly (W sequential updates of g_w / W == one averaged step); with a straggler the
+fast worker's clock leads by at most s + 1 under SSP(s) and runs away under ASP; ASP still
+converges.  Thread-ranks (loopback) and real processes (gloo + POSIX shared memory, native
+progress threads) both run."""
+import time
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ps_amd.parallel.transport import run_loopback
+
+from . import dist_util
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(10, 24), torch.nn.Tanh(), torch.nn.Linear(24, 3))
+
+
+def _data(n=48):
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(n, 10, generator=g), torch.randint(0, 3, (n,), generator=g)
+
+
+def _body(tp, staleness, steps, lr, delay_rank=-1, delay_s=0.0, models=None):
+    from ps_amd.parallel.async_ps import AsyncPS
+    from ps_amd.parallel.updaters import SimpleUpdater
+
+    m = models[tp.rank] if models is not None else _model(0)  # thread-ranks: built outside (global RNG)
+    ps = AsyncPS(m, SimpleUpdater(lr), tp, staleness=staleness)
+    x, y = _data()
+    xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
+    leads, losses = [], []
+    for _ in range(steps):
+        if tp.rank == delay_rank:
+            time.sleep(delay_s)
+        loss = F.cross_entropy(m(xs), ys)
+        loss.backward()
+        ps.finish_step()
+        losses.append(loss.item())
+        c = ps.snapshot()["clock"]
+        leads.append(c[tp.rank] - min(c))
+    ps.synchronize()
+    tp.barrier()
+    ps.refresh()  # every rank's pushes are applied: all replicas read the same final version
+    out = {n: p.detach().clone() for n, p in m.named_parameters()}
+    ps.close()
+    return out, leads, losses
+
+
+def _oracle(world, steps, lr):
+    ref = _model(0)
+    opt = torch.optim.SGD(ref.parameters(), lr=lr)
+    x, y = _data()
+    for _ in range(steps):
+        opt.zero_grad()
+        (sum(F.cross_entropy(ref(x[r::world]), y[r::world]) for r in range(world)) / world).backward()
+        opt.step()
+    return {n: p.detach() for n, p in ref.named_parameters()}
+
+
+def test_single_worker_is_plain_sgd():
+    res = run_loopback(_body, 1, 0, 5, 0.2, -1, 0.0, [_model(0)])
+    for k, v in _oracle(1, 5, 0.2).items():
+        torch.testing.assert_close(res[0][0][k], v, rtol=1e-6, atol=1e-7)
+
+
+def _close_to_sync(res, world, steps, lr):
+    # SSP(0) reads AT LEAST every update of the previous clock (it may also see a faster
+    # worker's newer push), so it tracks synchronous SGD closely but not bitwise
+    ref = _oracle(world, steps, lr)
+    for r in range(world):
+        for k, v in ref.items():
+            assert torch.equal(res[r][0][k], res[0][0][k])  # identical replicas at the end
+            torch.testing.assert_close(res[r][0][k], v, rtol=0, atol=5e-3)
+
+
+def test_ssp0_threads_tracks_sync_sgd():
+    _close_to_sync(run_loopback(_body, 3, 0, 5, 0.2, -1, 0.0, [_model(0) for _ in range(3)]), 3, 5, 0.2)
+
+
+def test_ssp0_processes_tracks_sync_sgd():
+    _close_to_sync(dist_util.run(_body, 2, (0, 6, 0.2)), 2, 6, 0.2)
+
+
+@pytest.mark.parametrize("s", [1, 2])
+def test_ssp_bound_with_straggler(s):
+    res = dist_util.run(_body, 2, (s, 12, 0.1, 1, 0.05))
+    assert max(res[0][1]) <= s + 1, res[0][1]  # the fast rank never runs further ahead
+    assert max(res[0][1]) >= s  # ... but it does use the slack
+
+
+def test_asp_runs_ahead_and_converges():
+    res = dist_util.run(_body, 2, (None, 20, 0.1, 1, 0.05))
+    assert max(res[0][1]) > 3, res[0][1]  # no bound: the fast worker runs away
+    assert res[0][2][-1] < res[0][2][0]
