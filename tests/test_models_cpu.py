@@ -20,26 +20,21 @@ MNIST = "/root/reference/src/main/resources/mnist_test.csv"
 
 
 @pytest.mark.skipif(not os.path.exists(MNIST), reason="reference MNIST fixture not mounted")
-def test_mnist_mlp_reference_config_learns():
-    """FullConnectedNN.buildModel(784, {150, 50, 10}), Adam 0.005 (reference constant bias
-    correction), batch 100 x 4 replicas.  Trained on 800 rows of the bundled CSV, evaluated on
-    the 200 held-out rows (README claims ~0.92 on the full training set; parity unpinned on
-    this 800-row subset, we require > 0.75)."""
-    d = load_reference_mnist(MNIST)
-    ctx.init()
-    torch.manual_seed(0)
-    gen = torch.Generator().manual_seed(0)
-    model = FullConnectedNN.build_model(784, [150, 50, 10], gen=gen)
-    tr = Trainer(model, CollectiveEngine(model), n_threads=4)
-    X, Y = d["X"][:800], d["Y"][:800]
-    for epoch in range(50):
-        perm = torch.randperm(800, generator=gen)
-        for i in range(0, 800, 400):
-            idx = perm[i:i + 400]
-            tr.train([{"X": X[idx[j:j + 100]], "Y": Y[idx[j:j + 100]]} for j in range(0, 400, 100)])
-    p = tr.predict([{"X": d["X"][800:]}])[0]
-    acc = SoftmaxPrecision(d["Y"][800:], p).calculate()
-    assert acc > 0.75, acc
+@pytest.mark.parametrize("kind,threshold", [("mlp", 0.86), ("cnn", 0.88)])
+def test_mnist_reference_config_quality(kind, threshold):
+    """The reference's MNIST models with the reference hyper-parameters (Adam 0.005 with the
+    constant bias correction, softmax T=10000 on RAW 0-255 pixels as MnistParser feeds them,
+    MLP 4 replicas x 100, CNN 1 x 100, early stop at loss <= 0.01) on the 800/200 split of the
+    bundled CSV.  Measured (docs/PARITY.md, scripts/mnist_parity.py): MLP 0.89-0.92, CNN
+    0.915-0.93 held-out over seeds 0-2; README claims ~0.92 / ~0.96 with the absent 60K
+    training file."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from mnist_parity import run
+
+    r = run(kind, 1, 100)
+    assert r["heldout_acc"] > threshold, r
 
 
 def test_cnn_reference_shapes_and_grad():
