@@ -62,6 +62,27 @@ __device__ __forceinline__ void store8(uint16_t* __restrict__ p, int64_t i, cons
   *reinterpret_cast<u16x8*>(p + i) = v;
 }
 
+// 4 consecutive elements as f32x4 (16 B of fp32 / 8 B of bf16); p + i must be aligned.
+__device__ __forceinline__ f32x4 load4(const float* __restrict__ p, int64_t i) {
+  return *reinterpret_cast<const f32x4*>(p + i);
+}
+__device__ __forceinline__ f32x4 load4(const uint16_t* __restrict__ p, int64_t i) {
+  const u16x4 v = *reinterpret_cast<const u16x4*>(p + i);
+  return f32x4{bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]), bf16_to_f32(v[3])};
+}
+__device__ __forceinline__ void store4(float* __restrict__ p, int64_t i, f32x4 v) {
+  *reinterpret_cast<f32x4*>(p + i) = v;
+}
+__device__ __forceinline__ void store4(uint16_t* __restrict__ p, int64_t i, f32x4 v) {
+  *reinterpret_cast<u16x4*>(p + i) = u16x4{f32_to_bf16(v.x), f32_to_bf16(v.y), f32_to_bf16(v.z), f32_to_bf16(v.w)};
+}
+
+// Sum over aligned groups of 2^lg lanes (every lane of the wave must execute this).
+__device__ __forceinline__ float group_sum(float v, int lg) {
+  for (int off = 1; off < (1 << lg); off <<= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
 // Wave64 sum via DPP-friendly xor shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -52,25 +52,46 @@ __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ 
   }
 }
 
+// 8 consecutive elements per thread (one byte of a packed word, one 16-B / 32-B output store):
+// a wave covers 512 elements = 8 words inside one 1024-element scale chunk, so per worker it
+// issues one 64-B coalesced word load and one broadcast scale load for 512 outputs.
 template <typename O>
 __global__ __launch_bounds__(256) void onebit_unpack_reduce_kernel(const uint64_t* __restrict__ words,
                                                                    const float* __restrict__ scales, int nworkers,
                                                                    int64_t n, int64_t wstride, int64_t sstride,
-                                                                   O* __restrict__ out, float mult, int accumulate) {
+                                                                   O* __restrict__ out, float mult, int accumulate,
+                                                                   int vec) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float acc = 0.f;
-    const int64_t wi = i >> 6;
-    const int bit = static_cast<int>(i & 63);
-    const int64_t si = i / kOnebitChunk;
+  const int64_t n8 = (n + 7) / 8;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    const int64_t i0 = t * 8;
+    const int64_t wi = i0 >> 6;
+    const int sh = static_cast<int>(i0 & 63);
+    const int64_t si = i0 / kOnebitChunk;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int w = 0; w < nworkers; ++w) {
-      const uint64_t word = words[w * wstride + wi];
+      const uint32_t byte = static_cast<uint32_t>(words[w * wstride + wi] >> sh) & 0xFFu;
       const float sc = scales[w * sstride + si];
-      acc += ((word >> bit) & 1ull) ? sc : -sc;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += ((byte >> k) & 1u) ? sc : -sc;
     }
-    acc *= mult;
-    if (accumulate) acc += Elem<O>::load(out, i);
-    Elem<O>::store(out, i, acc);
+    if (vec && i0 + 8 <= n) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] *= mult;
+      if (accumulate) {
+        float o[8];
+        load8(out, i0, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += o[k];
+      }
+      store8(out, i0, acc);
+    } else {
+      for (int k = 0; k < 8 && i0 + k < n; ++k) {
+        float v = acc[k] * mult;
+        if (accumulate) v += Elem<O>::load(out, i0 + k);
+        Elem<O>::store(out, i0 + k, v);
+      }
+    }
   }
 }
 
@@ -90,13 +111,15 @@ void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int
                                  int64_t words_stride, int64_t scales_stride, void* out, int odtype, float mult,
                                  int accumulate, hipStream_t s) {
   if (n <= 0) return;
-  const int grid = stream_grid(n, 256);
+  // 8-element vector stores need a 16-B aligned destination (else element stores)
+  const int vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const int grid = stream_grid((n + 7) / 8, 256);
   if (odtype == 1)
     hipLaunchKernelGGL(onebit_unpack_reduce_kernel<uint16_t>, dim3(grid), dim3(256), 0, s, words, scales, nworkers, n,
-                       words_stride, scales_stride, static_cast<uint16_t*>(out), mult, accumulate);
+                       words_stride, scales_stride, static_cast<uint16_t*>(out), mult, accumulate, vec);
   else
     hipLaunchKernelGGL(onebit_unpack_reduce_kernel<float>, dim3(grid), dim3(256), 0, s, words, scales, nworkers, n,
-                       words_stride, scales_stride, static_cast<float*>(out), mult, accumulate);
+                       words_stride, scales_stride, static_cast<float*>(out), mult, accumulate, vec);
 }
 
 }  // namespace psamd

@@ -269,6 +269,73 @@ __global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ tab
   }
 }
 
+// Vectorised form for dim = 4 * 2^k <= 256: 2^lg lanes share a row, each lane owns 4 adjacent
+// elements (16-B loads / stores), a wave updates 64 >> lg rows at once and a run's summed
+// gradient stays in registers (one pass over the pushed rows, none re-read).
+template <int KIND, typename G>
+__global__ __launch_bounds__(256) void sparse_opt_vec_kernel(float* __restrict__ table, float* __restrict__ st0,
+                                                              float* __restrict__ st1, const int64_t* __restrict__ rows,
+                                                              const int64_t* __restrict__ perm,
+                                                              const G* __restrict__ grad, int64_t nrows, int dim,
+                                                              int lg, OptParams p, int rowwise) {
+  float scale = p.gscale;
+  if (p.gscale_ptr) scale *= *p.gscale_ptr;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> lg;                  // row slot within the wave
+  const int c = (lane & ((1 << lg) - 1)) * 4;  // first element of this lane
+  const int per_wave = 64 >> lg;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * blockDim.x / 64;
+  for (int64_t rb = wave * per_wave; rb < nrows; rb += nwaves * per_wave) {  // wave-uniform loop
+    const int64_t r = rb + sub;
+    int64_t row = r < nrows ? rows[r] : -1;
+    if (row >= 0 && perm != nullptr && r > 0 && rows[r - 1] == row) row = -1;  // not a run head
+    f32x4 g = {0.f, 0.f, 0.f, 0.f};
+    if (row >= 0) {
+      if (perm == nullptr) {
+        g = load4(grad, r * dim + c);
+      } else {
+        for (int64_t j = r; j < nrows && rows[j] == row; ++j) g += load4(grad, perm[j] * dim + c);
+      }
+      g *= scale;
+    }
+    if (KIND == kAdagrad && rowwise) {
+      const float ss = group_sum(g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w, lg) / static_cast<float>(dim);
+      if (row < 0) continue;
+      const float h = st0[row] + ss;
+      if (c == 0) st0[row] = h;
+      const float k = p.lr / (sqrtf(h) + p.eps);
+      f32x4 w = load4(table, row * dim + c);
+      w -= k * g;
+      store4(table, row * dim + c, w);
+    } else {
+      // skip_zero (FtrlUpdater.java:52-54): the row's first gradient element, from its lane 0
+      const float g0 = __shfl(g.x, lane & ~((1 << lg) - 1), kWave);
+      if (row < 0 || (p.skip_zero && g0 == 0.f)) continue;
+      const int64_t o = row * dim + c;
+      f32x4 w = load4(table, o);
+      f32x4 a = st0 ? load4(st0, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 b = st1 ? load4(st1, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      float wv[4] = {w.x, w.y, w.z, w.w}, av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+      const float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) opt_apply<KIND>(wv[k], gv[k], av[k], bv[k], p);
+      store4(table, o, f32x4{wv[0], wv[1], wv[2], wv[3]});
+      if (st0) store4(st0, o, f32x4{av[0], av[1], av[2], av[3]});
+      if (st1) store4(st1, o, f32x4{bv[0], bv[1], bv[2], bv[3]});
+    }
+  }
+}
+
+static int vec_lanes_log2(int dim) {  // lanes per row for the vectorised kernels, -1 = scalar path
+  if (dim % 4 != 0 || dim > 256) return -1;
+  const int l = dim / 4;
+  if ((l & (l - 1)) != 0) return -1;
+  int lg = 0;
+  while ((1 << lg) < l) ++lg;
+  return lg;
+}
+
 void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
   if (a.nrows <= 0) return;
   OptParams p;
@@ -277,6 +344,29 @@ void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
   p.bc1 = a.bc1; p.bc2 = a.bc2; p.l1 = a.l1; p.l2 = a.l2; p.fbeta = a.fbeta; p.ftrl_mode = a.ftrl_mode;
   p.skip_zero = a.skip_zero; p.gscale = a.gscale; p.gscale_ptr = nullptr;
   const int block = 256;
+  const int lg = vec_lanes_log2(a.dim);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(a.table) | reinterpret_cast<uintptr_t>(a.st0) |
+                         reinterpret_cast<uintptr_t>(a.st1) | reinterpret_cast<uintptr_t>(a.grad)) & 15) == 0;
+  if (lg >= 0 && aligned) {
+    const int grid = stream_grid(((a.nrows << lg) + 63) / 64 * 64, block);
+#define PSAMD_SPARSE_VEC(K)                                                                                      \
+  if (a.g_bf16)                                                                                                  \
+    hipLaunchKernelGGL((sparse_opt_vec_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0,      \
+                       a.st1, a.rows, a.perm, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, lg, p,     \
+                       a.rowwise);                                                                               \
+  else                                                                                                           \
+    hipLaunchKernelGGL((sparse_opt_vec_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1, \
+                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, lg, p, a.rowwise);
+    switch (a.kind) {
+      case kSGD: PSAMD_SPARSE_VEC(kSGD); break;
+      case kAdam: PSAMD_SPARSE_VEC(kAdam); break;
+      case kAdagrad: PSAMD_SPARSE_VEC(kAdagrad); break;
+      case kFtrl: PSAMD_SPARSE_VEC(kFtrl); break;
+      default: break;
+    }
+#undef PSAMD_SPARSE_VEC
+    return;
+  }
   const int grid = stream_grid(a.nrows * 64, block);
 #define PSAMD_SPARSE_LAUNCH(K)                                                                                  \
   if (a.g_bf16)                                                                                                 \

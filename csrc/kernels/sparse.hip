@@ -118,9 +118,56 @@ __global__ __launch_bounds__(256) void segment_reduce_rows_kernel(const S* __res
   }
 }
 
+// vectorised: dim = 4 * 2^lg <= 256, 2^lg lanes per segment, 4 elements (16 B) per lane, the
+// segment's running sum in registers
+template <typename S, typename O>
+__global__ __launch_bounds__(256) void segment_reduce_rows_vec_kernel(const S* __restrict__ src,
+                                                                      const int64_t* __restrict__ perm,
+                                                                      const int64_t* __restrict__ seg_off,
+                                                                      int64_t nseg, int dim, int lg,
+                                                                      O* __restrict__ out, int mean) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> lg;
+  const int c = (lane & ((1 << lg) - 1)) * 4;
+  const int per_wave = 64 >> lg;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t ub = wave * per_wave; ub < nseg; ub += nwaves * per_wave) {
+    const int64_t u = ub + sub;
+    if (u >= nseg) continue;
+    const int64_t b = seg_off[u], e = seg_off[u + 1];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t j = b; j < e; ++j) acc += load4(src, perm[j] * dim + c);
+    if (mean) acc *= 1.f / static_cast<float>(e - b > 0 ? e - b : 1);
+    store4(out, u * dim + c, acc);
+  }
+}
+
+static int vec_lg(int dim) {
+  if (dim % 4 != 0 || dim > 256) return -1;
+  const int l = dim / 4;
+  if ((l & (l - 1)) != 0) return -1;
+  int lg = 0;
+  while ((1 << lg) < l) ++lg;
+  return lg;
+}
+
 void launch_segment_reduce_rows(const void* src, int sdtype, const int64_t* perm, const int64_t* seg_off,
                                 int64_t nseg, int dim, void* out, int odtype, int mean, hipStream_t s) {
   if (nseg <= 0) return;
+  const int lg = vec_lg(dim);
+  if (lg >= 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(out)) & 15) == 0) {
+    const int grid = stream_grid(((nseg << lg) + 63) / 64 * 64, 256);
+#define PSAMD_SV(S, O)                                                                                              \
+  hipLaunchKernelGGL((segment_reduce_rows_vec_kernel<S, O>), dim3(grid), dim3(256), 0, s, static_cast<const S*>(src), \
+                     perm, seg_off, nseg, dim, lg, static_cast<O*>(out), mean);
+    if (sdtype == 1 && odtype == 1) PSAMD_SV(uint16_t, uint16_t)
+    else if (sdtype == 1) PSAMD_SV(uint16_t, float)
+    else if (odtype == 1) PSAMD_SV(float, uint16_t)
+    else PSAMD_SV(float, float)
+#undef PSAMD_SV
+    return;
+  }
   const int grid = stream_grid(nseg * 64, 256);
 #define PSAMD_S(S, O)                                                                                           \
   hipLaunchKernelGGL((segment_reduce_rows_kernel<S, O>), dim3(grid), dim3(256), 0, s, static_cast<const S*>(src), \
@@ -225,14 +272,22 @@ __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__
   const int lane = threadIdx.x & 63;
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  const float span = hi - lo;
   for (int64_t r = wave; r < nrows; r += nwaves) {
     const int64_t row = rows[r];
     if (row < 0 || flags[row]) continue;  // wave-uniform
     const uint64_t grow = keys ? static_cast<uint64_t>(keys[r]) : static_cast<uint64_t>(row + row_base);
-    for (int c = lane; c < dim; c += 64) {
+    // one Philox call yields the 4 values of elements 4q .. 4q+3 (counter = key << 20 ^ q)
+    for (int q = lane; q * 4 < dim; q += 64) {
       uint32_t rnd[4];
-      Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(c), rnd);
-      table[row * dim + c] = lo + (hi - lo) * Philox::u01(rnd[0]);
+      Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(q), rnd);
+      float* dst = table + row * dim + q * 4;
+      if (q * 4 + 4 <= dim && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+        store4(dst, 0, f32x4{lo + span * Philox::u01(rnd[0]), lo + span * Philox::u01(rnd[1]),
+                             lo + span * Philox::u01(rnd[2]), lo + span * Philox::u01(rnd[3])});
+      } else {
+        for (int k = 0; k < 4 && q * 4 + k < dim; ++k) dst[k] = lo + span * Philox::u01(rnd[k]);
+      }
     }
     // rows may repeat inside one launch (several workers asked for the same row); flags is
     // written after the row so a duplicate wave either re-inits identically or skips.

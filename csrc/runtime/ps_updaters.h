@@ -130,7 +130,7 @@ class AdagradUpdater : public Updater {
 // Philox-4x32-10, bit-identical to psamd::Philox (csrc/include/psamd_device.h) and
 // ps_amd.ops.sparse.philox_u01: server-created rows get exactly the values the HIP lazy-init
 // kernel gives the same (seed, key) on the GPU path.
-inline float philox_u01(uint64_t seed, uint64_t ctr) {
+inline float philox_u01(uint64_t seed, uint64_t ctr, int word = 0) {
   uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), 0u, 0u};
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
   for (int r = 0; r < 10; ++r) {
@@ -143,7 +143,7 @@ inline float philox_u01(uint64_t seed, uint64_t ctr) {
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  return static_cast<float>(c[0] >> 8) * (1.0f / 16777216.0f);
+  return static_cast<float>(c[word & 3] >> 8) * (1.0f / 16777216.0f);
 }
 
 class FtrlUpdater : public Updater {

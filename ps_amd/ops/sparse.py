@@ -103,8 +103,8 @@ _M32 = 0xFFFFFFFF
 
 
 def philox_u01(seed: int, ctr: torch.Tensor) -> torch.Tensor:
-    """uniform [0, 1) from the first word of Philox-4x32-10(seed, ctr) -- bit-identical to
-    ``Philox::gen`` + ``u01`` in csrc/include/psamd_device.h (and the host copy in the native
+    """uniform [0, 1) from the 4 words of Philox-4x32-10(seed, ctr) -> [n, 4] -- bit-identical
+    to ``Philox::gen`` + ``u01`` in csrc/include/psamd_device.h (and the host copy in the native
     server), computed with int64 torch ops so the CPU oracle initialises rows exactly like the
     HIP kernel."""
     ctr = ctr.long()
@@ -120,14 +120,16 @@ def philox_u01(seed: int, ctr: torch.Tensor) -> torch.Tensor:
         c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
         k0 = (k0 + 0x9E3779B9) & _M32
         k1 = (k1 + 0xBB67AE85) & _M32
-    return (c0 >> 8).float() * (1.0 / 16777216.0)
+    return torch.stack([(c >> 8).float() * (1.0 / 16777216.0) for c in (c0, c1, c2, c3)], dim=-1)
 
 
 def init_values(seed: int, keys: torch.Tensor, dim: int, lo: float, hi: float) -> torch.Tensor:
-    """Deterministic first-touch values of rows ``keys`` ([n] int64 global keys) -> [n, dim]."""
-    c = torch.arange(dim, dtype=torch.int64, device=keys.device)
-    ctr = (keys.long()[:, None] << 20) ^ c[None, :]
-    return lo + (hi - lo) * philox_u01(seed, ctr.reshape(-1)).reshape(keys.numel(), dim)
+    """Deterministic first-touch values of rows ``keys`` ([n] int64 global keys) -> [n, dim]:
+    element c is word c % 4 of Philox(seed, key << 20 ^ c // 4) (one call per 4 elements)."""
+    q = torch.arange((dim + 3) // 4, dtype=torch.int64, device=keys.device)
+    ctr = (keys.long()[:, None] << 20) ^ q[None, :]
+    u = philox_u01(seed, ctr.reshape(-1)).reshape(keys.numel(), -1)[:, :dim]
+    return lo + (hi - lo) * u
 
 
 def lazy_init_rows(table: torch.Tensor, rows: torch.Tensor, flags: torch.Tensor, seed: int, row_base: int,
