@@ -82,7 +82,7 @@ def make_trainer(cfg: Config, model, device=None, conn=None) -> Trainer:
         tp = conn if conn is not None else (init_distributed(_backend(cfg)) if world > 1 else None)
         engine = CollectiveEngine(model, tp, bucket_mb=cfg.bucket_mb, staleness=cfg.staleness,
                                   clip_norm=cfg.clip_norm or None, compress=cfg.compress or None,
-                                  consistency=cfg.effective_consistency)
+                                  consistency=cfg.effective_consistency, compress_warmup=cfg.compress_warmup)
         if tp is not None:
             # heartbeat + watchdog on every rank (Config.heartbeat_s): a dead peer ends the job
             # with EXIT_PEER_LOST instead of a hang; ps_amd.launch then restarts it

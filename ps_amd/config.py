@@ -79,6 +79,7 @@ class Config:
     backend: str = "auto"  # auto | nccl | gloo | tcp
     bucket_mb: float = 25.0
     compress: str = ""  # "" | onebit
+    compress_warmup: int = 0  # full-precision PS rounds before the 1-bit push
     clip_norm: float = 0.0
     checkpoint_dir: str = ""
     checkpoint_every: int = 0

@@ -37,7 +37,8 @@ no gradient in a step are zero-filled at launch.
 
 Options: global-norm clipping (two-phase: push all, norm, then serve+pull), 1-bit
 compressed push with error feedback (compress="onebit": bits all-to-all to the owners +
-owner-side unpack-reduce kernel), arbitrary per-key-prefix updaters (resolve_updater).
+owner-side unpack-reduce kernel; ``compress_warmup`` full-precision rounds first),
+arbitrary per-key-prefix updaters (resolve_updater).
 """
 from __future__ import annotations
 
@@ -59,7 +60,8 @@ class ColocatedPS:
     def __init__(self, model: torch.nn.Module, updaters: Union[Updater, Dict[str, Updater]],
                  transport: Optional[Transport] = None, *, bucket_mb: float = 32.0, last_bucket_mb: float = 4.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
-                 average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False):
+                 average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
+                 compress_warmup: int = 0):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -72,6 +74,9 @@ class ColocatedPS:
         self.compress = compress
         if compress not in (None, "onebit"):
             raise ValueError(f"unknown compression {compress!r}")
+        # full-precision rounds before the 1-bit push takes over: the
+        # error-feedback state starts from zero at the switch
+        self.compress_warmup = int(compress_warmup)
         self.average = average
         self.overlap = overlap
         self.accumulating = False  # micro-batch accumulation: hooks stay quiet until the last one
@@ -304,7 +309,7 @@ class ColocatedPS:
         gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
         if self.world == 1:
             return
-        if self.compress == "onebit":
+        if self.compress == "onebit" and self.round >= self.compress_warmup:
             self._push_onebit(b, gin)
         else:
             self.t.reduce_scatter(self.gshard[b], gin)

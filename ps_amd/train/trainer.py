@@ -45,7 +45,7 @@ def _to(batch: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
 class CollectiveEngine:
     def __init__(self, model, transport: Optional[Transport] = None, *, bucket_mb: float = 25.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
-                 overlap: bool = True, consistency: str = "bsp"):
+                 overlap: bool = True, consistency: str = "bsp", compress_warmup: int = 0):
         """``consistency``: "bsp" (collective rounds; ``staleness`` > 0 pipelines them with the
         bound enforced by the collective), "ssp" / "asp" (parallel/async_ps.py: one-sided pushes
         into owner mailboxes, native progress threads, SSP(staleness) gate or none)."""
@@ -62,7 +62,8 @@ class CollectiveEngine:
                               staleness=None if consistency == "asp" else int(staleness))
         else:
             self.ps = ColocatedPS(model, model.get_updater(), self.t, bucket_mb=bucket_mb, staleness=staleness,
-                                  clip_norm=clip_norm, compress=compress, overlap=overlap)
+                                  clip_norm=clip_norm, compress=compress, overlap=overlap,
+                                  compress_warmup=compress_warmup)
 
     def accumulate(self, on: bool) -> None:
         if self.ps is not None:

@@ -98,3 +98,32 @@ def test_sharded_sparse_table_world2():
         torch.testing.assert_close(res[0][3], res[1][3])
         for ids, before, after, _ in res:
             assert (after < before).all()  # positive grads -> every touched row decreased
+
+
+def _warm_body(tp, warm):
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import SimpleUpdater
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(12, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    ps = ColocatedPS(m, SimpleUpdater(0.1), tp, bucket_mb=0.002, compress="onebit" if warm >= 0 else None,
+                     compress_warmup=max(0, warm))
+    g = torch.Generator().manual_seed(tp.rank)
+    x, y = torch.randn(32, 12, generator=g), torch.randint(0, 4, (32,), generator=g)
+    out = []
+    for _ in range(4):
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        ps.finish_step()
+        out.append({k: v.detach().clone() for k, v in m.named_parameters()})
+    return out
+
+
+def test_onebit_warmup_rounds_are_full_precision():
+    """compress_warmup=k: the first k rounds push full precision (identical to no
+    compression), later rounds are 1-bit (different)."""
+    full = dist_util.run(_warm_body, 2, (-1,))
+    warm = dist_util.run(_warm_body, 2, (2,))
+    for step in (0, 1):
+        for k in full[0][step]:
+            torch.testing.assert_close(warm[0][step][k], full[0][step][k], rtol=0, atol=0)
+    assert any(not torch.equal(warm[0][3][k], full[0][3][k]) for k in full[0][3])
