@@ -7,8 +7,9 @@ partition, push = RCCL reduce-scatter, server = fused HIP momentum-SGD on the fp
 shard, pull = RCCL all-gather, all overlapped with backward (ps_amd/parallel/colocated.py);
 BatchNorm+residual+ReLU run as fused HIP kernels (ps_amd/ops/bn.py).
 
-Weak scaling: ``--batch-per-gpu`` images per rank per step (default 512 -- sized for the
-288 GB HBM), synthetic ImageNet-shaped data resident on the GPU, random-init weights, bf16
+Weak scaling: ``--batch-per-gpu`` images per rank per step (default 1024 -- sized for the
+288 GB HBM: ~50 GB peak; measured 10.5K / 11.6K / 12.1K / 12.4K / 12.3K / 12.4K img/s at
+256 / 512 / 768 / 1024 / 1536 / 2048 per GPU, profiles/r2_resnet50_batch_sweep.txt), synthetic ImageNet-shaped data resident on the GPU, random-init weights, bf16
 compute (channels_last), full optimizer step inside the timed region.
 
 Other BASELINE configs: ``--config bert-ssp | dlrm | llama-onebit | mlp-tcp`` (see

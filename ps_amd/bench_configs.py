@@ -177,7 +177,7 @@ SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_
           "llama-onebit": setup_llama_onebit}
 
 DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not given
-    "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "512")), seq=0),
+    "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "1024")), seq=0),
     "bert-ssp": dict(batch=256, seq=128),
     "dlrm": dict(batch=16384, seq=0),
     "llama-onebit": dict(batch=1, seq=4096),
