@@ -318,6 +318,56 @@ void hash_slots(Tensor hkeys, Tensor ids, Tensor out, bool insert, Tensor status
                            out.data_ptr<int64_t>(), insert, status.data_ptr<int32_t>(), cur_stream(ids));
 }
 
+// ------------------------------------------------------------------------------ fused FC layer
+// dy, y [M, N]; x [M, K]; w [N, K]; all fp32 or all bf16, contiguous; outputs optional
+void fc_bwd(Tensor dy, Tensor y, Tensor x, Tensor w, c10::optional<Tensor> dw, c10::optional<Tensor> db,
+            c10::optional<Tensor> dx, int64_t act) {
+  for (auto* t : {&dy, &y, &x, &w}) check_gpu(*t, "fc_bwd operand");
+  const int code = dcode(dy, "dy");
+  TORCH_CHECK(dcode(y, "y") == code && dcode(x, "x") == code && dcode(w, "w") == code, "fc_bwd: one dtype");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && w.dim() == 2 && y.sizes() == dy.sizes(), "fc_bwd: 2-D operands");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M && w.size(0) == N && w.size(1) == K, "fc_bwd: shape mismatch");
+  void* pdw = nullptr;
+  void* pdx = nullptr;
+  float* pdb = nullptr;
+  if (dw.has_value() && dw->defined()) {
+    check_gpu(*dw, "dw");
+    TORCH_CHECK(dcode(*dw, "dw") == code && dw->numel() == N * K, "dw [N, K]");
+    pdw = dw->data_ptr();
+  }
+  if (db.has_value() && db->defined()) {
+    check_f32(*db, "db");
+    TORCH_CHECK(db->numel() == N && pdw != nullptr, "db [N] (computed with dW)");
+    pdb = db->data_ptr<float>();
+  }
+  if (dx.has_value() && dx->defined()) {
+    check_gpu(*dx, "dx");
+    TORCH_CHECK(dcode(*dx, "dx") == code && dx->numel() == M * K, "dx [M, K]");
+    pdx = dx->data_ptr();
+  }
+  const c10::DeviceGuard guard(dy.device());
+  psamd::launch_fc_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), w.data_ptr(), pdw, pdb, pdx, code,
+                       static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(act),
+                       cur_stream(dy));
+}
+
+void fc_fwd_f32(Tensor x, Tensor w, c10::optional<Tensor> b, Tensor y, int64_t act) {
+  check_f32(x, "x");
+  check_f32(w, "w");
+  check_f32(y, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "x [M, K], w [N, K]");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == w.size(0), "y [M, N]");
+  if (b.has_value() && b->defined()) {
+    check_f32(*b, "b");
+    TORCH_CHECK(b->numel() == w.size(0), "b [N]");
+  }
+  const c10::DeviceGuard guard(x.device());
+  psamd::launch_fc_fwd_f32(x.data_ptr<float>(), w.data_ptr<float>(), opt_ptr<const float>(b), y.data_ptr<float>(),
+                           static_cast<int>(x.size(0)), static_cast<int>(w.size(0)), static_cast<int>(x.size(1)),
+                           static_cast<int>(act), cur_stream(x));
+}
+
 // ------------------------------------------------------------------------------ reference ops
 void softmax_temp_fwd(Tensor x, Tensor y, double temp, double clamp_lo, double clamp_hi) {
   check_f32(x, "x");
@@ -1115,6 +1165,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout);
   m.def("uniform_init", &uniform_init);
   m.def("gemm_nt", &gemm_nt);
+  m.def("fc_bwd", &fc_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("dw") = py::none(),
+        py::arg("db") = py::none(), py::arg("dx") = py::none(), py::arg("act") = 0);
+  m.def("fc_fwd_f32", &fc_fwd_f32);
   m.def("act_bwd", &act_bwd);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_stats", &bn_stats);

@@ -87,6 +87,14 @@ void launch_lazy_init_rows(float* table, const int64_t* rows, const int64_t* key
 void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int64_t n, int64_t* out, int insert,
                        int32_t* status, hipStream_t s);
 
+// ---------------------------------------------------------------- fc.hip
+// fused FC backward: dW = (act'(y) * dy)^T x (+ db = column sums), dX = (act'(y) * dy) W;
+// dtype 0 fp32 / 1 bf16 for every operand; dw / db / dx nullable
+void launch_fc_bwd(const void* dy, const void* y, const void* x, const void* w, void* dw, float* db, void* dx,
+                   int dtype, int M, int N, int K, int act, hipStream_t s);
+void launch_fc_fwd_f32(const float* x, const float* w, const float* b, float* y, int M, int N, int K, int act,
+                       hipStream_t s);
+
 // ---------------------------------------------------------------- ref_ops.hip
 void launch_softmax_temp_fwd(const float* x, float* y, int64_t rows, int cols, float inv_temp, float clamp_lo,
                              float clamp_hi, hipStream_t s);

@@ -1,0 +1,275 @@
+// Fused FC-layer backward (K2 in SURVEY §2.5), bf16 and fp32, on MFMA.
+//
+// Reference: layer/FcLayer.java:93-110 -- delta = act'(delta); db = rowMean(delta);
+// dW = delta . A^T / N; delta_prev = W^T . delta.  The activation backward is folded into the
+// PROLOGUE of both GEMMs (dz = act'(y) * dy is formed while the dy tile is staged, it is never
+// written), the bias gradient is reduced from the same staged tile (the "rowMean fused into the
+// dW epilogue"), and the operands are used where they lie: dy [M, N], x [M, K] and W [N, K]
+// are all row-major, the reduction index of both GEMMs is their SLOW index for one operand,
+// so that operand is transposed while it is staged into LDS (no transposed copy in HBM).
+//
+//   fc_bwd_dw :  dW[N, K] = sum_m dz[m, n] x[m, k]   (+ db[n] = sum_m dz[m, n])
+//   fc_bwd_dx :  dX[M, K] = sum_n dz[m, n] W[n, k]
+//
+// Tiles: 256 threads = 4 waves, C tile 64x64, reduction 32 per stage, each wave a 32x32 quarter
+// = 2x2 16x16 MFMA tiles; bf16 operands use v_mfma_f32_16x16x32_bf16 (one 16-B LDS read per
+// operand per MFMA), fp32 operands v_mfma_f32_16x16x4_f32 (fp32 end to end for the
+// reference-parity fp32 models).  Next stage's global loads are issued before the MFMAs.
+// Activation codes as dense.hip: 0 none, 1 relu, 2 leaky 0.01, 3 reference clipped sigmoid
+// (backward dy * y * (1 - y) on the clipped output, Sigmoid.java).
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int kT = 64;   // C tile rows / cols
+constexpr int kR = 32;   // reduction per stage
+constexpr int kPad = 8;  // LDS row padding (elements)
+
+template <typename T> struct Ld;
+template <> struct Ld<float> {
+  __device__ __forceinline__ static float get(const float* p, int64_t i) { return p[i]; }
+};
+template <> struct Ld<uint16_t> {
+  __device__ __forceinline__ static float get(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
+};
+
+__device__ __forceinline__ float act_grad(float g, float y, int act) {
+  if (act == 1) return y > 0.f ? g : 0.f;
+  if (act == 2) return y > 0.f ? g : 0.01f * g;
+  if (act == 3) return g * y * (1.f - y);
+  return g;
+}
+
+template <typename T>
+__device__ __forceinline__ void lds_put(T* lds, int row, int col, float v);
+template <>
+__device__ __forceinline__ void lds_put<float>(float* lds, int row, int col, float v) {
+  lds[row * (kR + kPad) + col] = v;
+}
+template <>
+__device__ __forceinline__ void lds_put<uint16_t>(uint16_t* lds, int row, int col, float v) {
+  lds[row * (kR + kPad) + col] = f32_to_bf16(v);
+}
+
+// Stage one 64 x 32 operand tile of C-rows [r0, r0+64) x reduction [k0, k0+32) into LDS as
+// lds[row][k].  TRANS: element (row, k) lives at src[k * ld + row] (reduction = slow index);
+// else at src[row * ld + k].  With ACT >= 0, the value is act'(y) * src (y laid out like src)
+// and -- DB -- the per-row sums of that value are accumulated into dbacc (TRANS layout only).
+template <typename T, bool TRANS, bool GRAD, bool DB>
+__device__ __forceinline__ void stage(const T* __restrict__ src, const T* __restrict__ y, int64_t ld, int rows,
+                                      int kdim, int r0, int k0, int act, T* lds, float (&dbacc)[8]) {
+  const int t = threadIdx.x;
+  if constexpr (TRANS) {
+    const int k = t >> 3, rc = (t & 7) * 8;  // 32 reduction rows x 8 chunks of 8 C-rows
+    const int gk = k0 + k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = r0 + rc + j;
+      float v = 0.f;
+      if (gk < kdim && row < rows) {
+        const int64_t o = static_cast<int64_t>(gk) * ld + row;
+        v = Ld<T>::get(src, o);
+        if constexpr (GRAD) v = act_grad(v, Ld<T>::get(y, o), act);
+      }
+      if constexpr (DB) dbacc[j] += v;
+      lds_put<T>(lds, rc + j, k, v);
+    }
+  } else {
+    const int row = t >> 2, kc = (t & 3) * 8;  // 64 C-rows x 4 chunks of 8 reduction elements
+    const int grow = r0 + row;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int gk = k0 + kc + j;
+      float v = 0.f;
+      if (grow < rows && gk < kdim) {
+        const int64_t o = static_cast<int64_t>(grow) * ld + gk;
+        v = Ld<T>::get(src, o);
+        if constexpr (GRAD) v = act_grad(v, Ld<T>::get(y, o), act);
+      }
+      lds_put<T>(lds, row, kc + j, v);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void mma_stage(const T* la, const T* lb, int wm, int wn, int lane, f32x4v (&acc)[2][2]);
+
+template <>
+__device__ __forceinline__ void mma_stage<uint16_t>(const uint16_t* la, const uint16_t* lb, int wm, int wn, int lane,
+                                                    f32x4v (&acc)[2][2]) {
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  bf16x8_t af[2], bf[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    af[i] = *reinterpret_cast<const bf16x8_t*>(&la[(wm + i * 16 + fr) * (kR + kPad) + fk]);
+    bf[i] = *reinterpret_cast<const bf16x8_t*>(&lb[(wn + i * 16 + fr) * (kR + kPad) + fk]);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+}
+
+template <>
+__device__ __forceinline__ void mma_stage<float>(const float* la, const float* lb, int wm, int wn, int lane,
+                                                 f32x4v (&acc)[2][2]) {
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < kR / 4; ++s) {
+    float a[2], b[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a[i] = la[(wm + i * 16 + fr) * (kR + kPad) + 4 * s + fk];
+      b[i] = lb[(wn + i * 16 + fr) * (kR + kPad) + 4 * s + fk];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// C[R, Cc] = sum_k A'[r][k] B'[c][k]; A' from (a, ay) with the act' prologue, TA / TB select
+// the transposed staging of A' / B'.  DB: blocks of column tile 0 also write dbias[r] = sum_k A'[r][k].
+template <typename T, bool TA, bool TB, bool DB>
+__global__ __launch_bounds__(256) void fc_bwd_kernel(const T* __restrict__ a, const T* __restrict__ ay, int64_t lda,
+                                                     const T* __restrict__ b, int64_t ldb, T* __restrict__ c,
+                                                     int64_t ldc, float* __restrict__ dbias, int R, int Cc, int K,
+                                                     int act) {
+  __shared__ __attribute__((aligned(16))) T lds[2][kT * (kR + kPad)];
+  __shared__ float dbl[256][9];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int r0 = blockIdx.y * kT, c0 = blockIdx.x * kT;
+  const bool db_here = DB && blockIdx.x == 0;
+  f32x4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float dbacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += kR) {
+    if (db_here)
+      stage<T, TA, true, TA>(a, ay, lda, R, K, r0, k0, act, lds[0], dbacc);
+    else
+      stage<T, TA, true, false>(a, ay, lda, R, K, r0, k0, act, lds[0], dbacc);
+    stage<T, TB, false, false>(b, nullptr, ldb, Cc, K, c0, k0, 0, lds[1], dbacc);
+    __syncthreads();
+    mma_stage<T>(lds[0], lds[1], wm, wn, lane, acc);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = c0 + wn + j * 16 + (lane & 15);
+      if (col >= Cc) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = r0 + wm + i * 16 + (lane >> 4) * 4 + q;
+        if (row < R) Elem<T>::store(c, static_cast<int64_t>(row) * ldc + col, acc[i][j][q]);
+      }
+    }
+  if constexpr (DB && TA) {
+    if (!db_here) return;
+    // thread t staged C-rows (t & 7) * 8 .. +7 at reduction rows t >> 3 (+ 32 s): sum the 32
+    // reduction-row partials of each C-row
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dbl[threadIdx.x][j] = dbacc[j];
+    __syncthreads();
+    if (threadIdx.x < kT) {
+      const int rc = threadIdx.x >> 3, j = threadIdx.x & 7;
+      float s = 0.f;
+      for (int k = 0; k < 32; ++k) s += dbl[k * 8 + rc][j];
+      const int row = r0 + rc * 8 + j;
+      if (row < R) dbias[row] = s;
+    }
+  }
+}
+
+template <typename T>
+void launch_fc(const void* dy, const void* y, const void* x, const void* w, void* dw, float* db, void* dx, int M,
+               int N, int K, int act, hipStream_t s) {
+  const T* dyp = static_cast<const T*>(dy);
+  const T* yp = static_cast<const T*>(y);
+  if (dw != nullptr) {  // dW[N, K]: A' = dz^T (reduction m = slow index of dy), B' = x^T
+    dim3 grid((K + kT - 1) / kT, (N + kT - 1) / kT);
+    if (db != nullptr)
+      hipLaunchKernelGGL((fc_bwd_kernel<T, true, true, true>), grid, dim3(256), 0, s, dyp, yp, static_cast<int64_t>(N),
+                         static_cast<const T*>(x), static_cast<int64_t>(K), static_cast<T*>(dw),
+                         static_cast<int64_t>(K), db, N, K, M, act);
+    else
+      hipLaunchKernelGGL((fc_bwd_kernel<T, true, true, false>), grid, dim3(256), 0, s, dyp, yp,
+                         static_cast<int64_t>(N), static_cast<const T*>(x), static_cast<int64_t>(K),
+                         static_cast<T*>(dw), static_cast<int64_t>(K), nullptr, N, K, M, act);
+  }
+  if (dx != nullptr) {  // dX[M, K]: A' = dz (reduction n contiguous), B' = W^T (reduction n = slow index of W)
+    dim3 grid((K + kT - 1) / kT, (M + kT - 1) / kT);
+    hipLaunchKernelGGL((fc_bwd_kernel<T, false, true, false>), grid, dim3(256), 0, s, dyp, yp,
+                       static_cast<int64_t>(N), static_cast<const T*>(w), static_cast<int64_t>(K),
+                       static_cast<T*>(dx), static_cast<int64_t>(K), nullptr, M, K, N, act);
+  }
+}
+
+// Forward for fp32 operands: Y = act(X W^T + b) on v_mfma_f32_16x16x4_f32 (the bf16 forward is
+// dense.hip's gemm_nt).  Both operands are K-contiguous: no transposed staging.
+__global__ __launch_bounds__(256) void fc_fwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, float* __restrict__ y, int M,
+                                                          int N, int K, int act) {
+  __shared__ __attribute__((aligned(16))) float lds[2][kT * (kR + kPad)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int r0 = blockIdx.y * kT, c0 = blockIdx.x * kT;
+  f32x4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float unused[8];
+  for (int k0 = 0; k0 < K; k0 += kR) {
+    stage<float, false, false, false>(x, nullptr, K, M, K, r0, k0, 0, lds[0], unused);
+    stage<float, false, false, false>(w, nullptr, K, N, K, c0, k0, 0, lds[1], unused);
+    __syncthreads();
+    mma_stage<float>(lds[0], lds[1], wm, wn, lane, acc);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = c0 + wn + j * 16 + (lane & 15);
+      if (col >= N) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = r0 + wm + i * 16 + (lane >> 4) * 4 + q;
+        if (row >= M) continue;
+        float v = acc[i][j][q] + bv;
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        else if (act == 2) v = v > 0.f ? v : 0.01f * v;
+        else if (act == 3) v = 0.001f + 0.998f / (1.f + __expf(-v));
+        y[static_cast<int64_t>(row) * N + col] = v;
+      }
+    }
+}
+
+}  // namespace
+
+void launch_fc_bwd(const void* dy, const void* y, const void* x, const void* w, void* dw, float* db, void* dx,
+                   int dtype, int M, int N, int K, int act, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  if (dtype == 1) launch_fc<uint16_t>(dy, y, x, w, dw, db, dx, M, N, K, act, s);
+  else launch_fc<float>(dy, y, x, w, dw, db, dx, M, N, K, act, s);
+}
+
+void launch_fc_fwd_f32(const float* x, const float* w, const float* b, float* y, int M, int N, int K, int act,
+                       hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((N + kT - 1) / kT, (M + kT - 1) / kT);
+  hipLaunchKernelGGL(fc_fwd_f32_kernel, grid, dim3(256), 0, s, x, w, b, y, M, N, K, act);
+}
+
+}  // namespace psamd

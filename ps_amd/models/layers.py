@@ -73,8 +73,9 @@ class FcLayer(nn.Module):
         return self
 
     def forward(self, x):
-        if x.is_cuda and self.weights.dtype == torch.bfloat16:
-            # MFMA GEMM with bias + activation fused in the epilogue (ops/dense.py)
+        if x.is_cuda and self.weights.dtype in (torch.bfloat16, torch.float32):
+            # MFMA GEMM with bias + activation fused in the epilogue, K2 fused backward
+            # (ops/dense.py; fp32 models on v_mfma_f32_16x16x4_f32)
             code = _FUSED_ACT.get(type(self.activation), None) if self.activation is not None else 0
             if code is not None:
                 return _dense.linear_act(x, self.weights, self.bias, code)

@@ -1,10 +1,11 @@
-"""MFMA fused linear (csrc/kernels/dense.hip): y = act(x @ w^T + b), bf16 in/out, fp32 acc.
+"""MFMA fused linear: y = act(x @ w^T + b) -- the reference FcLayer (layer/FcLayer.java:74-110).
 
-Forward is ONE kernel (GEMM + bias + activation epilogue).  Backward: dz = act'(y) * dy
-(one elementwise kernel, the reference activation backwards), dx = dz @ w and
-dw = dz^T @ x on the same NT MFMA kernel (operands transposed to K-contiguous copies --
-the reference-scale layers are small, the copies are cheap), db = column sum of dz.
-CPU / non-bf16 tensors use torch (the numerics oracle).
+Forward: ONE kernel, GEMM + bias + activation epilogue (bf16: csrc/kernels/dense.hip gemm_nt on
+v_mfma_f32_16x16x32_bf16; fp32: csrc/kernels/fc.hip on v_mfma_f32_16x16x4_f32).
+Backward (K2): two kernels (csrc/kernels/fc.hip) -- dW with the activation backward folded into
+the prologue and db reduced from the same staged tile, dX with the same prologue; dy, y, x and
+W are read in place (the transposes happen while staging into LDS).  CPU tensors use torch
+(the numerics oracle).
 """
 from __future__ import annotations
 
@@ -45,7 +46,11 @@ class _LinearAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        y = gemm_nt(x2, w, b.float() if b is not None else None, act)
+        if w.dtype == torch.float32:
+            y = torch.empty(x2.shape[0], w.shape[0], dtype=torch.float32, device=x.device)
+            native().fc_fwd_f32(x2, w.contiguous(), b.float().contiguous() if b is not None else None, y, int(act))
+        else:
+            y = gemm_nt(x2, w, b.float() if b is not None else None, act)
         ctx.save_for_backward(x2, w, y)
         ctx.act, ctx.has_b, ctx.xshape, ctx.bdtype = act, b is not None, x.shape, (b.dtype if b is not None else None)
         return y.view(*x.shape[:-1], w.shape[0])
@@ -53,17 +58,21 @@ class _LinearAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, y = ctx.saved_tensors
-        dy2 = dy.reshape(-1, w.shape[0]).contiguous().to(torch.bfloat16)
-        dz = native().act_bwd(dy2, y, int(ctx.act)) if ctx.act else dy2
-        dx = gemm_nt(dz, w.t().contiguous()) if ctx.needs_input_grad[0] else None  # [M,N]x[K,N]^T
-        dw = gemm_nt(dz.t().contiguous(), x2.t().contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
-        db = dz.float().sum(0).to(ctx.bdtype) if ctx.has_b and ctx.needs_input_grad[2] else None
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
+        dy2 = dy.reshape(-1, w.shape[0]).contiguous().to(w.dtype)
+        want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
+        dx = torch.empty_like(x2) if want_dx else None
+        dw = torch.empty_like(w) if (want_dw or want_db) else None
+        db = torch.empty(w.shape[0], dtype=torch.float32, device=w.device) if want_db else None
+        native().fc_bwd(dy2, y, x2, w.contiguous(), dw, db, dx, int(ctx.act))
+        return ((dx.view(ctx.xshape) if dx is not None else None), (dw if want_dw else None),
+                (db.to(ctx.bdtype) if db is not None else None), None)
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: int = 0) -> torch.Tensor:
-    if x.is_cuda and w.dtype == torch.bfloat16:
-        return _LinearAct.apply(x.to(torch.bfloat16), w, b, int(act))
+    """act(x @ w^T + b); GPU fp32 / bf16 weights run the fused MFMA kernels (fwd + K2 bwd)."""
+    if x.is_cuda and w.dtype in (torch.bfloat16, torch.float32):
+        return _LinearAct.apply(x.to(w.dtype), w, b, int(act))
     z = F.linear(x.to(w.dtype), w, b)
     return _act_ref(z, act)
 
