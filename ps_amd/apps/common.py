@@ -99,6 +99,18 @@ def _backend(cfg: Config):
     return None if b in ("auto", "tcp") else b
 
 
+def worker_rank(cfg: Config, conn=None):
+    """(rank, world) of this worker for data sharding (reference Q11: DataSource offset/step are
+    never set, so every reference worker reads the same data): torchrun ranks, or the TCP worker
+    id (PS_AMD_WORKER_ID / RANK) among -DworkerNum workers."""
+    if conn is not None and hasattr(conn, "world"):
+        return conn.rank, conn.world
+    if ctx.is_distributed():
+        wid = int(os.environ.get("PS_AMD_WORKER_ID", os.environ.get("RANK", "0")))
+        return wid, max(1, cfg.worker_num)
+    return 0, 1
+
+
 def device() -> torch.device:
     if torch.cuda.is_available():
         local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -18,7 +18,7 @@ from ..eval.loss_surface import LossSurface
 from ..eval.metrics import AUC
 from ..models.reference import DNN, WideDeepNN
 from ..obs import metrics
-from .common import connect, device, make_trainer, maybe_run_server, setup
+from .common import connect, device, make_trainer, maybe_run_server, setup, worker_rank
 
 
 def main(argv=None):
@@ -45,7 +45,7 @@ def main(argv=None):
     model = model.to(dev)
     trainer = make_trainer(cfg, model, dev, conn)
     start = trainer.resume()  # newest committed checkpoint of -Dcheckpoint_dir (0 = fresh start)
-    rank, world = (conn.rank, conn.world) if hasattr(conn, "world") else (0, 1)
+    rank, world = worker_rank(cfg, conn)
     w0 = {n: p.detach().clone() for n, p in model.named_parameters()}
     test = synthetic_ctr(5000, wide_k=23 if a.wide else 0, seed=10 ** 6)
     gstep = 0

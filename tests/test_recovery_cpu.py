@@ -79,3 +79,38 @@ def test_uncommitted_step_is_not_resumed(tmp_path):
     b.save(4, None, None, blocking=True)
     a.save(4, None, None, blocking=True)
     assert a.latest() == 4 and b.latest() == 4
+
+
+def test_ctr_app_reference_dist_deployment(tmp_path):
+    """The reference's TCP deployment (CTR.java:73-82, README.md:78-94): one PS process started
+    with -Dmode=dist -Dps=1, two worker processes with -Dmode=dist -DpsAddrs; embedding rows live
+    in the server's row tables, dense keys in its key store, BSP barrier per step.  Both workers
+    finish and report a test AUC; the server saw the pushes and the barrier generations."""
+    import re
+    import socket
+
+    from ps_amd.parallel.tcp import PSClient
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    base = [sys.executable, "-m", "ps_amd.apps.ctr", "--epochs", "1", "--steps-per-epoch", "4", "--batch", "200",
+            "--init-scale", "0.1", "-Dmode=dist", "-DworkerNum=2"]
+    srv = subprocess.Popen(base + ["-Dps=1", f"-DpsPort={port}"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True)
+    try:
+        ws = [subprocess.Popen(base + [f"-DpsAddrs=127.0.0.1:{port}"], cwd=ROOT,
+                               env=dict(env, PS_AMD_WORKER_ID=str(w)), stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, text=True) for w in range(2)]
+        outs = [w.communicate(timeout=300)[0] for w in ws]
+        for w, o in zip(ws, outs):
+            assert w.returncode == 0, o[-2000:]
+            assert re.search(r"epoch 0 test auc 0\.\d+", o), o[-2000:]
+        st = PSClient("127.0.0.1", port).stats()
+        assert st["pushes"] > 0 and st["generation"] >= 4, st
+        PSClient("127.0.0.1", port).shutdown()
+        srv.wait(timeout=30)
+    finally:
+        if srv.poll() is None:
+            srv.kill()
