@@ -302,6 +302,19 @@ void lazy_init_rows(Tensor table, Tensor rows, Tensor flags, int64_t seed, int64
                                cur_stream(table));
 }
 
+// (ukeys [n], seg [n + 1]) from sorted keys and their unique indices (see sparse.hip)
+void unique_runs(Tensor srt, Tensor uidx, int64_t mask, Tensor ukeys, Tensor seg) {
+  check_i64(srt, "srt");
+  check_i64(uidx, "uidx");
+  check_i64(ukeys, "ukeys");
+  check_i64(seg, "seg");
+  const int64_t n = srt.numel();
+  TORCH_CHECK(uidx.numel() == n && ukeys.numel() >= n && seg.numel() >= n + 1, "unique_runs sizes");
+  const c10::DeviceGuard guard(srt.device());
+  psamd::launch_unique_runs(srt.data_ptr<int64_t>(), uidx.data_ptr<int64_t>(), n, mask, ukeys.data_ptr<int64_t>(),
+                            seg.data_ptr<int64_t>(), cur_stream(srt));
+}
+
 // out[i] = slot of ids[i] in the device hash map ``hkeys`` (int64 [capacity], power of two,
 // -1 = empty); insert claims a slot for a new id.  status (int32 [1]) is set on a miss/overflow.
 void hash_slots(Tensor hkeys, Tensor ids, Tensor out, bool insert, Tensor status) {
@@ -1155,6 +1168,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lazy_init_rows", &lazy_init_rows, py::arg("table"), py::arg("rows"), py::arg("flags"), py::arg("seed"),
         py::arg("row_base"), py::arg("lo"), py::arg("hi"), py::arg("keys") = py::none());
   m.def("hash_slots", &hash_slots);
+  m.def("unique_runs", &unique_runs);
   m.def("softmax_temp_fwd", &softmax_temp_fwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("bce", &bce);

@@ -84,6 +84,8 @@ void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int
                           const float* bias, float* out, hipStream_t s);
 void launch_lazy_init_rows(float* table, const int64_t* rows, const int64_t* keys, int64_t nrows, int dim,
                            uint8_t* init_flags, uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s);
+void launch_unique_runs(const int64_t* srt, const int64_t* uidx, int64_t n, int64_t mask, int64_t* ukeys,
+                        int64_t* seg, hipStream_t s);
 void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int64_t n, int64_t* out, int insert,
                        int32_t* status, hipStream_t s);
 

@@ -77,9 +77,57 @@ __global__ __launch_bounds__(256) void gather_rows_vec4_kernel(const float* __re
   }
 }
 
+// dim = 4 * 2^lg <= 256, fp32 table, fp32 or bf16 out: 2^lg lanes per row, 16-B loads, 64 >> lg
+// rows per wave in flight
+template <typename O>
+__global__ __launch_bounds__(256) void gather_rows_lg_kernel(const float* __restrict__ table,
+                                                             const int64_t* __restrict__ rows, int64_t nrows,
+                                                             int dim, int lg, O* __restrict__ out, int64_t out_ld,
+                                                             int64_t out_off, int act) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> lg;
+  const int c = (lane & ((1 << lg) - 1)) * 4;
+  const int per_wave = 64 >> lg;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t rb = wave * per_wave; rb < nrows; rb += nwaves * per_wave) {
+    const int64_t r = rb + sub;
+    if (r >= nrows) continue;
+    const int64_t row = rows[r];
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row >= 0) {
+      v = load4(table, row * dim + c);
+      v.x = apply_act(v.x, act); v.y = apply_act(v.y, act); v.z = apply_act(v.z, act); v.w = apply_act(v.w, act);
+    }
+    store4(out, r * out_ld + out_off + c, v);
+  }
+}
+
+static int lg_of(int dim) {
+  if (dim % 4 != 0 || dim > 256) return -1;
+  const int l = dim / 4;
+  if ((l & (l - 1)) != 0) return -1;
+  int lg = 0;
+  while ((1 << lg) < l) ++lg;
+  return lg;
+}
+
 void launch_gather_rows(const void* table, int tdtype, const int64_t* rows, int64_t nrows, int dim, void* out,
                         int odtype, int64_t out_ld, int64_t out_off, int act, hipStream_t s) {
   if (nrows <= 0) return;
+  const int lg = lg_of(dim);
+  const int oes = odtype == 1 ? 2 : 4;
+  if (tdtype == 0 && lg >= 0 && out_ld % 4 == 0 && out_off % 4 == 0 &&
+      ((reinterpret_cast<uintptr_t>(table) & 15) | (reinterpret_cast<uintptr_t>(out) & (oes * 4 - 1))) == 0) {
+    const int g = stream_grid(((nrows << lg) + 63) / 64 * 64, 256);
+    if (odtype == 1)
+      hipLaunchKernelGGL(gather_rows_lg_kernel<uint16_t>, dim3(g), dim3(256), 0, s, static_cast<const float*>(table),
+                         rows, nrows, dim, lg, static_cast<uint16_t*>(out), out_ld, out_off, act);
+    else
+      hipLaunchKernelGGL(gather_rows_lg_kernel<float>, dim3(g), dim3(256), 0, s, static_cast<const float*>(table),
+                         rows, nrows, dim, lg, static_cast<float*>(out), out_ld, out_off, act);
+    return;
+  }
   const int grid = stream_grid(nrows * 64, 256);
   const bool vec = tdtype == 0 && odtype == 0 && dim % 4 == 0 && out_ld % 4 == 0 && out_off % 4 == 0 &&
                    ((reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
@@ -137,7 +185,15 @@ __global__ __launch_bounds__(256) void segment_reduce_rows_vec_kernel(const S* _
     if (u >= nseg) continue;
     const int64_t b = seg_off[u], e = seg_off[u + 1];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t j = b; j < e; ++j) acc += load4(src, perm[j] * dim + c);
+    int64_t j = b;
+    // 4 independent row loads in flight: hot ids (long segments) are latency chains otherwise
+    for (; j + 4 <= e; j += 4) {
+      const int64_t p0 = perm[j], p1 = perm[j + 1], p2 = perm[j + 2], p3 = perm[j + 3];
+      const f32x4 v0 = load4(src, p0 * dim + c), v1 = load4(src, p1 * dim + c);
+      const f32x4 v2 = load4(src, p2 * dim + c), v3 = load4(src, p3 * dim + c);
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; j < e; ++j) acc += load4(src, perm[j] * dim + c);
     if (mean) acc *= 1.f / static_cast<float>(e - b > 0 ? e - b : 1);
     store4(out, u * dim + c, acc);
   }
@@ -273,32 +329,42 @@ __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const float span = hi - lo;
-  for (int64_t r = wave; r < nrows; r += nwaves) {
-    const int64_t row = rows[r];
-    if (row < 0 || flags[row]) continue;  // wave-uniform
-    const uint64_t grow = keys ? static_cast<uint64_t>(keys[r]) : static_cast<uint64_t>(row + row_base);
-    // one Philox call yields the 4 values of elements 4q .. 4q+3 (counter = key << 20 ^ q)
-    for (int q = lane; q * 4 < dim; q += 64) {
-      uint32_t rnd[4];
-      Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(q), rnd);
-      float* dst = table + row * dim + q * 4;
-      if (q * 4 + 4 <= dim && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
-        store4(dst, 0, f32x4{lo + span * Philox::u01(rnd[0]), lo + span * Philox::u01(rnd[1]),
-                             lo + span * Philox::u01(rnd[2]), lo + span * Philox::u01(rnd[3])});
-      } else {
-        for (int k = 0; k < 4 && q * 4 + k < dim; ++k) dst[k] = lo + span * Philox::u01(rnd[k]);
+  // 64 rows per wave step: every lane checks one row's flag, the rows still to be created are
+  // ballotted and then initialised one after the other by the whole wave (steady state: almost
+  // every row exists, so the kernel is one coalesced flag probe per 64 rows)
+  for (int64_t base = wave * 64; base < nrows; base += nwaves * 64) {
+    const int64_t r = base + lane;
+    const int64_t row = r < nrows ? rows[r] : -1;
+    const bool need = row >= 0 && flags[row] == 0;
+    const int64_t key = need ? (keys ? keys[r] : row + row_base) : 0;
+    uint64_t todo = __ballot(need);
+    while (todo) {
+      const int l = __ffsll(static_cast<unsigned long long>(todo)) - 1;
+      todo &= todo - 1;
+      const int64_t rr = __shfl(row, l, 64);
+      const uint64_t grow = static_cast<uint64_t>(__shfl(key, l, 64));
+      // one Philox call yields the 4 values of elements 4q .. 4q+3 (counter = key << 20 ^ q)
+      for (int q = lane; q * 4 < dim; q += 64) {
+        uint32_t rnd[4];
+        Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(q), rnd);
+        float* dst = table + rr * dim + q * 4;
+        if (q * 4 + 4 <= dim && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+          store4(dst, 0, f32x4{lo + span * Philox::u01(rnd[0]), lo + span * Philox::u01(rnd[1]),
+                               lo + span * Philox::u01(rnd[2]), lo + span * Philox::u01(rnd[3])});
+        } else {
+          for (int k = 0; k < 4 && q * 4 + k < dim; ++k) dst[k] = lo + span * Philox::u01(rnd[k]);
+        }
       }
     }
-    // rows may repeat inside one launch (several workers asked for the same row); flags is
-    // written after the row so a duplicate wave either re-inits identically or skips.
-    if (lane == 0) flags[row] = 1;
+    // duplicates inside one launch re-initialise identically; flags go up after the rows
+    if (need) flags[row] = 1;
   }
 }
 
 void launch_lazy_init_rows(float* table, const int64_t* rows, const int64_t* keys, int64_t nrows, int dim,
                            uint8_t* init_flags, uint64_t seed, int64_t row_base, float lo, float hi, hipStream_t s) {
   if (nrows <= 0) return;
-  const int grid = stream_grid(nrows * 64, 256);
+  const int grid = stream_grid((nrows + 63) / 64 * 64, 256);
   hipLaunchKernelGGL(lazy_init_rows_kernel, dim3(grid), dim3(256), 0, s, table, rows, keys, nrows, dim, init_flags,
                      seed, row_base, lo, hi);
 }
@@ -356,6 +422,30 @@ void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int
   const int grid = stream_grid(n, 256);
   hipLaunchKernelGGL(hash_slots_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(hkeys),
                      capacity - 1, ids, n, out, insert, status);
+}
+
+// Compaction of sorted keys: for every run head i (i == 0 or srt[i] != srt[i-1]) with unique
+// index uidx[i] (inclusive scan of the head flags, minus 1): ukeys[u] = srt[i] & mask,
+// seg[u] = i, and seg[nu] = n -- the (unique keys, segment offsets) of a pull plan without the
+// host needing nu first (outputs are sized n and n + 1).
+__global__ __launch_bounds__(256) void unique_runs_kernel(const int64_t* __restrict__ srt,
+                                                          const int64_t* __restrict__ uidx, int64_t n, int64_t mask,
+                                                          int64_t* __restrict__ ukeys, int64_t* __restrict__ seg) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t u = uidx[i];
+    if (i == 0 || srt[i] != srt[i - 1]) {
+      ukeys[u] = srt[i] & mask;
+      seg[u] = i;
+    }
+    if (i == n - 1) seg[u + 1] = n;
+  }
+}
+
+void launch_unique_runs(const int64_t* srt, const int64_t* uidx, int64_t n, int64_t mask, int64_t* ukeys,
+                        int64_t* seg, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(unique_runs_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, s, srt, uidx, n, mask, ukeys, seg);
 }
 
 }  // namespace psamd

@@ -349,11 +349,25 @@ class ShardedSparseTable:
         head = torch.ones(n, dtype=torch.bool, device=self.device)
         if n > 1:
             head[1:] = srt[1:] != srt[:-1]
-        uidx = torch.cumsum(head.long(), 0) - 1
+        cum = torch.cumsum(head.long(), 0)
+        uidx = cum - 1
         ubuf = torch.empty(n, dtype=torch.int64, device=self.device)
-        ubuf.scatter_(0, uidx, srt & KEY_MASK)  # duplicates write identical values
-        meta = torch.zeros(W + 1, dtype=torch.int64, device=self.device)
-        meta[:W].scatter_add_(0, srt >> OWNER_SHIFT, head.long())
+        seg_full = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        if n == 0:
+            seg_full.zero_()
+        elif self.gpu:  # one HIP pass: unique keys + segment starts (no atomics, no host size)
+            from ..ops._ext import native
+
+            native().unique_runs(srt, uidx, KEY_MASK, ubuf, seg_full)
+        else:
+            ubuf.scatter_(0, uidx, srt & KEY_MASK)  # duplicates write identical values
+            seg_full.fill_(n)
+            seg_full.scatter_reduce_(0, uidx, torch.arange(n, device=self.device), reduce="amin", include_self=True)
+        # per-owner unique counts from the owner-major sort order (binary search, no atomics)
+        bounds = torch.searchsorted(srt, torch.arange(W + 1, device=self.device, dtype=torch.int64) << OWNER_SHIFT)
+        cum0 = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), cum])
+        meta = torch.empty(W + 1, dtype=torch.int64, device=self.device)
+        meta[:W] = cum0[bounds[1:]] - cum0[bounds[:-1]]
         meta[W] = nbad
         if W > 1:
             recv = torch.empty(W, dtype=torch.int64, device=self.device)
@@ -369,8 +383,9 @@ class ShardedSparseTable:
         nu = sum(send)
         inv = torch.empty(n, dtype=torch.int64, device=self.device)
         inv[perm] = uidx
-        seg_off = torch.full((nu + 1,), n, dtype=torch.int64, device=self.device)
-        seg_off.scatter_reduce_(0, uidx, torch.arange(n, device=self.device), reduce="amin", include_self=True)
+        seg_off = seg_full[:nu + 1]
+        if not self.gpu:
+            seg_off[nu] = n
         return n, nu, inv, perm, seg_off, send, recv_l, ubuf[:nu]
 
     def _serve_keys(self, ukeys: torch.Tensor, send: List[int], recv: List[int]):
