@@ -100,7 +100,7 @@ class GpuAsyncServer {
   double beta1_, beta2_;
   int bias_mode_;
   psamd::FusedOptArgs a_{};
-  volatile bool stop_ = true;
+  std::atomic<bool> stop_{true};
   std::thread th_;
   int64_t applied_ = 0;
 };

@@ -24,6 +24,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <atomic>
 #include <chrono>
 #include <thread>
 
@@ -75,7 +76,12 @@ struct Backoff {
 };
 
 // A slot of owner o that holds no reader and is not the current one (-1 if none right now).
+// The full fence pairs with the one in pin(): "owner publishes cur, then reads pins" against
+// "reader bumps pins, then reads cur" is the store-buffer pattern -- with acquire/release alone
+// both could read the stale value (x86 store buffer) and the owner would overwrite a slot a
+// reader is copying.
 inline int free_slot(AsyncCtl* c, int o) {
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
   const int64_t cur = ld(&c->cur[o]);
   for (int s = 0; s < kSlots; ++s)
     if (s != cur && ld(&c->pins[o][s]) == 0) return s;
@@ -89,6 +95,7 @@ inline int pin(AsyncCtl* c, int o) {
   for (;;) {
     const int64_t s = ld(&c->cur[o]);
     add(&c->pins[o][s], 1);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // see free_slot()
     if (ld(&c->cur[o]) == s) return static_cast<int>(s);
     add(&c->pins[o][s], -1);
     bo();
@@ -113,11 +120,11 @@ inline int64_t min_ack(AsyncCtl* c) {
 // optimizer on the master shard with mailbox w and writes the new weights into ``slot``; it
 // returns only once the result is globally visible (stream synchronised).
 template <class Apply>
-void serve_loop(AsyncCtl* c, int me, const volatile bool* stop, Apply&& apply) {
+void serve_loop(AsyncCtl* c, int me, const std::atomic<bool>* stop, Apply&& apply) {
   const int W = static_cast<int>(c->world);
   int start = 0;
   Backoff idle;
-  while (!*stop && ld(&c->stop) == 0) {
+  while (!stop->load(std::memory_order_acquire) && ld(&c->stop) == 0) {
     bool did = false;
     for (int k = 0; k < W; ++k) {
       const int w = (start + k) % W;
@@ -127,7 +134,7 @@ void serve_loop(AsyncCtl* c, int me, const volatile bool* stop, Apply&& apply) {
       int slot;
       Backoff wait_slot;
       while ((slot = free_slot(c, me)) < 0) {
-        if (*stop || ld(&c->stop)) return;
+        if (stop->load(std::memory_order_acquire) || ld(&c->stop)) return;
         wait_slot();
       }
       const int64_t v = ld(&c->version[me]);

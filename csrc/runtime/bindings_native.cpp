@@ -358,7 +358,7 @@ class CpuAsyncServer {
   std::vector<float*> pub_;
   std::vector<std::vector<float>> states_;
   std::vector<float> tmp_;
-  volatile bool stop_ = true;
+  std::atomic<bool> stop_{true};
   std::thread th_;
   int64_t applied_ = 0;
 };

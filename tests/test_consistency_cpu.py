@@ -100,3 +100,24 @@ def test_bsp_barrier_with_dead_worker_times_out():
         assert len(out) == 2 and out[0] == out[1] == 1
     finally:
         srv.stop()
+
+
+def test_async_ctl_protocol_under_tsan(tmp_path):
+    """host ThreadSanitizer build of the async-PS control protocol stress
+    (csrc/runtime/tests/async_ctl_stress.cpp: owners' serve_loop vs workers' push / SSP gate /
+    pin-copy-unpin on plain host memory) -- no data race, every push applied once, no slot
+    rewritten while pinned, SSP bound held."""
+    import os
+    import shutil
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cxx = "/opt/rocm/lib/llvm/bin/clang++"
+    if not os.path.exists(cxx):
+        cxx = shutil.which("clang++") or shutil.which("g++")
+    exe = str(tmp_path / "stress")
+    subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread", f"-I{root}/csrc/include",
+                    f"{root}/csrc/runtime/tests/async_ctl_stress.cpp", "-o", exe], check=True, timeout=300)
+    r = subprocess.run([exe, "3", "150", "1"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and "violations=0" in r.stdout, r.stdout + r.stderr[-3000:]
