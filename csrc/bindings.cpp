@@ -382,6 +382,16 @@ void fc_fwd_f32(Tensor x, Tensor w, c10::optional<Tensor> b, Tensor y, int64_t a
 }
 
 // ------------------------------------------------------------------------------ reference ops
+void softmax_temp_bwd(Tensor p, Tensor dy, Tensor dx, double scale) {
+  check_f32(p, "p");
+  check_f32(dy, "dy");
+  check_f32(dx, "dx");
+  TORCH_CHECK(p.dim() == 2 && p.sizes() == dy.sizes() && p.sizes() == dx.sizes(), "p, dy, dx [rows, cols]");
+  const c10::DeviceGuard guard(p.device());
+  psamd::launch_softmax_temp_bwd(p.data_ptr<float>(), dy.data_ptr<float>(), dx.data_ptr<float>(), p.size(0),
+                                 static_cast<int>(p.size(1)), static_cast<float>(scale), cur_stream(p));
+}
+
 void softmax_temp_fwd(Tensor x, Tensor y, double temp, double clamp_lo, double clamp_hi) {
   check_f32(x, "x");
   check_f32(y, "y");
@@ -1170,6 +1180,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("hash_slots", &hash_slots);
   m.def("unique_runs", &unique_runs);
   m.def("softmax_temp_fwd", &softmax_temp_fwd);
+  m.def("softmax_temp_bwd", &softmax_temp_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("bce", &bce);
   m.def("maxpool2d_fwd", &maxpool2d_fwd);

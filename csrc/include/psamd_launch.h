@@ -100,6 +100,8 @@ void launch_fc_fwd_f32(const float* x, const float* w, const float* b, float* y,
 // ---------------------------------------------------------------- ref_ops.hip
 void launch_softmax_temp_fwd(const float* x, float* y, int64_t rows, int cols, float inv_temp, float clamp_lo,
                              float clamp_hi, hipStream_t s);
+void launch_softmax_temp_bwd(const float* p, const float* dy, float* dx, int64_t rows, int cols, float scale,
+                             hipStream_t s);
 void launch_softmax_xent(const float* p, const int64_t* labels, int64_t rows, int cols, float* loss,
                          float* grad, hipStream_t s);
 void launch_bce(const float* p, const float* y, int64_t n, float* loss, float* grad, hipStream_t s);

@@ -49,6 +49,32 @@ void launch_softmax_temp_fwd(const float* x, float* y, int64_t rows, int cols, f
                      inv_temp, clamp_lo, clamp_hi);
 }
 
+// Softmax backward (Jacobian-vector product, activations/Softmax.java:45-67): one wave per row,
+// dx = scale * p * (dy - sum_c dy_c p_c); scale = 1 reproduces the reference (which omits the
+// 1/T of the temperature, Q15), scale = 1/T is the exact gradient.
+__global__ __launch_bounds__(256) void softmax_temp_bwd_kernel(const float* __restrict__ p, const float* __restrict__ dy,
+                                                               float* __restrict__ dx, int64_t rows, int cols,
+                                                               float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = wave; r < rows; r += nwaves) {
+    const float* pr = p + r * cols;
+    const float* gr = dy + r * cols;
+    float d = 0.f;
+    for (int c = lane; c < cols; c += 64) d += gr[c] * pr[c];
+    d = wave_sum(d);
+    for (int c = lane; c < cols; c += 64) dx[r * cols + c] = scale * pr[c] * (gr[c] - d);
+  }
+}
+
+void launch_softmax_temp_bwd(const float* p, const float* dy, float* dx, int64_t rows, int cols, float scale,
+                             hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(softmax_temp_bwd_kernel, dim3(stream_grid(rows * 64, 256)), dim3(256), 0, s, p, dy, dx, rows,
+                     cols, scale);
+}
+
 // loss (scalar, pre-zeroed) += -mean log p[label]; grad[r, c] = (c == label) ? -1/p / rows : 0
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ p, const int64_t* __restrict__ labels,
                                                            int64_t rows, int cols, float* __restrict__ loss,

@@ -78,11 +78,8 @@ class _TempSoftmax(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (p,) = ctx.saved_tensors
-        dy = dy.float()
-        g = p * (dy - (dy * p).sum(dim=1, keepdim=True))
-        if not ctx.ref_bwd:
-            g = g / ctx.temp
-        return g, None, None
+        g = nn_ops.softmax_temp_bwd(p, dy, 1.0 if ctx.ref_bwd else 1.0 / ctx.temp)  # HIP on GPU
+        return g.to(dy.dtype), None, None
 
 
 class Softmax(Activation):

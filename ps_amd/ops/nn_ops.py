@@ -8,6 +8,17 @@ import torch.nn.functional as F
 from ._ext import native, use_native
 
 
+def softmax_temp_bwd(p: torch.Tensor, dy: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """scale * p * (dy - sum(dy * p)) per row (activations/Softmax.java:45-67; scale 1 = the
+    reference, which drops the 1/T, Q15)."""
+    p, dy = p.contiguous().float(), dy.contiguous().float()
+    if use_native(p):
+        dx = torch.empty_like(p)
+        native().softmax_temp_bwd(p, dy, dx, float(scale))
+        return dx
+    return scale * p * (dy - (dy * p).sum(dim=1, keepdim=True))
+
+
 def softmax_temp(x: torch.Tensor, temp: float = 10000.0, clamp_lo: float = 0.001, clamp_hi: float = 0.999):
     """Row softmax of x/temp with the reference's 0->0.001 / 1->0.999 clamps
     (activations/Softmax.java:11-40)."""

@@ -321,3 +321,13 @@ def test_dlrm_interact_fwd_bwd(B, T, D):
     assert cos(x.grad.float().flatten(), xr.grad.flatten(), dim=0) > 0.999
     assert cos(e.grad.float().flatten(), er.grad.flatten(), dim=0) > 0.999
     torch.testing.assert_close(e.grad.float(), er.grad, rtol=3e-2, atol=0.15 * (D ** 0.5) / 4)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-4])
+def test_softmax_temp_bwd(scale):
+    torch.manual_seed(5)
+    p = torch.softmax(torch.randn(1000, 10), dim=1)
+    dy = torch.randn(1000, 10)
+    ref = N.softmax_temp_bwd(p, dy, scale)
+    out = N.softmax_temp_bwd(p.to(DEV), dy.to(DEV), scale)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-7)
