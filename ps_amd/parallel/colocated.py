@@ -61,7 +61,7 @@ class ColocatedPS:
                  transport: Optional[Transport] = None, *, bucket_mb: float = 32.0, last_bucket_mb: float = 4.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
                  average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
-                 compress_warmup: int = 0):
+                 compress_warmup: int = 0, split_comm: Optional[bool] = None):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -162,6 +162,17 @@ class ColocatedPS:
         self._key_bucket = {n: R.keys[n].bucket for n in self.params}
         self._landing: List[Dict[str, torch.Tensor]] = [dict() for _ in R.buckets]  # parked grads
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
+        # separate push / pull communicators: the all-gather of bucket b runs on
+        # its own communicator + stream, so the reduce-scatter of bucket b+1 need not wait behind
+        # it; opt-in (PS_AMD_SPLIT_COMM=1) -- the default single communicator is what the
+        # measured multi-GPU configs use
+        import os as _os
+
+        if split_comm is None:
+            split_comm = _os.environ.get("PS_AMD_SPLIT_COMM", "0") == "1"
+        self.split_comm = bool(split_comm) and self.world > 1
+        self.tpull = self.t.split() if self.split_comm else self.t
+        self.comm_pull = torch.cuda.Stream(device=self.device) if (self.gpu and self.split_comm) else self.comm
         self.round_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
         # fault injection (PS_AMD_FAULT / HIPPS_FAULT): kill at a step, delay pushes
@@ -244,7 +255,12 @@ class ColocatedPS:
                 self._mark("push0")
                 self._push(b)
                 self._mark("push1")
-                if self.clip_norm is None:
+            if self.clip_norm is None:
+                if self.comm_pull is not self.comm:
+                    pev = torch.cuda.Event()
+                    pev.record(self.comm)
+                    self.comm_pull.wait_event(pev)
+                with torch.cuda.stream(self.comm_pull):
                     self._serve_pull(b)
         else:
             self._mark("push0")
@@ -348,7 +364,7 @@ class ColocatedPS:
             u.step_flat(self.master[b][a:z], st, g[a:z], wout=own[a:z], gscale=gscale, gscale_t=gst,
                         step=self.round + 1)
         self._mark("serve1")
-        self.t.all_gather(wfull[bk.start:bk.start + bk.size], own)
+        self.tpull.all_gather(wfull[bk.start:bk.start + bk.size], own)
         self._mark("pull1")
 
     def _clip_and_serve(self) -> None:
@@ -375,17 +391,20 @@ class ColocatedPS:
                 self._launch(b)
         if self.clip_norm is not None:
             if self.gpu:
-                with torch.cuda.stream(self.comm):
+                self.comm_pull.wait_stream(self.comm)
+                with torch.cuda.stream(self.comm_pull):
                     self._clip_and_serve()
             else:
                 self._clip_and_serve()
         if self.gpu:
+            if self.comm_pull is not self.comm:
+                self.comm_pull.wait_stream(self.comm)  # the round ends when both streams are done
             ev = torch.cuda.Event()
-            ev.record(self.comm)
+            ev.record(self.comm_pull)
             self.round_events.append(ev)
         if self.timing:
             if self.gpu:
-                with torch.cuda.stream(self.comm):
+                with torch.cuda.stream(self.comm_pull):
                     self._mark("round_end")
             else:
                 self._mark("round_end")

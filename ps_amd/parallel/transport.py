@@ -144,6 +144,15 @@ class Transport:
         dist.all_gather_object(res, obj, group=self.group)
         return res
 
+    def split(self) -> "Transport":
+        """A second transport over the same ranks with its OWN communicator (RCCL: its own
+        internal stream), e.g. for pulls that should not queue behind pushes.
+        Collective: every rank must call it, in the same order."""
+        if self.world == 1:
+            return Transport()
+        ranks = list(range(self.world)) if self.group is None else dist.get_process_group_ranks(self.group)
+        return Transport(group=dist.new_group(ranks), check_order=self.check_order)
+
     def barrier(self):
         if self.world > 1:
             if self.backend == "nccl":
@@ -188,6 +197,16 @@ class LoopbackHub:
         self.world = world
         self.slots: List[object] = [None] * world
         self.bar = threading.Barrier(world, timeout=timeout_s)
+        self.timeout_s = timeout_s
+        self._child = None
+        self._lock = threading.Lock()
+
+    def child(self) -> "LoopbackHub":
+        """The hub of the split (second) communicator, shared by every thread-rank."""
+        with self._lock:
+            if self._child is None:
+                self._child = LoopbackHub(self.world, self.timeout_s)
+            return self._child
 
     def exchange(self, rank: int, obj):
         self.slots[rank] = obj
@@ -276,6 +295,9 @@ class LoopbackTransport(Transport):
 
     def all_gather_object(self, obj):
         return self.hub.exchange(self.rank, obj)
+
+    def split(self) -> "LoopbackTransport":
+        return LoopbackTransport(self.hub.child(), self.rank, self.check_order)
 
     def barrier(self):
         self.hub.exchange(self.rank, None)

@@ -1,5 +1,6 @@
 """Co-located PS over multi-process gloo (world 2): BSP equivalence with a single process on
 the global batch, SSP(1) semantics, 1-bit compressed push, sharded sparse tables."""
+import pytest
 import torch
 
 from tests import dist_util
@@ -127,3 +128,41 @@ def test_onebit_warmup_rounds_are_full_precision():
         for k in full[0][step]:
             torch.testing.assert_close(warm[0][step][k], full[0][step][k], rtol=0, atol=0)
     assert any(not torch.equal(warm[0][3][k], full[0][3][k]) for k in full[0][3])
+
+
+def _split_model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(12, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+
+
+def _split_body(tp, split, clip, models=None):
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import MomentumUpdater
+
+    m = models[tp.rank] if models is not None else _split_model()  # thread-ranks: built outside
+    ps = ColocatedPS(m, MomentumUpdater(0.1, 0.9), tp, bucket_mb=0.001, split_comm=split, clip_norm=clip)
+    assert (ps.tpull is not ps.t) == (split and tp.world > 1)
+    g = torch.Generator().manual_seed(tp.rank)
+    for _ in range(4):
+        x, y = torch.randn(16, 12, generator=g), torch.randint(0, 4, (16,), generator=g)
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        ps.finish_step()
+    return {k: v.detach().clone() for k, v in m.named_parameters()}
+
+
+@pytest.mark.parametrize("clip", [None, 0.5])
+def test_split_push_pull_communicators_same_result(clip):
+    """pulls on their own communicator give bitwise the same training (gloo world 2)."""
+    a = dist_util.run(_split_body, 2, (False, clip))
+    b = dist_util.run(_split_body, 2, (True, clip))
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]) and torch.equal(b[0][k], b[1][k])
+
+
+def test_split_communicators_loopback_world3():
+    from ps_amd.parallel.transport import run_loopback
+
+    a = run_loopback(_split_body, 3, False, None, [_split_model() for _ in range(3)])
+    b = run_loopback(_split_body, 3, True, None, [_split_model() for _ in range(3)])
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k])

@@ -218,3 +218,14 @@ def test_dlrm_multirank_gpu_equals_single_rank():
         for k, v in w1[0].items():
             torch.testing.assert_close(w2[r][0][k], v, rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(w2[r][1], w1[1], rtol=1e-4, atol=1e-5)
+
+
+def test_split_push_pull_streams_multirank_gpu():
+    """Pull (all-gather) on its own communicator + HIP stream: same result as one communicator."""
+    from ps_amd.parallel.updaters import MomentumUpdater
+
+    upd = lambda: MomentumUpdater(0.1, 0.9, 1e-4)  # noqa: E731
+    one = run_loopback(_train, 2, [_model(0).to(DEV) for _ in range(2)], {}, 4, upd, DEV)
+    two = run_loopback(_train, 2, [_model(0).to(DEV) for _ in range(2)], {"split_comm": True}, 4, upd, DEV)
+    for k in one[0][0]:
+        torch.testing.assert_close(two[0][0][k], one[0][0][k], rtol=0, atol=0)
