@@ -36,6 +36,7 @@ from typing import Dict, List, Optional, Union
 
 import torch
 
+from ..obs import trace as _trace
 from .transport import Transport, side_stream
 from .updaters import AdamUpdater, Updater, resolve_updater
 
@@ -271,6 +272,10 @@ class AsyncPS:
         pull the newest weights the staleness bound allows."""
         if self.accumulating:
             return
+        with _trace.range(f"async_ps.step.c{self.clock}"):
+            self._finish_step()
+
+    def _finish_step(self) -> None:
         W, me, L, A = self.world, self.rank, self.L, self.A
         if self.gpu:
             torch.cuda.current_stream(self.device).wait_stream(self.push_stream)  # gflat free again

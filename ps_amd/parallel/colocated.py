@@ -49,6 +49,7 @@ from typing import Dict, List, Optional, Union
 
 import torch
 
+from ..obs import trace as _trace
 from ..ops import compress as _cmp
 from ..ops import reduce as _red
 from .registry import Registry
@@ -251,7 +252,7 @@ class ColocatedPS:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
             self.comm.wait_event(ev)
-            with torch.cuda.stream(self.comm):
+            with torch.cuda.stream(self.comm), _trace.range(f"ps.push.b{b}"):  # roctx
                 self._mark("push0")
                 self._push(b)
                 self._mark("push1")
@@ -260,7 +261,7 @@ class ColocatedPS:
                     pev = torch.cuda.Event()
                     pev.record(self.comm)
                     self.comm_pull.wait_event(pev)
-                with torch.cuda.stream(self.comm_pull):
+                with torch.cuda.stream(self.comm_pull), _trace.range(f"ps.serve_pull.b{b}"):
                     self._serve_pull(b)
         else:
             self._mark("push0")
@@ -384,6 +385,7 @@ class ColocatedPS:
         phases, advance the PS clock and bind the weights the next forward may use."""
         if self.fault is not None:
             self.fault.at_step(self.round)
+        _trace.mark(f"ps.finish_step.r{self.round}")
         if self.timing:
             self._mark("bwd_end")
         for b in range(len(self.reg.buckets)):

@@ -24,6 +24,7 @@ from typing import Callable, Dict, Optional, Union
 import torch
 
 from ..context import Stat, ctx
+from ..obs import trace as _trace
 from .updaters import Updater, resolve_updater
 
 Init = Callable[[], torch.Tensor]
@@ -158,10 +159,11 @@ class KVStore:
             self._fault.at_step(self.round)
         self.round += 1
         self.clock += 1
-        if self.consistency == "bsp":
-            self.client.barrier(self.worker_id)
-        elif self.consistency == "ssp":
-            self.client.clock(self.worker_id, self.clock)
+        with _trace.range(f"kv.{self.consistency}.wait"):
+            if self.consistency == "bsp":
+                self.client.barrier(self.worker_id)
+            elif self.consistency == "ssp":
+                self.client.clock(self.worker_id, self.clock)
 
     def barrier(self) -> None:
         if self.distributed:

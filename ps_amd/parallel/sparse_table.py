@@ -41,6 +41,7 @@ from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import torch
 
+from ..obs import trace as _trace
 from ..ops import sparse as _sp
 from .transport import Transport, side_stream
 from .updaters import Updater
@@ -405,6 +406,10 @@ class ShardedSparseTable:
         return back
 
     def _plan(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool = True):
+        with _trace.range(f"sparse.pull.{self.name}"):
+            return self._plan_impl(keys, nbad, fetch)
+
+    def _plan_impl(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool):
         self._wait_push()
         n, nu, inv, perm, seg_off, send, recv, ukeys = self._route(keys, nbad)
         rkeys, rslots = self._serve_keys(ukeys, send, recv)
@@ -457,6 +462,7 @@ class ShardedSparseTable:
         self._apply_acc(gscale, average)
 
     def _exchange_grads(self, plan: _Plan, g: torch.Tensor) -> None:
+        _trace.mark(f"sparse.push.{self.name}")
         if self.world > 1:
             rg = torch.empty(sum(plan.recv), self.dim, dtype=torch.float32, device=self.device)
             self.t.all_to_all(rg, g.contiguous(), plan.recv, plan.send)
