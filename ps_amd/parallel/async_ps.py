@@ -31,6 +31,7 @@ CPU processes, plain tensors between loopback thread-ranks).
 """
 from __future__ import annotations
 
+import os
 import uuid
 from typing import Dict, List, Optional, Union
 
@@ -49,6 +50,40 @@ def _native():
     return _native
 
 
+class _ShmSeg:
+    """A POSIX shared-memory segment (/dev/shm) mapped into this process -- created by one rank,
+    opened by name by the others.  No multiprocessing resource tracker: only the creator
+    unlinks, so ranks spawned from one parent cannot unregister each other's segments."""
+
+    def __init__(self, name: str, size: int = 0, create: bool = False):
+        import mmap
+
+        self.name = name.lstrip("/")
+        path = "/dev/shm/" + self.name
+        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
+        fd = os.open(path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, max(1, size))
+            self.size = os.fstat(fd).st_size
+            self.buf = mmap.mmap(fd, self.size)
+        finally:
+            os.close(fd)
+        self.created = create
+
+    def close(self) -> None:
+        try:
+            self.buf.close()
+        except BufferError:  # tensors still view it: the mapping goes with the process
+            pass
+
+    def unlink(self) -> None:
+        try:
+            os.unlink("/dev/shm/" + self.name)
+        except FileNotFoundError:
+            pass
+
+
 class _Shared:
     """Allocate buffers other ranks can map, and open theirs (see module docstring)."""
 
@@ -62,13 +97,11 @@ class _Shared:
     def alloc(self, shape, dtype) -> torch.Tensor:
         if self.device.type == "cuda" or self.threads:
             return torch.zeros(shape, dtype=dtype, device=self.device)
-        from multiprocessing import shared_memory
-
         n = 1
         for s in shape:
             n *= s
         nbytes = max(1, n * torch.tensor([], dtype=dtype).element_size())
-        seg = shared_memory.SharedMemory(create=True, size=nbytes, name=f"psamd_{uuid.uuid4().hex[:20]}")
+        seg = _ShmSeg(f"psamd_{uuid.uuid4().hex[:20]}", nbytes, create=True)
         self._segs.append(seg)
         t = torch.frombuffer(seg.buf, dtype=dtype, count=n).view(*shape)
         t.zero_()
@@ -90,11 +123,8 @@ class _Shared:
         if h[0] == "cuda":
             fn, args = h[1], h[2]
             return fn(*args)
-        from multiprocessing import shared_memory
-
         _, name, shape, dt = h
-        seg = shared_memory.SharedMemory(name=name)
-        _untrack(seg)  # the creating rank owns (and unlinks) it
+        seg = _ShmSeg(name)
         self._opened.append(seg)
         dtype = getattr(torch, dt)
         n = 1
@@ -120,17 +150,6 @@ class _Shared:
                 except Exception:  # noqa: BLE001
                     pass
         self._segs, self._opened = [], []
-
-
-def _untrack(seg) -> None:
-    """Python 3.10 registers ATTACHED segments with the resource tracker too, which would unlink
-    another rank's segment when this process exits."""
-    try:
-        from multiprocessing import resource_tracker
-
-        resource_tracker.unregister(seg._name, "shared_memory")  # noqa: SLF001
-    except Exception:  # noqa: BLE001
-        pass
 
 
 def _addr(seg) -> int:
@@ -194,18 +213,14 @@ class AsyncPS:
         with torch.no_grad():
             self.pub.copy_(self.flat[lo:lo + L].expand(3, L))
         # control block: rank 0 creates the shared segment, everyone maps it
-        from multiprocessing import shared_memory
-
         A = _native().async_ctl
         name = self.t.all_gather_object(f"psamd_ctl_{uuid.uuid4().hex[:16]}" if me == 0 else None)[0]
         if me == 0:
-            self._ctl = shared_memory.SharedMemory(create=True, size=A.SIZE, name=name)
+            self._ctl = _ShmSeg(name, A.SIZE, create=True)
             A.init(_addr(self._ctl), W)
         self.t.barrier()
         if me != 0:
-            self._ctl = shared_memory.SharedMemory(name=name)
-            if self.t.backend != "loopback":  # thread-ranks share the creator's registration
-                _untrack(self._ctl)
+            self._ctl = _ShmSeg(name)
         self.ctl = _addr(self._ctl)
         if not A.valid(self.ctl):
             raise RuntimeError("async PS control block not initialised")
@@ -337,6 +352,38 @@ class AsyncPS:
             torch.cuda.current_stream(self.device).synchronize()
             self.notifier.drain()
 
+    # ------------------------------------------------------------------ checkpoint
+    def shard_state(self) -> dict:
+        """This owner's shard (fp32 master, optimizer state, version) at a QUIESCENT point: every
+        rank calls it at the same step boundary; after the barrier no push is in flight."""
+        self.synchronize()
+        self.t.barrier()
+        st = self.states if self.gpu else [torch.from_numpy(a) for a in self.server.states()]
+        snap = {"rank": self.rank, "world": self.world, "round": self.round, "clock": self.clock,
+                "master": self.master.detach().to("cpu", copy=True),
+                "states": [s.detach().to("cpu", copy=True) for s in st], "staleness": self.staleness}
+        self.t.barrier()
+        return snap
+
+    def load_shard_state(self, st: dict) -> None:
+        if st["world"] != self.world or st["rank"] != self.rank:
+            raise ValueError("checkpoint was written with a different world size / rank")
+        self.synchronize()
+        self.t.barrier()  # every server idle: no push in flight anywhere
+        with torch.no_grad():
+            self.master.copy_(st["master"].to(self.master.device))
+            if self.gpu:
+                for s, src in zip(self.states, st["states"]):
+                    s.copy_(src.to(s.device))
+            else:
+                self.server.set_states([x.numpy() for x in st["states"]])
+            self.pub.copy_(self.master.to(self.dtype).expand(3, self.L))  # every slot = restored shard
+        if self.gpu:
+            torch.cuda.current_stream(self.device).synchronize()
+        self.round = int(st["round"])
+        self.t.barrier()
+        self.refresh()
+
     def refresh(self) -> None:
         """Pull the newest published weights (no staleness gate), e.g. after a final barrier."""
         self._pull_latest()
@@ -364,9 +411,6 @@ class AsyncPS:
         self.server = None
         self.peer_mbox = self.peer_pub = None
         self.share.close(unlink=not self.share.threads)
-        try:
-            self._ctl.close()
-            if self.rank == 0:
-                self._ctl.unlink()
-        except Exception:  # noqa: BLE001
-            pass
+        self._ctl.close()
+        if self.rank == 0:
+            self._ctl.unlink()
