@@ -819,16 +819,29 @@ struct WPlan {
   int tno, tko, tiles, nsplit, rows, groups;
 };
 
-// tile widths 128 where the channel counts allow (a k-tile must not straddle taps), splits so
-// that ~512 blocks run, >= 4 stages per split; > 16 slabs reduce in two fixed-order levels
+// tile widths 128 where the channel counts allow (a k-tile must not straddle taps), >= 4 stages
+// per split; > 16 slabs reduce in two fixed-order levels.  The split count fills WHOLE rounds of
+// the 512 resident blocks (2 per CU): 3x3 layers have 9 k-tiles per channel tile, and rounding
+// the block count UP past 512 (e.g. 9 tiles x 57 splits = 513) made a second round of one block
+// and halved the kernel's throughput.
 WPlan wplan(int M, int N, int K, int C) {
   WPlan w;
   w.tno = N % 128 == 0 ? 2 : 1;
   w.tko = C % 128 == 0 ? 2 : 1;
   w.tiles = (N / (64 * w.tno)) * (K / (64 * w.tko));
   const int chunks = (M + kWM - 1) / kWM;
-  int ns = (512 + w.tiles - 1) / w.tiles;
-  ns = std::max(1, std::min(ns, chunks / 4));
+  const int cap = std::max(1, chunks / 4);
+  int ns = 1;
+  double best = -1.0;
+  for (int rounds = 1; rounds <= 2; ++rounds) {  // one or two full rounds of 512 blocks
+    const int cand = std::max(1, std::min(rounds * 512 / w.tiles, cap));
+    const int blocks = cand * w.tiles;
+    const double eff = static_cast<double>(blocks) / (((blocks + 511) / 512) * 512.0);
+    if (eff > best + 0.02) {
+      best = eff;
+      ns = cand;
+    }
+  }
   w.rows = ((chunks + ns - 1) / ns) * kWM;
   w.nsplit = (M + w.rows - 1) / w.rows;
   w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;

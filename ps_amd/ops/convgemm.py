@@ -7,7 +7,7 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
 
   forward   z1 = conv1(x)            + bn1 statistics        (GEMM epilogue)
             y1 = relu(bn1(z1))                               (one apply pass)
-            z2 = conv2(y1) [MIOpen]    bn2 statistics        (one pass)
+            z2 = conv2(y1)           + bn2 statistics        (GEMM epilogue)
             z3 = conv3(relu(bn2(z2))) + bn3 statistics       (bn2 + ReLU in the GEMM prologue:
                                                               bn2's output is never written)
             zd = downsample(x)       + bn_d statistics       (stride-2 rows gathered in-kernel)
@@ -16,7 +16,8 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
             also the identity-branch gradient, recomputed from (dout, bits) where consumed
             conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
             with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
-            conv2 backward [MIOpen], bn1 backward
+            conv2 data grad (stride 1) -> ReLU mask + bn1 backward sums (GEMM epilogue), weight
+            grad [MIOpen]; stride-2 conv2 backward [MIOpen] + bn1 backward
             conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
             epilogue), weight grads.
 
@@ -96,6 +97,21 @@ def _mat(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(w.shape[0], w.shape[1])
 
 
+def _mat3(w: torch.Tensor) -> torch.Tensor:
+    """3x3 conv weight [N, C, 3, 3] -> [N, 9C] in (kh, kw, c) order (a view for channels_last)."""
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
+def _mat3_dgrad(w: torch.Tensor) -> torch.Tensor:
+    """The weight of the stride-1 3x3 data gradient as a forward conv over dz: wt[c][kh][kw][n] =
+    w[n][c][2 - kh][2 - kw] -> [C, 9N]."""
+    return w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1)
+
+
+def _conv3x3_enabled() -> bool:
+    return os.environ.get("PS_AMD_CONV3X3", "1") != "0"
+
+
 class _Link:
     """bn3 backward hand-off from block i (consumer of this block's output) to this block."""
 
@@ -131,10 +147,15 @@ class _BottleneckFn(torch.autograd.Function):
         z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
         m1, i1, cf1 = _finalize(p1, k1, n * h * w, bn1)
         y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)[0]
-        z2 = F.conv2d(image(y1, n, h, w), w2, None, s, 1)
-        z2r = rows(z2)
-        m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
-                                   float(bn2.eps))
+        if _conv3x3_enabled():
+            # our implicit GEMM (LDS-DMA staging at this depth) with bn2's statistics in the epilogue
+            k2 = bn2.running_mean
+            z2r, p2s = nat.conv_gemm(y1, _mat3(w2), geo(h, w, 3, s, 1), None, 1, None, k2)
+            m2, i2, cf2 = _finalize(p2s, k2, n * oh * ow, bn2)
+        else:
+            z2r = rows(F.conv2d(image(y1, n, h, w), w2, None, s, 1))
+            m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
+                                       float(bn2.eps))
         k3 = bn3.running_mean
         z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
         m3, i3, cf3 = _finalize(p3, k3, n * oh * ow, bn3)
@@ -181,10 +202,19 @@ class _BottleneckFn(torch.autograd.Function):
         gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
         dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
-        dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
-                                                          [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                          [True, True, False])
-        dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
+        if s == 1 and _conv3x3_enabled():
+            # data grad = the forward GEMM over dz2 with the flipped, transposed weight; its epilogue
+            # applies bn1's ReLU mask and reduces bn1's backward sums (no separate reduce pass)
+            gy1, p1b = nat.conv_gemm(dz2, _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1, None, cf1, m1, i1)
+            dw2 = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
+                                                      [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                      [False, True, False])[1]
+            dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
+        else:
+            dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
+                                                              [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                              [True, True, False])
+            dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
         w1t = _mat(w1).t()
         dwd = dgd = dbd = None
         li = ctx.link_in

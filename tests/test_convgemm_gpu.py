@@ -239,14 +239,17 @@ def test_bn_apply_coef_and_backward_from_partials():
     torch.testing.assert_close(dg.cpu(), (gr * xhat).sum(0), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("conv3x3", ["1", "0"])
 @pytest.mark.parametrize("inplanes,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2)])
-def test_fused_bottleneck_matches_module_path(inplanes, planes, stride):
+def test_fused_bottleneck_matches_module_path(inplanes, planes, stride, conv3x3, monkeypatch):
+    """Fused block (3x3 conv on our GEMMs or, PS_AMD_CONV3X3=0, on MIOpen) vs module path."""
     import torch.nn as nn
 
     from ps_amd.models.resnet import Bottleneck, prepare_for_mi355x
     from ps_amd.ops.bn import BatchNormAct2d
     from ps_amd.ops.convgemm import fused_block_ok
 
+    monkeypatch.setenv("PS_AMD_CONV3X3", conv3x3)
     torch.manual_seed(0)
     ds = None
     if stride != 1 or inplanes != planes * 4:
@@ -384,3 +387,29 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
     _close(ga, gb, tol=1e-2, amax=0.05)
     for n in pb:
         _close(pa[n], pb[n], tol=1e-2, amax=0.05)
+
+
+@pytest.mark.parametrize("n,h,w,C1,C2", [(3, 15, 13, 64, 64), (2, 9, 9, 128, 256)])
+def test_conv3x3_data_grad_with_bn_backward_sums(n, h, w, C1, C2):
+    """Stride-1 3x3 data gradient as the forward GEMM over dz with the flipped / transposed
+    weight (ops/convgemm._mat3_dgrad), epilogue 3: the ReLU mask of the bn1 output recomputed
+    from z1 and bn1's backward sums -- vs fp32 torch (conv2d_input)."""
+    from ps_amd.ops.convgemm import _mat3_dgrad
+
+    g = _gen(n * h + C1 + C2)
+    wt = _rnd(C2, C1, 3, 3, g=g, scale=(9 * C1) ** -0.5)
+    dz = _rnd(n, h, w, C2, g=g)
+    z1 = _rnd(n, h, w, C1, g=g)
+    coef = _coef(C1, g)
+    mean, invstd = torch.randn(C1, generator=g) * 0.1, torch.rand(C1, generator=g) + 0.5
+    dy = torch.nn.grad.conv2d_input((n, C1, h, w), wt, dz.permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    on = (z1 * coef[:C1] + coef[C1:]) > 0
+    gref = (dy.bfloat16().float() * on).reshape(-1, C1)
+    wd = _mat3_dgrad(_bf(wt))
+    c, part = native().conv_gemm(_bf(dz).reshape(-1, C2), wd, geo(h, w, 3, 1, 1), None, 3,
+                                 _bf(z1).reshape(-1, C1), None, coef.to(DEV), mean.to(DEV), invstd.to(DEV))
+    _close(c, gref)
+    gc = c.float().cpu()
+    xhat = (z1.reshape(-1, C1) - mean) * invstd
+    torch.testing.assert_close(part[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=2e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=2e-2)
