@@ -1077,7 +1077,9 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   TORCH_CHECK(M == gi.second * g.OH * g.OW, "dz rows must be images * OH * OW");
   TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
   const c10::DeviceGuard guard(dz.device());
-  auto ws = torch::empty({psamd::conv_wgrad_ws(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), g.C)},
+  const float* prop = f32_opt(pro, 2 * g.C, "pro");
+  auto ws = torch::empty({psamd::conv_wgrad_ws(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), g.C,
+                                               prop != nullptr)},
                          dz.options().dtype(torch::kFloat32));
   auto dw = torch::empty({N, K}, dz.options());
   psamd::ConvWgradArgs p{};
@@ -1087,7 +1089,7 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   p.N = static_cast<int>(N);
   p.K = static_cast<int>(K);
   p.g = g;
-  p.pro = f32_opt(pro, 2 * g.C, "pro");
+  p.pro = prop;
   p.ws = ws.data_ptr<float>();
   p.dw = u16m(dw);
   psamd::launch_conv_wgrad(p, cur_stream(dz));

@@ -266,7 +266,7 @@ struct ConvWgradArgs {
   float* ws;            // conv_wgrad_ws(M, N, K, C) floats
   uint16_t* dw;         // [N, K] bf16
 };
-int64_t conv_wgrad_ws(int M, int N, int K, int C);
+int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
 // BN helpers for the fused bottleneck (bn_act.hip): y = act(x*scale + shift [+ res [* rscale + rshift]])
 // mbits (nullable): also write the ReLU mask of y, 1 bit per element

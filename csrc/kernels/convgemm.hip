@@ -34,6 +34,7 @@
 // fixed channel tile per block), so the statistics accumulate in registers across pixel tiles
 // and the BN finalize kernels sum only [2][blocks][N] partials in fixed order.
 #include <algorithm>
+#include <cstdlib>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -101,10 +102,12 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // [64][RL] tiles read transposed (ds_read_b64_tr_b16): a 32-lane half reads rows r0..r0+3 x 64
 // contiguous bytes; the chunk XOR gives each of the 4 rows its own quarter of the bank row.
 template <int RL>
+__device__ __forceinline__ int tr_swz(int r) {
+  return RL >= 128 ? (r & 3) << 2 : ((r >> 1) & 1) << 2;  // rows of >= 256 B / 128 B
+}
+template <int RL>
 __device__ __forceinline__ int tr_off(int r, int col) {
-  const int c = col >> 3;
-  const int pc = RL == 128 ? (c ^ ((r & 3) << 2)) : (c ^ (((r >> 1) & 1) << 2));
-  return r * RL + pc * 8 + (col & 7);
+  return r * RL + ((col >> 3) ^ tr_swz<RL>(r)) * 8 + (col & 7);
 }
 
 // 32x32x16 MFMA operand from a [64][RL] tile read transposed: lane l receives
@@ -736,6 +739,169 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
       }
 }
 
+// ------------------------------------------------------------------------------ conv_wgrad (wide)
+// The weight gradient is L2-bandwidth bound at 128 x 128 tiles (64 FLOP per staged byte, one
+// block round of 2 x 4 waves per CU): this variant runs ONE 8-wave block per CU on a BNO x BKO
+// tile of up to 256 x 256 (128 FLOP / byte), WN x WK waves of (32 TN) x (32 TK) each, 32-pixel
+// stages through a 4-deep LDS ring filled by LDS-DMA (stage t + 3 in flight while t computes, one
+// barrier per stage).  The X tile's 16-B chunks carry their own tap, so a k-tile may span taps
+// (3x3 layers with C < BKO).  PRO (1x1 only): the BN + ReLU prologue is applied to the X
+// fragments in registers -- a fragment is 8 pixels of ONE channel, so one scale / shift per lane;
+// rows past the split read zeros from dz, so their transformed X never contributes.
+constexpr int kWP = 32;  // pixels per stage
+constexpr int kWS = 4;   // LDS ring depth
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 12, "vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int TN, int TK, int WN, int WK, bool PRO>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgradArgs p, int rows_per_split) {
+  constexpr int BNO = WN * 32 * TN, BKO = WK * 32 * TK;
+  static_assert(WN * WK == 8, "8 waves");
+  constexpr int STAGE = kWP * (BNO + BKO);
+  constexpr int GCPR = BNO / 8, XCPR = BKO / 8;                // 16-B chunks per tile row
+  constexpr int GI = kWP * GCPR / 512, XI = kWP * XCPR / 512;  // DMA instructions per wave per stage
+  constexpr int PER = GI + XI;
+  static_assert(GI >= 1 && XI >= 1 && kWP * GCPR % 512 == 0 && kWP * XCPR % 512 == 0, "tile / stage shape");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWS * STAGE];
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ntk = p.K / BKO, tiles = (p.N / BNO) * ntk;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, tile = L - split * tiles;
+  const int tn = tile / ntk;
+  const int n0 = tn * BNO, k0 = (tile - tn * ntk) * BKO;
+  const int mb = split * rows_per_split;
+  const int me = min(p.M, mb + rows_per_split);
+  const int nst = me > mb ? (me - mb + kWP - 1) / kWP : 0;  // block-uniform
+
+  // per-lane DMA sources: tile row and (swizzled) logical chunk of each instruction
+  int grow[GI], gcol[GI], xrow[XI], xkh[XI], xkw[XI], xcc[XI];
+#pragma unroll
+  for (int i = 0; i < GI; ++i) {
+    const int Lc = (wave * GI + i) * 64 + lane, r = Lc / GCPR, pc = Lc % GCPR;
+    grow[i] = r;
+    gcol[i] = n0 + (pc ^ tr_swz<BNO>(r)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int Lc = (wave * XI + i) * 64 + lane, r = Lc / XCPR, pc = Lc % XCPR;
+    const int k = k0 + (pc ^ tr_swz<BKO>(r)) * 8, tap = k / g.C;
+    xrow[i] = r;
+    xcc[i] = k - tap * g.C;
+    xkh[i] = tap / g.ks;
+    xkw[i] = tap - xkh[i] * g.ks;
+  }
+  auto issue = [&](int st, int buf) {
+    const int mc = mb + st * kWP;
+    uint16_t* Gs = lds + buf * STAGE;
+    uint16_t* Xs = Gs + kWP * BNO;
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int m = mc + grow[i];
+      const uint16_t* src = m < me ? p.dz + static_cast<int64_t>(m) * p.N + gcol[i] : kZeroPage;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Gs + (wave * GI + i) * 512), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int m = mc + xrow[i];
+      const PixSrc ps = pix_src(m < me ? m : p.M, p.M, g);
+      const int64_t o = tap_off(ps, xkh[i], xkw[i], xcc[i], g);
+      const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
+    }
+  };
+
+  const int wn = (wave / WK) * (32 * TN), wk = (wave % WK) * (32 * TK);
+  float psc[TK], psh[TK];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < TK; ++j) {
+      const int c = (k0 + wk + 32 * j + (lane & 31)) % g.C;
+      psc[j] = p.pro[c];
+      psh[j] = p.pro[g.C + c];
+    }
+  }
+  f32x16 acc[TN][TK];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  auto mma = [&](int buf) {
+    const uint16_t* Gs = lds + buf * STAGE;
+    const uint16_t* Xs = Gs + kWP * BNO;
+#pragma unroll
+    for (int s = 0; s < kWP / 16; ++s) {
+      bf16x8_t ga[TN], xb[TK];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) ga[i] = tr_frag_asm<BNO>(Gs, s, wn + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < TK; ++j) xb[j] = tr_frag_asm<BKO>(Xs, s, wk + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) asm volatile("" : "+v"(ga[i]));
+#pragma unroll
+      for (int j = 0; j < TK; ++j) asm volatile("" : "+v"(xb[j]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < TN; ++i) asm volatile("" : "+v"(ga[i]));
+#pragma unroll
+      for (int j = 0; j < TK; ++j) asm volatile("" : "+v"(xb[j]));
+      if constexpr (PRO) {
+#pragma unroll
+        for (int j = 0; j < TK; ++j) {
+          u16x8 v = __builtin_bit_cast(u16x8, xb[j]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = bf16_to_f32(v[e]) * psc[j] + psh[j];
+            v[e] = f32_to_bf16(f > 0.f ? f : 0.f);
+          }
+          xb[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int pre = nst < kWS - 1 ? nst : kWS - 1;
+  for (int st = 0; st < pre; ++st) issue(st, st);
+  for (int st = 0; st < nst; ++st) {
+    // this wave's DMAs of stage st landed (later stages may stay in flight), then everyone's
+    const int ahead = min(kWS - 2, nst - 1 - st);
+    if (ahead >= 2) wait_vmcnt<2 * PER>();
+    else if (ahead == 1) wait_vmcnt<PER>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
+    if (st + kWS - 1 < nst) issue(st + kWS - 1, (st + kWS - 1) % kWS);
+    mma(st % kWS);
+  }
+  float* sl = p.ws + static_cast<int64_t>(split) * p.N * p.K;
+  const int h = lane >> 5, kl = lane & 31;
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int n = n0 + wn + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+        sl[static_cast<int64_t>(n) * p.K + k0 + wk + 32 * j + kl] = acc[i][j][q];
+      }
+}
+
 // out[y][e] = sum_{b in [y*per, y*per + per)} in[b][e] in fixed order (bf16 or fp32 out)
 template <bool BF16>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int nslab, int per, int64_t E,
@@ -817,57 +983,95 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
 namespace {
 struct WPlan {
   int tno, tko, tiles, nsplit, rows, groups;
+  int wide;  // 0: conv_wgrad_kernel; wide tiles 1: 256 x 256, 2: 256 x 128, 3: 128 x 256, 4: 128 x 384
 };
 
-// tile widths 128 where the channel counts allow (a k-tile must not straddle taps), >= 4 stages
-// per split; > 16 slabs reduce in two fixed-order levels.  The split count fills WHOLE rounds of
-// the 512 resident blocks (2 per CU): 3x3 layers have 9 k-tiles per channel tile, and rounding
-// the block count UP past 512 (e.g. 9 tiles x 57 splits = 513) made a second round of one block
-// and halved the kernel's throughput.
-WPlan wplan(int M, int N, int K, int C) {
-  WPlan w;
-  w.tno = N % 128 == 0 ? 2 : 1;
-  w.tko = C % 128 == 0 ? 2 : 1;
-  w.tiles = (N / (64 * w.tno)) * (K / (64 * w.tko));
-  const int chunks = (M + kWM - 1) / kWM;
-  const int cap = std::max(1, chunks / 4);
+bool wide_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_WGRAD_WIDE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// Split count that fills WHOLE rounds of `slots` resident blocks (one or two rounds), at most
+// `cap` splits: rounding the block count up past a round (e.g. 9 tiles x 57 splits = 513 of 512)
+// adds a round of one block and halves the kernel's throughput.
+int fill_rounds(int tiles, int slots, int cap) {
   int ns = 1;
   double best = -1.0;
-  for (int rounds = 1; rounds <= 2; ++rounds) {  // one or two full rounds of 512 blocks
-    const int cand = std::max(1, std::min(rounds * 512 / w.tiles, cap));
-    const int blocks = cand * w.tiles;
-    const double eff = static_cast<double>(blocks) / (((blocks + 511) / 512) * 512.0);
+  for (int rounds = 1; rounds <= 2; ++rounds) {
+    const int cand = std::max(1, std::min(rounds * slots / tiles, cap));
+    const int blocks = cand * tiles;
+    const double eff = static_cast<double>(blocks) / (((blocks + slots - 1) / slots) * static_cast<double>(slots));
     if (eff > best + 0.02) {
       best = eff;
       ns = cand;
     }
   }
-  w.rows = ((chunks + ns - 1) / ns) * kWM;
+  return ns;
+}
+
+// Wide tiles (one 8-wave block per CU) where N and K allow a 256-wide side and the prologue, if
+// any, is on a 1x1 layer; else 64 / 128 tiles (a k-tile must not straddle taps), 2 blocks per CU.
+// >= 4 (8 for wide) stages per split; > 16 slabs reduce in two fixed-order levels.
+WPlan wplan(int M, int N, int K, int C, bool pro) {
+  WPlan w{};
+  const bool ks1 = K == C;
+  int bno = N % 256 == 0 ? 256 : 128, bko = K % 256 == 0 ? 256 : 128;
+  if (bno == 128 && bko == 128 && K % 384 == 0) bko = 384;  // 3x3 at C = 128: 3 taps per k-tile
+  if (wide_enabled() && (!pro || ks1) && N % 128 == 0 && K % 128 == 0 && C % 8 == 0 && (bno == 256 || bko > 128)) {
+    w.wide = bno == 256 ? (bko == 256 ? 1 : 2) : bko == 256 ? 3 : 4;
+    w.tiles = (N / bno) * (K / bko);
+    const int chunks = (M + kWP - 1) / kWP;
+    const int ns = fill_rounds(w.tiles, 256, std::max(1, chunks / 8));
+    w.rows = ((chunks + ns - 1) / ns) * kWP;
+  } else {
+    w.tno = N % 128 == 0 ? 2 : 1;
+    w.tko = C % 128 == 0 ? 2 : 1;
+    w.tiles = (N / (64 * w.tno)) * (K / (64 * w.tko));
+    const int chunks = (M + kWM - 1) / kWM;
+    const int ns = fill_rounds(w.tiles, 512, std::max(1, chunks / 4));
+    w.rows = ((chunks + ns - 1) / ns) * kWM;
+  }
   w.nsplit = (M + w.rows - 1) / w.rows;
   w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;
   return w;
 }
 }  // namespace
 
-int64_t conv_wgrad_ws(int M, int N, int K, int C) {
-  const WPlan w = wplan(M, N, K, C);
+int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro) {
+  const WPlan w = wplan(M, N, K, C, pro);
   return static_cast<int64_t>(w.nsplit + w.groups) * N * K;
 }
 
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
-  const WPlan w = wplan(a.M, a.N, a.K, a.g.C);
+  const WPlan w = wplan(a.M, a.N, a.K, a.g.C, a.pro != nullptr);
   const int nblk = w.tiles * w.nsplit;
+#define PSAMD_CWW(TN, TK, WN, WK)                                                                                 \
+  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true>), dim3(nblk), dim3(512), 0, s, a, \
+                                w.rows);                                                                        \
+  else hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false>), dim3(nblk), dim3(512), 0, s, a, w.rows)
 #define PSAMD_CW(TN, TK, PRO, GL) \
   hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO, GL>), dim3(nblk), dim3(256), 0, s, a, w.rows)
   // without the prologue both operands are plain row slices: LDS-DMA staging
 #define PSAMD_CWP(TN, TK) \
   if (a.pro) { PSAMD_CW(TN, TK, true, false); } else { PSAMD_CW(TN, TK, false, true); }
-  if (w.tno == 2) {
+  if (w.wide == 1) {
+    PSAMD_CWW(2, 4, 4, 2);
+  } else if (w.wide == 2) {
+    PSAMD_CWW(2, 2, 4, 2);
+  } else if (w.wide == 3) {
+    PSAMD_CWW(2, 2, 2, 4);
+  } else if (w.wide == 4) {
+    PSAMD_CWW(2, 3, 2, 4);
+  } else if (w.tno == 2) {
     if (w.tko == 2) { PSAMD_CWP(2, 2) } else { PSAMD_CWP(2, 1) }
   } else {
     if (w.tko == 2) { PSAMD_CWP(1, 2) } else { PSAMD_CWP(1, 1) }
   }
+#undef PSAMD_CWW
 #undef PSAMD_CWP
 #undef PSAMD_CW
   const int64_t E = static_cast<int64_t>(a.N) * a.K;

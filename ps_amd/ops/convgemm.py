@@ -17,7 +17,7 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
             conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
             with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
             conv2 data grad (stride 1) -> ReLU mask + bn1 backward sums (GEMM epilogue), weight
-            grad [MIOpen]; stride-2 conv2 backward [MIOpen] + bn1 backward
+            grad (C >= 128; MIOpen below); stride-2 conv2 data grad [MIOpen] + bn1 backward
             conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
             epilogue), weight grads.
 
@@ -106,6 +106,9 @@ def _mat3_dgrad(w: torch.Tensor) -> torch.Tensor:
     """The weight of the stride-1 3x3 data gradient as a forward conv over dz: wt[c][kh][kw][n] =
     w[n][c][2 - kh][2 - kw] -> [C, 9N]."""
     return w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1)
+
+
+WGRAD3X3_MIN_C = 256
 
 
 def _conv3x3_enabled() -> bool:
@@ -202,18 +205,24 @@ class _BottleneckFn(torch.autograd.Function):
         gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
         dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
-        if s == 1 and _conv3x3_enabled():
+        c1 = w2.shape[1]
+        ours_dgrad = s == 1 and _conv3x3_enabled()
+        # weight grad on the wide-tile kernel from 256 input channels up (on par with / faster than
+        # MIOpen there; at 64 / 128 channels MIOpen's is faster: profiles/r2_wgrad_probe.jsonl)
+        ours_wgrad = _conv3x3_enabled() and c1 >= WGRAD3X3_MIN_C
+        dy1 = dw2 = None
+        if not (ours_dgrad and ours_wgrad):
+            dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
+                                                              [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                              [not ours_dgrad, not ours_wgrad, False])
+        if ours_wgrad:
+            dw2 = nat.conv_wgrad(dz2, y1, geo(h, w, 3, s, 1)).view(w2.shape[0], 3, 3, c1).permute(0, 3, 1, 2)
+        if ours_dgrad:
             # data grad = the forward GEMM over dz2 with the flipped, transposed weight; its epilogue
             # applies bn1's ReLU mask and reduces bn1's backward sums (no separate reduce pass)
             gy1, p1b = nat.conv_gemm(dz2, _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1, None, cf1, m1, i1)
-            dw2 = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
-                                                      [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                      [False, True, False])[1]
             dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
-            dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
-                                                              [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                              [True, True, False])
             dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
         w1t = _mat(w1).t()
         dwd = dgd = dbd = None

@@ -1,0 +1,10 @@
+#!/bin/bash
+# rocprofv3 kernel trace of the default ResNet-50 bench step (bs1024) + per-family breakdown
+# usage: scripts/gpu_prof_step.sh OUTDIR
+O=${1:-gpurun_out/pstep}
+mkdir -p $O
+export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
+R=$PWD
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python $R/bench.py --steps 6 --warmup 3 > $R/$O/prof.log 2>&1 || exit $?
+cd $R && python scripts/step_breakdown.py $(ls $O/prof/*kernel_trace.csv | head -1) > $O/breakdown.txt
+head -45 $O/breakdown.txt

@@ -132,6 +132,28 @@ def test_conv3x3_implicit_gemm_forward_and_wgrad(cin, cout, hw, stride, pro):
     _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, 9 * cin))
 
 
+@pytest.mark.parametrize("ks,cin,cout,hw,stride,pro", [
+    (1, 256, 256, 9, 1, False), (1, 256, 256, 9, 1, True), (1, 128, 512, 7, 1, True), (1, 512, 128, 7, 1, False),
+    (1, 256, 512, 11, 2, False), (3, 256, 256, 7, 1, False), (3, 256, 256, 9, 2, False), (3, 512, 256, 5, 1, False),
+    (3, 128, 128, 9, 1, False), (3, 128, 128, 11, 2, False)])
+def test_wide_wgrad_kernel(ks, cin, cout, hw, stride, pro):
+    """conv_wgrad on the 8-wave 256 x 256 / 256 x 128 / 128 x 256 tiles (4-deep LDS-DMA ring,
+    32-pixel stages, BN prologue on the X fragments for 1x1) vs fp32 autograd; pixel counts
+    are not multiples of the 32-pixel stage."""
+    n = 5
+    g = _gen(ks * 1000 + cin + cout + hw + stride + pro)
+    x = _rnd(n, hw, hw, cin, g=g)
+    coef = _coef(cin, g) if pro else None
+    xin = _bn_relu(x, coef) if pro else x
+    gg = geo(hw, hw, ks, stride, ks // 2)
+    dz = _rnd(n * gg[2] * gg[3], cout, g=g)
+    wv = torch.zeros(cout, cin, ks, ks, requires_grad=True)
+    yr = F.conv2d(xin.permute(0, 3, 1, 2), wv, None, stride, ks // 2)
+    dw_ref = torch.autograd.grad(yr, wv, dz.view(n, gg[2], gg[3], cout).permute(0, 3, 1, 2))[0]
+    dw = native().conv_wgrad(_bf(dz), _bf(x.reshape(-1, cin)), gg, coef.to(DEV) if pro else None)
+    _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, ks * ks * cin))
+
+
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5])
 def test_deep_k_lds_dma_path_all_epilogues(epi):
     """K % 256 == 0, 128-channel tiles, no prologue: the LDS-DMA kernel with fragment-packed
@@ -240,7 +262,7 @@ def test_bn_apply_coef_and_backward_from_partials():
 
 
 @pytest.mark.parametrize("conv3x3", ["1", "0"])
-@pytest.mark.parametrize("inplanes,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2)])
+@pytest.mark.parametrize("inplanes,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2), (512, 128, 1)])
 def test_fused_bottleneck_matches_module_path(inplanes, planes, stride, conv3x3, monkeypatch):
     """Fused block (3x3 conv on our GEMMs or, PS_AMD_CONV3X3=0, on MIOpen) vs module path."""
     import torch.nn as nn
