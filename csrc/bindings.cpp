@@ -1038,7 +1038,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   const c10::DeviceGuard guard(a.device());
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
-  const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K)).gm;
+  const bool has_pro = pro.has_value() && pro->defined();
+  const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), has_pro).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;

@@ -249,12 +249,12 @@ struct ConvGemmArgs {
   const float* mc;      // epi 3: [scale | shift] (2N) of that BN (ReLU mask)
   const float* mean;    // epi 3/6-8: [N]
   const float* invstd;  // epi 3/6-8: [N]
-  float* part;          // epi 1/3/6-8: [2][conv_fwd_plan(M, N, K).gm][N] block partial sums
+  float* part;          // epi 1/3/6-8: [2][conv_fwd_plan(M, N, K, pro).gm][N] block partial sums
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
-ConvFwdPlan conv_fwd_plan(int M, int N, int K);
+ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 
 struct ConvWgradArgs {

@@ -924,21 +924,32 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------------------ launchers
-// Forward tile plan.  HBM-bound shallow-K layers (<= 2 stages) run a persistent grid of 2 blocks
-// per CU (cross-tile prefetch, statistics kept in registers); deeper K runs one block per tile
-// so the hardware balances the tail.
-ConvFwdPlan conv_fwd_plan(int M, int N, int K) {
+// Forward tile plan.  HBM-bound shallow-K layers (<= 2 stages; <= 4 with the BN prologue, whose
+// register staging gains most from the cross-tile prefetch: scripts/probe_conv_fwd.py) run a
+// persistent grid of 2 blocks per CU (statistics kept in registers); deeper K runs one block per
+// tile so the hardware balances the tail.
+int persist_nk_pro() {
+  static const int v = [] {
+    const char* e = std::getenv("PS_AMD_PERSIST_NK_PRO");
+    return e ? std::atoi(e) : 4;  // 4-stage PRO layers: cross-tile prefetch pays (L3 conv3 -8%)
+  }();
+  return v;
+}
+
+ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   ConvFwdPlan pl;
   pl.bn = N % 128 == 0 ? 128 : 64;
   const int nN = N / pl.bn;
   pl.bm = 128;  // (64-pixel tiles measured slower on every ResNet-50 shape: scripts/probe_convgemm.py)
-  pl.gm = K / kBK > 2 ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
+  const int nk = K / kBK;
+  const bool persist = nk <= 2 || (pro && nk <= persist_nk_pro());
+  pl.gm = !persist ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
   return pl;
 }
 
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
-  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K);
+  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K, a.pro != nullptr);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   const bool ks1 = a.g.ks == 1;
