@@ -56,6 +56,9 @@ def parse():
                          "ResNet-50: 32.7 vs 31.6 ms, profiles/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--comm-probe", type=int, default=1,
+                    help="world > 1: after the timed region, measure RS / AG / AR bandwidth (ps_amd/parallel/"
+                         "comm_probe.py) and report it in the JSON config")
     ap.add_argument("--checkpoint-dir", type=str, default=os.environ.get("PS_AMD_CHECKPOINT_DIR", ""),
                     help="after the timed region: one sharded checkpoint of every rank's server shard (timed, "
                          "reported on stderr) -- utils/checkpoint.py")
@@ -163,17 +166,32 @@ def main():
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
     value = bench.samples_per_step * world * args.steps / elapsed
-    if args.timing and getattr(bench.engine, "timing_summary", None) is not None:
+    # after the timed region: per-phase PS timing (default 3 steps at world > 1, so the driver's
+    # multi-GPU lines show how much of the push / pull the backward hides) and the collective
+    # bandwidth curve of this node's RCCL / xGMI plane
+    tsum = comm = None
+    n_timing = args.timing if args.timing else (3 if world > 1 else 0)
+    if n_timing and getattr(bench.engine, "timing_summary", None) is not None and not use_graph:
         eng = bench.engine
-        eng.timing = True
-        eng._mark("step0")
-        for _ in range(args.timing):
-            step()
-        torch.cuda.synchronize()
-        tsum = eng.timing_summary()
-        if rank == 0:
-            print("[bench-timing] " + json.dumps({k: round(v, 3) for k, v in tsum.items()}), file=sys.stderr,
-                  flush=True)
+        try:
+            eng.timing = True
+            eng._mark("step0")
+            for _ in range(n_timing):
+                step()
+            torch.cuda.synchronize()
+            tsum = {k: round(v, 3) for k, v in eng.timing_summary().items()}
+        except Exception as e:  # diagnostics only: never lose the measured line
+            print(f"[bench-timing] failed: {e!r}", file=sys.stderr, flush=True)
+        eng.timing = False
+        if rank == 0 and tsum:
+            print("[bench-timing] " + json.dumps(tsum), file=sys.stderr, flush=True)
+    if world > 1 and args.comm_probe:
+        from ps_amd.parallel.comm_probe import probe
+
+        try:
+            comm = probe(dev)
+        except Exception as e:
+            print(f"[bench-comm-probe] failed: {e!r}", file=sys.stderr, flush=True)
     if args.checkpoint_dir and getattr(bench.engine, "shard_state", None) is not None:
         from ps_amd.utils.checkpoint import CheckpointManager
 
@@ -199,6 +217,10 @@ def main():
         cfg["hip_graph"] = bool(use_graph)
         cfg["final_loss"] = round(float(loss.item()), 4)
         cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        if tsum:
+            cfg["ps_phase_ms_per_step"] = tsum  # measured after the timed region
+        if comm:
+            cfg["rccl_probe"] = comm  # measured after the timed region
         rec = {
             "metric": bench.metric,
             "value": round(value, 2),

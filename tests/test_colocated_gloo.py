@@ -166,3 +166,22 @@ def test_split_communicators_loopback_world3():
     b = run_loopback(_split_body, 3, True, None, [_split_model() for _ in range(3)])
     for k in a[0]:
         assert torch.equal(a[0][k], b[0][k])
+
+
+def _probe_body(tp):
+    from ps_amd.parallel.comm_probe import probe
+
+    return probe(torch.device("cpu"), sizes_mb=(0.25, 1), iters=2, dtype=torch.float32)
+
+
+def test_comm_probe_world2():
+    """bench.py's after-the-timed-region collective probe: same result structure on every rank,
+    MAX-over-ranks times (identical), busbw = algbw * (n-1)/n for RS / AG, 2(n-1)/n for AR."""
+    res = dist_util.run(_probe_body, 2, ())
+    assert res[0] == res[1]
+    for name in ("reduce_scatter", "all_gather", "all_reduce"):
+        for size in ("0.25MB", "1MB"):
+            r = res[0][name][size]
+            assert r["us"] > 0 and r["algbw_GBps"] >= 0
+            fac = 1.0 if name == "all_reduce" else 0.5
+            assert abs(r["busbw_GBps"] - r["algbw_GBps"] * fac) <= 0.11
