@@ -179,7 +179,7 @@ def test_comm_probe_world2():
     MAX-over-ranks times (identical), busbw = algbw * (n-1)/n for RS / AG, 2(n-1)/n for AR."""
     res = dist_util.run(_probe_body, 2, ())
     assert res[0] == res[1]
-    for name in ("reduce_scatter", "all_gather", "all_reduce"):
+    for name in ("reduce_scatter", "all_gather", "all_reduce", "reduce_scatter_direct", "all_gather_direct"):
         for size in ("0.25MB", "1MB"):
             r = res[0][name][size]
             assert r["us"] > 0 and r["algbw_GBps"] >= 0
