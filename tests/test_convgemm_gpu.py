@@ -29,6 +29,16 @@ def _close(out, ref, tol=1e-2, amax=0.05):
     assert (out - ref).abs().max().item() <= amax * ref.abs().max().item() + 1e-3
 
 
+def _close_flips(out, ref, tol, amax, frac=5e-4):
+    """_close with the max-abs bound on all but a fraction ``frac`` of the elements."""
+    out = out.float().cpu()
+    ref = ref.float().cpu()
+    err = ((out - ref).norm() / ref.norm().clamp_min(1e-12)).item()
+    assert err < tol, f"relative error {err:.3g}"
+    bad = ((out - ref).abs() > amax * ref.abs().max() + 1e-3).float().mean().item()
+    assert bad <= frac, f"{bad:.2e} of the elements off by more than {amax} x max"
+
+
 def _gen(seed):
     return torch.Generator().manual_seed(seed)
 
@@ -293,7 +303,9 @@ def test_fused_bottleneck_matches_module_path(inplanes, planes, stride, conv3x3,
     gout = torch.randn_like(ya)
     ya.backward(gout)
     yb.backward(gout)
-    _close(xa.grad, xb.grad, tol=3e-2, amax=0.25)  # bf16 ReLU-mask flips near 0 differ per path
+    # bf16 ReLU-mask flips near 0 differ per path (and per MIOpen solver choice): a flipped
+    # element may differ by O(its own magnitude), so the max-abs bound is on all but 0.05 %
+    _close_flips(xa.grad, xb.grad, tol=3e-2, amax=0.25)
     for (name, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
         assert p.grad is not None, name
         _close(p.grad, q.grad, tol=3e-2, amax=0.25)
