@@ -659,6 +659,56 @@ std::vector<Tensor> layernorm_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean
   return {dx, dout, dg, db};
 }
 
+// Fused short-sequence attention (attention.hip): qkv [B, S, 3 * H * 64] -> [out [B, S, H * 64], lse [B, H, S]]
+static void check_attn(const Tensor& qkv, int64_t heads) {
+  check_rows(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3 && heads > 0 && qkv.size(2) == 3 * heads * 64, "qkv [B, S, 3 * heads * 64]");
+  const int64_t S = qkv.size(1);
+  TORCH_CHECK(S > 0 && S % 32 == 0 && S <= 128, "sequence length a multiple of 32, <= 128");
+  TORCH_CHECK(qkv.size(0) * heads < (int64_t(1) << 31), "batch * heads");
+}
+
+std::vector<Tensor> attn_fwd(Tensor qkv, int64_t heads, double p, int64_t seed) {
+  check_attn(qkv, heads);
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p in [0, 1)");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  const c10::DeviceGuard guard(qkv.device());
+  auto out = torch::empty({B, S, heads * 64}, qkv.options());
+  auto lse = torch::empty({B, heads, S}, qkv.options().dtype(torch::kFloat32));
+  psamd::launch_attn_fwd(u16(qkv), u16m(out), lse.data_ptr<float>(), static_cast<int>(B), static_cast<int>(S),
+                         static_cast<int>(heads), 0.125f, static_cast<float>(p), static_cast<uint64_t>(seed),
+                         cur_stream(qkv));
+  return {out, lse};
+}
+
+Tensor attn_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, int64_t heads, double p, int64_t seed) {
+  check_attn(qkv, heads);
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  check_rows(out, "out");
+  check_rows(dout, "dout");
+  TORCH_CHECK(out.sizes() == torch::IntArrayRef({B, S, heads * 64}) && dout.sizes() == out.sizes(),
+              "out / dout [B, S, heads * 64]");
+  check_gpu(lse, "lse");
+  TORCH_CHECK(lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * heads * S,
+              "lse fp32 [B, heads, S]");
+  const c10::DeviceGuard guard(qkv.device());
+  auto dqkv = torch::empty_like(qkv);
+  psamd::launch_attn_bwd(u16(qkv), u16(out), u16(dout), lse.data_ptr<float>(), u16m(dqkv), static_cast<int>(B),
+                         static_cast<int>(S), static_cast<int>(heads), 0.125f, static_cast<float>(p),
+                         static_cast<uint64_t>(seed), cur_stream(qkv));
+  return dqkv;
+}
+
+// keep mask [B * H, S, S] (uint8) of the attention dropout for (p, seed) -- tests
+Tensor attn_dropout_mask(Tensor like, int64_t bh, int64_t S, double p, int64_t seed) {
+  check_gpu(like, "like");
+  const c10::DeviceGuard guard(like.device());
+  auto m = torch::empty({bh, S, S}, like.options().dtype(torch::kUInt8));
+  psamd::launch_attn_dropout_mask(m.data_ptr<uint8_t>(), m.numel(), static_cast<float>(p),
+                                  static_cast<uint64_t>(seed), cur_stream(like));
+  return m;
+}
+
 Tensor swiglu_fwd(Tensor gu) {
   check_rows(gu, "gu");
   const int64_t F2 = gu.size(-1), R = gu.numel() / F2;
@@ -1208,6 +1258,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_dropout_mask", &attn_dropout_mask);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_split_fwd", &rope_split_fwd);

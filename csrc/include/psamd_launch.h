@@ -267,6 +267,13 @@ struct ConvWgradArgs {
   uint16_t* dw;         // [N, K] bf16
 };
 int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro);
+// Fused short-sequence attention (attention.hip): qkv [B, S, 3, H, 64] bf16 (Linear layout),
+// out [B, S, H * 64], lse [B, H, S] fp32; S % 32 == 0, S <= 128; dropout p on the probabilities
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int S, int H, float scale, float p,
+                     uint64_t seed, hipStream_t s);
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, uint16_t* dqkv,
+                     int B, int S, int H, float scale, float p, uint64_t seed, hipStream_t s);
+void launch_attn_dropout_mask(uint8_t* mask, int64_t n, float p, uint64_t seed, hipStream_t s);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
 // BN helpers for the fused bottleneck (bn_act.hip): y = act(x*scale + shift [+ res [* rscale + rshift]])
 // mbits (nullable): also write the ReLU mask of y, 1 bit per element

@@ -4,7 +4,8 @@ checkpoints, no network).
 Compact in-repo definitions (transformers is not needed on the hot path): parameter shapes
 and counts match the published architectures -- BERT-base 110M (12 x 768, 12 heads, FFN
 3072, vocab 30522), Llama-3-8B 8.03B (32 x 4096, 32 q / 8 kv heads, FFN 14336, vocab
-128256, RoPE theta 500000).  Attention runs through torch SDPA (flash kernels on ROCm);
+128256, RoPE theta 500000).  BERT attention (S <= 128) runs the fused MFMA kernel of
+csrc/kernels/attention.hip, Llama's causal GQA attention torch SDPA (flash kernels on ROCm);
 everything is bf16 on the GPU with fp32 masters on the parameter-server shards.
 """
 from __future__ import annotations
@@ -18,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
-from ..ops.transformer import layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
+from ..ops.transformer import attention_qkv, layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
 
 
 # ------------------------------------------------------------------------------------ BERT
@@ -47,12 +48,9 @@ class BertLayer(nn.Module):
         self.ln2 = nn.LayerNorm(c.hidden, eps=c.eps)
 
     def forward(self, x, mask: Optional[torch.Tensor] = None):
-        b, s, h = x.shape
-        nh = self.c.heads
-        q, k, v = self.qkv(x).view(b, s, 3, nh, h // nh).permute(2, 0, 3, 1, 4)
         p = self.c.dropout if self.training else 0.0
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
-        a = a.transpose(1, 2).reshape(b, s, h)
+        # fused MFMA attention over the qkv projection for S <= 128 (ops/transformer.py), SDPA else
+        a = attention_qkv(self.qkv(x), self.c.heads, p, mask)
         # post-LN epilogues: LN(x + dropout(sublayer)) as one fused HIP pass each way
         x = layer_norm_residual(x, self.proj(a), self.ln1.weight, self.ln1.bias, self.c.eps, p, self.training)
         f = self.fc2(F.gelu(self.fc1(x)))

@@ -4,12 +4,15 @@
   layer_norm_residual(x, o, g, b, eps, p)    -> LN(x + dropout_p(o))        (BERT post-LN)
   swiglu(gu)                                  -> silu(gu[..., :F]) * gu[..., F:]
   rope_split(qkv, cs, H, KV)                  -> q, k, v  (RoPE + head split + transpose)
+  attention_qkv(qkv, H, p, mask)              -> dropout_p(softmax(q k^T / 8)) v over the fused qkv
+                                                 projection (csrc/kernels/attention.hip, S <= 128)
 
 GPU bf16 tensors (row length <= 4096, multiple of 8) take the HIP kernels; everything else
 runs the plain torch composition, which is also the numerics oracle in the GPU tests.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -164,3 +167,39 @@ def rope_split(qkv: torch.Tensor, cs: torch.Tensor, H: int, KV: int):
     x = qkv.transpose(1, 2)
     q, k, v = x.split([H, KV, KV], dim=1)
     return _rope_ref(q, cs), _rope_ref(k, cs), v
+
+
+# ------------------------------------------------------------------------------ attention
+def attention_qkv_ok(qkv: torch.Tensor, heads: int, mask) -> bool:
+    """The fused kernel's domain: GPU bf16, head dim 64, S a multiple of 32 up to 128, no mask."""
+    return (mask is None and _hip(qkv) and qkv.dim() == 3 and qkv.shape[2] == 3 * heads * 64
+            and qkv.shape[1] % 32 == 0 and 0 < qkv.shape[1] <= 128
+            and os.environ.get("PS_AMD_FUSED_ATTN", "1") != "0")
+
+
+class _FusedAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads, p):
+        qkv = qkv.contiguous()
+        seed = _seed() if p > 0 else 0
+        out, lse = native().attn_fwd(qkv, heads, float(p), seed)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads, ctx.p, ctx.seed = heads, float(p), seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        return native().attn_bwd(qkv, out, dout.contiguous(), lse, ctx.heads, ctx.p, ctx.seed), None, None
+
+
+def attention_qkv(qkv: torch.Tensor, heads: int, p: float = 0.0, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Multi-head self-attention over the fused projection ``qkv`` [B, S, 3 * H * D] (q | k | v,
+    heads inner) -> [B, S, H * D], dropout ``p`` on the probabilities.  On the fused kernel the
+    heads are never split into separate q / k / v tensors and the output is already merged."""
+    if attention_qkv_ok(qkv, heads, mask):
+        return _FusedAttention.apply(qkv, heads, float(p))
+    b, s, _ = qkv.shape
+    q, k, v = qkv.view(b, s, 3, heads, -1).permute(2, 0, 3, 1, 4)
+    a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
+    return a.transpose(1, 2).reshape(b, s, -1)
