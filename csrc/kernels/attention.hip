@@ -12,8 +12,9 @@
 // [B, S, 3, H, 64] and O is written as [B, S, H * 64] (no head split / merge copies); the
 // backward writes dq / dk / dv into one [B, S, 3, H, 64] gradient (no concatenation).
 //
-// Dropout on the attention probabilities: keep(b, h, i, j) = hash(seed, ((bh * S + i) * S + j))
-// >= p * 2^32, regenerated in the backward (nothing stored); kept values scaled by 1 / (1 - p).
+// Dropout on the attention probabilities: element e = (bh * S + i) * S + j is kept if its 16-bit
+// half of hash(seed, e >> 1) is >= p * 2^16 (one hash per key pair), regenerated in the backward
+// (nothing stored); kept values scaled by 1 / (1 - p).
 // The backward stores the per-row log-sum-exp of the forward and recomputes P:
 //   dV = P_drop^T dO,   dP = (dO V^T) * mask / (1 - p),   dS = P * (dP - rowsum(dO * O)),
 //   dQ = scale dS K,    dK = scale dS^T Q.
@@ -78,10 +79,12 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t idx, uint32_t thr) {
-  const uint32_t hsh = mix32(mix32(idx ^ static_cast<uint32_t>(seed)) + static_cast<uint32_t>(seed >> 32));
-  return hsh >= thr;
+// one 32-bit hash per PAIR of elements (2j, 2j + 1): a 16-bit draw each, kept if >= p * 2^16
+__device__ __forceinline__ uint32_t pair_hash(uint64_t seed, uint32_t pair) {
+  return mix32(mix32(pair ^ static_cast<uint32_t>(seed)) + static_cast<uint32_t>(seed >> 32));
 }
+__device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t thr) { return (h & 0xffffu) >= thr; }
+__device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return static_cast<uint32_t>(f32_to_bf16(a)) | (static_cast<uint32_t>(f32_to_bf16(b)) << 16);
@@ -117,11 +120,13 @@ template <bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                        float* __restrict__ lse, int S, int H, float scale,
                                                        uint64_t seed, uint32_t thr, float rkeep) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kS * kD];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[kS * kD];
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const int64_t rs = 3LL * H * kD;
   const uint16_t* base = qkv + static_cast<int64_t>(b) * S * rs + h * kD;
+  stage64(Ks, base + H * kD, rs, S);
   stage64(Vs, base + 2 * H * kD, rs, S);
   __syncthreads();
   const int q0 = w * 32;
@@ -140,8 +145,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
     if (kb < nkb) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(base + H * kD + (kb * 32 + c) * rs + 16 * s + 8 * hl);
-        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag<64>(Ks, kb * 32 + c, 2 * s + hl), qf[s], st[kb], 0, 0, 0);
       }
     }
   }
@@ -171,13 +175,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      float p = st[kb][e] * inv;
-      if constexpr (DROP) {
+    for (int e = 0; e < 16; e += 2) {
+      float p0 = st[kb][e] * inv, p1 = st[kb][e + 1] * inv;
+      if constexpr (DROP) {  // keys key, key + 1 (key even): one hash
         const int key = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-        p = keep_elem(seed, rowbase + key, thr) ? p * rkeep : 0.f;
+        const uint32_t hh = pair_hash(seed, (rowbase + key) >> 1);
+        p0 = keep_lo(hh, thr) ? p0 * rkeep : 0.f;
+        p1 = keep_hi(hh, thr) ? p1 * rkeep : 0.f;
       }
-      st[kb][e] = p;
+      st[kb][e] = p0;
+      st[kb][e + 1] = p1;
     }
   // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]
   f32x16 o[2];
@@ -215,7 +222,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   __shared__ __attribute__((aligned(16))) uint16_t Qs[kS * kD];
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kS * kD];
   __shared__ __attribute__((aligned(16))) uint16_t dOs[kS * kD];
-  __shared__ __attribute__((aligned(16))) uint16_t T[kS * kS];  // [key][query]: P_drop^T, then dS^T
+  __shared__ __attribute__((aligned(16))) uint16_t T[kS * kS];  // [query][key]: P_drop, then dS
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const int64_t rs = 3LL * H * kD, ors = static_cast<int64_t>(H) * kD;
@@ -269,28 +276,41 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float p = kb < nkb ? exp2f(pt[kb][e] * k2 - l2) : 0.f;
-        float dp = ds[kb][e];
-        float pd = p;
-        if constexpr (DROP) {
+      for (int e = 0; e < 16; e += 2) {
+        uint32_t hh = 0;
+        if constexpr (DROP) {  // keys key, key + 1 (key even): one hash
           const int key = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-          const bool kp = keep_elem(seed, rowbase + key, thr);
-          pd = kp ? p * rkeep : 0.f;
-          dp = kp ? dp * rkeep : 0.f;
+          hh = pair_hash(seed, (rowbase + key) >> 1);
         }
-        ds[kb][e] = p * (dp - dd);
-        pt[kb][e] = pd;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float p = kb < nkb ? exp2f(pt[kb][e + u] * k2 - l2) : 0.f;
+          float dp = ds[kb][e + u];
+          float pd = p;
+          if constexpr (DROP) {
+            const bool kp = u ? keep_hi(hh, thr) : keep_lo(hh, thr);
+            pd = kp ? p * rkeep : 0.f;
+            dp = kp ? dp * rkeep : 0.f;
+          }
+          ds[kb][e + u] = p * (dp - dd);
+          pt[kb][e + u] = pd;
+        }
       }
   }
-  // P_drop^T -> T[key][q] (columns of idle waves' queries are zero)
+  // P_drop -> T[q][key]: a lane's 4 consecutive keys of its query row per 8-B store (rows of idle
+  // waves' queries are zero)
+  auto put = [&](const f32x16 (&v)[4]) {
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
+    for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-      T[off<128>(key, q)] = f32_to_bf16(act ? pt[kb][e] : 0.f);
-    }
+      for (int g = 0; g < 4; ++g) {
+        const u16x4 x = act ? u16x4{f32_to_bf16(v[kb][4 * g]), f32_to_bf16(v[kb][4 * g + 1]),
+                                    f32_to_bf16(v[kb][4 * g + 2]), f32_to_bf16(v[kb][4 * g + 3])}
+                            : u16x4{0, 0, 0, 0};
+        *reinterpret_cast<u16x4*>(T + off<128>(q, kb * 32 + 8 * g + 4 * hl)) = x;
+      }
+  };
+  put(pt);
   __syncthreads();
   const int k0 = w * 32;
   const bool kact = k0 < S;
@@ -315,21 +335,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[db][e] = 0.f;
     for (int s = 0; s < nqs; ++s) {
-      const bf16x8_t pb = frag<128>(T, k0 + c, 2 * s + hl);
+      const bf16x8_t pb = tfrag<128>(T, s, k0, lane);  // P_drop[16 s + 8 hl + j][k0 + c]
 #pragma unroll
       for (int db = 0; db < 2; ++db)
         acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tfrag<64>(dOs, s, db * 32, lane), pb, acc[db], 0, 0, 0);
     }
     store_t(acc, krow + 2 * H * kD, 1.f);
   }
-  __syncthreads();  // P_drop^T read out
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-      T[off<128>(key, q)] = f32_to_bf16(act ? ds[kb][e] : 0.f);
-    }
+  __syncthreads();  // P_drop read out
+  put(ds);
   __syncthreads();
   if (kact) {
     // dK^T[d][key] = scale sum_q Q^T[d][q] dS[q][key]
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[db][e] = 0.f;
     for (int s = 0; s < nqs; ++s) {
-      const bf16x8_t sb = frag<128>(T, k0 + c, 2 * s + hl);
+      const bf16x8_t sb = tfrag<128>(T, s, k0, lane);  // dS[16 s + 8 hl + j][k0 + c]
 #pragma unroll
       for (int db = 0; db < 2; ++db)
         acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tfrag<64>(Qs, s, db * 32, lane), sb, acc[db], 0, 0, 0);
@@ -352,7 +366,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[db][e] = 0.f;
     for (int s = 0; s < 2 * nkb; ++s) {
-      const bf16x8_t sb = tfrag<128>(T, s, q0, lane);
+      const bf16x8_t sb = frag<128>(T, q0 + c, 2 * s + hl);  // dS[q0 + c][16 s + 8 hl + j]
 #pragma unroll
       for (int db = 0; db < 2; ++db)
         acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tfrag<64>(Ks, s, db * 32, lane), sb, acc[db], 0, 0, 0);
@@ -364,15 +378,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
 // keep mask of the attention dropout (tests / debugging): mask[bh][i][j] = 1 if kept
 __global__ void attn_dropout_mask_kernel(uint8_t* __restrict__ mask, int64_t n, uint64_t seed, uint32_t thr) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) mask[i] = keep_elem(seed, static_cast<uint32_t>(i), thr) ? 1 : 0;
+  if (i < n) {
+    const uint32_t e = static_cast<uint32_t>(i), hh = pair_hash(seed, e >> 1);
+    mask[i] = ((e & 1) ? keep_hi(hh, thr) : keep_lo(hh, thr)) ? 1 : 0;
+  }
 }
 
 }  // namespace
 
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int S, int H, float scale, float p,
                      uint64_t seed, hipStream_t s) {
-  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
-  const float rkeep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 65536.0 + 0.5);
+  const float rkeep = thr > 0 ? static_cast<float>(65536.0 / (65536.0 - thr)) : 1.f;  // 1 / (1 - p_eff)
   const dim3 grid(B * H);
   if (p > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, qkv, out, lse, S, H, scale, seed, thr, rkeep);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, qkv, out, lse, S, H, scale, seed, thr, rkeep);
@@ -380,8 +397,8 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
 
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, uint16_t* dqkv,
                      int B, int S, int H, float scale, float p, uint64_t seed, hipStream_t s) {
-  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
-  const float rkeep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 65536.0 + 0.5);
+  const float rkeep = thr > 0 ? static_cast<float>(65536.0 / (65536.0 - thr)) : 1.f;  // 1 / (1 - p_eff)
   const dim3 grid(B * H);
   if (p > 0.f)
     hipLaunchKernelGGL(attn_bwd_kernel<true>, grid, dim3(256), 0, s, qkv, out, dout, lse, dqkv, S, H, scale, seed, thr,
@@ -392,7 +409,7 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
 }
 
 void launch_attn_dropout_mask(uint8_t* mask, int64_t n, float p, uint64_t seed, hipStream_t s) {
-  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
+  const uint32_t thr = static_cast<uint32_t>(static_cast<double>(p) * 65536.0 + 0.5);
   hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, mask, n,
                      seed, thr);
 }

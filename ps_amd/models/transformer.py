@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
+from ..ops.dense import SplitKLinear
 from ..ops.transformer import attention_qkv, layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
 
 
@@ -40,11 +41,12 @@ class BertLayer(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
         self.c = c
-        self.qkv = nn.Linear(c.hidden, 3 * c.hidden)
-        self.proj = nn.Linear(c.hidden, c.hidden)
+        # split-K weight gradients (ops/dense.py SplitKLinear): 32K tokens into small dW
+        self.qkv = SplitKLinear(c.hidden, 3 * c.hidden)
+        self.proj = SplitKLinear(c.hidden, c.hidden)
         self.ln1 = nn.LayerNorm(c.hidden, eps=c.eps)
-        self.fc1 = nn.Linear(c.hidden, c.ffn)
-        self.fc2 = nn.Linear(c.ffn, c.hidden)
+        self.fc1 = SplitKLinear(c.hidden, c.ffn)
+        self.fc2 = SplitKLinear(c.ffn, c.hidden)
         self.ln2 = nn.LayerNorm(c.hidden, eps=c.eps)
 
     def forward(self, x, mask: Optional[torch.Tensor] = None):

@@ -77,6 +77,60 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act:
     return _act_ref(z, act)
 
 
+# ------------------------------------------------------------------------------ split-K weight gradient
+def _wgrad_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
+    """Long-reduction, small-output weight gradients (BERT: 32K tokens into a 768 x 2304 dW make
+    27 output tiles of 256 x 256, which hipBLASLt runs on 27 of the 256 CUs at 200-500 TF/s) go
+    to the split-M wide-tile kernel of csrc/kernels/convgemm.hip as a 1x1 "convolution"."""
+    import os
+
+    T, K = x2.shape
+    N = dy2.shape[1]
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16 and N % 128 == 0
+            and K % 128 == 0 and (N % 256 == 0 or K % 256 == 0) and T >= 4096 and T < 2 ** 31
+            and (N // 256 + 1) * (K // 256 + 1) < 256 and os.environ.get("PS_AMD_SPLITK_WGRAD", "1") != "0")
+
+
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW [N, K] = dy2^T x2 (fp32 accumulation, fixed-order split reduction)."""
+    if _wgrad_ok(x2, dy2):
+        T = x2.shape[0]
+        return native().conv_wgrad(dy2, x2, [T, 1, T, 1, 1, 1, 0])
+    return dy2.t() @ x2
+
+
+class _SplitKLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        n, k = w.shape
+        dy2 = dy.reshape(-1, n)
+        dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
+        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, k)
+            dw = linear_wgrad(dy2, x2 if x2.is_contiguous() else x2.contiguous()).to(w.dtype)
+        db = dy2.sum(0).to(w.dtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+class SplitKLinear(torch.nn.Linear):
+    """nn.Linear (same parameters / state_dict) whose weight gradient runs split-K on GPU bf16
+    when the reduction (tokens) is long and the output small (``linear_wgrad``)."""
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled():
+            return _SplitKLinear.apply(x, self.weight, self.bias)
+        return super().forward(x)
+
+
 # ------------------------------------------------------------------------------ DLRM interaction
 def _interact_ref(x: torch.Tensor, e: torch.Tensor) -> torch.Tensor:
     z = torch.cat([x.unsqueeze(1), e], dim=1)
