@@ -123,7 +123,10 @@ __global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const uint16_t* __restr
 
 // dy, s: [R, D]; ds_in: optional gradient already flowing into s (residual branch);
 // dx = rstd * (g - xhat * mean(g * xhat)) [+ ds_in], g = dy * w.  wpart: [gridDim.x, D].
-template <int VPT, bool ADD, typename WT>
+// WG = false: dx only (D > 2048: the per-lane weight-gradient registers would cut occupancy to
+// one wave per SIMD and the per-block fold of 4 rows would write as many partial bytes as it
+// reads; rms_dw_kernel reduces dw over row partitions instead).
+template <int VPT, bool ADD, typename WT, bool WG = true>
 __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy,
                                                          const uint16_t* __restrict__ s,
                                                          const WT* __restrict__ w, const float* __restrict__ rstd,
@@ -152,7 +155,7 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const uint16_t* __restr
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = bf16_to_f32(f32_to_bf16(xh[k][j] * rs));  // forward's rounded xhat
-          acc[k][j] += d[j] * xh[k][j];
+          if constexpr (WG) acc[k][j] += d[j] * xh[k][j];
           g[k][j] = d[j] * wv[j];
           dot += g[k][j] * xh[k][j];
         }
@@ -176,9 +179,32 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const uint16_t* __restr
       }
     }
   }
-  // fold the 4 waves' column partials in LDS (fixed wave order), one partial row per block
-  __shared__ __attribute__((aligned(16))) float lacc[4096];
-  block_fold_rows<VPT>(acc, lacc, D, wpart + static_cast<int64_t>(blockIdx.x) * D);
+  if constexpr (WG) {
+    // fold the 4 waves' column partials in LDS (fixed wave order), one partial row per block
+    __shared__ __attribute__((aligned(16))) float lacc[4096];
+    block_fold_rows<VPT>(acc, lacc, D, wpart + static_cast<int64_t>(blockIdx.x) * D);
+  }
+}
+
+// dw partials: part[y][c] = sum_{r = y, y + P, ...} dy[r][c] * bf16(s[r][c] * rstd[r]) for 8
+// columns per thread (grid: D / 2048 column blocks x P row partitions)
+__global__ __launch_bounds__(kT) void rms_dw_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
+                                                    const float* __restrict__ rstd, float* __restrict__ part, int R,
+                                                    int D) {
+  const int c = (blockIdx.x * kT + threadIdx.x) * 8;
+  if (c >= D) return;
+  const int P = gridDim.y;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = blockIdx.y; r < R; r += P) {
+    const int64_t o = static_cast<int64_t>(r) * D + c;
+    const float rs = rstd[r];
+    float d[8], x[8];
+    load8(dy, o, d);
+    load8(s, o, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += d[j] * bf16_to_f32(f32_to_bf16(x[j] * rs));
+  }
+  store8(part, static_cast<int64_t>(blockIdx.y) * D + c, a);
 }
 
 // out[y][c] = sum_{b = y, y + Y, ...} part[b][c] (Y = gridDim.y), 8 independent chains per
@@ -505,6 +531,21 @@ int rmsnorm_bwd_parts(int R) { return part_grid(R) + 32; }  // + colsum scratch 
 void launch_rmsnorm_bwd(const uint16_t* dy, const uint16_t* s, const void* w, bool w_bf16, const float* rstd,
                         const uint16_t* ds_in, uint16_t* dx, float* wpart, float* dw, int R, int D, hipStream_t st) {
   if (R <= 0) return;
+  if (D > 2048) {  // dx row kernel without weight-gradient registers + a row-partitioned dw reduction
+    const int g = row_grid(R), P = part_grid(R) < 256 ? part_grid(R) : 256;
+#define PSAMD_RMS_DX(VPTV, ADDV, WTV) \
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<VPTV, ADDV, WTV, false>), dim3(g), dim3(kT), 0, st, dy, s, \
+                     static_cast<const WTV*>(w), rstd, ds_in, dx, wpart, R, D)
+    if (w_bf16) {
+      if (ds_in) PSAMD_RMS_DX(8, true, uint16_t); else PSAMD_RMS_DX(8, false, uint16_t);
+    } else {
+      if (ds_in) PSAMD_RMS_DX(8, true, float); else PSAMD_RMS_DX(8, false, float);
+    }
+#undef PSAMD_RMS_DX
+    hipLaunchKernelGGL(rms_dw_kernel, dim3((D / 8 + kT - 1) / kT, P), dim3(kT), 0, st, dy, s, rstd, wpart, R, D);
+    colsum2(wpart, P, D, wpart + static_cast<int64_t>(P) * D, dw, st);
+    return;
+  }
   const int g = part_grid(R);
   PSAMD_VPT_SWITCH(D, {
     if (w_bf16) {

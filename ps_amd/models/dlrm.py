@@ -24,14 +24,15 @@ import torch.nn.functional as F
 from ..parallel.sparse_table import ShardedSparseTable
 from ..parallel.transport import Transport
 from ..parallel.updaters import AdagradUpdater, Updater
-from ..ops.dense import dlrm_interact
+from ..ops.dense import SplitKLinear, dlrm_interact
 from .layers import SparseLayerMixin
 
 
 def mlp(dims: Sequence[int], last_act: bool = True) -> nn.Sequential:
     layers: List[nn.Module] = []
     for i in range(len(dims) - 1):
-        layers.append(nn.Linear(dims[i], dims[i + 1]))
+        # nn.Linear with split-K weight gradients on GPU bf16 (batch-long reductions into small dW)
+        layers.append(SplitKLinear(dims[i], dims[i + 1]))
         if i < len(dims) - 2 or last_act:
             layers.append(nn.ReLU())
     return nn.Sequential(*layers)
