@@ -123,9 +123,6 @@ __global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const uint16_t* __restr
 
 // dy, s: [R, D]; ds_in: optional gradient already flowing into s (residual branch);
 // dx = rstd * (g - xhat * mean(g * xhat)) [+ ds_in], g = dy * w.  wpart: [gridDim.x, D].
-// WG = false: dx only (D > 2048: the per-lane weight-gradient registers would cut occupancy to
-// one wave per SIMD and the per-block fold of 4 rows would write as many partial bytes as it
-// reads; rms_dw_kernel reduces dw over row partitions instead).
 template <int VPT, bool ADD, typename WT, bool WG = true>
 __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const uint16_t* __restrict__ dy,
                                                          const uint16_t* __restrict__ s,
@@ -186,16 +183,61 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const uint16_t* __restr
   }
 }
 
-// dw partials: part[y][c] = sum_{r = y, y + P, ...} dy[r][c] * bf16(s[r][c] * rstd[r]) for 8
-// columns per thread (grid: D / 2048 column blocks x P row partitions)
+// dx only, two passes over the row (the second re-reads dy / s from L2): nothing is held across
+// the row reduction, so occupancy stays high for 4096-wide rows (holding xhat and g for
+// 8 vectors per lane took 256 VGPRs, one wave per SIMD and serialised the HBM loads).
+template <bool ADD, typename WT>
+__global__ __launch_bounds__(kT) void rmsnorm_bwd_dx2_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ s, const WT* __restrict__ w,
+                                                             const float* __restrict__ rstd,
+                                                             const uint16_t* __restrict__ ds_in,
+                                                             uint16_t* __restrict__ dx, int R, int D) {
+  const int nv = D / 8;
+  PSAMD_ROW_LOOP(R) {
+    const int64_t base = static_cast<int64_t>(row) * D;
+    const float rs = rstd[row];
+    float dot = 0.f;
+#pragma unroll 4
+    for (int vi = lane_; vi < nv; vi += kL) {
+      float d[8], x[8], wv[8];
+      load8(dy, base + vi * 8, d);
+      load8(s, base + vi * 8, x);
+      loadw8(w, vi * 8, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot += d[j] * wv[j] * bf16_to_f32(f32_to_bf16(x[j] * rs));
+    }
+    const float c = wave_sum(dot) / static_cast<float>(D);
+#pragma unroll 4
+    for (int vi = lane_; vi < nv; vi += kL) {
+      float d[8], x[8], wv[8], o[8];
+      load8(dy, base + vi * 8, d);
+      load8(s, base + vi * 8, x);
+      loadw8(w, vi * 8, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rs * (d[j] * wv[j] - bf16_to_f32(f32_to_bf16(x[j] * rs)) * c);
+      if constexpr (ADD) {
+        float q[8];
+        load8(ds_in, base + vi * 8, q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += q[j];
+      }
+      store8(dx, base + vi * 8, o);
+    }
+  }
+}
+
+// dw partials: part[y][c] = sum over row partition y (contiguous rows) of dy[r][c] *
+// bf16(s[r][c] * rstd[r]), 8 columns per thread (grid: D / 2048 column blocks x P partitions)
 __global__ __launch_bounds__(kT) void rms_dw_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s,
                                                     const float* __restrict__ rstd, float* __restrict__ part, int R,
                                                     int D) {
   const int c = (blockIdx.x * kT + threadIdx.x) * 8;
   if (c >= D) return;
-  const int P = gridDim.y;
+  const int P = gridDim.y, per = (R + P - 1) / P;  // a contiguous row range per partition
+  const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = blockIdx.y; r < R; r += P) {
+#pragma unroll 4
+  for (int r = r0; r < r1; ++r) {
     const int64_t o = static_cast<int64_t>(r) * D + c;
     const float rs = rstd[r];
     float d[8], x[8];
@@ -532,14 +574,14 @@ void launch_rmsnorm_bwd(const uint16_t* dy, const uint16_t* s, const void* w, bo
                         const uint16_t* ds_in, uint16_t* dx, float* wpart, float* dw, int R, int D, hipStream_t st) {
   if (R <= 0) return;
   if (D > 2048) {  // dx row kernel without weight-gradient registers + a row-partitioned dw reduction
-    const int g = row_grid(R), P = part_grid(R) < 256 ? part_grid(R) : 256;
-#define PSAMD_RMS_DX(VPTV, ADDV, WTV) \
-  hipLaunchKernelGGL((rmsnorm_bwd_kernel<VPTV, ADDV, WTV, false>), dim3(g), dim3(kT), 0, st, dy, s, \
-                     static_cast<const WTV*>(w), rstd, ds_in, dx, wpart, R, D)
+    const int g = row_grid(R), P = part_grid(R) < 512 ? part_grid(R) : 512;
+#define PSAMD_RMS_DX(ADDV, WTV) \
+  hipLaunchKernelGGL((rmsnorm_bwd_dx2_kernel<ADDV, WTV>), dim3(g), dim3(kT), 0, st, dy, s, static_cast<const WTV*>(w), \
+                     rstd, ds_in, dx, R, D)
     if (w_bf16) {
-      if (ds_in) PSAMD_RMS_DX(8, true, uint16_t); else PSAMD_RMS_DX(8, false, uint16_t);
+      if (ds_in) PSAMD_RMS_DX(true, uint16_t); else PSAMD_RMS_DX(false, uint16_t);
     } else {
-      if (ds_in) PSAMD_RMS_DX(8, true, float); else PSAMD_RMS_DX(8, false, float);
+      if (ds_in) PSAMD_RMS_DX(true, float); else PSAMD_RMS_DX(false, float);
     }
 #undef PSAMD_RMS_DX
     hipLaunchKernelGGL(rms_dw_kernel, dim3((D / 8 + kT - 1) / kT, P), dim3(kT), 0, st, dy, s, rstd, wpart, R, D);
