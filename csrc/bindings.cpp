@@ -1147,6 +1147,39 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   return dw;
 }
 
+// Linear weight + bias gradient in one pass over dz: [dW [N, K] bf16, db [N] fp32] with
+// dW = dz^T x (x [M, K] rows), db = column sums of dz (fused into the wide split-K kernel; a
+// torch reduction where the plan is not wide)
+std::vector<Tensor> linear_wgrad_db(Tensor dz, Tensor x) {
+  check_rows(dz, "dz");
+  check_rows(x, "x");
+  TORCH_CHECK(dz.dim() == 2 && x.dim() == 2 && dz.size(0) == x.size(0), "dz [M, N], x [M, K]");
+  const int64_t M = dz.size(0), N = dz.size(1), K = x.size(1);
+  TORCH_CHECK(N % 64 == 0 && N <= 8192 && K % 64 == 0 && M < (int64_t(1) << 31), "N, K multiples of 64");
+  const int m = static_cast<int>(M), n = static_cast<int>(N), k = static_cast<int>(K);
+  const c10::DeviceGuard guard(dz.device());
+  const bool wide = psamd::conv_wgrad_is_wide(m, n, k, k, false);
+  const int64_t wsz = psamd::conv_wgrad_ws(m, n, k, k, false);
+  const int64_t dbsz = wide ? static_cast<int64_t>(psamd::conv_wgrad_splits(m, n, k, k, false)) * N : 0;
+  auto ws = torch::empty({wsz + dbsz}, dz.options().dtype(torch::kFloat32));
+  auto dw = torch::empty({N, K}, dz.options());
+  auto db = wide ? torch::empty({N}, dz.options().dtype(torch::kFloat32)) : dz.sum(0, false, torch::kFloat32);
+  psamd::ConvWgradArgs p{};
+  p.dz = u16(dz);
+  p.x = u16(x);
+  p.M = m;
+  p.N = n;
+  p.K = k;
+  p.g = psamd::ConvGeo{m, 1, m, 1, k, 1, 1, 0};
+  p.pro = nullptr;
+  p.ws = ws.data_ptr<float>();
+  p.dw = u16m(dw);
+  p.db = wide ? db.data_ptr<float>() : nullptr;
+  p.dbws = wide ? ws.data_ptr<float>() + wsz : nullptr;
+  psamd::launch_conv_wgrad(p, cur_stream(dz));
+  return {dw, db};
+}
+
 // y = act(x * scale + shift [+ res [* rscale + rshift]]) from precomputed coefficients [scale | shift]
 // -> [y, ReLU mask bits (uint8 [R*C/8], with want_mask) or empty]
 std::vector<Tensor> bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> res, c10::optional<Tensor> rcoef,
@@ -1205,6 +1238,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
         py::arg("aux2") = py::none(), py::arg("bits2") = py::none());
+  m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);

@@ -265,7 +265,11 @@ struct ConvWgradArgs {
   const float* pro;     // [scale | shift] (2C) applied to x while staging; nullable
   float* ws;            // conv_wgrad_ws(M, N, K, C) floats
   uint16_t* dw;         // [N, K] bf16
+  float* db;            // nullable: [N] fp32 column sums of dz (a Linear's bias gradient; wide plan only)
+  float* dbws;          // [conv_wgrad_splits(...)][N] fp32 scratch when db is set
 };
+int conv_wgrad_splits(int M, int N, int K, int C, bool pro);
+bool conv_wgrad_is_wide(int M, int N, int K, int C, bool pro);
 int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro);
 // Fused short-sequence attention (attention.hip): qkv [B, S, 3, H, 64] bf16 (Linear layout),
 // out [B, S, H * 64], lse [B, H, S] fp32; S % 32 == 0, S <= 128; dropout p on the probabilities

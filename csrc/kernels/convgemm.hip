@@ -762,7 +762,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int TN, int TK, int WN, int WK, bool PRO>
+template <int TN, int TK, int WN, int WK, bool PRO, bool DB = false>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgradArgs p, int rows_per_split) {
   constexpr int BNO = WN * 32 * TN, BKO = WK * 32 * TK;
   static_assert(WN * WK == 8, "8 waves");
@@ -877,6 +877,11 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
     }
   };
 
+  // DB: the blocks of k-tile 0 also sum the staged dz tile's columns (bias gradient): thread t
+  // owns 16-B column chunk t % GCPR of rows t / GCPR + (512 / GCPR) i
+  const bool dbt = DB && (tile % ntk) == 0;  // block-uniform
+  constexpr int DBR = 512 / GCPR;            // threads per column chunk
+  float dbacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int pre = nst < kWS - 1 ? nst : kWS - 1;
   for (int st = 0; st < pre; ++st) issue(st, st);
   for (int st = 0; st < nst; ++st) {
@@ -887,7 +892,34 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
     else wait_vmcnt<0>();
     lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
     if (st + kWS - 1 < nst) issue(st + kWS - 1, (st + kWS - 1) % kWS);
+    if constexpr (DB) {
+      if (dbt) {
+        const uint16_t* Gs = lds + (st % kWS) * STAGE;
+        const int cc = t % GCPR;
+#pragma unroll
+        for (int r = t / GCPR; r < kWP; r += DBR) {
+          const u16x8 v = *reinterpret_cast<const u16x8*>(Gs + r * BNO + ((cc ^ tr_swz<BNO>(r)) << 3));
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dbacc[j] += bf16_to_f32(v[j]);
+        }
+      }
+    }
     mma(st % kWS);
+  }
+  if constexpr (DB) {
+    if (dbt) {
+      lds_barrier();  // every wave done with the ring: reuse it for the cross-thread fold
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[t * 8 + j] = dbacc[j];
+      lds_barrier();
+      if (t < BNO) {
+        const int cc = t >> 3, j = t & 7;
+        float sum = 0.f;
+        for (int k = 0; k < DBR; ++k) sum += red[(k * GCPR + cc) * 8 + j];  // fixed order
+        p.dbws[static_cast<int64_t>(split) * p.N + n0 + t] = sum;
+      }
+    }
   }
   float* sl = p.ws + static_cast<int64_t>(split) * p.N * p.K;
   const int h = lane >> 5, kl = lane & 31;
@@ -1051,6 +1083,9 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
 }
 }  // namespace
 
+int conv_wgrad_splits(int M, int N, int K, int C, bool pro) { return wplan(M, N, K, C, pro).nsplit; }
+bool conv_wgrad_is_wide(int M, int N, int K, int C, bool pro) { return wplan(M, N, K, C, pro).wide != 0; }
+
 int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro) {
   const WPlan w = wplan(M, N, K, C, pro);
   return static_cast<int64_t>(w.nsplit + w.groups) * N * K;
@@ -1060,9 +1095,11 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const WPlan w = wplan(a.M, a.N, a.K, a.g.C, a.pro != nullptr);
   const int nblk = w.tiles * w.nsplit;
-#define PSAMD_CWW(TN, TK, WN, WK)                                                                                 \
-  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true>), dim3(nblk), dim3(512), 0, s, a, \
-                                w.rows);                                                                        \
+#define PSAMD_CWW(TN, TK, WN, WK)                                                                                   \
+  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true>), dim3(nblk), dim3(512), 0, s, a,   \
+                                w.rows);                                                                          \
+  else if (a.db) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, true>), dim3(nblk), dim3(512), \
+                                    0, s, a, w.rows);                                                             \
   else hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false>), dim3(nblk), dim3(512), 0, s, a, w.rows)
 #define PSAMD_CW(TN, TK, PRO, GL) \
   hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO, GL>), dim3(nblk), dim3(256), 0, s, a, w.rows)
@@ -1085,6 +1122,9 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
 #undef PSAMD_CWW
 #undef PSAMD_CWP
 #undef PSAMD_CW
+  if (w.wide && a.db != nullptr && a.pro == nullptr)  // bias gradient: fold the per-split column sums
+    hipLaunchKernelGGL(slab_reduce_kernel<false>, dim3((a.N + 255) / 256), dim3(256), 0, s, a.dbws, w.nsplit,
+                       w.nsplit, static_cast<int64_t>(a.N), static_cast<void*>(a.db));
   const int64_t E = static_cast<int64_t>(a.N) * a.K;
   const unsigned eb = static_cast<unsigned>((E + 255) / 256);
   void* dw = a.dw;

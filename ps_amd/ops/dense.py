@@ -113,11 +113,20 @@ class _SplitKLinear(torch.autograd.Function):
         dy2 = dy.reshape(-1, n)
         dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
         dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
-        dw = None
+        dw = db = None
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, k)
-            dw = linear_wgrad(dy2, x2 if x2.is_contiguous() else x2.contiguous()).to(w.dtype)
-        db = dy2.sum(0).to(w.dtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+            x2 = x2 if x2.is_contiguous() else x2.contiguous()
+            if want_db and _wgrad_ok(x2, dy2):
+                # bias gradient from the dz tiles the split-K kernel stages anyway (one pass over dy)
+                dw, db = native().linear_wgrad_db(dy2, x2)
+                db = db.to(w.dtype)
+            else:
+                dw = linear_wgrad(dy2, x2)
+            dw = dw.to(w.dtype)
+        if want_db and db is None:
+            db = dy2.sum(0).to(w.dtype)
         return dx, dw, db
 
 

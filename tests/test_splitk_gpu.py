@@ -24,6 +24,18 @@ def test_linear_wgrad_split_k(T, K, N):
     assert _rel(dw, dy.float().t() @ x.float()) < 5e-3
 
 
+@pytest.mark.parametrize("T,K,N", [(8192, 768, 2304), (4100, 768, 768), (5000, 3072, 768)])
+def test_linear_wgrad_with_fused_bias_grad(T, K, N):
+    from ps_amd.ops import native
+
+    g = torch.Generator().manual_seed(T + 3 * K + N)
+    x = torch.randn(T, K, generator=g).bfloat16().to(DEV)
+    dy = torch.randn(T, N, generator=g).bfloat16().to(DEV)
+    dw, db = native().linear_wgrad_db(dy, x)
+    assert _rel(dw, dy.float().t() @ x.float()) < 5e-3
+    torch.testing.assert_close(db, dy.float().sum(0), rtol=1e-4, atol=1e-2)
+
+
 def test_splitk_linear_module_matches_linear():
     torch.manual_seed(0)
     a = SplitKLinear(768, 2304).to(DEV).bfloat16()
