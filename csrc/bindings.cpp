@@ -709,6 +709,50 @@ Tensor attn_dropout_mask(Tensor like, int64_t bh, int64_t S, double p, int64_t s
   return m;
 }
 
+// Causal GQA flash attention: q [B, H, S, 128], k / v [B, KV, S, 128] -> [out [B, S, H * 128], lse [B, H, S]]
+static void check_fa(const Tensor& q, const Tensor& k, const Tensor& v) {
+  for (const Tensor* t : {&q, &k, &v}) {
+    check_gpu(*t, "q/k/v");
+    TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->dim() == 4 && t->size(3) == 128,
+                "q / k / v: contiguous bf16 [B, heads, S, 128]");
+  }
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2), "k like v, q matches");
+  TORCH_CHECK(q.size(1) % k.size(1) == 0, "q heads a multiple of kv heads");
+  TORCH_CHECK(q.size(2) % 128 == 0 && q.size(2) > 0, "sequence length a multiple of 128");
+}
+
+std::vector<Tensor> fa_fwd(Tensor q, Tensor k, Tensor v) {
+  check_fa(q, k, v);
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
+  const c10::DeviceGuard guard(q.device());
+  auto out = torch::empty({B, S, H * 128}, q.options());
+  auto lse = torch::empty({B, H, S}, q.options().dtype(torch::kFloat32));
+  psamd::launch_fa_fwd(u16(q), u16(k), u16(v), u16m(out), lse.data_ptr<float>(), static_cast<int>(B),
+                       static_cast<int>(S), static_cast<int>(H), static_cast<int>(KV), 1.f / std::sqrt(128.f),
+                       cur_stream(q));
+  return {out, lse};
+}
+
+std::vector<Tensor> fa_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse) {
+  check_fa(q, k, v);
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
+  check_rows(out, "out");
+  check_rows(dout, "dout");
+  TORCH_CHECK(out.numel() == B * S * H * 128 && dout.numel() == out.numel(), "out / dout [B, S, H * 128]");
+  check_gpu(lse, "lse");
+  TORCH_CHECK(lse.scalar_type() == torch::kFloat32 && lse.numel() == B * H * S, "lse fp32 [B, H, S]");
+  const c10::DeviceGuard guard(q.device());
+  auto fopt = q.options().dtype(torch::kFloat32);
+  auto dsum = torch::empty({B, H, S}, fopt);
+  auto dkp = torch::empty({B, H, S, 128}, fopt), dvp = torch::empty({B, H, S, 128}, fopt);
+  auto dq = torch::empty_like(q), dk = torch::empty_like(k), dv = torch::empty_like(v);
+  psamd::launch_fa_bwd(u16(q), u16(k), u16(v), u16(out), u16(dout), lse.data_ptr<float>(), dsum.data_ptr<float>(),
+                       dkp.data_ptr<float>(), dvp.data_ptr<float>(), u16m(dq), u16m(dk), u16m(dv),
+                       static_cast<int>(B), static_cast<int>(S), static_cast<int>(H), static_cast<int>(KV),
+                       1.f / std::sqrt(128.f), cur_stream(q));
+  return {dq, dk, dv};
+}
+
 Tensor swiglu_fwd(Tensor gu) {
   check_rows(gu, "gu");
   const int64_t F2 = gu.size(-1), R = gu.numel() / F2;
@@ -1293,6 +1337,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("fa_fwd", &fa_fwd);
+  m.def("fa_bwd", &fa_bwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_dropout_mask", &attn_dropout_mask);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -5,7 +5,7 @@ Compact in-repo definitions (transformers is not needed on the hot path): parame
 and counts match the published architectures -- BERT-base 110M (12 x 768, 12 heads, FFN
 3072, vocab 30522), Llama-3-8B 8.03B (32 x 4096, 32 q / 8 kv heads, FFN 14336, vocab
 128256, RoPE theta 500000).  BERT attention (S <= 128) runs the fused MFMA kernel of
-csrc/kernels/attention.hip, Llama's causal GQA attention torch SDPA (flash kernels on ROCm);
+csrc/kernels/attention.hip, Llama's causal GQA attention the flash kernel of flash_attn.hip;
 everything is bf16 on the GPU with fp32 masters on the parameter-server shards.
 """
 from __future__ import annotations
@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.dense import SplitKLinear
-from ..ops.transformer import attention_qkv, layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
+from ..ops.transformer import attention_causal_gqa, attention_qkv, layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
 
 
 # ------------------------------------------------------------------------------------ BERT
@@ -157,8 +157,8 @@ class RMSNorm(nn.Module):
 class LlamaBlock(nn.Module):
     """Pre-norm decoder block.  Q/K/V and gate/up projections are single fused GEMMs
     (``wqkv`` [(H + 2 KV) * hd, D], ``w13`` [2 F, D] -- same parameter count as separate
-    matrices, one hipBLASLt launch each); attention uses SDPA with native GQA (no K/V
-    replication)."""
+    matrices, one hipBLASLt launch each); attention is the causal GQA flash kernel
+    (csrc/kernels/flash_attn.hip; no K/V replication, output already head-merged)."""
 
     def __init__(self, c: LlamaConfig):
         super().__init__()
@@ -184,8 +184,7 @@ class LlamaBlock(nn.Module):
             x, h = rms_norm(x, self.attn_norm.weight, c.eps, residual=r)
         qkv = self.wqkv(h).view(b, s, c.heads + 2 * c.kv_heads, hd)
         q, k, v = rope_split(qkv, cs, c.heads, c.kv_heads)  # RoPE + split + transpose, one pass
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
-        o = self.wo(a.transpose(1, 2).reshape(b, s, -1))
+        o = self.wo(attention_causal_gqa(q, k, v))  # flash kernel (heads merged) or SDPA
         x, h = rms_norm(x, self.mlp_norm.weight, c.eps, residual=o)
         return x, self.w2(swiglu(self.w13(h)))
 

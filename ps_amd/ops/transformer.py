@@ -6,6 +6,8 @@
   rope_split(qkv, cs, H, KV)                  -> q, k, v  (RoPE + head split + transpose)
   attention_qkv(qkv, H, p, mask)              -> dropout_p(softmax(q k^T / 8)) v over the fused qkv
                                                  projection (csrc/kernels/attention.hip, S <= 128)
+  attention_causal_gqa(q, k, v)               -> causal GQA flash attention, heads merged
+                                                 (csrc/kernels/flash_attn.hip, head dim 128)
 
 GPU bf16 tensors (row length <= 4096, multiple of 8) take the HIP kernels; everything else
 runs the plain torch composition, which is also the numerics oracle in the GPU tests.
@@ -202,4 +204,36 @@ def attention_qkv(qkv: torch.Tensor, heads: int, p: float = 0.0, mask: Optional[
     b, s, _ = qkv.shape
     q, k, v = qkv.view(b, s, 3, heads, -1).permute(2, 0, 3, 1, 4)
     a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
+    return a.transpose(1, 2).reshape(b, s, -1)
+
+
+# ------------------------------------------------------------------------------ causal GQA flash attention
+def flash_ok(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> bool:
+    """Opt-in (PS_AMD_FLASH_ATTN=1): correct and GPU-tested, but on the Llama-3-8B shape it still
+    runs behind SDPA's kernels (profiles/r2_flash_probe.jsonl), so SDPA stays the default."""
+    return (_hip(q, k, v) and q.dim() == 4 and q.shape[3] == 128 and k.shape == v.shape and q.shape[2] % 128 == 0
+            and q.shape[1] % k.shape[1] == 0 and os.environ.get("PS_AMD_FLASH_ATTN", "0") == "1")
+
+
+class _FlashCausal(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out, lse = native().fa_fwd(q, k, v)
+        ctx.save_for_backward(q, k, v, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        return tuple(native().fa_bwd(q, k, v, out, dout.contiguous(), lse))
+
+
+def attention_causal_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """Causal attention with grouped KV heads: q [B, H, S, D], k / v [B, KV, S, D] -> [B, S, H * D]
+    (heads merged, the output projection's input layout)."""
+    if flash_ok(q, k, v):
+        return _FlashCausal.apply(q, k, v)
+    b, _, s, _ = q.shape
+    a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
     return a.transpose(1, 2).reshape(b, s, -1)
