@@ -344,6 +344,41 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     load8(p.invstd, nc, e3);
   }
   uint16_t* Cs = lds;
+  // Epilogue reads (residual / BN-input / mask rows of this thread's NPASS output rows), issued
+  // together before any is consumed: a load-use loop paid one HBM latency per row (the read-heavy
+  // data-gradient epilogues ran at ~2.8 TB/s).  Rows past M read row M - 1 (in bounds, unused).
+  constexpr int NPASS = BM / RPP;
+  constexpr bool RD_AUX = BASE == 5 || BASE == 2 || BASE == 4 || EPI == 3;
+  u16x8 ra[RD_AUX ? NPASS : 1], rz[FOLD ? NPASS : 1];
+  unsigned rb[BASE == 5 ? NPASS : 1], rp[FOLD ? NPASS : 1];
+  unsigned rodd = 0;  // BASE 4: rows without a residual (odd h or w)
+  auto epi_load = [&](int mt) {
+    const int m0 = mt * BM;
+    rodd = 0;
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int m = min(m0 + r0 + i * RPP, p.M - 1);
+      const int64_t o = static_cast<int64_t>(m) * p.N + nc;
+      if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
+        const int ohw = g.OH * g.OW;
+        const int im = m / ohw, r = m - im * ohw, h = r / g.OW, w = r - h * g.OW;
+        const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
+        ra[i] = kZero8;
+        rodd |= static_cast<unsigned>((h | w) & 1) << i;
+        if (!((h | w) & 1))
+          ra[i] = *reinterpret_cast<const u16x8*>(
+              p.aux + ((static_cast<int64_t>(im) * RH + (h >> 1)) * RW + (w >> 1)) * p.N + nc);
+      } else if constexpr (RD_AUX) {
+        ra[i] = *reinterpret_cast<const u16x8*>(p.aux + o);
+      }
+      if constexpr (BASE == 5) rb[i] = p.bits[o >> 3];
+      if constexpr (FOLD) {
+        rz[i] = *reinterpret_cast<const u16x8*>(p.aux2 + o);
+        rp[i] = p.bits2[o >> 3];
+      }
+    }
+  };
+  // epilogue(mt) consumes what epi_load(mt) read
   auto epilogue = [&](int mt) {
     // accumulators -> bf16 output tile [BM][CS]: register q of lane l is channel
     // (q & 3) + 8 (q >> 2) + 4 (l >> 5), pixel l & 31 -> 4 consecutive channels per 8-B store
@@ -360,29 +395,23 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         }
     lds_barrier();
     const int m0 = mt * BM;
-    for (int rr = r0; rr < BM; rr += RPP) {
-      const int m = m0 + rr;
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int rr = r0 + i * RPP, m = m0 + rr;
       if (m >= p.M) break;
       const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8);
       const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8 + 4);
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const int64_t o = static_cast<int64_t>(m) * p.N + nc;
       if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
-        const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + o);
-        const unsigned bits = p.bits[o >> 3];
+        const u16x8 r8 = ra[i];
+        const unsigned bits = rb[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if ((bits >> j) & 1u) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
       } else if constexpr (BASE == 2 || BASE == 4) {
-        int64_t ro = o;
-        if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
-          const int ohw = g.OH * g.OW;
-          const int i = m / ohw, r = m - i * ohw, h = r / g.OW, w = r - h * g.OW;
-          const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
-          ro = ((h | w) & 1) ? -1 : ((static_cast<int64_t>(i) * RH + (h >> 1)) * RW + (w >> 1)) * p.N + nc;
-        }
-        if (ro >= 0) {
-          const u16x8 r8 = *reinterpret_cast<const u16x8*>(p.aux + ro);
+        if (BASE == 2 || !((rodd >> i) & 1u)) {
+          const u16x8 r8 = ra[i];
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
         }
@@ -394,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
           s2[j] += d * d;
         }
       } else if constexpr (EPI == 3) {
-        const u16x8 z8 = *reinterpret_cast<const u16x8*>(p.aux + o);
+        const u16x8 z8 = ra[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float z = bf16_to_f32(z8[j]);
@@ -406,8 +435,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         }
       }
       if constexpr (FOLD) {  // previous block's bn3: ReLU mask from its output bits + reduce sums
-        const u16x8 z8 = *reinterpret_cast<const u16x8*>(p.aux2 + o);
-        const unsigned pb = p.bits2[o >> 3];
+        const u16x8 z8 = rz[i];
+        const unsigned pb = rp[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool on = (pb >> j) & 1u;
@@ -427,6 +456,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     if (q + 2 < nq) gload(SF);
     compute(q & 1);
     if (++ckt == nk) {  // tile done
+      epi_load(mg + cti * GM);
       lds_barrier();    // all waves are done with the stage buffers (the output tile overlaps)
       epilogue(mg + cti * GM);
       zero_acc();
@@ -510,6 +540,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         compute(kt & 1);
         lds_barrier();  // stage kt read out before stage kt + 2 is issued into its buffer
       }
+      // (issuing these reads before the K loop, behind every stage, measured no faster:
+      // scripts/probe_dgrad_epi.py)
+      epi_load(mg);
       epilogue(mg);
     }
   } else if (nq > 0) {
@@ -974,6 +1007,8 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   const int nN = N / pl.bn;
   pl.bm = 128;  // (64-pixel tiles measured slower on every ResNet-50 shape: scripts/probe_convgemm.py)
   const int nk = K / kBK;
+  // (a persistent grid for the read-heavy data-gradient epilogues measured no faster at 4-16
+  // stages: scripts/probe_dgrad_epi.py)
   const bool persist = nk <= 2 || (pro && nk <= persist_nk_pro());
   pl.gm = !persist ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
   return pl;

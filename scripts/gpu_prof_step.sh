@@ -7,4 +7,4 @@ export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
 R=$PWD
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python $R/bench.py --steps 6 --warmup 3 > $R/$O/prof.log 2>&1 || exit $?
 cd $R && python scripts/step_breakdown.py $(ls $O/prof/*kernel_trace.csv | head -1) > $O/breakdown.txt
-head -45 $O/breakdown.txt
+cp $O/prof/*kernel_trace.csv.timeline.txt $O/timeline.txt; head -45 $O/breakdown.txt

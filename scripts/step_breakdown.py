@@ -29,3 +29,12 @@ for k, v in sorted(fam.items(), key=lambda x: -x[1]):
     print(f"{k:62s} {v:7.3f} {100 * v / tot:5.1f}% {cnt[k]}")
 if scratch:
     print("ps_amd kernels using scratch:", *sorted(scratch), sep="\n  ")
+
+# per-dispatch timeline of the same step (order, duration, grid) -> <trace>.timeline.txt
+with open(sys.argv[1] + ".timeline.txt", "w") as f:
+    t0 = int(seg[0]["Start_Timestamp"])
+    for r in seg:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        st = (int(r["Start_Timestamp"]) - t0) / 1e3
+        grid = r.get("Grid_Size_X", r.get("Grid_Size", ""))
+        f.write(f"{st:10.1f} {d:9.1f}us grid={grid:>8s} {r['Kernel_Name'][:110]}\n")
