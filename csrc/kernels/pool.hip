@@ -10,6 +10,8 @@
 //
 // Reference counterpart: layer/PoolingLayer.java:62-101 (forward, argmax multimap) and
 // :116-134 (backward scatter); the reference CNN path keeps its own NCHW kernel in ref_ops.hip.
+#include <algorithm>
+
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
@@ -17,26 +19,55 @@ namespace psamd {
 
 // IDX: 32-bit index math when the element count allows it (64-bit div/mod is a long
 // instruction sequence on CDNA and dominated these HBM-light, address-heavy kernels)
+// LCV >= 0 (C / 8 a power of two, 2^LCV): one output row (n, oh) per block iteration, its
+// (ow, channel-group) elements over the threads by shift / mask -- no per-element division (the
+// generic mapping's three runtime-divisor div/mods were most of these kernels' instructions).
 template <bool BN, typename IDX>
 __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const float* __restrict__ coef,
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
                                                                int N, int H, int W, int C, int OH, int OW, int k,
-                                                               int s, int p) {
+                                                               int s, int p, int lcv) {
   const IDX cv = C / 8;
-  const IDX total = static_cast<IDX>(N) * OH * OW * cv;
-  const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
-  for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
-    const int c8 = static_cast<int>(v % cv);
-    IDX r = v / cv;
-    const int ow = static_cast<int>(r % OW);
-    r /= OW;
-    const int oh = static_cast<int>(r % OH);
-    const int n = static_cast<int>(r / OH);
+  auto one = [&](IDX v, int n, int oh, int ow, int c8) {
     float sc[8], sh[8];
     if constexpr (BN) {
       load8(coef, c8 * 8, sc);
       load8(coef + C, c8 * 8, sh);
+    }
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    if constexpr (BN) {
+      // relu(bn(x)) rounded to bf16 is >= +0, so its bits order like the values: the window max
+      // and its first argmax are one unsigned max over key = bits << 8 | (255 - tap) per element
+      // (ties keep the lowest tap, as the unfused path's first-max-wins scan does)
+      unsigned key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int kh = 0; kh < k; ++kh) {
+        const int h = h0 + kh;
+        if (h < 0 || h >= H) continue;
+        for (int kw = 0; kw < k; ++kw) {
+          const int w = w0 + kw;
+          if (w < 0 || w >= W) continue;
+          const u16x8 a = *reinterpret_cast<const u16x8*>(x + ((static_cast<int64_t>(n) * H + h) * W + w) * C + c8 * 8);
+          const unsigned tag = 255u - static_cast<unsigned>(kh * k + kw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = bf16_to_f32(a[j]) * sc[j] + sh[j];
+            t = t > 0.f ? t : 0.f;
+            const unsigned kj = (static_cast<unsigned>(f32_to_bf16(t)) << 8) | tag;
+            key[j] = kj > key[j] ? kj : key[j];
+          }
+        }
+      }
+      u16x8 yv;
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        yv[j] = static_cast<uint16_t>(key[j] >> 8);
+        packed |= static_cast<uint64_t>(255u - (key[j] & 255u)) << (8 * j);
+      }
+      *reinterpret_cast<u16x8*>(y + static_cast<int64_t>(v) * 8) = yv;
+      *reinterpret_cast<uint64_t*>(idx + static_cast<int64_t>(v) * 8) = packed;
+      return;
     }
     float best[8];
     uint8_t bi[8];
@@ -45,7 +76,6 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* _
       best[j] = -INFINITY;
       bi[j] = 0;
     }
-    const int h0 = oh * s - p, w0 = ow * s - p;
     for (int kh = 0; kh < k; ++kh) {
       const int h = h0 + kh;
       if (h < 0 || h >= H) continue;
@@ -57,12 +87,7 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* _
         const uint8_t code = static_cast<uint8_t>(kh * k + kw);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float t = a[j];
-          if constexpr (BN) {
-            t = t * sc[j] + sh[j];
-            t = t > 0.f ? t : 0.f;
-            t = bf16_to_f32(f32_to_bf16(t));  // compare what the unfused path would have stored
-          }
+          const float t = a[j];
           if (t > best[j] || (t != t && best[j] == best[j])) {  // first max wins; NaN propagates
             best[j] = t;
             bi[j] = code;
@@ -75,31 +100,80 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) packed |= static_cast<uint64_t>(bi[j]) << (8 * j);
     *reinterpret_cast<uint64_t*>(idx + static_cast<int64_t>(v) * 8) = packed;
+  };
+  if (lcv >= 0) {
+    const int per_row = OW << lcv;
+    for (int row = blockIdx.x; row < N * OH; row += gridDim.x) {
+      const int n = row / OH, oh = row - n * OH;
+      for (int e = threadIdx.x; e < per_row; e += blockDim.x)
+        one(static_cast<IDX>(row) * per_row + e, n, oh, e >> lcv, e & ((1 << lcv) - 1));
+    }
+    return;
   }
-}
-
-template <typename IDX>
-__global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                               const uint8_t* __restrict__ idx,
-                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
-                                                               int OH, int OW, int k, int s, int p) {
-  const IDX cv = C / 8;
-  const IDX total = static_cast<IDX>(N) * H * W * cv;
+  const IDX total = static_cast<IDX>(N) * OH * OW * cv;
   const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
   for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
     const int c8 = static_cast<int>(v % cv);
     IDX r = v / cv;
-    const int w = static_cast<int>(r % W);
-    r /= W;
-    const int h = static_cast<int>(r % H);
-    const int n = static_cast<int>(r / H);
+    const int ow = static_cast<int>(r % OW);
+    r /= OW;
+    const int oh = static_cast<int>(r % OH);
+    one(v, static_cast<int>(r / OH), oh, ow, c8);
+  }
+}
+
+// S2K3: k = 3, s = 2 (the ResNet stem pool) -- the window bounds become shifts instead of four
+// integer divisions by a runtime stride
+template <typename IDX, bool S2K3>
+__global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                               int OH, int OW, int k, int s, int p, int lcv) {
+  if constexpr (S2K3) {
+    k = 3;
+    s = 2;
+  }
+  const IDX cv = C / 8;
+  auto one = [&](IDX v, int n, int h, int w, int c8) {
     // output windows covering (h, w): oh*s - p <= h <= oh*s - p + k - 1
     const int hp = h + p, wp = w + p;
-    const int oh_lo = hp - k + 1 > 0 ? (hp - k + 1 + s - 1) / s : 0;
-    const int oh_hi = min(OH - 1, hp / s);
-    const int ow_lo = wp - k + 1 > 0 ? (wp - k + 1 + s - 1) / s : 0;
-    const int ow_hi = min(OW - 1, wp / s);
+    int oh_lo, oh_hi, ow_lo, ow_hi;
+    if constexpr (S2K3) {
+      oh_lo = hp - 2 > 0 ? (hp - 1) >> 1 : 0;
+      oh_hi = min(OH - 1, hp >> 1);
+      ow_lo = wp - 2 > 0 ? (wp - 1) >> 1 : 0;
+      ow_hi = min(OW - 1, wp >> 1);
+    } else {
+      oh_lo = hp - k + 1 > 0 ? (hp - k + 1 + s - 1) / s : 0;
+      oh_hi = min(OH - 1, hp / s);
+      ow_lo = wp - k + 1 > 0 ? (wp - k + 1 + s - 1) / s : 0;
+      ow_hi = min(OW - 1, wp / s);
+    }
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (S2K3) {
+      // at most 2 x 2 covering windows: issue all four (idx, dy) reads (clamped in bounds) before
+      // any is used, then accumulate the valid ones in the generic loop's (oh, ow) order
+      uint64_t pk[4];
+      u16x8 gv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oh = min(oh_lo + (q >> 1), OH - 1), ow = min(ow_lo + (q & 1), OW - 1);
+        const int64_t o = ((static_cast<int64_t>(n) * OH + oh) * OW + ow) * C + c8 * 8;
+        pk[q] = *reinterpret_cast<const uint64_t*>(idx + o);
+        gv[q] = *reinterpret_cast<const u16x8*>(dy + o);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
+        if (oh > oh_hi || ow > ow_hi) continue;
+        const uint8_t code = static_cast<uint8_t>((hp - oh * 2) * 3 + (wp - ow * 2));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (static_cast<uint8_t>(pk[q] >> (8 * j)) == code) acc[j] += bf16_to_f32(gv[q][j]);
+      }
+      store8(dx, static_cast<int64_t>(v) * 8, acc);
+      return;
+    }
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         const uint8_t code = static_cast<uint8_t>((hp - oh * s) * k + (wp - ow * s));
@@ -113,18 +187,50 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* _
       }
     }
     store8(dx, static_cast<int64_t>(v) * 8, acc);
+  };
+  if (lcv >= 0) {
+    const int per_row = W << lcv;
+    for (int row = blockIdx.x; row < N * H; row += gridDim.x) {
+      const int n = row / H, h = row - n * H;
+      for (int e = threadIdx.x; e < per_row; e += blockDim.x)
+        one(static_cast<IDX>(row) * per_row + e, n, h, e >> lcv, e & ((1 << lcv) - 1));
+    }
+    return;
   }
+  const IDX total = static_cast<IDX>(N) * H * W * cv;
+  const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
+  for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
+    const int c8 = static_cast<int>(v % cv);
+    IDX r = v / cv;
+    const int w = static_cast<int>(r % W);
+    r /= W;
+    const int h = static_cast<int>(r % H);
+    one(v, static_cast<int>(r / H), h, w, c8);
+  }
+}
+
+// log2(C / 8) when the row mapping applies (C / 8 a power of two, rows of >= 64 elements so a
+// block's threads stay busy, row indices in int range), else -1 (generic flat mapping)
+static int row_lcv(int C, int width, int64_t rows) {
+  const int cv = C / 8;
+  if (cv <= 0 || (cv & (cv - 1)) || static_cast<int64_t>(width) * cv < 64 || rows * width * cv >= (int64_t(1) << 31))
+    return -1;
+  int l = 0;
+  while ((1 << l) < cv) ++l;
+  return l;
 }
 
 void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W,
                              int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(N) * OH * OW * (C / 8);
   if (total <= 0) return;
-  const int grid = stream_grid(total, 256);
-  const bool i32 = total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(grid) * 256;
+  const int lcv = row_lcv(C, OW, static_cast<int64_t>(N) * OH);
+  const int grid = lcv >= 0 ? static_cast<int>(std::min<int64_t>(static_cast<int64_t>(N) * OH, 1 << 20))
+                            : stream_grid(total, 256);
+  const bool i32 = total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(stream_grid(total, 256)) * 256;
 #define PSAMD_MPF(BN, T) \
   hipLaunchKernelGGL((maxpool_nhwc_fwd_kernel<BN, T>), dim3(grid), dim3(256), 0, st, x, coef, y, idx, N, H, W, C, OH, \
-                     OW, k, s, p)
+                     OW, k, s, p, lcv)
   if (coef) {
     if (i32) { PSAMD_MPF(true, uint32_t); } else { PSAMD_MPF(true, int64_t); }
   } else {
@@ -137,13 +243,19 @@ void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* d
                              int OW, int k, int s, int p, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(N) * H * W * (C / 8);
   if (total <= 0) return;
-  const int grid = stream_grid(total, 256);
-  if (total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(grid) * 256)
-    hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, dy, idx, dx, N, H, W, C, OH,
-                       OW, k, s, p);
-  else
-    hipLaunchKernelGGL(maxpool_nhwc_bwd_kernel<int64_t>, dim3(grid), dim3(256), 0, st, dy, idx, dx, N, H, W, C, OH,
-                       OW, k, s, p);
+  const int lcv = row_lcv(C, W, static_cast<int64_t>(N) * H);
+  const int grid = lcv >= 0 ? static_cast<int>(std::min<int64_t>(static_cast<int64_t>(N) * H, 1 << 20))
+                            : stream_grid(total, 256);
+  const bool i32 = total < (int64_t(1) << 31) - 2 * static_cast<int64_t>(stream_grid(total, 256)) * 256;
+#define PSAMD_MPB(T, SK) \
+  hipLaunchKernelGGL((maxpool_nhwc_bwd_kernel<T, SK>), dim3(grid), dim3(256), 0, st, dy, idx, dx, N, H, W, C, OH, OW, \
+                     k, s, p, lcv)
+  if (k == 3 && s == 2) {
+    if (i32) { PSAMD_MPB(uint32_t, true); } else { PSAMD_MPB(int64_t, true); }
+  } else {
+    if (i32) { PSAMD_MPB(uint32_t, false); } else { PSAMD_MPB(int64_t, false); }
+  }
+#undef PSAMD_MPB
 }
 
 }  // namespace psamd

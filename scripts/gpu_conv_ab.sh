@@ -3,7 +3,7 @@
 O=${1:-gpurun_out/ab}
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
-timeout -k 10 600 python -u -m pytest tests/test_convgemm_gpu.py tests/test_bn_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest ${AB_TESTS:-tests/test_convgemm_gpu.py tests/test_bn_gpu.py} -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "rc=$rc" >> $O/pytest.log; tail -3 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || exit $?

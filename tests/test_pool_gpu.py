@@ -121,3 +121,32 @@ def test_stem_fused_block_matches_unfused(N, H):
     for a, b in ((conv.weight.grad, rconv.weight.grad), (bn.weight.grad, rbn.weight.grad),
                  (bn.bias.grad, rbn.bias.grad)):
         assert cos(a.float().flatten(), b.flatten(), dim=0) > 0.99
+
+
+@pytest.mark.parametrize("H,k,s,p", [(112, 3, 2, 1), (15, 3, 2, 1), (10, 3, 1, 1), (9, 2, 2, 0)])
+def test_fused_bn_pool_value_and_first_argmax_exact(H, k, s, p):
+    """BN-apply + ReLU + pool kernel vs the unfused semantics: the max of the bf16-rounded
+    relu(x * scale + shift) (one fp32 rounding, as the kernel's fma) and the FIRST tap (kh, kw)
+    order attaining it -- bitwise, including ties (many zeros after the ReLU)."""
+    from ps_amd.ops import native
+
+    torch.manual_seed(1)
+    N, C = 2, 16
+    x = torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    sc = torch.rand(C, device="cuda") + 0.5
+    sh = torch.randn(C, device="cuda") * 0.5
+    coef = torch.cat([sc, sh]).float().contiguous()
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    y, idx = native().maxpool_nhwc_fwd(xn, coef, k, s, p)
+    # reference: exact product-sum in fp64 -> one rounding to fp32 (= fma) -> bf16
+    a = torch.relu(x.double() * sc.double().view(1, C, 1, 1) + sh.double().view(1, C, 1, 1)).float().bfloat16()
+    ap = torch.nn.functional.pad(a.float(), (p, p, p, p), value=-1.0)  # padding never wins (a >= 0)
+    cols = torch.nn.functional.unfold(ap, k, stride=s)  # [N, C*k*k, L], tap-major within a channel
+    OH = (H + 2 * p - k) // s + 1
+    cols = cols.view(N, C, k * k, OH, OH)
+    ref = cols.max(dim=2).values
+    first = (cols == ref.unsqueeze(2)).float().argmax(dim=2)  # first tap attaining the max
+    yk = y.view(N, OH, OH, C).permute(0, 3, 1, 2).float()
+    ik = idx.view(N, OH, OH, C).permute(0, 3, 1, 2).long()
+    assert torch.equal(yk, ref)
+    assert torch.equal(ik, first)
