@@ -180,8 +180,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce
   constexpr bool FOLD = EPI >= 6;
   constexpr int BASE = EPI == 6 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
-  constexpr int TN = BN / 64;              // 32-channel MFMA blocks per wave
-  constexpr int TM = BM / 64;              // 32-pixel MFMA blocks per wave
+  // waves 2 x 2 over the tile; the tall 256 x 64 tile (LDS-DMA path only) stacks them 4 x 1 so
+  // every wave still computes 64 x 64 (a 128 x 64 tile gave each wave 64 x 32: 1.5 fragment
+  // reads per MFMA instead of 1, and half the weight-tile reuse)
+  constexpr bool TALL = BM == 256;
+  static_assert(!TALL || (BN == 64 && GLDS), "the 256-pixel tile is the LDS-DMA 64-channel variant");
+  constexpr int TN = TALL ? BN / 32 : BN / 64;  // 32-channel MFMA blocks per wave
+  constexpr int TM = TALL ? 2 : BM / 64;        // 32-pixel MFMA blocks per wave
   constexpr int AR = BM / 32;              // A-tile chunks per thread per stage
   constexpr int BCH = BN / 32;             // B-tile chunks per thread per stage
   // output tile row stride (bf16): 2 dwords mod 32 banks, so the 16 rows of a ds_write_b64 lane
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     }
   };
 
-  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int wm = TALL ? wave * 64 : (wave >> 1) * (BM / 2), wn = TALL ? 0 : (wave & 1) * (BN / 2);
   const int fr = lane & 31, fh = lane >> 5;
   f32x16 acc[TN][TM];
   auto zero_acc = [&]() {
@@ -531,7 +536,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         if (kt + 1 < nk) {
           issue(kt + 1, (kt + 1) & 1);
           // this wave's stage-kt DMAs retired (the AI + BI just issued may stay in flight)
-          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if constexpr (AI + BI == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1001,8 +1007,22 @@ int persist_nk_pro() {
   return v;
 }
 
+bool tall_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_TALL");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   ConvFwdPlan pl;
+  if (!pro && N == 64 && K / kBK >= 8 && tall_enabled()) {  // 64-channel 3x3 (K = 576): 256 x 64 tiles
+    pl.bm = 256;
+    pl.bn = 64;
+    pl.gm = (M + 255) / 256;
+    return pl;
+  }
   pl.bn = N % 128 == 0 ? 128 : 64;
   const int nN = N / pl.bn;
   pl.bm = 128;  // (64-pixel tiles measured slower on every ResNet-50 shape: scripts/probe_convgemm.py)
@@ -1021,7 +1041,7 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   const int nblk = GM * (a.N / pl.bn);
   const bool ks1 = a.g.ks == 1;
   // deep K without the BN prologue: LDS-DMA staging (one tile per block)
-  const bool glds = !a.pro && pl.gm == (a.M + 127) / 128 && a.K / kBK > 2;
+  const bool glds = !a.pro && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
 #define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \
   if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, GL>), dim3(nblk), dim3(256), 0, s, a, GM); \
   else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, GL>), dim3(nblk), dim3(256), 0, s, a, GM)
@@ -1041,6 +1061,22 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
     case 7: PSAMD_CF(BN, PRO, 7); break; \
     case 8: PSAMD_CF(BN, PRO, 8); break; \
     default: PSAMD_CF(BN, PRO, 0); break; \
+  }
+  if (pl.bm == 256) {  // LDS-DMA only (no prologue, deep K)
+#define PSAMD_CFT(EPI) PSAMD_CF3(256, 64, false, EPI, true)
+    switch (a.epi) {
+      case 1: PSAMD_CFT(1); break;
+      case 2: PSAMD_CFT(2); break;
+      case 3: PSAMD_CFT(3); break;
+      case 4: PSAMD_CFT(4); break;
+      case 5: PSAMD_CFT(5); break;
+      case 6: PSAMD_CFT(6); break;
+      case 7: PSAMD_CFT(7); break;
+      case 8: PSAMD_CFT(8); break;
+      default: PSAMD_CFT(0); break;
+    }
+#undef PSAMD_CFT
+    return;
   }
   // the BN prologue only appears on forward convolutions (epilogue 0 / 1)
   if (pl.bn == 128) {

@@ -164,11 +164,13 @@ def test_wide_wgrad_kernel(ks, cin, cout, hw, stride, pro):
     _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, ks * ks * cin))
 
 
+@pytest.mark.parametrize("N", [256, 64])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5])
-def test_deep_k_lds_dma_path_all_epilogues(epi):
-    """K % 256 == 0, 128-channel tiles, no prologue: the LDS-DMA kernel with fragment-packed
-    weights (given here as a strided transposed view, as the block backward passes them)."""
-    n, h, w, K, N = 2, 13, 11, 512, 256
+def test_deep_k_lds_dma_path_all_epilogues(epi, N):
+    """K % 256 == 0, no prologue: the LDS-DMA kernel (128-channel tiles; N = 64: the tall
+    256 x 64 tile) with the weight given as a strided transposed view, as the block backward
+    passes it."""
+    n, h, w, K = 2, 13, 11, 512
     M = n * h * w
     g = _gen(40 + epi)
     a, bt = _rnd(M, K, g=g), _rnd(K, N, g=g, scale=K ** -0.5)
@@ -202,10 +204,12 @@ def test_deep_k_lds_dma_path_all_epilogues(epi):
         torch.testing.assert_close(part[1].sum(0).cpu(), (cb * cb).sum(0), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("cin,cout", [(256, 128), (64, 64)])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_conv3x3_deep_k_lds_dma_path(stride):
-    """3x3, C = 256 (K = 2304): padding taps of the LDS-DMA kernel come from its zero page."""
-    n, hw, cin, cout = 2, 9, 256, 128
+def test_conv3x3_deep_k_lds_dma_path(stride, cin, cout):
+    """3x3, C = 256 (K = 2304) / C = 64 (K = 576, the tall 256 x 64 tile): padding taps of the
+    LDS-DMA kernel come from its zero page."""
+    n, hw = 2, 9
     g = _gen(50 + stride)
     x = _rnd(n, hw, hw, cin, g=g)
     wt = _rnd(cout, cin, 3, 3, g=g, scale=(9 * cin) ** -0.5)
