@@ -35,6 +35,9 @@ def parse():
     ap.add_argument("--config", default=os.environ.get("PS_AMD_BENCH_CONFIG", "resnet50"),
                     choices=["resnet50", "bert-ssp", "dlrm", "llama-onebit", "mlp-tcp"])
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: contract dry run of the same code path on CPU tensors over gloo (tests only; "
+                         "the fused HIP paths fall back to the torch module path)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-per-gpu", type=int, default=0, help="0 = config default")
@@ -123,17 +126,24 @@ def main():
                "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
     setup_miopen_db()
-    if not torch.cuda.is_available():
+    cpu = args.device == "cpu"
+    if not cpu and not torch.cuda.is_available():
         print(json.dumps({"metric": args.config, "value": None, "error": "no GPU visible"}))
         return 1
     from ps_amd.parallel.transport import init_distributed
     import torch.distributed as dist
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    tp = init_distributed()
+    if not cpu:
+        torch.cuda.set_device(local)
+    tp = init_distributed(backend="gloo" if cpu else None)
     rank, world = tp.rank, tp.world
-    dev = torch.device("cuda", local)
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.manual_seed(1234)
     bench = BC.SETUPS[args.config](args, tp, dev)
@@ -148,17 +158,17 @@ def main():
     else:
         for _ in range(args.warmup):
             step()
-    torch.cuda.synchronize()
+    sync()
     if rank == 0:
         print(f"[bench] {args.config}: warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
               f"(includes MIOpen find/compile for new conv shapes)", file=sys.stderr, flush=True)
     tp.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     tp.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -178,7 +188,7 @@ def main():
             eng._mark("step0")
             for _ in range(n_timing):
                 step()
-            torch.cuda.synchronize()
+            sync()
             tsum = {k: round(v, 3) for k, v in eng.timing_summary().items()}
         except Exception as e:  # diagnostics only: never lose the measured line
             print(f"[bench-timing] failed: {e!r}", file=sys.stderr, flush=True)
@@ -208,7 +218,7 @@ def main():
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for _ in range(args.profile_steps):
                 step()
-            torch.cuda.synchronize()
+            sync()
         os.makedirs("gpurun_out", exist_ok=True)
         with open("gpurun_out/torch_profile.txt", "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
@@ -216,7 +226,7 @@ def main():
         cfg = dict(bench.config)
         cfg["hip_graph"] = bool(use_graph)
         cfg["final_loss"] = round(float(loss.item()), 4)
-        cfg["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         if tsum:
             cfg["ps_phase_ms_per_step"] = tsum  # measured after the timed region
         if comm:

@@ -1,0 +1,38 @@
+"""bench.py driver contract, exercised on CPU tensors over gloo (``--device cpu``): the same
+torchrun self-launch, barrier-bracketed timed region, MAX-over-ranks elapsed time, per-phase PS
+timing and collective probe as the multi-GPU runs, ending in exactly ONE JSON line from rank 0
+with the BASELINE.json metric."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_json_contract_cpu(world, tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", str(world), "--steps", "2",
+           "--warmup", "1", "--batch-per-gpu", "2", "--image-size", "32"]
+    out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec)
+    baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert rec["metric"] == baseline["metric"]
+    assert rec["n_gpus"] == world and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["config"]["model"] == "ResNet-50" and rec["config"]["global_batch"] == 2 * world
+    # value is the whole-job rate: global batch x steps / (max over ranks of the timed region)
+    assert rec["value"] == pytest.approx(2 * world * 1e3 / rec["ms_per_step"], rel=1e-2)
+    if world > 1:
+        assert set(rec["config"]["ps_phase_ms_per_step"]) >= {"push_ms", "serve_ms", "pull_ms"}
