@@ -146,9 +146,9 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
     cfg = LlamaConfig.tiny() if args.tiny else LlamaConfig.llama3_8b()
     torch.manual_seed(0)
     with torch.device(dev):
-        # no activation checkpointing: bs 1 x 4096 activations (~26 GB) + weights/grads (32 GB) +
-        # fp32 master/Adam state (96 GB, 1/W of it per rank) fit the 288 GB HBM -- recomputing
-        # the forward would cost ~25 % of the step
+        # no activation checkpointing: 4 x 4096 tokens of activations (~26 GB per sequence) +
+        # weights/grads (32 GB) + fp32 master/Adam state (96 GB, 1/W of it per rank) fit the 288 GB
+        # HBM -- recomputing the forward would cost ~25 % of the step
         model = LlamaForCausalLM(cfg, checkpointing=bool(int(os.environ.get("PS_AMD_LLAMA_CKPT", "0")))).to(
             torch.bfloat16)
     upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
@@ -180,7 +180,10 @@ DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not giv
     "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "1024")), seq=0),
     "bert-ssp": dict(batch=256, seq=128),
     "dlrm": dict(batch=16384, seq=0),
-    "llama-onebit": dict(batch=1, seq=4096),
+    # 4 x 4096 tokens per GPU: 215.6 GB peak at world 1 (sized for the 288 GB HBM; the per-step
+    # optimizer / PS cost amortises over 4x the tokens): 16.9K vs 15.7K (2 x 4096) and 14.0K tok/s
+    # (1 x 4096), profiles/r2_llama_batch_sweep.txt
+    "llama-onebit": dict(batch=4, seq=4096),
 }
 
 
