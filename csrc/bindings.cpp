@@ -1161,6 +1161,66 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   return {c, part};
 }
 
+// Data gradient of a 3x3 / stride-2 / pad-1 convolution as four stride-1 phase GEMMs over dz:
+// input pixel (2i + a, 2j + b) gathers dz rows i (+1) with the taps kh = 1 (a = 0) or kh = 2, 0
+// (a = 1) -- likewise for the width -- so phase (a, b) is a 1x1 / 1x2 / 2x1 / 2x2 "convolution"
+// over the dz map whose epilogue writes every other row of dx.  Every dx pixel is written by
+// exactly one phase (H, W even): no zero fill, no scatter-add.  epi 3 (z1, mc, mean, invstd):
+// ReLU mask of the BN that produced the conv input + its backward sums; partials of the four
+// phases are concatenated along the partial-row axis.
+//   dz [n*OH*OW, C2], wph: 4 weights [C1, nh*nw*C2] in phase order (0,0) (0,1) (1,0) (1,1)
+std::vector<Tensor> conv_dgrad_s2(Tensor dz, std::vector<Tensor> wph, int64_t H, int64_t W, int64_t epi,
+                                  c10::optional<Tensor> z, c10::optional<Tensor> mc, c10::optional<Tensor> mean,
+                                  c10::optional<Tensor> invstd) {
+  check_rows(dz, "dz");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && H > 0 && W > 0, "stride-2 phases need an even input map");
+  TORCH_CHECK(wph.size() == 4, "four phase weights");
+  TORCH_CHECK(epi == 0 || epi == 3, "epi 0 or 3");
+  const int64_t OH = H / 2, OW = W / 2, C2 = dz.size(1);
+  TORCH_CHECK(C2 % 64 == 0 && dz.size(0) % (OH * OW) == 0, "dz must be [images*OH*OW, C2], C2 % 64 == 0");
+  const int64_t imgs = dz.size(0) / (OH * OW), M = imgs * OH * OW, C1 = wph[0].size(0);
+  TORCH_CHECK(C1 % 64 == 0 && C1 <= 8192 && imgs * H * W < (int64_t(1) << 31), "C1 / size");
+  const uint16_t* zp = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(z.has_value() && z->defined() && mc.has_value() && mean.has_value() && invstd.has_value(),
+                "epi 3 needs z, mc, mean, invstd");
+    check_rows(*z, "z");
+    TORCH_CHECK(z->numel() == imgs * H * W * C1, "z must be [images*H*W, C1]");
+    zp = u16(*z);
+  }
+  const c10::DeviceGuard guard(dz.device());
+  auto dx = torch::empty({imgs * H * W, C1}, dz.options());
+  std::vector<Tensor> parts;
+  for (int ph = 0; ph < 4; ++ph) {
+    const int a = ph >> 1, b = ph & 1, nh = a ? 2 : 1, nw = b ? 2 : 1;
+    Tensor w = wph[ph].contiguous();
+    check_rows(w, "phase weight");
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == C1 && w.size(1) == nh * nw * C2, "phase weight [C1, nh*nw*C2]");
+    psamd::ConvGemmArgs p{};
+    p.a = u16(dz);
+    p.b = u16(w);
+    p.c = u16m(dx);
+    p.M = static_cast<int>(M);
+    p.N = static_cast<int>(C1);
+    p.K = static_cast<int>(nh * nw * C2);
+    p.g = psamd::ConvGeo{static_cast<int>(OH), static_cast<int>(OW), static_cast<int>(OH), static_cast<int>(OW),
+                         static_cast<int>(C2), nh, 1, 0, nw, static_cast<int>(H), static_cast<int>(W), a, b};
+    p.epi = static_cast<int>(epi);
+    if (epi == 3) {
+      const int G = psamd::conv_fwd_plan(p.M, p.N, p.K, false).gm;
+      parts.push_back(torch::empty({2, G, C1}, dz.options().dtype(torch::kFloat32)));
+      p.aux = zp;
+      p.mc = f32_opt(mc, 2 * C1, "mc");
+      p.mean = f32_opt(mean, C1, "mean");
+      p.invstd = f32_opt(invstd, C1, "invstd");
+      p.part = parts.back().data_ptr<float>();
+    }
+    psamd::launch_conv_fwd(p, cur_stream(dz));  // (a temporary contiguous w is freed stream-ordered)
+  }
+  Tensor part = epi == 3 ? torch::cat(parts, 1) : Tensor();
+  return {dx, part};
+}
+
 // dW [N, ks*ks*C] (bf16) = sum_m dz[m, :]^T f(x[src(m, k)])
 Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<Tensor> pro) {
   check_rows(dz, "dz");
@@ -1283,6 +1343,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
         py::arg("aux2") = py::none(), py::arg("bits2") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("dz"), py::arg("wph"), py::arg("H"), py::arg("W"),
+        py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
+        py::arg("invstd") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);

@@ -228,6 +228,9 @@ void launch_dlrm_interact_bwd(const uint16_t* x, const uint16_t* e, const uint16
 // ks with stride / pad.  Reduction index k = (kh * ks + kw) * C + c (channels_last weight order).
 struct ConvGeo {
   int H, W, OH, OW, C, ks, stride, pad;
+  int ksw;             // taps along the width (0: = ks, square kernel)
+  int RH, RW, ra, rb;  // RH > 0: output pixel (i, oh, ow) lands at row (i, 2 oh + ra, 2 ow + rb) of an
+                       // RH x RW map (one phase of a stride-2 data gradient); 0: rows in order
 };
 struct ConvGemmArgs {
   const uint16_t* a;    // [images, H, W, C] bf16

@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     pcc += kBK;
     if (pcc == g.C) {
       pcc = 0;
-      if (++pkw == g.ks) {
+      if (++pkw == (g.ksw ? g.ksw : g.ks)) {
         pkw = 0;
         ++pkh;
       }
@@ -353,6 +353,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // together before any is consumed: a load-use loop paid one HBM latency per row (the read-heavy
   // data-gradient epilogues ran at ~2.8 TB/s).  Rows past M read row M - 1 (in bounds, unused).
   constexpr int NPASS = BM / RPP;
+  // destination row of output pixel m (a stride-2 data-gradient phase scatters to every other row)
+  auto orow = [&](int m) -> int64_t {
+    if (g.RH == 0) return m;
+    const int ohw = g.OH * g.OW, im = m / ohw, r = m - im * ohw, i = r / g.OW, j = r - i * g.OW;
+    return (static_cast<int64_t>(im) * g.RH + 2 * i + g.ra) * g.RW + 2 * j + g.rb;
+  };
   constexpr bool RD_AUX = BASE == 5 || BASE == 2 || BASE == 4 || EPI == 3;
   u16x8 ra[RD_AUX ? NPASS : 1], rz[FOLD ? NPASS : 1];
   unsigned rb[BASE == 5 ? NPASS : 1], rp[FOLD ? NPASS : 1];
@@ -363,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
 #pragma unroll
     for (int i = 0; i < NPASS; ++i) {
       const int m = min(m0 + r0 + i * RPP, p.M - 1);
-      const int64_t o = static_cast<int64_t>(m) * p.N + nc;
+      const int64_t o = orow(m) * p.N + nc;
       if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
         const int ohw = g.OH * g.OW;
         const int im = m / ohw, r = m - im * ohw, h = r / g.OW, w = r - h * g.OW;
@@ -407,7 +413,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8);
       const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8 + 4);
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int64_t o = static_cast<int64_t>(m) * p.N + nc;
+      const int64_t o = orow(m) * p.N + nc;
       if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
         const u16x8 r8 = ra[i];
         const unsigned bits = rb[i];
@@ -524,7 +530,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       qcc += kBK;
       if (qcc == g.C) {
         qcc = 0;
-        if (++qkw == g.ks) {
+        if (++qkw == (g.ksw ? g.ksw : g.ks)) {
           qkw = 0;
           ++qkh;
         }
@@ -1039,7 +1045,7 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K, a.pro != nullptr);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
-  const bool ks1 = a.g.ks == 1;
+  const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
   // deep K without the BN prologue: LDS-DMA staging (one tile per block)
   const bool glds = !a.pro && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
 #define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \

@@ -16,8 +16,8 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
             also the identity-branch gradient, recomputed from (dout, bits) where consumed
             conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
             with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
-            conv2 data grad (stride 1) -> ReLU mask + bn1 backward sums (GEMM epilogue), weight
-            grad (C >= 128; MIOpen below); stride-2 conv2 data grad [MIOpen] + bn1 backward
+            conv2 data grad -> ReLU mask + bn1 backward sums (GEMM epilogue; stride 2 as four
+            phase GEMMs), weight grad (C >= 256; MIOpen below)
             conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
             epilogue), weight grads.
 
@@ -106,6 +106,45 @@ def _mat3_dgrad(w: torch.Tensor) -> torch.Tensor:
     """The weight of the stride-1 3x3 data gradient as a forward conv over dz: wt[c][kh][kw][n] =
     w[n][c][2 - kh][2 - kw] -> [C, 9N]."""
     return w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1)
+
+
+_PHASE_IDX: dict = {}
+
+
+def _phase_weights(w: torch.Tensor) -> List[torch.Tensor]:
+    """Weights of the four stride-2 data-gradient phases (csrc conv_dgrad_s2): input pixel
+    (2i + a, 2j + b) takes dz row i with tap kh = 1 (a = 0), or dz rows i, i + 1 with taps kh = 2, 0
+    (a = 1); likewise for the width.  Phase (a, b): [C1, nh * nw * C2] in (dh, dw, c2) order.
+    One gather from the (kh, kw, c1)-ordered weight into a phase-major buffer (the index is
+    built once per shape), so each phase weight is a contiguous view."""
+    c2, c1 = w.shape[0], w.shape[1]
+    key = (c2, c1, w.device)
+    idx = _PHASE_IDX.get(key)
+    if idx is None:
+        parts = []
+        ar2 = torch.arange(c2).view(1, 1, 1, c2)
+        ar1 = torch.arange(c1).view(c1, 1, 1, 1)
+        for a in (0, 1):
+            for b in (0, 1):
+                kh = torch.tensor([1] if a == 0 else [2, 0]).view(1, -1, 1, 1)
+                kw = torch.tensor([1] if b == 0 else [2, 0]).view(1, 1, -1, 1)
+                parts.append((((ar2 * 3 + kh) * 3 + kw) * c1 + ar1).reshape(-1))  # [c1, dh, dw, c2]
+        idx = _PHASE_IDX[key] = torch.cat(parts).to(w.device)
+    flat = w.permute(0, 2, 3, 1).reshape(-1)[idx]  # (c2, kh, kw, c1) source order
+    out, o = [], 0
+    for nh, nw in ((1, 1), (1, 2), (2, 1), (2, 2)):
+        k = nh * nw * c2
+        out.append(flat[o:o + c1 * k].view(c1, k))
+        o += c1 * k
+    return out
+
+
+def _dgrad_s2_min_c() -> int:
+    """Stride-2 data gradients on the phase GEMMs from this many channels up (PS_AMD_DGRAD_S2_MIN_C,
+    0 = never): at 256 / 512 channels they beat MIOpen's kernel even before its zero fill and the
+    separate bn1 reduce; at 128 (56x56) MIOpen's is faster (profiles/r2_probe_dgrad_s2.jsonl)."""
+    v = int(os.environ.get("PS_AMD_DGRAD_S2_MIN_C", "256"))
+    return v if v > 0 else 1 << 30
 
 
 WGRAD3X3_MIN_C = 256
@@ -206,7 +245,8 @@ class _BottleneckFn(torch.autograd.Function):
         dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
         c1 = w2.shape[1]
-        ours_dgrad = s == 1 and _conv3x3_enabled()
+        ours_dgrad = _conv3x3_enabled() and (s == 1 or (s == 2 and h % 2 == 0 and w % 2 == 0
+                                                         and w2.shape[1] >= _dgrad_s2_min_c()))
         # weight grad on the wide-tile kernel from 256 input channels up (on par with / faster than
         # MIOpen there; at 64 / 128 channels MIOpen's is faster: profiles/r2_wgrad_probe.jsonl)
         ours_wgrad = _conv3x3_enabled() and c1 >= WGRAD3X3_MIN_C
@@ -220,7 +260,10 @@ class _BottleneckFn(torch.autograd.Function):
         if ours_dgrad:
             # data grad = the forward GEMM over dz2 with the flipped, transposed weight; its epilogue
             # applies bn1's ReLU mask and reduces bn1's backward sums (no separate reduce pass)
-            gy1, p1b = nat.conv_gemm(dz2, _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1, None, cf1, m1, i1)
+            if s == 1:
+                gy1, p1b = nat.conv_gemm(dz2, _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1, None, cf1, m1, i1)
+            else:  # four stride-1 phase GEMMs, each writing every other dx row (no zero fill)
+                gy1, p1b = nat.conv_dgrad_s2(dz2, _phase_weights(w2), h, w, 3, z1, cf1, m1, i1)
             dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
             dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)

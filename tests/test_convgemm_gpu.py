@@ -451,3 +451,35 @@ def test_conv3x3_data_grad_with_bn_backward_sums(n, h, w, C1, C2):
     xhat = (z1.reshape(-1, C1) - mean) * invstd
     torch.testing.assert_close(part[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=2e-2)
     torch.testing.assert_close(part[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=2e-2)
+
+
+@pytest.mark.parametrize("n,h,w,C1,C2,epi", [(2, 14, 10, 128, 128, 3), (3, 8, 8, 64, 256, 0), (1, 28, 28, 256, 64, 3),
+                                             (2, 6, 12, 512, 128, 0)])
+def test_conv3x3_stride2_data_grad_phases(n, h, w, C1, C2, epi):
+    """Stride-2 3x3 data gradient as four stride-1 phase GEMMs over dz (csrc conv_dgrad_s2), each
+    writing every other dx row; epilogue 3: bn1's ReLU mask from z1 and its backward sums over
+    the concatenated phase partials -- vs fp32 torch (conv2d_input)."""
+    from ps_amd.ops.convgemm import _phase_weights
+
+    g = _gen(7 * n + h + C1 + C2 + epi)
+    oh, ow = h // 2, w // 2
+    wt = _rnd(C2, C1, 3, 3, g=g, scale=(9 * C1) ** -0.5)
+    dz = _rnd(n, oh, ow, C2, g=g)
+    dy = torch.nn.grad.conv2d_input((n, C1, h, w), wt, dz.permute(0, 3, 1, 2), stride=2, padding=1)
+    dy = dy.permute(0, 2, 3, 1).reshape(-1, C1)
+    if epi == 0:
+        c, _ = native().conv_dgrad_s2(_bf(dz).reshape(-1, C2), _phase_weights(_bf(wt)), h, w)
+        _close(c, dy)
+        return
+    z1 = _rnd(n, h, w, C1, g=g).reshape(-1, C1)
+    coef = _coef(C1, g)
+    mean, invstd = torch.randn(C1, generator=g) * 0.1, torch.rand(C1, generator=g) + 0.5
+    on = (z1 * coef[:C1] + coef[C1:]) > 0
+    gref = dy.bfloat16().float() * on
+    c, part = native().conv_dgrad_s2(_bf(dz).reshape(-1, C2), _phase_weights(_bf(wt)), h, w, 3, _bf(z1),
+                                     coef.to(DEV), mean.to(DEV), invstd.to(DEV))
+    _close(c, gref)
+    gc = c.float().cpu()
+    xhat = (z1 - mean) * invstd
+    torch.testing.assert_close(part[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=2e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=2e-2)

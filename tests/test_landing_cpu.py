@@ -71,3 +71,21 @@ def test_landing_with_microbatch_accumulation():
         opt.step()
     for (n, p), q in zip(m.named_parameters(), ref.parameters()):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6, msg=n)
+
+
+def test_stride2_phase_weights_gather_matches_indexing():
+    """ops/convgemm._phase_weights (one cached gather) == per-phase advanced indexing."""
+    import torch
+
+    from ps_amd.ops.convgemm import _phase_weights
+
+    w = torch.randn(16, 8, 3, 3).contiguous(memory_format=torch.channels_last)
+    got = _phase_weights(w)
+    i = 0
+    for a in (0, 1):
+        for b in (0, 1):
+            kh = [1] if a == 0 else [2, 0]
+            kw = [1] if b == 0 else [2, 0]
+            ref = w[:, :, kh][:, :, :, kw].permute(1, 2, 3, 0).reshape(w.shape[1], -1)
+            assert torch.equal(got[i], ref) and got[i].is_contiguous()
+            i += 1
