@@ -178,8 +178,11 @@ SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_
 
 DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not given
     "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "1024")), seq=0),
-    "bert-ssp": dict(batch=256, seq=128),
-    "dlrm": dict(batch=16384, seq=0),
+    # per-GPU batches sized for the 288 GB HBM (weak scaling; profiles/r2_bert_dlrm_batch_sweep.txt):
+    # BERT 1024 x 128 (8.41K vs 7.22K seq/s at 256, 45.7 GB peak); DLRM 65536 (12.3M vs 6.9M
+    # samples/s at 16384: the per-step sparse exchange / row optimizer cost amortises)
+    "bert-ssp": dict(batch=1024, seq=128),
+    "dlrm": dict(batch=65536, seq=0),
     # 4 x 4096 tokens per GPU: 215.6 GB peak at world 1 (sized for the 288 GB HBM; the per-step
     # optimizer / PS cost amortises over 4x the tokens): 16.9K vs 15.7K (2 x 4096) and 14.0K tok/s
     # (1 x 4096), profiles/r2_llama_batch_sweep.txt
