@@ -141,9 +141,10 @@ def _phase_weights(w: torch.Tensor) -> List[torch.Tensor]:
 
 def _dgrad_s2_min_c() -> int:
     """Stride-2 data gradients on the phase GEMMs from this many channels up (PS_AMD_DGRAD_S2_MIN_C,
-    0 = never): at 256 / 512 channels they beat MIOpen's kernel even before its zero fill and the
-    separate bn1 reduce; at 128 (56x56) MIOpen's is faster (profiles/r2_probe_dgrad_s2.jsonl)."""
-    v = int(os.environ.get("PS_AMD_DGRAD_S2_MIN_C", "256"))
+    0 = never): at 256 / 512 channels they beat MIOpen's kernel alone; at 128 (56x56) the four
+    phases (747 us) trail its kernel (728 us) but not its zero fill + the separate bn1 reduce
+    (profiles/r2_probe_dgrad_s2.jsonl: bench A/B 13.53-13.56K vs 13.52K img/s)."""
+    v = int(os.environ.get("PS_AMD_DGRAD_S2_MIN_C", "128"))
     return v if v > 0 else 1 << 30
 
 
