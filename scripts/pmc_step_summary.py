@@ -1,6 +1,6 @@
 """Achieved HBM bandwidth per kernel over the last N ResNet-50 steps.
 
-usage: python scripts/pmc_step_summary.py FETCH_DIR WRITE_DIR CLEAN_DB [--steps 2] [--per-step 5]
+usage: python scripts/pmc_step_summary.py FETCH_DIR WRITE_DIR CLEAN_DB_OR_TRACE_CSV [--steps 2] [--per-step 5]
 FETCH_SIZE / WRITE_SIZE (KB, rocprofv3 --pmc, one counter per pass) give the bytes each kernel
 moved through HBM; durations come from a clean (counter-free) kernel trace of the same tree,
 matched by kernel name.  Prints per kernel: dispatches/step, ms/step, GB/step, TB/s.
@@ -36,8 +36,13 @@ def pmc(dirname, counter, steps, per_step):
 
 
 def durations(db, steps=5, per_step=5):
-    c = sqlite3.connect(db)
-    rows = list(c.execute("select name,start,end from kernels order by start"))
+    if db.endswith(".csv"):  # a clean rocprofv3 --kernel-trace csv of the same tree
+        with open(db) as fh:
+            rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                           for r in csv.DictReader(fh)), key=lambda r: r[1])
+    else:
+        c = sqlite3.connect(db)
+        rows = list(c.execute("select name,start,end from kernels order by start"))
     idx = [i for i, r in enumerate(rows) if "fused_opt" in r[0]]
     ends = idx[per_step - 1::per_step]
     lo, hi = ends[-steps - 1] + 1, ends[-1] + 1
