@@ -4,5 +4,5 @@ O=gpurun_out/pl
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
 R=$PWD
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python $R/bench.py --config llama-onebit --steps 3 --warmup 2 > $R/$O/prof.log 2>&1 || exit $?
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python $R/bench.py --config llama-onebit --steps 2 --warmup 1 > $R/$O/prof.log 2>&1 || exit $?
 cd $R && python scripts/kernel_stats_top.py $O/prof/run_kernel_stats.csv 45 > $O/top.txt 2>&1; head -40 $O/top.txt; tail -1 $O/prof.log | cut -c1-200
