@@ -30,6 +30,36 @@ struct FusedOptArgs {
 };
 void launch_fused_opt(const FusedOptArgs& a, hipStream_t s);
 
+// Multi-source gradient of the xGMI plane (optim.hip): element q of the gradient is the sum over
+// s < nsrc, in order, of source s's value at chunk element off + q -- read from g[s] (bf16 when
+// the FusedOptArgs say g_bf16, else fp32), or decoded from 1-bit words[s] / scales[s] (onebit;
+// word q >> 6, scale q / kOnebitChunk, pointers at chunk element 0).
+constexpr int kPlaneMaxSrc = 16;
+struct MultiGrad {
+  const void* g[kPlaneMaxSrc];
+  const uint64_t* words[kPlaneMaxSrc];
+  const float* scales[kPlaneMaxSrc];
+  int nsrc;
+  int onebit;
+  int64_t off;
+};
+// fused optimizer over a segment (a.w / st / wout at the segment's first element; a.g unused)
+void launch_fused_opt_multi(const FusedOptArgs& a, const MultiGrad& m, hipStream_t s);
+// reduce only: out[0, n) fp32 = the multi-source gradient of the segment
+void launch_reduce_multi(const MultiGrad& m, int g_bf16, int64_t n, float* out, hipStream_t s);
+
+// ---------------------------------------------------------------- plane.hip
+// up to kPlaneMaxSrc (src -> dst) copies of equal size, issued as one launch
+struct PlaneCopies {
+  const void* src[kPlaneMaxSrc];
+  void* dst[kPlaneMaxSrc];
+  int nseg;
+};
+void launch_plane_gather(const PlaneCopies& c, int64_t nbytes, hipStream_t s);
+// total = sum_r *(float*)c.src[r] (rank order); factor = min(1, max_norm / (sqrt(total) + 1e-6))
+void launch_plane_clip_factor(const PlaneCopies& c, float max_norm, float* total, float* factor, hipStream_t s);
+void launch_plane_fill(float* p, int64_t n, float v, hipStream_t s);
+
 struct SparseOptArgs {
   int kind;
   float* table;  // [rows_total, dim] owner-local fp32 table

@@ -179,13 +179,18 @@ static void dispatch_grad(const FusedOptArgs& a, const OptParams& p, hipStream_t
   else dispatch_out<KIND, float>(a, p, s);
 }
 
-void launch_fused_opt(const FusedOptArgs& a, hipStream_t s) {
-  if (a.n <= 0) return;
+static OptParams opt_params(const FusedOptArgs& a) {
   OptParams p;
   p.lr = a.lr; p.beta1 = a.beta1; p.beta2 = a.beta2; p.eps = a.eps; p.wd = a.wd;
   p.momentum = a.momentum; p.dampening = a.dampening; p.nesterov = a.nesterov; p.adamw = a.adamw;
   p.bc1 = a.bc1; p.bc2 = a.bc2; p.l1 = a.l1; p.l2 = a.l2; p.fbeta = a.fbeta; p.ftrl_mode = a.ftrl_mode;
   p.skip_zero = 0; p.gscale = a.gscale; p.gscale_ptr = a.gscale_ptr;
+  return p;
+}
+
+void launch_fused_opt(const FusedOptArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  const OptParams p = opt_params(a);
   switch (a.kind) {
     case kSGD: dispatch_grad<kSGD>(a, p, s); break;
     case kAdam: dispatch_grad<kAdam>(a, p, s); break;
@@ -193,6 +198,192 @@ void launch_fused_opt(const FusedOptArgs& a, hipStream_t s) {
     case kFtrl: dispatch_grad<kFtrl>(a, p, s); break;
     default: break;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Owner-side "reduce + serve" of the xGMI parameter-server plane (ps_amd/parallel/plane.py,
+// csrc/plane.cpp): the gradient of every element is the sum, in fixed rank order, of the W
+// workers' pushed values read straight out of their IPC-mapped gradient buckets (or decoded
+// from their 1-bit packed pushes), accumulated in fp32 and fed to the fused optimizer in the
+// same pass.  One kernel replaces reduce-scatter + owner optimizer: the reduced gradient never
+// round-trips through HBM, and each lane keeps W 16-B loads in flight -- one per peer -- so all
+// of a GPU's xGMI links stream concurrently.
+//
+// Segments start at an arbitrary chunk element ``off`` (key boundaries inside a bucket): block
+// 0 handles the unaligned head and the tail element by element, everything else moves 8
+// elements (16 B of bf16) per lane per source.
+//
+// Coherence: the producers' data is published by a HIP event (system-scope release) that the
+// host observed before launching this kernel; the system-scope acquire at entry makes sure no
+// stale line of a peer's buffer is served from this GPU's caches.
+// ---------------------------------------------------------------------------------------
+template <int ONEBIT, typename G>
+__device__ __forceinline__ float multi_load1(const MultiGrad& m, int64_t q) {
+  float acc = 0.f;
+  for (int s = 0; s < m.nsrc; ++s) {
+    if constexpr (ONEBIT) {
+      const uint64_t wd = m.words[s][q >> 6];
+      const float sc = m.scales[s][q / kOnebitChunk];
+      acc += ((wd >> (q & 63)) & 1ull) ? sc : -sc;
+    } else {
+      acc += Elem<G>::load(static_cast<const G*>(m.g[s]), q);
+    }
+  }
+  return acc;
+}
+
+template <int ONEBIT, typename G>
+__device__ __forceinline__ void multi_load8(const MultiGrad& m, int64_t q0, float (&acc)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if constexpr (ONEBIT) {
+    const int sh = static_cast<int>(q0 & 63);
+    for (int s = 0; s < m.nsrc; ++s) {
+      const uint32_t byte = static_cast<uint32_t>(m.words[s][q0 >> 6] >> sh) & 0xFFu;
+      const float sc = m.scales[s][q0 / kOnebitChunk];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += ((byte >> k) & 1u) ? sc : -sc;
+    }
+  } else {
+    // issue every source's 16-B load before the first add: W loads in flight per lane
+    float v[kPlaneMaxSrc][8];
+#pragma unroll
+    for (int s = 0; s < kPlaneMaxSrc; ++s)
+      if (s < m.nsrc) load8(static_cast<const G*>(m.g[s]), q0, v[s]);
+#pragma unroll
+    for (int s = 0; s < kPlaneMaxSrc; ++s)
+      if (s < m.nsrc) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[s][k];
+      }
+  }
+}
+
+template <int KIND, int ONEBIT, typename G, int OUT>
+__global__ __launch_bounds__(256) void fused_opt_multi_kernel(float* __restrict__ w, float* __restrict__ st0,
+                                                               float* __restrict__ st1, const MultiGrad m,
+                                                               void* __restrict__ wout, int64_t n, int64_t head,
+                                                               OptParams p) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  float scale = p.gscale;
+  if (p.gscale_ptr) scale *= *p.gscale_ptr;
+  const bool use_st0 = st0 != nullptr;
+  const bool use_st1 = st1 != nullptr;
+  const int64_t nv = (n - head) / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = head + v * 8;
+    float wr[8], gr[8], a[8], b[8];
+    multi_load8<ONEBIT, G>(m, m.off + i, gr);
+    load8(w, i, wr);
+    if (use_st0) load8(st0, i, a);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    }
+    if (use_st1) load8(st1, i, b);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) opt_apply<KIND>(wr[j], gr[j] * scale, a[j], b[j], p);
+    store8(w, i, wr);
+    if (use_st0) store8(st0, i, a);
+    if (use_st1) store8(st1, i, b);
+    if constexpr (OUT == 1) store8(static_cast<uint16_t*>(wout), i, wr);
+    if constexpr (OUT == 2) store8(static_cast<float*>(wout), i, wr);
+  }
+  if (blockIdx.x == 0) {  // unaligned head [0, head) and tail [head + 8 nv, n)
+    const int64_t tail0 = head + nv * 8;
+    const int64_t ntail = n - tail0;
+    for (int64_t t = threadIdx.x; t < head + ntail; t += blockDim.x) {
+      const int64_t i = t < head ? t : tail0 + (t - head);
+      float wr = w[i], a = use_st0 ? st0[i] : 0.f, b = use_st1 ? st1[i] : 0.f;
+      opt_apply<KIND>(wr, multi_load1<ONEBIT, G>(m, m.off + i) * scale, a, b, p);
+      w[i] = wr;
+      if (use_st0) st0[i] = a;
+      if (use_st1) st1[i] = b;
+      if constexpr (OUT == 1) static_cast<uint16_t*>(wout)[i] = f32_to_bf16(wr);
+      if constexpr (OUT == 2) static_cast<float*>(wout)[i] = wr;
+    }
+  }
+}
+
+template <int KIND, int ONEBIT, typename G>
+static void launch_multi_out(const FusedOptArgs& a, const MultiGrad& m, const OptParams& p, int64_t head,
+                             hipStream_t s) {
+  const int grid = stream_grid((a.n - head + 7) / 8, 256);
+  if (a.wout == nullptr)
+    hipLaunchKernelGGL((fused_opt_multi_kernel<KIND, ONEBIT, G, 0>), dim3(grid), dim3(256), 0, s, a.w, a.st0, a.st1,
+                       m, a.wout, a.n, head, p);
+  else if (a.wout_bf16)
+    hipLaunchKernelGGL((fused_opt_multi_kernel<KIND, ONEBIT, G, 1>), dim3(grid), dim3(256), 0, s, a.w, a.st0, a.st1,
+                       m, a.wout, a.n, head, p);
+  else
+    hipLaunchKernelGGL((fused_opt_multi_kernel<KIND, ONEBIT, G, 2>), dim3(grid), dim3(256), 0, s, a.w, a.st0, a.st1,
+                       m, a.wout, a.n, head, p);
+}
+
+template <int KIND>
+static void launch_multi_kind(const FusedOptArgs& a, const MultiGrad& m, const OptParams& p, int64_t head,
+                              hipStream_t s) {
+  if (m.onebit) launch_multi_out<KIND, 1, float>(a, m, p, head, s);
+  else if (a.g_bf16) launch_multi_out<KIND, 0, uint16_t>(a, m, p, head, s);
+  else launch_multi_out<KIND, 0, float>(a, m, p, head, s);
+}
+
+void launch_fused_opt_multi(const FusedOptArgs& a, const MultiGrad& m, hipStream_t s) {
+  if (a.n <= 0) return;
+  const OptParams p = opt_params(a);
+  // elements before the first 8-aligned chunk index are done element-wise (every array of the
+  // segment shares the phase of m.off: masters / states / wout start at the segment too)
+  int64_t head = (8 - (m.off & 7)) & 7;
+  if (head > a.n) head = a.n;
+  switch (a.kind) {
+    case kSGD: launch_multi_kind<kSGD>(a, m, p, head, s); break;
+    case kAdam: launch_multi_kind<kAdam>(a, m, p, head, s); break;
+    case kAdagrad: launch_multi_kind<kAdagrad>(a, m, p, head, s); break;
+    case kFtrl: launch_multi_kind<kFtrl>(a, m, p, head, s); break;
+    default: break;
+  }
+}
+
+// Reduce-only form (global-norm clipping needs the whole reduced gradient before any update):
+// out[i] = sum over sources, fp32, in rank order.
+template <int ONEBIT, typename G>
+__global__ __launch_bounds__(256) void reduce_multi_kernel(const MultiGrad m, int64_t n, int64_t head,
+                                                            float* __restrict__ out) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int64_t nv = (n - head) / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = head + v * 8;
+    float gr[8];
+    multi_load8<ONEBIT, G>(m, m.off + i, gr);
+    store8(out, i, gr);
+  }
+  if (blockIdx.x == 0) {
+    const int64_t tail0 = head + nv * 8;
+    const int64_t ntail = n - tail0;
+    for (int64_t t = threadIdx.x; t < head + ntail; t += blockDim.x) {
+      const int64_t i = t < head ? t : tail0 + (t - head);
+      out[i] = multi_load1<ONEBIT, G>(m, m.off + i);
+    }
+  }
+}
+
+void launch_reduce_multi(const MultiGrad& m, int g_bf16, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t head = (8 - (m.off & 7)) & 7;
+  if (head > n) head = n;
+  const int grid = stream_grid((n - head + 7) / 8, 256);
+  if (m.onebit)
+    hipLaunchKernelGGL((reduce_multi_kernel<1, float>), dim3(grid), dim3(256), 0, s, m, n, head, out);
+  else if (g_bf16)
+    hipLaunchKernelGGL((reduce_multi_kernel<0, uint16_t>), dim3(grid), dim3(256), 0, s, m, n, head, out);
+  else
+    hipLaunchKernelGGL((reduce_multi_kernel<0, float>), dim3(grid), dim3(256), 0, s, m, n, head, out);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -62,7 +62,8 @@ class ColocatedPS:
                  transport: Optional[Transport] = None, *, bucket_mb: float = 32.0, last_bucket_mb: float = 4.0,
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
                  average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
-                 compress_warmup: int = 0, split_comm: Optional[bool] = None):
+                 compress_warmup: int = 0, split_comm: Optional[bool] = None, plane: Optional[str] = None,
+                 timeout_s: float = 600.0):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -95,17 +96,34 @@ class ColocatedPS:
         # keys stored channels_last in the flat buffers (element order O, kh, kw, I)
         self.cl_keys = {n for n, p in params if _wants_channels_last(p)}
         R = self.reg
+        # ---------------- data plane: one-sided xGMI plane (plane.py) or collectives (transport)
+        from .plane import XgmiPlane, env_plane, plane_available
+
+        req = plane or env_plane()
+        if req not in ("auto", "xgmi", "collective"):
+            raise ValueError(f"unknown plane {req!r}")
+        use_plane = self.world > 1 and (req == "xgmi" or (req == "auto" and self.gpu
+                                                             and plane_available(self.t, self.device)))
+        self.plane_kind = "xgmi" if use_plane else ("collective" if self.world > 1 else "local")
+        self.plane = (XgmiPlane(self.t, R, self.device, self.nslots, onebit=compress == "onebit", clip_norm=clip_norm,
+                                average=average, timeout_s=timeout_s) if use_plane else None)
         # ---------------- replica buffers (rings of s+1 slots)
-        self.wbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
-                         for _ in range(self.nslots)] for g in R.group_size}
-        self.gbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
-                         for _ in range(self.nslots)] for g in R.group_size}
+        if self.plane is not None:
+            self.wbuf = self.plane.slots("w")
+            self.gbuf = self.plane.slots("g")
+        else:
+            self.wbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
+                             for _ in range(self.nslots)] for g in R.group_size}
+            self.gbuf = {g: [torch.zeros(R.group_size[g], dtype=R.group_dtype[g], device=self.device)
+                             for _ in range(self.nslots)] for g in R.group_size}
         with torch.no_grad():
             for n, p in params:
                 ki = R.keys[n]
                 src = p.detach().permute(0, 2, 3, 1) if n in self.cl_keys else p.detach()
                 self.wbuf[ki.group][0][ki.offset:ki.offset + ki.numel].view(src.shape).copy_(src)
-            if broadcast_init:
+            if broadcast_init and self.plane is not None:
+                self.plane.broadcast_weights(self.wbuf, src=0)
+            elif broadcast_init:
                 for g in self.wbuf:
                     self.t.broadcast(self.wbuf[g][0], src=0)
             for g in self.wbuf:
@@ -135,12 +153,15 @@ class ColocatedPS:
             segs[-1] = (segs[-1][0], segs[-1][1], hi - lo)
             self.segs.append(segs)
             self.states.append([u.new_states(m[a:z]) for (u, a, z) in segs])
-            if self.world > 1:
+            if self.world > 1 and self.plane is None:
                 self.gshard.append(torch.empty(b.chunk, dtype=R.group_dtype[b.group], device=self.device))
             else:
                 self.gshard.append(None)
-        # 1-bit compression state: error-feedback buffer per bucket (full bucket, fp32)
-        if compress == "onebit":
+        # 1-bit compression state: error-feedback buffer per bucket (full bucket, fp32); with the
+        # plane the packed words / scales live in its arena (one per gradient slot)
+        if compress == "onebit" and self.plane is not None:
+            self.err = [torch.zeros(b.size, dtype=torch.float32, device=self.device) for b in R.buckets]
+        elif compress == "onebit":
             self.err = [torch.zeros(b.size, dtype=torch.float32, device=self.device) for b in R.buckets]
             self.cwords = []
             self.cscales = []
@@ -192,6 +213,8 @@ class ColocatedPS:
         self._prev_marks: List[tuple] = []
         self._bind(self.wslot, self.gslot)
         self._mark("step0")
+        if self.plane is not None:
+            self.plane.attach(self)
         self._hooks = [p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
 
     # ------------------------------------------------------------------ views
@@ -248,6 +271,16 @@ class ColocatedPS:
         self._land(b)
         if self.fault is not None:
             self.fault.before_push()
+        if self.plane is not None:
+            onebit = self.compress == "onebit" and self.round >= self.compress_warmup
+            if onebit:
+                bk = self.reg.buckets[b]
+                gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
+                words, scales = self.plane.words(b, self.gslot)
+                _cmp.onebit_pack(gin, self.err[b], words, scales)
+            with _trace.range(f"ps.push.b{b}"):
+                self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
+            return
         if self.gpu:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
@@ -391,6 +424,9 @@ class ColocatedPS:
         for b in range(len(self.reg.buckets)):
             if not self.launched[b]:
                 self._launch(b)
+        if self.plane is not None:
+            self._finish_plane_round()
+            return
         if self.clip_norm is not None:
             if self.gpu:
                 self.comm_pull.wait_stream(self.comm)
@@ -430,6 +466,29 @@ class ColocatedPS:
         if self.timing:
             self._close_timing_deferred()
 
+    def _finish_plane_round(self) -> None:
+        """Round bookkeeping of the xGMI plane: the engine runs serve / pull on its own streams;
+        the compute stream waits only for the round the next forward must see."""
+        self.round += 1
+        self.stats["rounds"] += 1
+        v = max(0, self.round - self.staleness)
+        need_round = v - 1
+        if need_round >= 0:
+            self.plane.wait_pulled(need_round)
+        if self.timing:
+            self._mark("round_end")
+        self.wslot = v % self.nslots
+        self.gslot = self.round % self.nslots
+        self.pending = [len(b.keys) for b in self.reg.buckets]
+        self.launched = [False] * len(self.reg.buckets)
+        self._bind(self.wslot, self.gslot)
+        if self.timing:
+            self._close_timing_deferred()
+
+    def plane_stats(self, reset: bool = False) -> Dict[str, float]:
+        """Per-round means of the xGMI plane engine (serve / pull kernel ms, waits for peers)."""
+        return self.plane.stats(reset) if self.plane is not None else {}
+
     def _close_timing_deferred(self) -> None:
         # keep one step in flight: fold the PREVIOUS step's marks (already complete or nearly)
         # so timing adds no per-step host sync to the critical path
@@ -443,6 +502,10 @@ class ColocatedPS:
 
     def synchronize(self) -> None:
         """Drain every in-flight round (checkpoint / eval boundary)."""
+        if self.plane is not None:
+            if self.round > 0:
+                self.plane.wait_pulled(self.round - 1)
+            return
         if self.gpu:
             while self.round_events:
                 torch.cuda.current_stream(self.device).wait_event(self.round_events.popleft())
@@ -477,7 +540,15 @@ class ColocatedPS:
                         s.copy_(src.to(s.device))
             self.round = int(st["round"])
             # rebuild every replica slot by one pull of the restored masters
-            for b, bk in enumerate(self.reg.buckets):
+            if self.plane is not None:
+                for b, bk in enumerate(self.reg.buckets):
+                    lo, hi = bk.owner_range(self.rank)
+                    for slot in range(self.nslots):
+                        wfull = self.wbuf[bk.group][slot]
+                        wfull[lo:hi].copy_(self.master[b].to(wfull.dtype))
+                for slot in range(self.nslots):
+                    self.plane.gather_all(slot)
+            for b, bk in enumerate(self.reg.buckets if self.plane is None else []):
                 lo, hi = bk.owner_range(self.rank)
                 for slot in range(self.nslots):
                     wfull = self.wbuf[bk.group][slot]
@@ -494,6 +565,13 @@ class ColocatedPS:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self.plane is not None:
+            pl, self.plane = self.plane, None
+            try:
+                pl.close()
+            finally:
+                self.t.barrier()
+                pl.release()
 
 
 def _snap(t: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,216 @@
+"""The xGMI plane on the MI355X: W real PROCESSES on cuda:0, each mapping the others' device
+arenas through CUDA-IPC handles, the native engine issuing the fused multi-source optimizer
+and the owner-dealt pull kernels, pushes fired from autograd hooks (overlap=True, the
+production configuration).  Compared with single-process fp32 oracles: BSP at W = 2 and 4,
+SSP(1), global-norm clipping, per-prefix updaters, 1-bit pushes (vs the CPU oracle of the
+same compression), and a bf16 ResNet-tiny trajectory at W = 4 (fp32 sum of the pushes on
+the owner) against fp32 torch.  The control plane (handle exchange, barriers) is gloo."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ps_amd.parallel.transport import run_loopback
+from tests import dist_util
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(40, 64), torch.nn.Tanh(), torch.nn.Linear(64, 5))
+
+
+def _data(n=64, dev=DEV):
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(n, 40, generator=g).to(dev), torch.randint(0, 5, (n,), generator=g).to(dev)
+
+
+def _body(tp, kw, steps, upd="momentum", models=None):
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import AdamUpdater, MomentumUpdater, SimpleUpdater
+
+    torch.cuda.set_device(0)
+    m = (models[tp.rank] if models is not None else _model(seed=tp.rank)).to(DEV)
+    u = {"momentum": lambda: MomentumUpdater(0.1, 0.9, 1e-4), "sgd": lambda: SimpleUpdater(0.2),
+         "mixed": lambda: {"0.": AdamUpdater(0.01), "default": MomentumUpdater(0.1, 0.9)}}[upd]()
+    ps = ColocatedPS(m, u, tp, bucket_mb=0.004, last_bucket_mb=0.002, plane="xgmi", timeout_s=60, **kw)
+    x, y = _data()
+    xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
+    losses = []
+    for _ in range(steps):
+        loss = F.cross_entropy(m(xs), ys)
+        loss.backward()
+        ps.finish_step()
+        losses.append(loss.item())
+    ps.synchronize()
+    torch.cuda.synchronize()
+    out = {n: p.detach().float().cpu().clone() for n, p in m.named_parameters()}
+    st = ps.plane_stats()
+    kind = ps.plane_kind
+    ps.close()
+    return out, losses, kind, st
+
+
+def _oracle(world, steps, opt_factory, clip=None):
+    ref = _model(0).to(DEV)
+    opt = opt_factory(ref.parameters())
+    x, y = _data()
+    for _ in range(steps):
+        opt.zero_grad()
+        (sum(F.cross_entropy(ref(x[r::world]), y[r::world]) for r in range(world)) / world).backward()
+        if clip is not None:
+            torch.nn.utils.clip_grad_norm_(ref.parameters(), clip)
+        opt.step()
+    return {n: p.detach().cpu() for n, p in ref.named_parameters()}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_plane_processes_bsp_equals_single_process(world):
+    res = dist_util.run(_body, world, ({}, 5))
+    assert res[0][2] == "xgmi"
+    for r in range(1, world):
+        for k in res[0][0]:
+            assert torch.equal(res[0][0][k], res[r][0][k])
+    ref = _oracle(world, 5, lambda p: torch.optim.SGD(p, lr=0.1, momentum=0.9, weight_decay=1e-4))
+    for k, v in ref.items():
+        torch.testing.assert_close(res[0][0][k], v, rtol=1e-5, atol=1e-5)
+    st = res[0][3]
+    assert st["rounds"] >= 1 and st["serve_ms"] > 0 and st["pull_ms"] > 0
+
+
+def test_plane_processes_ssp1_matches_delayed_sgd():
+    world, steps, lr, s = 2, 6, 0.2, 1
+    res = dist_util.run(_body, world, ({"staleness": s}, steps, "sgd", [_model(0), _model(0)]))
+    ref = _model(0).to(DEV)
+    x, y = _data()
+    versions = [{n: p.detach().clone() for n, p in ref.named_parameters()}]
+    for t in range(steps):
+        probe = copy.deepcopy(ref)
+        with torch.no_grad():
+            for n, p in probe.named_parameters():
+                p.copy_(versions[max(0, t - s)][n])
+        loss = sum(F.cross_entropy(probe(x[r::world]), y[r::world]) for r in range(world)) / world
+        grads = torch.autograd.grad(loss, list(probe.parameters()))
+        versions.append({n: versions[-1][n] - lr * g for (n, _), g in zip(probe.named_parameters(), grads)})
+    want = versions[max(0, steps - s)]
+    for k in want:
+        torch.testing.assert_close(res[0][0][k], want[k].cpu(), rtol=1e-5, atol=1e-5)
+
+
+def test_plane_processes_clip_norm():
+    res = dist_util.run(_body, 2, ({"clip_norm": 0.05}, 4, "sgd"))
+    ref = _oracle(2, 4, lambda p: torch.optim.SGD(p, lr=0.2), clip=0.05)
+    for k, v in ref.items():
+        torch.testing.assert_close(res[0][0][k], v, rtol=1e-5, atol=1e-5)
+
+
+def test_plane_processes_mixed_updaters():
+    res = dist_util.run(_body, 2, ({}, 5, "mixed"))
+    ref = _model(0).to(DEV)
+    opts = [torch.optim.Adam(ref[0].parameters(), lr=0.01, eps=1e-8),
+            torch.optim.SGD(ref[2].parameters(), lr=0.1, momentum=0.9)]
+    x, y = _data()
+    for _ in range(5):
+        for o in opts:
+            o.zero_grad()
+        (sum(F.cross_entropy(ref(x[r::2]), y[r::2]) for r in range(2)) / 2).backward()
+        for o in opts:
+            o.step()
+    for n, p in ref.named_parameters():
+        torch.testing.assert_close(res[0][0][n], p.detach().cpu(), rtol=1e-4, atol=1e-5)
+
+
+def _cpu_onebit(tp, steps):
+    # the same 1-bit training on CPU thread-ranks (python oracles of pack / unpack-reduce)
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import MomentumUpdater
+
+    m = copy.deepcopy(_CPU_MODELS[tp.rank])
+    ps = ColocatedPS(m, MomentumUpdater(0.1, 0.9, 1e-4), tp, bucket_mb=0.004, last_bucket_mb=0.002,
+                     plane="collective", compress="onebit", compress_warmup=1)
+    x, y = _data(dev="cpu")
+    xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
+    for _ in range(steps):
+        F.cross_entropy(m(xs), ys).backward()
+        ps.finish_step()
+    ps.synchronize()
+    return {n: p.detach().clone() for n, p in m.named_parameters()}
+
+
+_CPU_MODELS = None
+
+
+def test_plane_processes_onebit_matches_cpu_oracle():
+    global _CPU_MODELS
+    res = dist_util.run(_body, 2, ({"compress": "onebit", "compress_warmup": 1}, 6, "momentum",
+                                   [_model(0), _model(0)]))
+    _CPU_MODELS = [_model(0), _model(0)]
+    want = run_loopback(_cpu_onebit, 2, 6)[0]
+    for k in want:
+        assert torch.equal(res[0][0][k], res[1][0][k])
+        torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-4, atol=1e-4)
+
+
+def test_plane_thread_ranks_gpu():
+    # thread-ranks of one process share raw device pointers instead of IPC handles
+    models = [_model(0).to(DEV) for _ in range(3)]
+    res = run_loopback(_body, 3, {}, 4, "momentum", models)
+    ref = _oracle(3, 4, lambda p: torch.optim.SGD(p, lr=0.1, momentum=0.9, weight_decay=1e-4))
+    for k, v in ref.items():
+        torch.testing.assert_close(res[0][0][k], v, rtol=1e-5, atol=1e-5)
+
+
+def _resnet_body(tp, steps):
+    from ps_amd.models.resnet import prepare_for_mi355x, resnet_tiny
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import MomentumUpdater
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    net = prepare_for_mi355x(resnet_tiny(num_classes=10, fused_bn=True).cuda())
+    ps = ColocatedPS(net, MomentumUpdater(0.05, 0.9, 0.0), tp, bucket_mb=0.25, plane="xgmi", timeout_s=60)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
+    losses = []
+    for _ in range(steps):
+        loss = F.cross_entropy(net(xs.bfloat16()).float(), ys)
+        loss.backward()
+        ps.finish_step()
+        losses.append(loss.item())
+    ps.synchronize()
+    torch.cuda.synchronize()
+    ps.close()
+    return losses
+
+
+def test_plane_processes_resnet_tiny_bf16_trajectory_vs_fp32():
+    from ps_amd.models.resnet import resnet_tiny
+
+    world, steps = 4, 6
+    res = dist_util.run(_resnet_body, world, (steps,))
+    torch.manual_seed(0)
+    ref = resnet_tiny(num_classes=10, fused_bn=True)
+    for mod in ref.modules():
+        if hasattr(mod, "fuse_block"):
+            mod.fuse_block = False
+    ref = ref.cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    lref = []
+    for _ in range(steps):
+        opt.zero_grad()
+        ls = [F.cross_entropy(ref(x[r::world]), y[r::world]) for r in range(world)]
+        (sum(ls) / world).backward()
+        opt.step()
+        lref.append(ls[0].item())
+    la = res[0]
+    for a, b in zip(la, lref):
+        assert abs(a - b) < 0.05 * max(1.0, abs(b)), (la, lref)
+    assert la[-1] < la[0], la
