@@ -3,8 +3,11 @@
 
 BASELINE.json metric: "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X
 workers" -- one process per GPU (torchrun), every rank a worker + the server of its range
-partition, push = RCCL reduce-scatter, server = fused HIP momentum-SGD on the fp32 master
-shard, pull = RCCL all-gather, all overlapped with backward (ps_amd/parallel/colocated.py);
+partition (ps_amd/parallel/colocated.py).  Data plane (``--plane``, default auto = xgmi on one
+node): push = land the bucket in the rank's own IPC-mapped buffer, serve = ONE kernel per owner
+reading its chunk from all W peers over xGMI, fp32 sum fused with the HIP momentum-SGD step,
+pull = ONE kernel copying every other owner's fresh chunk (ps_amd/parallel/plane.py); or
+``collective`` = RCCL reduce-scatter / all-gather.  Both overlap with backward.
 BatchNorm+residual+ReLU run as fused HIP kernels (ps_amd/ops/bn.py).
 
 Weak scaling: ``--batch-per-gpu`` images per rank per step (default 1024 -- sized for the
@@ -46,6 +49,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("PS_AMD_BUCKET_MB", "25")))
     ap.add_argument("--last-bucket-mb", type=float, default=2.0)
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--plane", default=os.environ.get("PS_AMD_PLANE", "auto"), choices=["auto", "xgmi", "collective"],
+                    help="PS data plane at world > 1: one-sided xGMI plane (IPC) or RCCL collectives")
     ap.add_argument("--bn-fp32", type=int, default=1)
     ap.add_argument("--fused-bn", type=int, default=int(os.environ.get("PS_AMD_FUSED_BN", "1")),
                     help="HIP fused BatchNorm+residual+ReLU kernels (ops/bn.py) instead of MIOpen BN")
@@ -134,9 +139,14 @@ def main():
     import torch.distributed as dist
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-GPU path on a one-GPU box: every rank on cuda:0, gloo for the
+    # control plane (RCCL refuses two ranks on one device); the xGMI plane still runs its IPC path
+    one_gpu = os.environ.get("PS_AMD_BENCH_ONE_GPU", "0") == "1"
+    if one_gpu:
+        local = 0
     if not cpu:
         torch.cuda.set_device(local)
-    tp = init_distributed(backend="gloo" if cpu else None)
+    tp = init_distributed(backend="gloo" if (cpu or one_gpu) else None)
     rank, world = tp.rank, tp.world
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)
 
@@ -170,7 +180,7 @@ def main():
     tp.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if tp.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -190,6 +200,12 @@ def main():
                 step()
             sync()
             tsum = {k: round(v, 3) for k, v in eng.timing_summary().items()}
+            if getattr(eng, "plane", None) is not None:
+                eng.plane_stats(reset=True)
+                for _ in range(n_timing):
+                    step()
+                sync()
+                tsum.update({"plane_" + k: round(float(v), 3) for k, v in eng.plane_stats(reset=True).items()})
         except Exception as e:  # diagnostics only: never lose the measured line
             print(f"[bench-timing] failed: {e!r}", file=sys.stderr, flush=True)
         eng.timing = False
@@ -225,6 +241,8 @@ def main():
     if rank == 0:
         cfg = dict(bench.config)
         cfg["hip_graph"] = bool(use_graph)
+        if getattr(bench.engine, "plane_kind", None) is not None:
+            cfg["data_plane"] = bench.engine.plane_kind
         cfg["final_loss"] = round(float(loss.item()), 4)
         cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         if tsum:

@@ -11,7 +11,9 @@
 //                  blocks the host that keeps launching the next step's kernels.
 #include <torch/extension.h>
 
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -58,6 +60,8 @@ class GpuAsyncServer {
     a_.dampening = dampening; a_.nesterov = nesterov; a_.adamw = adamw; a_.bc1 = 1.f; a_.bc2 = 1.f;
     a_.l1 = l1; a_.l2 = l2; a_.fbeta = fbeta; a_.ftrl_mode = static_cast<int>(ftrl_mode);
     a_.gscale = gscale; a_.gscale_ptr = nullptr;
+    // test hook: a slow owner (the worker's host then runs far ahead of the server)
+    if (const char* d = std::getenv("PS_AMD_ASYNC_SERVE_DELAY_US")) delay_us_ = std::atoi(d);
   }
   ~GpuAsyncServer() { stop(); }
 
@@ -76,6 +80,7 @@ class GpuAsyncServer {
           a.bc1 = 1.f / (1.f - beta1_);
           a.bc2 = 1.f / (1.f - beta2_);
         }
+        if (delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
         a.g = mbox_[static_cast<size_t>(w)].data_ptr();
         a.wout = pub_[static_cast<size_t>(slot)].data_ptr();
         psamd::launch_fused_opt(a, s);
@@ -103,6 +108,7 @@ class GpuAsyncServer {
   std::atomic<bool> stop_{true};
   std::thread th_;
   int64_t applied_ = 0;
+  int delay_us_ = 0;
 };
 
 class GpuNotifier {

@@ -126,8 +126,10 @@ struct Philox {
     uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
     c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
   }
-  __device__ __forceinline__ static void gen(uint64_t seed, uint64_t ctr, uint32_t (&out)[4]) {
-    uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), 0u, 0u};
+  // 128-bit counter: ctr = low 64 bits, ctr_hi = high 64 bits
+  __device__ __forceinline__ static void gen(uint64_t seed, uint64_t ctr, uint32_t (&out)[4], uint64_t ctr_hi = 0) {
+    uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr_hi),
+                     static_cast<uint32_t>(ctr_hi >> 32)};
     uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {

@@ -343,10 +343,11 @@ __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__
       todo &= todo - 1;
       const int64_t rr = __shfl(row, l, 64);
       const uint64_t grow = static_cast<uint64_t>(__shfl(key, l, 64));
-      // one Philox call yields the 4 values of elements 4q .. 4q+3 (counter = key << 20 ^ q)
+      // one Philox call yields the 4 values of elements 4q .. 4q+3: 128-bit counter (q, key), so
+      // map-mode keys (field << 44 | id) keep their field bits and every field gets its own rows
       for (int q = lane; q * 4 < dim; q += 64) {
         uint32_t rnd[4];
-        Philox::gen(seed, (grow << 20) ^ static_cast<uint64_t>(q), rnd);
+        Philox::gen(seed, static_cast<uint64_t>(q), rnd, grow);
         float* dst = table + rr * dim + q * 4;
         if (q * 4 + 4 <= dim && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
           store4(dst, 0, f32x4{lo + span * Philox::u01(rnd[0]), lo + span * Philox::u01(rnd[1]),

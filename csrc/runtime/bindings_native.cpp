@@ -423,6 +423,21 @@ PYBIND11_MODULE(_native, m) {
       bo();
     }
   }, py::call_guard<py::gil_scoped_release>());
+  // wait until owner o has APPLIED at least ``target`` pushes of worker w: before queueing push
+  // number target + 1 into the 1-deep mailbox the worker gates on its OWN push count, not on
+  // seq (which the completion thread bumps only after the previous copy landed)
+  a.def("wait_ack", [](uintptr_t addr, int o, int w, int64_t target, double timeout_s) {
+    auto* c = ctl_at(addr);
+    const auto t0 = std::chrono::steady_clock::now();
+    psasync::Backoff bo;
+    while (psasync::ld(&c->ack[o][w]) < target) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        throw std::runtime_error("async PS: owner did not apply the previous push in time (dead server?)");
+      bo();
+    }
+  }, py::call_guard<py::gil_scoped_release>());
+  // checkpoint restore: the owner's update count (Adam bias correction continues from it)
+  a.def("set_version", [](uintptr_t addr, int o, int64_t v) { psasync::st(&ctl_at(addr)->version[o], v); });
   a.def("bump_seq", [](uintptr_t addr, int o, int w) { return psasync::add(&ctl_at(addr)->seq[o][w], 1); });
   a.def("bump_clock", [](uintptr_t addr, int w) { return psasync::add(&ctl_at(addr)->clock[w], 1); });
   a.def("wait_min_ack", [](uintptr_t addr, int64_t target, double timeout_s) {

@@ -323,7 +323,7 @@ uint16_t PSServer::handle(Op op, Reader& in, Writer& out) {
             e.w.resize(dim, 0.f);
             if (lo != 0.f || hi != 0.f)
               for (uint32_t c = 0; c < dim; ++c)  // word c%4 of the call for c/4 (as the HIP kernel)
-                e.w[c] = lo + (hi - lo) * philox_u01(seed, (static_cast<uint64_t>(keys[i]) << 20) ^ (c / 4), c % 4);
+                e.w[c] = lo + (hi - lo) * philox_u01(seed, c / 4, c % 4, static_cast<uint64_t>(keys[i]));
             it = t.rows.emplace(keys[i], std::move(e)).first;
           }
           std::memcpy(rows.data() + static_cast<size_t>(i) * dim, it->second.w.data(), dim * sizeof(float));

@@ -130,8 +130,11 @@ class AdagradUpdater : public Updater {
 // Philox-4x32-10, bit-identical to psamd::Philox (csrc/include/psamd_device.h) and
 // ps_amd.ops.sparse.philox_u01: server-created rows get exactly the values the HIP lazy-init
 // kernel gives the same (seed, key) on the GPU path.
-inline float philox_u01(uint64_t seed, uint64_t ctr, int word = 0) {
-  uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), 0u, 0u};
+// 128-bit counter (ctr low 64 bits, ctr_hi high 64 bits): lazily initialised rows use
+// (element group, global key) so every key -- field bits included -- gets its own stream
+inline float philox_u01(uint64_t seed, uint64_t ctr, int word = 0, uint64_t ctr_hi = 0) {
+  uint32_t c[4] = {static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr_hi),
+                   static_cast<uint32_t>(ctr_hi >> 32)};
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c[0];

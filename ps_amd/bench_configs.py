@@ -47,7 +47,7 @@ def setup_resnet50(args, tp, dev) -> Bench:
     model = prepare_for_mi355x(resnet50(fused_bn=bool(args.fused_bn)).to(dev), bn_fp32=bool(args.bn_fp32))
     upd = MomentumUpdater(lr=args.lr, momentum=0.9, weight_decay=5e-5)
     ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
-                     staleness=args.staleness)
+                     staleness=args.staleness, plane=getattr(args, "plane", None))
     B, S = args.batch_per_gpu, args.image_size
     g = torch.Generator(device=dev).manual_seed(tp.rank)
     pool = [(torch.randn(B, 3, S, S, device=dev, generator=g).to(torch.bfloat16).contiguous(
@@ -117,7 +117,7 @@ def setup_dlrm(args, tp, dev) -> Bench:
     model.bottom.to(torch.bfloat16)
     model.top.to(torch.bfloat16)
     ps = ColocatedPS(model, AdagradUpdater(0.01, 1e-8), tp, bucket_mb=args.bucket_mb,
-                     last_bucket_mb=args.last_bucket_mb)
+                     last_bucket_mb=args.last_bucket_mb, plane=getattr(args, "plane", None))
     B = args.batch_per_gpu
     # 4x the usual pool: every step brings new ids, so dedupe, lazy row creation and the row
     # exchange are measured on fresh data rather than on one memorised batch
@@ -153,7 +153,7 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
             torch.bfloat16)
     upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
-                     compress="onebit" if tp.world > 1 else None)
+                     compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None))
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)
     pool = [torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g) for _ in range(POOL)]

@@ -102,15 +102,19 @@ def sparse_lr_fwd(w: torch.Tensor, ids: torch.Tensor, bias: torch.Tensor | None,
 _M32 = 0xFFFFFFFF
 
 
-def philox_u01(seed: int, ctr: torch.Tensor) -> torch.Tensor:
+def philox_u01(seed: int, ctr: torch.Tensor, ctr_hi: torch.Tensor | None = None) -> torch.Tensor:
     """uniform [0, 1) from the 4 words of Philox-4x32-10(seed, ctr) -> [n, 4] -- bit-identical
     to ``Philox::gen`` + ``u01`` in csrc/include/psamd_device.h (and the host copy in the native
     server), computed with int64 torch ops so the CPU oracle initialises rows exactly like the
     HIP kernel."""
     ctr = ctr.long()
     c0, c1 = ctr & _M32, (ctr >> 32) & _M32
-    c2 = torch.zeros_like(c0)
-    c3 = torch.zeros_like(c0)
+    if ctr_hi is None:
+        c2 = torch.zeros_like(c0)
+        c3 = torch.zeros_like(c0)
+    else:  # 128-bit counter: high 64 bits
+        hi = ctr_hi.long().expand_as(ctr)
+        c2, c3 = hi & _M32, (hi >> 32) & _M32
     k0, k1 = int(seed) & _M32, (int(seed) >> 32) & _M32
     for _ in range(10):
         p0 = 0xD2511F53 * c0  # < 2^64: wraps in int64 with the same low bits
@@ -125,10 +129,12 @@ def philox_u01(seed: int, ctr: torch.Tensor) -> torch.Tensor:
 
 def init_values(seed: int, keys: torch.Tensor, dim: int, lo: float, hi: float) -> torch.Tensor:
     """Deterministic first-touch values of rows ``keys`` ([n] int64 global keys) -> [n, dim]:
-    element c is word c % 4 of Philox(seed, key << 20 ^ c // 4) (one call per 4 elements)."""
+    element c is word c % 4 of Philox(seed, counter = (c // 4, key)) -- a 128-bit counter, so
+    keys that differ only in their high (field) bits still get independent rows."""
     q = torch.arange((dim + 3) // 4, dtype=torch.int64, device=keys.device)
-    ctr = (keys.long()[:, None] << 20) ^ q[None, :]
-    u = philox_u01(seed, ctr.reshape(-1)).reshape(keys.numel(), -1)[:, :dim]
+    ctr = q[None, :].expand(keys.numel(), -1)
+    khi = keys.long()[:, None].expand_as(ctr)
+    u = philox_u01(seed, ctr.reshape(-1), khi.reshape(-1)).reshape(keys.numel(), -1)[:, :dim]
     return lo + (hi - lo) * u
 
 

@@ -295,8 +295,12 @@ class AsyncPS:
         if self.gpu:
             torch.cuda.current_stream(self.device).wait_stream(self.push_stream)  # gflat free again
         self._land()
-        for r in range(W):  # each owner must have consumed our previous push (1-deep mailbox)
-            A.wait_free(self.ctl, r, me, self.timeout_s)
+        # each owner must have APPLIED every earlier push of ours before the next copy lands in the
+        # 1-deep mailbox: gate on our own push count (seq lags behind on GPU -- it is bumped by
+        # the completion thread after the copy finished -- so "ack == seq" could pass while the
+        # previous copy is still queued, and the owner would read a mailbox being overwritten)
+        for r in range(W):
+            A.wait_ack(self.ctl, r, me, self.clock, self.timeout_s)
         if self.gpu:
             cur = torch.cuda.current_stream(self.device)
             self.push_stream.wait_stream(cur)
@@ -359,7 +363,8 @@ class AsyncPS:
         self.synchronize()
         self.t.barrier()
         st = self.states if self.gpu else [torch.from_numpy(a) for a in self.server.states()]
-        snap = {"rank": self.rank, "world": self.world, "round": self.round, "clock": self.clock,
+        version = int(self.A.snapshot(self.ctl)["version"][self.rank])
+        snap = {"rank": self.rank, "world": self.world, "round": self.round, "clock": self.clock, "version": version,
                 "master": self.master.detach().to("cpu", copy=True),
                 "states": [s.detach().to("cpu", copy=True) for s in st], "staleness": self.staleness}
         self.t.barrier()
@@ -378,6 +383,9 @@ class AsyncPS:
             else:
                 self.server.set_states([x.numpy() for x in st["states"]])
             self.pub.copy_(self.master.to(self.dtype).expand(3, self.L))  # every slot = restored shard
+            # the owner's update count drives Adam's bias correction (serve_loop applies with
+            # step = version + 1): a fresh control block would restart it at 1 on warm moments
+            self.A.set_version(self.ctl, self.rank, int(st.get("version", 0)))
         if self.gpu:
             torch.cuda.current_stream(self.device).synchronize()
         self.round = int(st["round"])

@@ -104,9 +104,20 @@ class ColocatedPS:
             raise ValueError(f"unknown plane {req!r}")
         use_plane = self.world > 1 and (req == "xgmi" or (req == "auto" and self.gpu
                                                              and plane_available(self.t, self.device)))
-        self.plane_kind = "xgmi" if use_plane else ("collective" if self.world > 1 else "local")
-        self.plane = (XgmiPlane(self.t, R, self.device, self.nslots, onebit=compress == "onebit", clip_norm=clip_norm,
-                                average=average, timeout_s=timeout_s) if use_plane else None)
+        self.plane = None
+        if use_plane:
+            from .plane import PlaneUnavailable
+
+            try:
+                self.plane = XgmiPlane(self.t, R, self.device, self.nslots, onebit=compress == "onebit",
+                                       clip_norm=clip_norm, average=average, timeout_s=timeout_s)
+            except PlaneUnavailable as e:  # raised on every rank alike: the fallback is uniform
+                if req == "xgmi":
+                    raise
+                import sys
+
+                print(f"[ps_amd] {e}; using the collective data plane", file=sys.stderr, flush=True)
+        self.plane_kind = "xgmi" if self.plane is not None else ("collective" if self.world > 1 else "local")
         # ---------------- replica buffers (rings of s+1 slots)
         if self.plane is not None:
             self.wbuf = self.plane.slots("w")

@@ -64,6 +64,11 @@ def _C():
     return m
 
 
+class PlaneUnavailable(RuntimeError):
+    """Raised on EVERY rank (the ranks agree at each step) when the plane cannot be set up --
+    the caller may fall back to the collective path without the ranks diverging."""
+
+
 def plane_available(transport: Transport, device: torch.device) -> bool:
     """The xGMI plane needs every rank on this host (one node) and at most MAX_WORLD ranks."""
     if transport.world <= 1:
@@ -118,18 +123,33 @@ class XgmiPlane:
         self.sq_off = self._take(2 * 4)
         self.probe_off = self._take(self.W * 64 * 4)
         self.nbytes = self._off
-        # ---------------- allocate + share
+        # ---------------- allocate + share (every fallible local step ends in an agreement, so a
+        # failure raises PlaneUnavailable on all ranks at the same point)
         self._arena = None
         self._seg = None
+        self._ctl = None
+        self._tmp_engine = None
         self._opened: List[_ShmSeg] = []
         if self.gpu:
-            self._arena = P.Arena(self.nbytes, device.index)
-            self.arena = self._arena.tensor()
-            if self.threads:
-                bases = self.t.all_gather_object(self._arena.base)
-            else:
-                hs = self.t.all_gather_object((self._arena.handle(), device.index))
-                bases = [self._arena.base if r == self.me else self._arena.open(h, d) for r, (h, d) in enumerate(hs)]
+            err = None
+            try:
+                self._arena = P.Arena(self.nbytes, device.index)
+                self.arena = self._arena.tensor()
+                mine = (self._arena.handle() if not self.threads else self._arena.base, device.index)
+            except Exception as e:  # noqa: BLE001 -- reported through the agreement
+                err, mine = e, None
+            hs = self.t.all_gather_object(mine)
+            self._agree(err is None and all(h is not None for h in hs), f"arena allocation failed: {err!r}")
+            bases = []
+            try:
+                for r, (h, d) in enumerate(hs):
+                    if r == self.me or self.threads:
+                        bases.append(self._arena.base if r == self.me else int(h))
+                    else:
+                        bases.append(self._arena.open(h, d))
+            except Exception as e:  # noqa: BLE001
+                err = e
+            self._agree(err is None, f"mapping the peer arenas failed: {err!r}")
             self.bases = bases
             self.peers = None
         else:
@@ -165,6 +185,19 @@ class XgmiPlane:
         self._hyper_round = -1
         self._uids: Dict[int, int] = {}
         self._ups: List = []
+        if self.gpu and not self.threads:
+            err = None
+            try:
+                self.self_test()
+            except Exception as e:  # noqa: BLE001
+                err = e
+            self._agree(err is None, f"self-test failed: {err!r}")
+
+    def _agree(self, ok: bool, what: str) -> None:
+        oks = self.t.all_gather_object(bool(ok))
+        if not all(oks):
+            bad = [r for r, o in enumerate(oks) if not o]
+            raise PlaneUnavailable(f"xGMI plane unavailable (ranks {bad}): " + (what if not ok else "peer failure"))
 
     # ------------------------------------------------------------------ layout helpers
     def _take(self, nbytes: int) -> int:
@@ -228,8 +261,7 @@ class XgmiPlane:
         if not self.gpu:
             eng.set_callback(self._callback)
         self.engine = eng
-        if self.gpu and not self.threads:
-            self.self_test()
+        self._tmp_engine = None
         eng.start()
 
     def _uid(self, u) -> int:
@@ -295,7 +327,7 @@ class XgmiPlane:
         if self.engine is not None:
             return self.engine
         # before attach(): a bare engine for the start-up copies (never started)
-        if getattr(self, "_tmp_engine", None) is None:
+        if self._tmp_engine is None:
             P = _C().plane
             self._tmp_engine = P.Engine(self.ctl, self.me, self.W, len(self.reg.buckets), self.nslots, True,
                                         self.device.index, 60.0, 0.0, True)
@@ -311,6 +343,7 @@ class XgmiPlane:
         first real round: a mapping that does not work, or reads that come back stale, fail
         here loudly instead of corrupting training."""
         probe = self.view(self.probe_off, torch.float32, self.W * 64)
+        eng = self.engine_or_tmp()
         for it in range(2):
             val = float(1000 * (it + 1) + self.me + 1)
             probe[self.me * 64:(self.me + 1) * 64].fill_(val)
@@ -319,7 +352,7 @@ class XgmiPlane:
             st = torch.cuda.current_stream(self.device).cuda_stream
             for p in range(self.W):
                 if p != self.me:
-                    self.engine.copy_peer(p, self.probe_off + p * 256, 256, st)
+                    eng.copy_peer(p, self.probe_off + p * 256, 256, st)
             self._sync()
             got = probe.view(self.W, 64).cpu()
             for p in range(self.W):

@@ -182,3 +182,45 @@ def test_async_ps_checkpoint_resume(tmp_path):
         # the resumed run continued from the saved state: its moments moved on from there
         assert not torch.equal(a[r][1], b[r][1])
         assert torch.isfinite(b[r][1]).all()
+
+
+def _resume_parity_body(tp, split):
+    """6 Adam(bias_correction="step") steps, either straight through or 3 + checkpoint + a
+    FRESH AsyncPS (new control block) restored from it + 3."""
+    from ps_amd.parallel.async_ps import AsyncPS
+    from ps_amd.parallel.updaters import AdamUpdater
+
+    x, y = _data()
+
+    def run(ps, m, n):
+        for _ in range(n):
+            F.cross_entropy(m(x), y).backward()
+            ps.finish_step()
+
+    m = _MODELS[0]
+    ps = AsyncPS(m, AdamUpdater(0.05, bias_correction="step"), tp, staleness=0)
+    run(ps, m, 3 if split else 6)
+    st = ps.shard_state()
+    ps.close()
+    if split:
+        ps = AsyncPS(m, AdamUpdater(0.05, bias_correction="step"), tp, staleness=0)
+        ps.load_shard_state(st)
+        run(ps, m, 3)
+        st = ps.shard_state()
+        ps.close()
+    return st
+
+
+_MODELS = None
+
+
+def test_async_resume_restores_adam_step_count():
+    """the owner's update count (Adam's t) is part of the shard state; a resumed
+    owner must continue at t = 4, not restart bias correction at t = 1 on warm moments."""
+    global _MODELS
+    _MODELS = [_model(0)]
+    a = run_loopback(_resume_parity_body, 1, False)[0]
+    _MODELS = [_model(0)]
+    b = run_loopback(_resume_parity_body, 1, True)[0]
+    assert a["version"] == b["version"] == 6
+    torch.testing.assert_close(a["master"], b["master"], rtol=0, atol=0)

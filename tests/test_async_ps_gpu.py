@@ -87,3 +87,39 @@ def test_two_processes_ipc_mailboxes_on_one_gpu():
     for k in res[0][0]:
         assert torch.equal(res[0][0][k], res[1][0][k])
     assert res[0][1][-1] < res[0][1][0]
+
+
+def _exact_body(tp, steps, models):
+    from ps_amd.parallel.async_ps import AsyncPS
+    from ps_amd.parallel.updaters import SimpleUpdater
+
+    torch.cuda.set_device(0)
+    m = models[tp.rank]
+    ps = AsyncPS(m, SimpleUpdater(0.25), tp, staleness=None, timeout_s=60)  # ASP
+    c = torch.full((16, 64), float(tp.rank + 1), device=DEV)
+    for _ in range(steps):
+        (m.weight * c).sum().backward()  # gradient == c: independent of the weights read
+        ps.finish_step()
+    ps.synchronize()
+    tp.barrier()
+    ps.refresh()
+    out = m.weight.detach().cpu().clone()
+    ps.close()
+    return out
+
+
+def test_asp_slow_server_applies_every_push_exactly_once(monkeypatch):
+    """ADVICE r2 (mailbox race): with a slow owner the worker's host runs far ahead; every push
+    must still be applied exactly once and never read while being overwritten.  SGD with a
+    weight-independent gradient makes the final weights an exact sum:
+    w = w0 - lr / W * steps * (c_0 + c_1), exactly representable in fp32."""
+    monkeypatch.setenv("PS_AMD_ASYNC_SERVE_DELAY_US", "3000")
+    steps = 12
+    models = [torch.nn.Linear(64, 16, bias=False).to(DEV) for _ in range(2)]
+    with torch.no_grad():
+        for mm in models:
+            mm.weight.fill_(1.0)
+    res = run_loopback(_exact_body, 2, steps, models)
+    want = 1.0 - 0.25 / 2 * steps * (1.0 + 2.0)
+    for r in range(2):
+        assert torch.equal(res[r], torch.full((16, 64), want)), res[r].unique()

@@ -220,3 +220,15 @@ def test_map_mode_checkpoint_resume(tmp_path):
     probe = torch.tensor([900, 7, 123456, 55, 4242])
     assert torch.equal(a.pull(probe), b.pull(probe))
     assert not torch.equal(b.pull(torch.tensor([55])), b.pull(torch.tensor([900])))
+
+
+def test_lazy_init_fields_with_same_id_get_independent_rows():
+    # map-mode keys are field << 44 | id: the Philox counter carries the whole key (128-bit
+    # counter), so the same raw id in two fields must not start from the same vector
+    from ps_amd.ops.sparse import init_values
+
+    keys = torch.tensor([(0 << 44) | 5, (1 << 44) | 5, (2 << 44) | 5, 5 + (1 << 20)], dtype=torch.int64)
+    rows = init_values(7, keys, 8, -0.5, 0.5)
+    for i in range(len(keys)):
+        for j in range(i + 1, len(keys)):
+            assert not torch.allclose(rows[i], rows[j])
