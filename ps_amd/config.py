@@ -12,7 +12,7 @@ from __future__ import annotations
 import dataclasses
 import os
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 _ALIASES = {
     # reference name (Context.java / README)  ->  field
@@ -99,6 +99,17 @@ class Config:
             return "asp"
         return self.consistency
 
+    def given(self, name: str) -> bool:
+        """True if ``name`` was set explicitly (a -D flag, --flag or PS_AMD_* variable)."""
+        return name in self.__dict__.get("_given", ())
+
+    def ui_address(self) -> Optional[Tuple[str, int]]:
+        """(uiHost, uiPort) of the metrics UI when the job was told about one (-DuiHost /
+        -DuiPort, Context.java:81-82 -> visual/UiClient.java:25-27), else None."""
+        if self.given("ui_port") or self.given("ui_host"):
+            return self.ui_host, int(self.ui_port)
+        return None
+
     def set(self, key: str, value) -> None:
         name = _ALIASES.get(key, key.replace("-", "_"))
         if name == "mode":
@@ -108,6 +119,7 @@ class Config:
             raise KeyError(f"unknown config key {key!r}")
         t = f.type if isinstance(f.type, type) else {"int": int, "float": float, "bool": bool, "str": str}[f.type]
         setattr(self, name, _to_bool(value) if t is bool else t(value))
+        self.__dict__.setdefault("_given", set()).add(name)
 
     # ----------------------------------------------------------------- sources
     @classmethod

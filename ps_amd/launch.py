@@ -38,6 +38,13 @@ def run_attempt(cmd: List[str], nproc: int, attempt: int, env_extra: dict, poll_
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PS_AMD_RESTART=str(attempt), **env_extra)
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
     rc = 0
+    clean = False
+    # ranks run in their own sessions (terminal SIGINT does not reach them): forward SIGTERM /
+    # SIGINT to the launcher into a teardown of the attempt
+    def _on_signal(signum, frame):
+        raise KeyboardInterrupt(f"signal {signum}")
+
+    old = {sg: signal.signal(sg, _on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
     try:
         while True:
             codes = [p.poll() for p in procs]
@@ -46,10 +53,13 @@ def run_attempt(cmd: List[str], nproc: int, attempt: int, env_extra: dict, poll_
                 rc = bad[0]
                 break
             if all(c == 0 for c in codes):
+                clean = True
                 return 0
             time.sleep(poll_s)
     finally:
-        if rc != 0:
+        for sg, h in old.items():
+            signal.signal(sg, h)
+        if not clean:  # a failed rank, or the launcher itself interrupted: no rank may outlive it
             for p in procs:  # tear the attempt down: every rank's own process group
                 if p.poll() is None:
                     try:

@@ -3,7 +3,10 @@
 ``plot(id, y, x)`` records a point in-process, appends a JSON line to ``PS_AMD_METRICS_PATH``
 (one file per rank) and, when a UI server address is configured, hands the point to a
 background sender thread (never blocks the training step -- same contract as the
-reference's gzip'd async gRPC stub).  Structured step records (``log_step``) carry
+reference's gzip'd async gRPC stub).  The address comes from the reference flags
+``-DuiHost`` / ``-DuiPort`` (context/Context.java:81-82, visual/UiClient.java:25-27) or
+``PS_AMD_UI_ADDR``; only the reporting replica sends -- replica 0 of a ``-DisMajor=1`` worker
+(``ctx.is_report_ui()``, context/Context.java:94-100).  Structured step records (``log_step``) carry
 samples/s, push/pull bytes, staleness and server-update time.
 """
 from __future__ import annotations
@@ -51,8 +54,14 @@ def plot(name: str, y: float, x: float) -> None:
         if f is not None:
             f.write(json.dumps({"t": time.time(), "series": name, "x": x, "y": y}) + "\n")
     c = _client or _auto_client()
-    if c is not None:
+    if c is not None and _report_ui():
         c.send(name, x, y)
+
+
+def _report_ui() -> bool:
+    from ..context import ctx
+
+    return ctx.is_report_ui()
 
 
 def log_step(**fields) -> None:
@@ -116,14 +125,25 @@ class UiClient:
             time.sleep(0.01)
 
 
+_auto: Dict[Tuple[str, int], "UiClient"] = {}
+
+
 def _auto_client():
-    global _client
+    """The UI client of the configured address (one sender thread per address)."""
     addr = os.environ.get("PS_AMD_UI_ADDR", "")
-    if not addr:
-        return None
-    host, port = addr.rsplit(":", 1)
-    _client = UiClient(host, int(port))
-    return _client
+    if addr:
+        host, port = addr.rsplit(":", 1)
+        key = (host, int(port))
+    else:
+        from ..context import ctx
+
+        key = ctx.cfg.ui_address()
+        if key is None:
+            return None
+    c = _auto.get(key)
+    if c is None:
+        c = _auto[key] = UiClient(*key)
+    return c
 
 
 def set_client(c: Optional[UiClient]) -> None:

@@ -6,11 +6,15 @@ Same HTTP contract as the reference's NanoHTTPD server on :8888:
   GET      ``/``                -> the dashboard page (polls act=data every second)
 plus ``POST /plot`` (the ingest endpoint, replacing the reference's gRPC ``plot`` RPC on
 uiPort; body = list of {id, x, y}).  ThreadingHTTPServer, so ingest never blocks a reader.
+Like the reference the server listens on two ports -- the dashboard on ``-DuiHttpPort``
+(8888, visual/UiServer.java:36) and the workers' ingest on ``-DuiPort`` (8990,
+Context.java:81) -- both serving every route.
 """
 from __future__ import annotations
 
 import json
 import threading
+from typing import Optional
 from collections import defaultdict
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from urllib.parse import parse_qs, urlparse
@@ -36,7 +40,7 @@ poll();
 
 
 class UiServer:
-    def __init__(self, host: str = "127.0.0.1", port: int = 8888):
+    def __init__(self, host: str = "127.0.0.1", port: int = 8888, plot_port: Optional[int] = None):
         self.series = defaultdict(list)
         self.lock = threading.Lock()
         srv = self
@@ -94,27 +98,42 @@ class UiServer:
 
         self.httpd = ThreadingHTTPServer((host, port), H)
         self.port = self.httpd.server_address[1]
-        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+        self._servers = [self.httpd]
+        self.plot_port = None
+        if plot_port is not None:  # the workers' ingest port (reference uiPort)
+            ingest = ThreadingHTTPServer((host, plot_port), H)
+            self.plot_port = ingest.server_address[1]
+            self._servers.append(ingest)
+        self.threads = [threading.Thread(target=s.serve_forever, daemon=True) for s in self._servers]
 
     def start(self) -> "UiServer":
-        self.thread.start()
+        for t in self.threads:
+            t.start()
         return self
 
     def stop(self) -> None:
-        self.httpd.shutdown()
-        self.httpd.server_close()
+        for s in self._servers:
+            s.shutdown()
+            s.server_close()
 
 
 def main():  # pragma: no cover - CLI
     import argparse
     import time
 
+    import sys
+
+    from ..config import Config
+
+    # reference flags: -DuiHost, -DuiHttpPort (dashboard), -DuiPort (ingest)
+    cfg = Config.from_args([a for a in sys.argv[1:] if a.startswith("-D")])
     ap = argparse.ArgumentParser()
-    ap.add_argument("--host", default="127.0.0.1")
-    ap.add_argument("--port", type=int, default=8888)
-    a = ap.parse_args()
-    s = UiServer(a.host, a.port).start()
-    print(f"ps_amd UI on http://{a.host}:{s.port}/", flush=True)
+    ap.add_argument("--host", default=cfg.ui_host)
+    ap.add_argument("--port", type=int, default=cfg.ui_http_port)
+    ap.add_argument("--plot-port", type=int, default=cfg.ui_port)
+    a, _ = ap.parse_known_args()
+    s = UiServer(a.host, a.port, a.plot_port).start()
+    print(f"ps_amd UI on http://{a.host}:{s.port}/ (ingest on :{s.plot_port})", flush=True)
     while True:
         time.sleep(3600)
 

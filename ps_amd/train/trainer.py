@@ -134,20 +134,49 @@ class Trainer:
         if self.ckpt is None:
             return
         if isinstance(self.engine, KVEngine):
+            # dedicated TCP servers hold the whole model: worker 0 asks every server to write its
+            # store, then marks the step COMMITTED (resume() only trusts committed steps)
             if self.engine.kv.client is not None and self.engine.kv.worker_id == 0:
                 import os
 
                 d = os.path.join(self.ckpt.dir, f"tcp_step{step:08d}")
                 os.makedirs(d, exist_ok=True)
                 self.engine.kv.client.save(os.path.join(d, "server"))
+                with open(os.path.join(d, "COMMIT"), "w") as f:
+                    f.write(str(step))
             return
         self.engine.synchronize()
         self.ckpt.save(step, getattr(self.engine, "ps", None), self._tables(), extra={"step": step, **(extra or {})},
                        blocking=blocking)
 
+    def _tcp_latest(self) -> Optional[str]:
+        import os
+
+        if self.ckpt is None or not os.path.isdir(self.ckpt.dir):
+            return None
+        done = sorted(d for d in os.listdir(self.ckpt.dir)
+                      if d.startswith("tcp_step") and os.path.exists(os.path.join(self.ckpt.dir, d, "COMMIT")))
+        return os.path.join(self.ckpt.dir, done[-1]) if done else None
+
     def resume(self) -> int:
-        """Restore the newest committed checkpoint (if any); returns the step to continue from."""
-        if self.ckpt is None or isinstance(self.engine, KVEngine) or self.ckpt.latest() is None:
+        """Restore the newest committed checkpoint (if any); returns the step to continue from.
+
+        TCP topology: worker 0 has every server reload its store from the newest committed
+        ``tcp_step*`` directory; every worker continues from that step."""
+        if self.ckpt is None:
+            return 0
+        if isinstance(self.engine, KVEngine):
+            import os
+
+            d = self._tcp_latest()
+            if d is None:
+                return 0
+            if self.engine.kv.client is not None and self.engine.kv.worker_id == 0:
+                self.engine.kv.client.load(os.path.join(d, "server"))
+            step = int(os.path.basename(d)[len("tcp_step"):])
+            ctx.set_step(step)
+            return step
+        if self.ckpt.latest() is None:
             return 0
         st = self.ckpt.load(None, getattr(self.engine, "ps", None), self._tables())
         step = int(st.get("extra", {}).get("step", st["step"]))

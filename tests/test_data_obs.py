@@ -108,3 +108,48 @@ def test_metrics_jsonl_and_ui_server(tmp_path, monkeypatch):
     finally:
         metrics.set_client(None)
         srv.stop()
+
+
+def test_reference_ui_flags_route_and_gate_plots():
+    """-DuiHost/-DuiPort build the worker's UI client (Context.java:81-82, UiClient.java:25-27);
+    only replica 0 of a -DisMajor=1 worker reports (Context.java:94-100); the server listens on
+    the dashboard port (-DuiHttpPort) and the ingest port (-DuiPort)."""
+    import json
+    import time
+    import urllib.request
+
+    from ps_amd import context as C
+    from ps_amd.config import Config
+    from ps_amd.obs import metrics
+    from ps_amd.obs.ui_server import UiServer
+
+    srv = UiServer("127.0.0.1", 0, plot_port=0).start()
+    saved = C.ctx.cfg
+    try:
+        metrics.set_client(None)
+        for major, name in ((1, "major_loss"), (0, "minor_loss")):
+            C.ctx.init(Config.from_args(["-Dmode=dist", "-DuiHost=127.0.0.1", f"-DuiPort={srv.plot_port}",
+                                         f"-DisMajor={major}"]))
+            C.ctx.model_index = 0
+            metrics.plot(name, 0.5, 1)
+            C.ctx.model_index = 1  # replica 1 never reports
+            metrics.plot(name + "_r1", 0.5, 1)
+            C.ctx.model_index = 0
+        for c in list(metrics._auto.values()):
+            c.flush()
+        deadline = time.time() + 5
+        got = []
+        while time.time() < deadline:  # dashboard port serves what arrived on the ingest port
+            with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/?act=list_graph", timeout=2) as r:
+                got = json.loads(r.read())
+            if "major_loss" in got:
+                break
+            time.sleep(0.05)
+        assert got == ["major_loss"], got
+        # without UI flags no client is built at all
+        C.ctx.init(Config.from_args(["-Dmode=dist"]))
+        assert Config.from_args([]).ui_address() is None
+        assert metrics._auto_client() is None or "PS_AMD_UI_ADDR" in __import__("os").environ
+    finally:
+        C.ctx.init(saved)
+        srv.stop()

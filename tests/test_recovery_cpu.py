@@ -114,3 +114,52 @@ def test_ctr_app_reference_dist_deployment(tmp_path):
     finally:
         if srv.poll() is None:
             srv.kill()
+
+
+def _tcp_run(port, ckdir, steps, resume, x, y):
+    from ps_amd.context import ctx
+    from ps_amd.models.reference import FullConnectedNN
+    from ps_amd.parallel.kvstore import KVStore
+    from ps_amd.parallel.tcp import PSRouterClient
+    from ps_amd.train.trainer import KVEngine, Trainer
+
+    ctx.init()
+    m = FullConnectedNN.build_model(10, [8, 3], gen=torch.Generator().manual_seed(3), softmax_temp=1.0,
+                                    reference_backward=False)
+    client = PSRouterClient([f"127.0.0.1:{port}"])
+    tr = Trainer(m, KVEngine(m, KVStore(client, worker_id=0, consistency="bsp")), checkpoint_dir=ckdir)
+    start = tr.resume() if resume else 0
+    for s in range(start, steps):
+        tr.train([{"X": x, "Y": y}])
+        if s + 1 == 3:
+            tr.save(3, blocking=True)
+    tr.engine.pull()
+    return start, {n: p.detach().clone() for n, p in m.named_parameters()}
+
+
+def test_tcp_topology_resumes_from_committed_server_checkpoint(tmp_path):
+    """the dedicated-server topology must resume like the co-located one: worker 0
+    has the servers reload the newest COMMITTED tcp_step* directory and the job continues from
+    that step (6 straight steps == 3 + restart with fresh servers + 3)."""
+    from ps_amd.parallel.tcp import PServer
+
+    x, y = torch.randn(32, 10, generator=torch.Generator().manual_seed(1)), torch.arange(32) % 3
+    srv = PServer(0, workers=1, mode="bsp").start()
+    try:
+        _, want = _tcp_run(srv.port, str(tmp_path / "a"), 6, False, x, y)
+    finally:
+        srv.stop()
+    srv = PServer(0, workers=1, mode="bsp").start()
+    try:
+        _tcp_run(srv.port, str(tmp_path / "b"), 3, False, x, y)
+    finally:
+        srv.stop()
+    assert os.path.exists(tmp_path / "b" / "tcp_step00000003" / "COMMIT")
+    srv = PServer(0, workers=1, mode="bsp").start()  # the "restarted" job: fresh, empty servers
+    try:
+        start, got = _tcp_run(srv.port, str(tmp_path / "b"), 6, True, x, y)
+    finally:
+        srv.stop()
+    assert start == 3
+    for k in want:
+        torch.testing.assert_close(got[k], want[k], rtol=1e-6, atol=1e-7)
