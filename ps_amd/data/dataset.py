@@ -291,6 +291,14 @@ def synthetic_images(n: int, c: int = 3, hw: int = 224, classes: int = 1000, see
 def load_reference_mnist(path: Optional[str] = None) -> Dict[str, torch.Tensor]:
     """The 1000-row MNIST CSV bundled with the reference (src/main/resources/mnist_test.csv):
     a plain-text fixture, read with numpy (no pickle)."""
-    path = path or "/root/reference/src/main/resources/mnist_test.csv"
+    if path is None:
+        import os
+
+        # the reference checkout, else a local copy (data_cache/ is git-ignored: the fixture is
+        # not committed, it only travels with the working tree to a GPU box)
+        ref = "/root/reference/src/main/resources/mnist_test.csv"
+        local = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                             "data_cache", "mnist_test.csv")
+        path = os.environ.get("PS_AMD_MNIST_CSV") or (ref if os.path.exists(ref) else local)
     arr = np.loadtxt(path, delimiter=",", dtype=np.float32)
     return {"X": torch.from_numpy(arr[:, 1:] / 255.0), "Y": torch.from_numpy(arr[:, 0]).long()}

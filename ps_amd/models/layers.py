@@ -338,11 +338,42 @@ class _Im2colConv(torch.autograd.Function):
         return dx, dw.to(w.dtype), db, None, None, None
 
 
+class _Im2col(torch.autograd.Function):
+    """[N, C, H, W] -> [N*OH*OW, C*k*k] patches with the HIP im2col; backward = HIP col2im
+    (the gather formulation, K12 / K15)."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        ctx.meta = (x.shape, k, s, p)
+        return nn_ops.im2col(x.float(), k, s, p)
+
+    @staticmethod
+    def backward(ctx, dcol):
+        xshape, k, s, p = ctx.meta
+        return nn_ops.col2im(dcol, xshape, k, s, p), None, None, None
+
+
+def conv_k12(x, w2, b, k: int, s: int, p: int, act: int = 0):
+    """The reference conv on the in-house kernels (layer/Conv2DLayer.java:146-240):
+    HIP im2col -> the fused MFMA linear (fc.hip: fp32 16x16x4 MFMA, bias + activation in the
+    epilogue) -> [N, K, OH, OW]; backward = the fused K2 kernel (act' in the prologue, dW, db
+    from the staged tile, dcol) -> HIP col2im."""
+    n, _, h, wd = x.shape
+    oh, ow = (h + 2 * p - k) // s + 1, (wd + 2 * p - k) // s + 1
+    col = _Im2col.apply(x, k, s, p)  # [N*OH*OW, C*k*k]
+    y2 = _dense.linear_act(col, w2, b, act)  # [N*OH*OW, K]
+    return y2.view(n, oh, ow, -1).permute(0, 3, 1, 2).contiguous()
+
+
 class Conv2DLayer(nn.Module):
     """Square-kernel conv + bias + activation (layer/Conv2DLayer.java).  Weights [K, C, k, k]
-    init U(+-4*sqrt(6/(K + C*k*k))), bias U[0,1) (:64-76).  ``impl="miopen"`` (default on
-    GPU) runs MIOpen; ``impl="im2col"`` reproduces the reference algorithm on the HIP
-    im2col/col2im kernels (Q8's misaligned ReLU mask is not reproduced)."""
+    init U(+-4*sqrt(6/(K + C*k*k))), bias U[0,1) (:64-76).
+
+    ``impl``: ``"auto"`` (default) runs the reference im2col + GEMM algorithm -- on GPU through
+    the in-house kernels (HIP im2col, the fp32 MFMA fused linear with the bias + ReLU / leaky /
+    clipped-sigmoid epilogue, the fused K2 backward, HIP col2im: ``conv_k12``), on CPU through
+    torch matmuls; ``"im2col"`` forces the torch-matmul form; ``"miopen"`` uses F.conv2d.
+    Q8's misaligned ReLU mask is not reproduced."""
 
     def __init__(self, name: str, input_w: int, input_h: int, input_d: int, kernel_size: int, stride: int,
                  output_num: int, padding: int = 0, activation: Optional[A.Activation] = None, impl: str = "auto",
@@ -383,6 +414,13 @@ class Conv2DLayer(nn.Module):
 
     def forward(self, x):
         x = x.view(x.shape[0], self.input_d, self.input_h, self.input_w)
+        if self.impl == "auto" and x.is_cuda and self.weights.dtype == torch.float32:
+            code = _FUSED_ACT.get(type(self.activation), None) if self.activation is not None else 0
+            w2 = self.weights.view(self.K, -1)
+            z = conv_k12(x, w2, self.bias, self.kernel_size, self.stride, self.padding, code or 0)
+            if code is not None:
+                return z
+            return self.activation(z)
         if self.impl == "im2col" or (self.impl == "auto" and not x.is_cuda):
             w2 = self.weights.view(self.K, -1)
             z = _Im2colConv.apply(x, w2, self.bias, self.kernel_size, self.stride, self.padding)

@@ -63,7 +63,7 @@ class ColocatedPS:
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
                  average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
                  compress_warmup: int = 0, split_comm: Optional[bool] = None, plane: Optional[str] = None,
-                 timeout_s: float = 600.0):
+                 timeout_s: float = 600.0, reduce_fp32: Optional[bool] = None):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -81,6 +81,13 @@ class ColocatedPS:
         self.compress_warmup = int(compress_warmup)
         self.average = average
         self.overlap = overlap
+        import os as _os0
+
+        # collective plane: reduce-scatter bf16 buckets in fp32 (the W-way sum is otherwise rounded
+        # in bf16 by RCCL); the xGMI plane always sums in fp32 on the owner
+        if reduce_fp32 is None:
+            reduce_fp32 = _os0.environ.get("PS_AMD_REDUCE_FP32", "0") == "1"
+        self.reduce_fp32 = bool(reduce_fp32)
         self.accumulating = False  # micro-batch accumulation: hooks stay quiet until the last one
         params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         if not params:
@@ -165,7 +172,8 @@ class ColocatedPS:
             self.segs.append(segs)
             self.states.append([u.new_states(m[a:z]) for (u, a, z) in segs])
             if self.world > 1 and self.plane is None:
-                self.gshard.append(torch.empty(b.chunk, dtype=R.group_dtype[b.group], device=self.device))
+                gdt = torch.float32 if (self.reduce_fp32 and compress is None) else R.group_dtype[b.group]
+                self.gshard.append(torch.empty(b.chunk, dtype=gdt, device=self.device))
             else:
                 self.gshard.append(None)
         # 1-bit compression state: error-feedback buffer per bucket (full bucket, fp32); with the
@@ -372,6 +380,8 @@ class ColocatedPS:
             return
         if self.compress == "onebit" and self.round >= self.compress_warmup:
             self._push_onebit(b, gin)
+        elif self.gshard[b].dtype != gin.dtype:  # fp32 reduction of a bf16 bucket
+            self.t.reduce_scatter(self.gshard[b], gin.float())
         else:
             self.t.reduce_scatter(self.gshard[b], gin)
 

@@ -12,7 +12,11 @@ Trains the reference's two MNIST models with the reference hyper-parameters on t
   CNN  CNN.buildModel(28, 28, 1, {150, 50, 10}); same Adam; 1 replica, batch 100
        (CnnMnist.java:68-86); 100 epochs or early stop.
 
-    python scripts/mnist_parity.py [--seeds 0 1 2] [--epochs 100] [--model mlp|cnn|both]
+    python scripts/mnist_parity.py [--seeds 0 1 2] [--epochs 100] [--model mlp|cnn|both] [--device cuda]
+
+On ``--device cuda`` the models run the in-house GPU kernels (FC: fused MFMA linear + K2
+backward; CNN convs: HIP im2col -> fp32 MFMA linear -> K2 -> HIP col2im; HIP max-pool,
+softmax-T, fused Adam on the PS shard).
 """
 from __future__ import annotations
 
@@ -33,7 +37,7 @@ from ps_amd.models.reference import CNN, FullConnectedNN  # noqa: E402
 from ps_amd.train.trainer import CollectiveEngine, Trainer  # noqa: E402
 
 
-def run(kind: str, seed: int, epochs: int, raw: bool = True) -> dict:
+def run(kind: str, seed: int, epochs: int, raw: bool = True, device: str = "cpu") -> dict:
     d = load_reference_mnist()
     X = d["X"] * (255.0 if raw else 1.0)
     Y = d["Y"]
@@ -44,7 +48,9 @@ def run(kind: str, seed: int, epochs: int, raw: bool = True) -> dict:
         model, k, bs = FullConnectedNN.build_model(784, [150, 50, 10], gen=gen), 4, 100
     else:
         model, k, bs = CNN.build_model(28, 28, 1, [150, 50, 10], gen=gen), 1, 100
-    tr = Trainer(model, CollectiveEngine(model), n_threads=k)
+    dev = torch.device(device)
+    model.to(dev)
+    tr = Trainer(model, CollectiveEngine(model), n_threads=k, device=dev if dev.type == "cuda" else None)
     Xt, Yt = X[:800], Y[:800]
     t0 = time.time()
     ep = 0
@@ -58,9 +64,9 @@ def run(kind: str, seed: int, epochs: int, raw: bool = True) -> dict:
         if ctx.finish:
             break
     p = tr.predict([{"X": X[800:]}])[0]
-    acc = SoftmaxPrecision(Y[800:], p).calculate()
+    acc = SoftmaxPrecision(Y[800:], p.cpu()).calculate()
     return {"model": kind, "seed": seed, "epochs_run": ep + 1, "heldout_acc": round(float(acc), 4),
-            "raw_pixels": raw, "seconds": round(time.time() - t0, 1)}
+            "raw_pixels": raw, "device": device, "seconds": round(time.time() - t0, 1)}
 
 
 def main():
@@ -68,12 +74,13 @@ def main():
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--epochs", type=int, default=100)
     ap.add_argument("--model", default="both", choices=["mlp", "cnn", "both"])
+    ap.add_argument("--device", default="cpu", choices=["cpu", "cuda"])
     a = ap.parse_args()
     torch.set_num_threads(4)
     kinds = ["mlp", "cnn"] if a.model == "both" else [a.model]
     for kind in kinds:
         for s in a.seeds:
-            print(json.dumps(run(kind, s, a.epochs)), flush=True)
+            print(json.dumps(run(kind, s, a.epochs, device=a.device)), flush=True)
 
 
 if __name__ == "__main__":

@@ -70,3 +70,30 @@ def test_fp32_reference_mlp_on_gpu_matches_cpu():
         out.append({k: v.detach().cpu() for k, v in m.named_parameters()})
     for k in out[0]:
         torch.testing.assert_close(out[1][k], out[0][k], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k_out,hw,act", [(1, 16, 28, "relu"), (16, 32, 14, "relu"), (3, 8, 9, "none")])
+def test_reference_conv_on_inhouse_kernels_vs_fp32_conv2d(c, k_out, hw, act):
+    """CnnMnist convs (CNN.java:37-49) on the GPU default path: HIP im2col -> fp32 MFMA fused
+    linear (bias + ReLU epilogue) -> K2 backward -> HIP col2im, vs fp32 F.conv2d autograd."""
+    from ps_amd.models import activations as A
+    from ps_amd.models.layers import Conv2DLayer
+
+    torch.manual_seed(0)
+    layer = Conv2DLayer("conv", hw, hw, c, 3, 1, k_out, padding=1,
+                        activation=A.Relu() if act == "relu" else None).cuda()
+    x = torch.randn(32, c * hw * hw, device="cuda", requires_grad=True)
+    y = layer(x)
+    w, b = layer.weights.detach().clone().requires_grad_(), layer.bias.detach().clone().requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr.view(32, c, hw, hw), w, b, 1, 1)
+    if act == "relu":
+        yr = torch.relu(yr)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(layer.weights.grad, w.grad, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(layer.bias.grad, b.grad, rtol=1e-4, atol=2e-3)

@@ -214,3 +214,140 @@ def test_plane_processes_resnet_tiny_bf16_trajectory_vs_fp32():
     for a, b in zip(la, lref):
         assert abs(a - b) < 0.05 * max(1.0, abs(b)), (la, lref)
     assert la[-1] < la[0], la
+
+
+def _resnet8_body(tp, steps):
+    import copy as _copy
+
+    from ps_amd.models.resnet import prepare_for_mi355x, resnet_tiny
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import MomentumUpdater
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    net = prepare_for_mi355x(resnet_tiny(num_classes=10, fused_bn=True).cuda())
+    ps = ColocatedPS(net, MomentumUpdater(0.05, 0.9, 0.0), tp, bucket_mb=0.25, plane="xgmi", timeout_s=120)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
+    losses = []
+    for _ in range(steps):
+        loss = F.cross_entropy(net(xs.bfloat16()).float(), ys)
+        loss.backward()
+        ps.finish_step()
+        losses.append(loss.item())
+    ps.synchronize()
+    torch.cuda.synchronize()
+    ps.close()
+    return losses
+
+
+def test_world8_processes_bf16_resnet_tiny_tracks_fp32_oracle():
+    """W = 8 processes, bf16 ResNet-tiny; the xGMI plane sums the 8 bf16
+    pushes in fp32 on the owner -- the trajectory tracks fp32 torch (per-rank BN batches)."""
+    from ps_amd.models.resnet import resnet_tiny
+
+    world, steps = 8, 5
+    res = dist_util.run(_resnet8_body, world, (steps,), timeout=400)
+    torch.manual_seed(0)
+    ref = resnet_tiny(num_classes=10, fused_bn=True)
+    for mod in ref.modules():
+        if hasattr(mod, "fuse_block"):
+            mod.fuse_block = False
+    ref = ref.cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    lref = []
+    for _ in range(steps):
+        opt.zero_grad()
+        ls = [F.cross_entropy(ref(x[r::world]), y[r::world]) for r in range(world)]
+        (sum(ls) / world).backward()
+        opt.step()
+        lref.append(ls[0].item())
+    la = res[0]
+    for a, b in zip(la, lref):
+        assert abs(a - b) < 0.05 * max(1.0, abs(b)), (la, lref)
+
+
+def _mlp8_body(tp, models, steps, reduce_fp32):
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import SimpleUpdater
+
+    m = models[tp.rank]
+    ps = ColocatedPS(m, SimpleUpdater(0.5), tp, bucket_mb=0.05, plane="collective", overlap=False,
+                     reduce_fp32=reduce_fp32)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(256, 64, generator=g).to(DEV)
+    y = torch.randint(0, 8, (256,), generator=g).to(DEV)
+    for _ in range(steps):
+        F.cross_entropy(m(x[tp.rank::tp.world].bfloat16()).float(), y[tp.rank::tp.world]).backward()
+        ps.finish_step()
+    ps.synchronize()
+    torch.cuda.synchronize()
+    return {n: p.detach().float().cpu() for n, p in m.named_parameters()}
+
+
+def test_world8_collective_fp32_reduction_closer_to_fp32_oracle():
+    """The collective plane's reduce_fp32 option: the 8-way reduce-scatter of bf16 buckets runs
+    in fp32 (thread-ranks); the bf16 replicas track the fp32 oracle."""
+    world, steps = 8, 6
+
+    def mk():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.Tanh(), torch.nn.Linear(256, 8))
+
+    errs = {}
+    ref = mk().to(DEV)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.5)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(256, 64, generator=g).to(DEV)
+    y = torch.randint(0, 8, (256,), generator=g).to(DEV)
+    for _ in range(steps):
+        opt.zero_grad()
+        (sum(F.cross_entropy(ref(x[r::world]), y[r::world]) for r in range(world)) / world).backward()
+        opt.step()
+    for fp32 in (False, True):
+        models = [mk().to(DEV).bfloat16() for _ in range(world)]
+        res = run_loopback(_mlp8_body, world, models, steps, fp32, timeout_s=300)
+        errs[fp32] = max((res[0][n] - p.detach().cpu()).abs().max().item() for n, p in ref.named_parameters())
+    print("max |w - w_fp32| after 6 steps, bf16 vs fp32 reduction:", errs)
+    assert errs[True] < 0.05, errs
+
+
+def _llama_body(tp, steps):
+    from ps_amd.models.transformer import LlamaConfig, LlamaForCausalLM
+    from ps_amd.parallel.colocated import ColocatedPS
+    from ps_amd.parallel.updaters import AdamUpdater
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny()
+    model = LlamaForCausalLM(cfg).cuda().to(torch.bfloat16)
+    ps = ColocatedPS(model, AdamUpdater(3e-3, 0.9, 0.95, 1e-8, bias_correction="step"), tp, bucket_mb=0.05,
+                     compress="onebit", compress_warmup=2, plane="xgmi", timeout_s=60)
+    g = torch.Generator(device="cuda").manual_seed(tp.rank)
+    ids = torch.randint(0, 64, (4, 64), device="cuda", generator=g)  # a small learnable vocabulary
+    losses = []
+    for _ in range(steps):
+        loss = model(ids, ids)
+        loss.backward()
+        ps.finish_step()
+        losses.append(loss.item())
+    ps.synchronize()
+    torch.cuda.synchronize()
+    out = {n: p.detach().float().cpu().clone() for n, p in model.named_parameters()}
+    ps.close()
+    return out, losses
+
+
+def test_tiny_llama_onebit_two_processes_on_the_plane():
+    """the Llama config's 1-bit push (owner decodes the W packed pushes inside
+    the fused Adam kernel) with 2 processes: replicas stay identical, the loss falls."""
+    res = dist_util.run(_llama_body, 2, (25,))
+    for k in res[0][0]:
+        assert torch.equal(res[0][0][k], res[1][0][k])
+    for _, losses in res:
+        assert sum(losses[-5:]) / 5 < 0.8 * sum(losses[:5]) / 5, losses
