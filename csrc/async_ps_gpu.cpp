@@ -1,10 +1,12 @@
 // GPU side of the asynchronous parameter server (see csrc/include/async_ctl.h for the protocol).
 //
 //  GpuAsyncServer  owner progress thread: waits for deposited pushes in the shared control
-//                  block, runs the fused HIP optimizer (csrc/kernels/optim.hip) on the fp32
-//                  master shard with the worker's mailbox as gradient, writing the new weights
-//                  straight into a free published slot, synchronises its own stream, then
-//                  publishes + acknowledges.  Its stream never touches the training streams.
+//                  block, runs the fused HIP optimizer (csrc/kernels/optim.hip) of every
+//                  updater segment of the fp32 master shard (per-key-prefix updaters, e.g.
+//                  FTRL wide rows + Adam elsewhere) with the worker's mailbox as gradient,
+//                  writing the new weights straight into a free published slot, synchronises
+//                  its own stream, then publishes + acknowledges.  Its stream never touches the
+//                  training streams.
 //  GpuNotifier     worker completion thread: the training thread records an event after the
 //                  peer copies of a push (or a pull) and hands the follow-up bookkeeping (bump
 //                  seq / clock, unpin slots) to this thread, so neither the push nor the pull
@@ -12,6 +14,7 @@
 #include <torch/extension.h>
 
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdlib>
 #include <deque>
@@ -32,58 +35,86 @@ void hip_ok(hipError_t e, const char* what) {
 
 class GpuAsyncServer {
  public:
-  // kind / hyper-parameters as ops/optim.py fused_opt; bias_mode 0 none, 1 1-beta^t, 2 constant
-  GpuAsyncServer(uintptr_t ctl, int64_t me, int64_t kind, Tensor master, c10::optional<Tensor> st0,
-                 c10::optional<Tensor> st1, std::vector<Tensor> mbox, std::vector<Tensor> pub, double lr,
-                 double beta1, double beta2, double eps, double wd, double momentum, double dampening, bool nesterov,
-                 bool adamw, int64_t bias_mode, double l1, double l2, double fbeta, int64_t ftrl_mode,
+  // mbox: W * kMbox mailboxes (worker w, slot m at w * kMbox + m); pub: kSlots published slots.
+  // Updater segments (per-key-prefix updaters, ColocatedPS-style) are added before start().
+  GpuAsyncServer(uintptr_t ctl, int64_t me, Tensor master, std::vector<Tensor> mbox, std::vector<Tensor> pub,
                  double gscale)
-      : ctl_(ctl_at(ctl)), me_(static_cast<int>(me)), master_(master), mbox_(mbox), pub_(pub),
-        beta1_(beta1), beta2_(beta2), bias_mode_(static_cast<int>(bias_mode)) {
+      : ctl_(ctl_at(ctl)), me_(static_cast<int>(me)), master_(master), mbox_(mbox), pub_(pub), gscale_(gscale) {
     TORCH_CHECK(master.is_cuda() && master.scalar_type() == torch::kFloat32 && master.is_contiguous(), "master");
     TORCH_CHECK(static_cast<int64_t>(pub.size()) == psasync::kSlots, "need ", psasync::kSlots, " published slots");
-    TORCH_CHECK(static_cast<int64_t>(mbox.size()) == ctl_->world, "one mailbox per worker");
+    TORCH_CHECK(static_cast<int64_t>(mbox.size()) == ctl_->world * psasync::kMbox, "W x kMbox mailboxes");
     const int64_t n = master.numel();
     for (auto& t : mbox) TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.numel() == n, "mailbox shape");
     for (auto& t : pub) TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.numel() == n, "slot shape");
+    TORCH_CHECK(mbox[0].scalar_type() == pub[0].scalar_type(), "mailbox / slot dtype");
     dev_ = master.device().index();
-    if (st0.has_value() && st0->defined()) st0_ = *st0;
-    if (st1.has_value() && st1->defined()) st1_ = *st1;
-    a_.kind = static_cast<int>(kind);
-    a_.w = master.data_ptr<float>();
-    a_.st0 = st0_.defined() ? st0_.data_ptr<float>() : nullptr;
-    a_.st1 = st1_.defined() ? st1_.data_ptr<float>() : nullptr;
-    a_.g_bf16 = mbox[0].scalar_type() == torch::kBFloat16;
-    a_.wout_bf16 = pub[0].scalar_type() == torch::kBFloat16;
-    a_.n = n;
-    a_.lr = lr; a_.beta1 = beta1; a_.beta2 = beta2; a_.eps = eps; a_.wd = wd; a_.momentum = momentum;
-    a_.dampening = dampening; a_.nesterov = nesterov; a_.adamw = adamw; a_.bc1 = 1.f; a_.bc2 = 1.f;
-    a_.l1 = l1; a_.l2 = l2; a_.fbeta = fbeta; a_.ftrl_mode = static_cast<int>(ftrl_mode);
-    a_.gscale = gscale; a_.gscale_ptr = nullptr;
+    bf16_ = mbox[0].scalar_type() == torch::kBFloat16;
+    esize_ = bf16_ ? 2 : 4;
     // test hook: a slow owner (the worker's host then runs far ahead of the server)
     if (const char* d = std::getenv("PS_AMD_ASYNC_SERVE_DELAY_US")) delay_us_ = std::atoi(d);
   }
   ~GpuAsyncServer() { stop(); }
 
+  // [lo, hi) of the shard with its own kernel kind, state tensors (segment-sized) and
+  // hyper-parameters (ps_amd/parallel/plane.py order); bias_mode 0 none, 1 1-beta^t, 2 constant
+  void add_segment(int64_t kind, int64_t lo, int64_t hi, c10::optional<Tensor> st0, c10::optional<Tensor> st1,
+                   std::vector<double> h, int64_t bias_mode) {
+    TORCH_CHECK(h.size() == 16, "16 hyper-parameters");
+    TORCH_CHECK(lo >= 0 && hi <= master_.numel() && lo < hi, "segment range");
+    Seg sg;
+    sg.lo = lo;
+    sg.hi = hi;
+    sg.bias_mode = static_cast<int>(bias_mode);
+    if (st0.has_value() && st0->defined()) sg.st0 = *st0;
+    if (st1.has_value() && st1->defined()) sg.st1 = *st1;
+    for (auto* t : {&sg.st0, &sg.st1})
+      if (t->defined())
+        TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->numel() == hi - lo, "segment state");
+    psamd::FusedOptArgs& a = sg.a;
+    a.kind = static_cast<int>(kind);
+    a.w = master_.data_ptr<float>() + lo;
+    a.st0 = sg.st0.defined() ? sg.st0.data_ptr<float>() : nullptr;
+    a.st1 = sg.st1.defined() ? sg.st1.data_ptr<float>() : nullptr;
+    a.g_bf16 = bf16_;
+    a.wout_bf16 = bf16_;
+    a.n = hi - lo;
+    a.lr = h[0]; a.beta1 = h[1]; a.beta2 = h[2]; a.eps = h[3]; a.wd = h[4]; a.momentum = h[5];
+    a.dampening = h[6]; a.nesterov = h[7] != 0.0; a.adamw = h[8] != 0.0; a.bc1 = h[9]; a.bc2 = h[10];
+    a.l1 = h[11]; a.l2 = h[12]; a.fbeta = h[13]; a.ftrl_mode = static_cast<int>(h[14]);
+    a.gscale = static_cast<float>(h[15] * gscale_);
+    a.gscale_ptr = nullptr;
+    segs_.push_back(sg);
+  }
+
   void start() {
+    TORCH_CHECK(!segs_.empty(), "async server without updater segments");
     stop_ = false;
     th_ = std::thread([this] {
       hip_ok(hipSetDevice(dev_), "hipSetDevice");
       hipStream_t s;
       hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-      psasync::serve_loop(ctl_, me_, &stop_, [&](int w, int slot, int64_t step) {
-        psamd::FusedOptArgs a = a_;
-        if (bias_mode_ == 1) {
-          a.bc1 = 1.f / (1.f - std::pow(beta1_, static_cast<double>(step)));
-          a.bc2 = 1.f / (1.f - std::pow(beta2_, static_cast<double>(step)));
-        } else if (bias_mode_ == 2) {
-          a.bc1 = 1.f / (1.f - beta1_);
-          a.bc2 = 1.f / (1.f - beta2_);
-        }
+      psasync::serve_loop(ctl_, me_, &stop_, [&](int w, int mslot, int slot, int64_t step) {
         if (delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
-        a.g = mbox_[static_cast<size_t>(w)].data_ptr();
-        a.wout = pub_[static_cast<size_t>(slot)].data_ptr();
-        psamd::launch_fused_opt(a, s);
+        const void* g = mbox_[static_cast<size_t>(w * psasync::kMbox + mslot)].data_ptr();
+        char* out = static_cast<char*>(pub_[static_cast<size_t>(slot)].data_ptr());
+        for (const Seg& sg : segs_) {
+          psamd::FusedOptArgs a = sg.a;
+          if (sg.bias_mode == 1) {
+            a.bc1 = 1.f / (1.f - std::pow(static_cast<double>(a.beta1), static_cast<double>(step)));
+            a.bc2 = 1.f / (1.f - std::pow(static_cast<double>(a.beta2), static_cast<double>(step)));
+          } else if (sg.bias_mode == 2) {
+            a.bc1 = 1.f / (1.f - a.beta1);
+            a.bc2 = 1.f / (1.f - a.beta2);
+          }
+          a.wout = out + sg.lo * esize_;
+          // the mailbox was written by a peer GPU's copy kernel: the multi-source form (one
+          // source) starts with the system-scope acquire that keeps stale lines out
+          psamd::MultiGrad m{};
+          m.nsrc = 1;
+          m.g[0] = g;
+          m.off = sg.lo;
+          psamd::launch_fused_opt_multi(a, m, s);
+        }
         hip_ok(hipStreamSynchronize(s), "async server step");
         applied_ += 1;
       });
@@ -97,14 +128,21 @@ class GpuAsyncServer {
   int64_t applied() const { return applied_; }
 
  private:
+  struct Seg {
+    int64_t lo, hi;
+    int bias_mode;
+    Tensor st0, st1;
+    psamd::FusedOptArgs a{};
+  };
   psasync::AsyncCtl* ctl_;
   int me_;
   int dev_ = 0;
-  Tensor master_, st0_, st1_;
+  Tensor master_;
   std::vector<Tensor> mbox_, pub_;
-  double beta1_, beta2_;
-  int bias_mode_;
-  psamd::FusedOptArgs a_{};
+  double gscale_;
+  bool bf16_ = true;
+  int64_t esize_ = 2;
+  std::vector<Seg> segs_;
   std::atomic<bool> stop_{true};
   std::thread th_;
   int64_t applied_ = 0;
@@ -190,9 +228,8 @@ class GpuNotifier {
 
 void register_async_ps(pybind11::module& m) {
   pybind11::class_<GpuAsyncServer>(m, "GpuAsyncServer")
-      .def(pybind11::init<uintptr_t, int64_t, int64_t, Tensor, c10::optional<Tensor>, c10::optional<Tensor>,
-                          std::vector<Tensor>, std::vector<Tensor>, double, double, double, double, double, double,
-                          double, bool, bool, int64_t, double, double, double, int64_t, double>())
+      .def(pybind11::init<uintptr_t, int64_t, Tensor, std::vector<Tensor>, std::vector<Tensor>, double>())
+      .def("add_segment", &GpuAsyncServer::add_segment)
       .def("start", &GpuAsyncServer::start)
       .def("stop", &GpuAsyncServer::stop, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def_property_readonly("applied", &GpuAsyncServer::applied);

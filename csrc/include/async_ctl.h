@@ -5,10 +5,12 @@
 // in the reference; here SSP(s) bounds it.
 //
 // Data plane (one node): every rank owns a contiguous range shard of the flat parameter space.
-// The owner keeps per-worker gradient MAILBOXES and 3 PUBLISHED weight slots in its own device
-// memory; the other ranks write their gradient slice straight into the owner's mailbox and read
-// the owner's current slot back with peer copies over xGMI (IPC-mapped buffers) -- one-sided,
-// so no rank ever waits for another rank to reach a matching collective.
+// The owner keeps per-worker gradient MAILBOXES (kMbox = 2 deep: push k of worker w lands in
+// mailbox slot k % 2, so a worker only waits when its push k-2 is still unapplied) and 3
+// PUBLISHED weight slots in its own device memory; the other ranks write their gradient slice
+// straight into the owner's mailbox and read the owner's current slot back with peer copies over
+// xGMI (IPC-mapped buffers) -- one-sided, so no rank ever waits for another rank to reach a
+// matching collective.
 //
 // Control plane: this block, in POSIX shared memory, all fields int64 accessed with acquire /
 // release atomics:
@@ -33,6 +35,7 @@ namespace psasync {
 constexpr int64_t kMagic = 0x50534153594e4331ll;  // "PSASYNC1"
 constexpr int kMaxW = 64;
 constexpr int kSlots = 3;
+constexpr int kMbox = 2;  // mailbox depth per (owner, worker)
 
 struct AsyncCtl {
   int64_t magic;
@@ -116,9 +119,10 @@ inline int64_t min_ack(AsyncCtl* c) {
 }
 
 // Owner progress loop: apply every deposited push in arrival order (round-robin over workers
-// for fairness), publish into a free slot, then acknowledge.  ``apply(w, slot, step)`` runs the
-// optimizer on the master shard with mailbox w and writes the new weights into ``slot``; it
-// returns only once the result is globally visible (stream synchronised).
+// for fairness), publish into a free slot, then acknowledge.  ``apply(w, mslot, slot, step)``
+// runs the optimizer on the master shard with worker w's mailbox slot ``mslot`` (= push number
+// % kMbox) and writes the new weights into published ``slot``; it returns only once the result
+// is globally visible (stream synchronised).
 template <class Apply>
 void serve_loop(AsyncCtl* c, int me, const std::atomic<bool>* stop, Apply&& apply) {
   const int W = static_cast<int>(c->world);
@@ -138,7 +142,7 @@ void serve_loop(AsyncCtl* c, int me, const std::atomic<bool>* stop, Apply&& appl
         wait_slot();
       }
       const int64_t v = ld(&c->version[me]);
-      apply(w, slot, v + 1);
+      apply(w, static_cast<int>(a % kMbox), slot, v + 1);
       st(&c->cur[me], slot);
       st(&c->version[me], v + 1);
       st(&c->ack[me][w], a + 1);

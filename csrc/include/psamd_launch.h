@@ -49,13 +49,17 @@ void launch_fused_opt_multi(const FusedOptArgs& a, const MultiGrad& m, hipStream
 void launch_reduce_multi(const MultiGrad& m, int g_bf16, int64_t n, float* out, hipStream_t s);
 
 // ---------------------------------------------------------------- plane.hip
-// up to kPlaneMaxSrc (src -> dst) copies of equal size, issued as one launch
+// up to kPlaneMaxSrc (src -> dst) copies issued as one launch (16-B aligned, sizes in bytes)
 struct PlaneCopies {
   const void* src[kPlaneMaxSrc];
   void* dst[kPlaneMaxSrc];
+  int64_t nbytes[kPlaneMaxSrc];
   int nseg;
 };
+// every segment ``nbytes`` long
 void launch_plane_gather(const PlaneCopies& c, int64_t nbytes, hipStream_t s);
+// segment sizes from c.nbytes
+void launch_plane_copy(const PlaneCopies& c, hipStream_t s);
 // total = sum_r *(float*)c.src[r] (rank order); factor = min(1, max_norm / (sqrt(total) + 1e-6))
 void launch_plane_clip_factor(const PlaneCopies& c, float max_norm, float* total, float* factor, hipStream_t s);
 void launch_plane_fill(float* p, int64_t n, float v, hipStream_t s);

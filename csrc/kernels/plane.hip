@@ -17,10 +17,11 @@
 
 namespace psamd {
 
-__global__ __launch_bounds__(256) void plane_gather_kernel(const PlaneCopies c, int64_t nbytes, int blocks_per_seg) {
+__global__ __launch_bounds__(256) void plane_gather_kernel(const PlaneCopies c, int blocks_per_seg) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int seg = blockIdx.x % c.nseg;
   const int lb = blockIdx.x / c.nseg;
+  const int64_t nbytes = c.nbytes[seg];
   const f32x4* __restrict__ src = static_cast<const f32x4*>(c.src[seg]);
   f32x4* __restrict__ dst = static_cast<f32x4*>(c.dst[seg]);
   const int64_t n16 = nbytes / 16;
@@ -42,15 +43,24 @@ __global__ __launch_bounds__(256) void plane_gather_kernel(const PlaneCopies c, 
   }
 }
 
-void launch_plane_gather(const PlaneCopies& c, int64_t nbytes, hipStream_t s) {
-  if (c.nseg <= 0 || nbytes <= 0) return;
-  // ~8 blocks per CU over the whole launch; at least one block per owner
-  int64_t per = (nbytes / 16 + 255) / 256;
+void launch_plane_copy(const PlaneCopies& c, hipStream_t s) {
+  if (c.nseg <= 0) return;
+  int64_t mx = 0;
+  for (int k = 0; k < c.nseg; ++k) mx = c.nbytes[k] > mx ? c.nbytes[k] : mx;
+  if (mx <= 0) return;
+  // ~8 blocks per CU over the whole launch; at least one block per segment
+  int64_t per = (mx / 16 + 255) / 256;
   int64_t cap = (2048 + c.nseg - 1) / c.nseg;
   if (per > cap) per = cap;
   if (per < 1) per = 1;
-  hipLaunchKernelGGL(plane_gather_kernel, dim3(static_cast<unsigned>(per * c.nseg)), dim3(256), 0, s, c, nbytes,
+  hipLaunchKernelGGL(plane_gather_kernel, dim3(static_cast<unsigned>(per * c.nseg)), dim3(256), 0, s, c,
                      static_cast<int>(per));
+}
+
+void launch_plane_gather(const PlaneCopies& c, int64_t nbytes, hipStream_t s) {
+  PlaneCopies e = c;
+  for (int k = 0; k < e.nseg; ++k) e.nbytes[k] = nbytes;
+  launch_plane_copy(e, s);
 }
 
 // Global-norm clip factor from every rank's partial sum of squares (read from the peers'

@@ -38,6 +38,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "async_ctl.h"
@@ -811,6 +812,22 @@ void register_plane(pybind11::module& m) {
     std::vector<int64_t> v(static_cast<size_t>(ctl_words(b[1], b[2])));
     for (size_t i = 0; i < v.size(); ++i) v[i] = psasync::ld(b + i);
     return v;
+  });
+  // (src, dst, nbytes) copies -- peer arenas included -- as ONE launch on ``stream`` (async PS
+  // pushes into owner mailboxes / pulls of published slots / row traffic; <= MAX_WORLD pieces)
+  pm.def("copy_many", [](std::vector<std::tuple<int64_t, int64_t, int64_t>> segs, int64_t stream, int64_t device) {
+    TORCH_CHECK(static_cast<int>(segs.size()) <= psamd::kPlaneMaxSrc, "too many copy segments");
+    psamd::PlaneCopies c{};
+    for (auto& t : segs) {
+      if (std::get<2>(t) <= 0) continue;
+      c.src[c.nseg] = reinterpret_cast<const void*>(std::get<0>(t));
+      c.dst[c.nseg] = reinterpret_cast<void*>(std::get<1>(t));
+      c.nbytes[c.nseg] = std::get<2>(t);
+      TORCH_CHECK(((std::get<0>(t) | std::get<1>(t)) & 15) == 0, "copy_many: 16-B aligned pointers");
+      c.nseg += 1;
+    }
+    hip_ok(hipSetDevice(static_cast<int>(device)), "hipSetDevice");
+    psamd::launch_plane_copy(c, reinterpret_cast<hipStream_t>(stream));
   });
   py::class_<PlaneEngine>(pm, "Engine")
       .def(py::init<uintptr_t, int64_t, int64_t, int64_t, int64_t, bool, int64_t, double, double, bool>())

@@ -4,7 +4,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <memory>
+#include <mutex>
+#include <string>
 #include <thread>
 
 #include "async_ctl.h"
@@ -303,26 +306,39 @@ py::object batch_to_dict(Batch& b, int dims, int fields) {
 psasync::AsyncCtl* ctl_at(uintptr_t addr) { return reinterpret_cast<psasync::AsyncCtl*>(addr); }
 
 // Owner progress thread of the asynchronous PS for CPU (fp32) shards: the same serve_loop as
-// the GPU server (csrc/async_ps_gpu.cpp) with the CPU updaters of the TCP server.
+// the GPU server (csrc/async_ps_gpu.cpp) with the CPU updaters of the TCP server, one updater
+// per key-prefix segment [lo, hi) of the shard.
 class CpuAsyncServer {
  public:
-  CpuAsyncServer(uintptr_t ctl, int me, const std::string& spec, int64_t n, uintptr_t master,
-                 std::vector<uintptr_t> mbox, std::vector<uintptr_t> pub, double gscale)
+  CpuAsyncServer(uintptr_t ctl, int me, int64_t n, uintptr_t master, std::vector<uintptr_t> mbox,
+                 std::vector<uintptr_t> pub, double gscale)
       : ctl_(ctl_at(ctl)), me_(me), n_(n), master_(reinterpret_cast<float*>(master)), gscale_(gscale) {
-    upd_ = make_updater(spec);
+    if (static_cast<int64_t>(mbox.size()) != ctl_->world * psasync::kMbox)
+      throw std::runtime_error("async PS: W x kMbox mailboxes expected");
     for (auto p : mbox) mbox_.push_back(reinterpret_cast<const float*>(p));
     for (auto p : pub) pub_.push_back(reinterpret_cast<float*>(p));
-    states_.assign(static_cast<size_t>(upd_->n_state()), std::vector<float>(static_cast<size_t>(n), 0.f));
     tmp_.resize(static_cast<size_t>(n));
   }
   ~CpuAsyncServer() { stop(); }
+  void add_segment(const std::string& spec, int64_t lo, int64_t hi) {
+    if (lo < 0 || hi > n_ || lo >= hi) throw std::runtime_error("async PS: bad segment");
+    Seg sg;
+    sg.lo = lo;
+    sg.hi = hi;
+    sg.upd = make_updater(spec);
+    sg.states.assign(static_cast<size_t>(sg.upd->n_state()), std::vector<float>(static_cast<size_t>(hi - lo), 0.f));
+    segs_.push_back(std::move(sg));
+  }
   void start() {
+    if (segs_.empty()) throw std::runtime_error("async PS: no updater segments");
     stop_ = false;
     th_ = std::thread([this] {
-      psasync::serve_loop(ctl_, me_, &stop_, [this](int w, int slot, int64_t step) {
-        const float* g = mbox_[static_cast<size_t>(w)];
+      psasync::serve_loop(ctl_, me_, &stop_, [this](int w, int mslot, int slot, int64_t step) {
+        const float* g = mbox_[static_cast<size_t>(w * psasync::kMbox + mslot)];
         for (int64_t i = 0; i < n_; ++i) tmp_[static_cast<size_t>(i)] = g[i] * static_cast<float>(gscale_);
-        upd_->update(master_, tmp_.data(), static_cast<size_t>(n_), states_, static_cast<long>(step));
+        for (auto& sg : segs_)
+          sg.upd->update(master_ + sg.lo, tmp_.data() + sg.lo, static_cast<size_t>(sg.hi - sg.lo), sg.states,
+                         static_cast<long>(step));
         std::memcpy(pub_[static_cast<size_t>(slot)], master_, static_cast<size_t>(n_) * sizeof(float));
         applied_ += 1;
       });
@@ -333,34 +349,127 @@ class CpuAsyncServer {
     if (th_.joinable()) th_.join();
   }
   int64_t applied() const { return applied_; }
+  // every segment's state tensors, in segment order
   py::list states() {
     py::list out;
-    for (auto& v : states_) {
-      py::array_t<float> a(static_cast<py::ssize_t>(v.size()));
-      std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
-      out.append(a);
-    }
+    for (auto& sg : segs_)
+      for (auto& v : sg.states) {
+        py::array_t<float> a(static_cast<py::ssize_t>(v.size()));
+        std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+        out.append(a);
+      }
     return out;
   }
   void set_states(const std::vector<F32>& st) {
-    for (size_t i = 0; i < st.size() && i < states_.size(); ++i)
-      std::memcpy(states_[i].data(), st[i].data(), std::min<size_t>(states_[i].size(), st[i].size()) * 4);
+    size_t k = 0;
+    for (auto& sg : segs_)
+      for (auto& v : sg.states) {
+        if (k >= st.size()) return;
+        std::memcpy(v.data(), st[k].data(), std::min<size_t>(v.size(), st[k].size()) * 4);
+        ++k;
+      }
   }
 
  private:
+  struct Seg {
+    int64_t lo, hi;
+    std::unique_ptr<Updater> upd;
+    std::vector<std::vector<float>> states;
+  };
   psasync::AsyncCtl* ctl_;
   int me_;
   int64_t n_;
   float* master_;
   double gscale_;
-  std::unique_ptr<Updater> upd_;
+  std::vector<Seg> segs_;
   std::vector<const float*> mbox_;
   std::vector<float*> pub_;
-  std::vector<std::vector<float>> states_;
   std::vector<float> tmp_;
   std::atomic<bool> stop_{true};
   std::thread th_;
   int64_t applied_ = 0;
+};
+
+// Row service of the asynchronous sparse tables (ps_amd/parallel/async_rows.py): one thread per
+// owner and table watching the table's control words (RowCtl below, POSIX shared memory) and
+// handing every posted pull request / deposited row push to a Python callback that does the
+// owner-side work (hash lookup-or-insert, lazy init, gather / row optimizer on the shard), then
+// acknowledging it.  Workers never wait for each other: a pull waits for its owner's service
+// only, a push not at all (2-deep mailboxes).
+//
+// int64 words: [magic, world, stop, pad] req[W][W] resp[W][W] nreq[W][W] pseq[W][W] pack[W][W]
+// npush[W][W][kMbox]  -- [o][w] = owner o, worker w
+constexpr int64_t kRowMagic = 0x524f57535256ll;  // "ROWSRV"
+inline int64_t row_ctl_words(int64_t W) { return 4 + 5 * W * W + W * W * psasync::kMbox; }
+
+class RowPoller {
+ public:
+  RowPoller(uintptr_t ctl, int me, py::object cb) : b_(reinterpret_cast<int64_t*>(ctl)), me_(me), cb_(cb) {
+    if (psasync::ld(b_) != kRowMagic) throw std::runtime_error("row control block not initialised");
+    W_ = b_[1];
+  }
+  ~RowPoller() { stop(); }
+  void start() {
+    stop_ = false;
+    th_ = std::thread([this] { run(); });
+  }
+  void stop() {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  std::string error() {
+    std::lock_guard<std::mutex> g(mu_);
+    return err_;
+  }
+
+ private:
+  int64_t* w(int k, int64_t o, int64_t wk) const { return b_ + 4 + k * W_ * W_ + o * W_ + wk; }
+  int64_t* npush(int64_t o, int64_t wk, int m) const {
+    return b_ + 4 + 5 * W_ * W_ + (o * W_ + wk) * psasync::kMbox + m;
+  }
+  void run() {
+    psasync::Backoff idle;
+    while (!stop_.load(std::memory_order_acquire) && psasync::ld(b_ + 2) == 0) {
+      bool did = false;
+      for (int64_t k = 0; k < W_; ++k) {
+        const int64_t rq = psasync::ld(w(0, me_, k)), rs = psasync::ld(w(1, me_, k));
+        if (rq > rs) {
+          if (!call("pull", k, psasync::ld(w(2, me_, k)), 0)) return;
+          psasync::st(w(1, me_, k), rq);
+          did = true;
+        }
+        const int64_t ps = psasync::ld(w(3, me_, k)), pa = psasync::ld(w(4, me_, k));
+        if (ps > pa) {
+          const int m = static_cast<int>(pa % psasync::kMbox);
+          if (!call("push", k, psasync::ld(npush(me_, k, m)), m)) return;
+          psasync::st(w(4, me_, k), pa + 1);
+          did = true;
+        }
+      }
+      if (did) idle.n = 0;
+      else idle();
+    }
+  }
+  bool call(const char* op, int64_t worker, int64_t n, int m) {
+    py::gil_scoped_acquire gil;
+    try {
+      cb_(op, worker, n, m);
+      return true;
+    } catch (py::error_already_set& e) {
+      std::lock_guard<std::mutex> g(mu_);
+      err_ = std::string(op) + ": " + e.what();
+      psasync::st(b_ + 2, 1);  // stop every service of the table: workers time out loudly
+      return false;
+    }
+  }
+  int64_t* b_;
+  int64_t W_ = 1;
+  int me_;
+  py::object cb_;
+  std::atomic<bool> stop_{true};
+  std::thread th_;
+  std::mutex mu_;
+  std::string err_;
 };
 
 }  // namespace
@@ -454,6 +563,40 @@ PYBIND11_MODULE(_native, m) {
         py::call_guard<py::gil_scoped_release>());
   a.def("unpin", [](uintptr_t addr, int o, int s) { psasync::unpin(ctl_at(addr), o, s); });
   a.def("set_stop", [](uintptr_t addr, int64_t v) { psasync::st(&ctl_at(addr)->stop, v); });
+  a.def("MBOX", []() { return psasync::kMbox; });
+
+  // generic shared-memory words (acquire / release) for the async row tables
+  auto sh = m.def_submodule("shm", "int64 words in shared memory");
+  sh.def("ld", [](uintptr_t p) { return psasync::ld(reinterpret_cast<int64_t*>(p)); });
+  sh.def("st", [](uintptr_t p, int64_t v) { psasync::st(reinterpret_cast<int64_t*>(p), v); });
+  sh.def("add", [](uintptr_t p, int64_t v) { return psasync::add(reinterpret_cast<int64_t*>(p), v); });
+  sh.def("wait_ge", [](std::vector<uintptr_t> ps, int64_t v, uintptr_t stop_word, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    psasync::Backoff bo;
+    for (;;) {
+      bool ok = true;
+      for (auto p : ps) ok = ok && psasync::ld(reinterpret_cast<int64_t*>(p)) >= v;
+      if (ok) return;
+      if (stop_word && psasync::ld(reinterpret_cast<int64_t*>(stop_word)) != 0)
+        throw std::runtime_error("async rows: the service of this table stopped (owner error)");
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        throw std::runtime_error("async rows: timed out waiting for an owner (dead rank?)");
+      bo();
+    }
+  }, py::call_guard<py::gil_scoped_release>());
+  auto rw = m.def_submodule("rows", "asynchronous sparse-row tables: control block + service thread");
+  rw.def("ctl_size", [](int64_t W) { return row_ctl_words(W) * 8; });
+  rw.def("ctl_init", [](uintptr_t addr, int64_t W) {
+    int64_t* b = reinterpret_cast<int64_t*>(addr);
+    for (int64_t i = 0; i < row_ctl_words(W); ++i) b[i] = 0;
+    b[1] = W;
+    psasync::st(b, kRowMagic);
+  });
+  py::class_<RowPoller>(rw, "Service")
+      .def(py::init<uintptr_t, int, py::object>())
+      .def("start", &RowPoller::start)
+      .def("stop", &RowPoller::stop, py::call_guard<py::gil_scoped_release>())
+      .def("error", &RowPoller::error);
   a.def("snapshot", [](uintptr_t addr) {
     auto* c = ctl_at(addr);
     const int W = static_cast<int>(c->world);
@@ -477,8 +620,8 @@ PYBIND11_MODULE(_native, m) {
     return d;
   });
   py::class_<CpuAsyncServer>(m, "CpuAsyncServer")
-      .def(py::init<uintptr_t, int, const std::string&, int64_t, uintptr_t, std::vector<uintptr_t>,
-                    std::vector<uintptr_t>, double>())
+      .def(py::init<uintptr_t, int, int64_t, uintptr_t, std::vector<uintptr_t>, std::vector<uintptr_t>, double>())
+      .def("add_segment", &CpuAsyncServer::add_segment)
       .def("start", &CpuAsyncServer::start)
       .def("stop", &CpuAsyncServer::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("applied", &CpuAsyncServer::applied)

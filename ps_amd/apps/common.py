@@ -65,6 +65,12 @@ def connect(cfg: Config, device=None):
         return client, tcp_table_factory(client, device, seed=cfg.seed)
     if world > 1:
         tp = init_distributed(_backend(cfg))
+        cons = cfg.effective_consistency
+        if cons in ("asp", "ssp"):  # rows reached one-sidedly, no lockstep all-to-alls
+            from ..parallel.async_rows import async_table_factory
+
+            return tp, async_table_factory(tp, device, seed=cfg.seed,
+                                           staleness=None if cons == "asp" else int(cfg.staleness))
         return tp, sharded_table_factory(tp, device, seed=cfg.seed, overlap=device is not None and
                                          torch.device(device).type == "cuda")
     return None, local_table_factory(device, seed=cfg.seed)

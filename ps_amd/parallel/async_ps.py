@@ -7,18 +7,25 @@ a per-GPU server progress thread and bounded staleness (SSP).
 
 MI355X-native design (one node, one process per GPU, or threads / CPU processes in tests):
 
-* the flat parameter space is range-partitioned; rank r OWNS shard r: fp32 master + optimizer
-  state, W gradient MAILBOXES (one per worker) and 3 PUBLISHED weight slots, all in its HBM;
-* push  = the worker copies its gradient slice for shard r straight into mailbox[w] of owner r
-          (peer copies over xGMI into IPC-mapped memory, on a side stream), then a native
-          completion thread bumps seq[r][w] once the copies landed -- the training thread never
-          waits for it;
+* the flat parameter space (laid out in BACKWARD order, cut into 64-element-aligned buckets) is
+  range-partitioned; rank r OWNS shard r: fp32 master + the optimizer state of every updater
+  SEGMENT (per-key-prefix updaters resolved exact -> longest prefix -> default, as
+  store/KVStore.java:242-252 -- e.g. FTRL on ``wide.*`` and Adam elsewhere), 2 gradient
+  MAILBOXES per worker (push k lands in slot k % 2) and 3 PUBLISHED weight slots, all in its HBM;
+* push  = as soon as a bucket's last gradient is accumulated (autograd hook) the worker lands it
+          in its gradient flat and ONE copy kernel (csrc/kernels/plane.hip) writes the bucket's
+          pieces straight into the owners' IPC-mapped mailboxes -- all owners' links at once --
+          on a side stream; at ``finish_step`` a native completion thread bumps seq[r][w] once
+          every copy landed.  The training thread never waits for a copy, and waits for an
+          owner only if that owner has not yet applied the worker's push from TWO steps ago;
 * serve = a NATIVE progress thread per owner (csrc/async_ps_gpu.cpp; CPU: csrc/runtime)
-          polls the shared control block, runs the fused HIP optimizer on each deposited push
-          in arrival order (Hogwild-style, one update per push, gradient scaled by 1/W), writes
-          the new weights into a free slot, publishes it and acknowledges the push;
+          polls the shared control block, runs the fused HIP optimizer of every segment on each
+          deposited push in arrival order (Hogwild-style, one update per push, gradient scaled
+          by 1/W), writes the new weights into a free slot, publishes it and acknowledges;
 * pull  = the worker pins every owner's current slot (the owner never overwrites a pinned
-          slot: no torn reads) and copies it into its replica;
+          slot: no torn reads) and ONE copy kernel on a pull stream fills the BACK replica
+          buffer; the compute stream waits on that copy (the host does not), then the buffers
+          swap -- the pull overlaps the tail of the step that still reads the front buffer;
 * SSP(s): before pulling at clock c the worker waits until every owner has APPLIED every
           worker's first c - s pushes (so the weights read contain all updates older than
           s steps); s = 0 is BSP semantics without any collective, ``staleness=None`` is ASP.
@@ -27,17 +34,20 @@ No rank ever blocks on another rank reaching a matching collective: a slow worke
 the others through the staleness bound (SSP) or not at all (ASP).  The control block lives in
 POSIX shared memory (csrc/include/async_ctl.h); buffers are exchanged once at start-up through
 the transport's object all-gather (CUDA IPC handles between processes, named shared memory for
-CPU processes, plain tensors between loopback thread-ranks).
+CPU processes, plain tensors between loopback thread-ranks).  Sparse rows take the same
+one-sided path (parallel/async_rows.py).
 """
 from __future__ import annotations
 
 import os
 import uuid
+from functools import partial
 from typing import Dict, List, Optional, Union
 
 import torch
 
 from ..obs import trace as _trace
+from ..ops import optim as _o
 from .transport import Transport, side_stream
 from .updaters import AdamUpdater, Updater, resolve_updater
 
@@ -160,60 +170,82 @@ def _addr(seg) -> int:
 
 class AsyncPS:
     """Drop-in for ColocatedPS when the consistency mode is ASP or SSP-without-lockstep:
-    ``finish_step()`` after backward pushes asynchronously and pulls what the staleness bound
-    allows; parameters are views of the flat replica."""
+    gradients leave bucket by bucket from the backward hooks (one-sided copies into the owners'
+    mailboxes), ``finish_step()`` closes the push and pulls what the staleness bound allows into
+    the back replica buffer; parameters are views of the front buffer."""
 
     def __init__(self, model: torch.nn.Module, updaters: Union[Updater, Dict[str, Updater]],
                  transport: Optional[Transport] = None, *, staleness: Optional[int] = None,
-                 gscale: Optional[float] = None, timeout_s: float = 600.0):
+                 gscale: Optional[float] = None, timeout_s: float = 600.0, bucket_mb: float = 25.0,
+                 overlap: bool = True):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
         W, me = self.world, self.rank
-        umap = updaters if isinstance(updaters, dict) else {"default": updaters}
+        self.umap = updaters if isinstance(updaters, dict) else {"default": updaters}
         params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         if not params:
             raise ValueError("model has no trainable parameters")
-        us = {id(resolve_updater(n, umap)) for n, _ in params}
-        if len(us) != 1:
-            raise ValueError("AsyncPS applies one updater to the whole flat space")
-        self.updater = resolve_updater(params[0][0], umap)
         dtypes = {p.dtype for _, p in params}
         if len(dtypes) != 1:
             raise ValueError("AsyncPS needs one parameter dtype")
         self.dtype = dtypes.pop()
         self.device = params[0][1].device
         self.gpu = self.device.type == "cuda"
+        if not self.gpu and self.dtype != torch.float32:
+            raise ValueError("CPU AsyncPS shards are fp32")
         self.staleness = staleness
         self.timeout_s = timeout_s
         self.gscale = (1.0 / W) if gscale is None else float(gscale)
         self.params = dict(params)
-        n = sum(p.numel() for _, p in params)
-        self.L = ((n + W - 1) // W + 63) // 64 * 64
+        self.overlap = overlap
+        self.threads = self.t.backend == "loopback"
+        # ---------------- flat layout in BACKWARD order, cut into buckets (64-element aligned
+        # starts, so every piece of a bucket copy is 16-B aligned)
+        esz = torch.empty((), dtype=self.dtype).element_size()
+        cap = max(64, int(bucket_mb * 2**20) // esz)
+        self.offsets: Dict[str, tuple] = {}
+        self.buckets: List[List[str]] = []
+        self.bucket_range: List[tuple] = []
+        off, cur, start = 0, [], 0
+        for nme, p in reversed(params):
+            if cur and off - start + p.numel() > cap:
+                self.buckets.append(cur)
+                self.bucket_range.append((start, off))
+                off = (off + 63) // 64 * 64
+                cur, start = [], off
+            self.offsets[nme] = (off, p.numel(), p.shape)
+            cur.append(nme)
+            off += p.numel()
+        self.buckets.append(cur)
+        self.bucket_range.append((start, off))
+        self._key_bucket = {n: b for b, ks in enumerate(self.buckets) for n in ks}
+        self.L = ((off + W - 1) // W + 63) // 64 * 64
         L = self.L
-        # ---------------- replica + gradient flats (parameters are views)
-        self.flat = torch.zeros(W * L, dtype=self.dtype, device=self.device)
+        # ---------------- double-buffered replica + gradient flat (parameters are views)
+        self.flats = [torch.zeros(W * L, dtype=self.dtype, device=self.device) for _ in range(2)]
+        self.cur = 0
         self.gflat = torch.zeros(W * L, dtype=self.dtype, device=self.device)
-        self.offsets = {}
-        off = 0
         with torch.no_grad():
             for nme, p in params:
-                self.flat[off:off + p.numel()].copy_(p.detach().reshape(-1))
-                self.offsets[nme] = (off, p.numel(), p.shape)
-                off += p.numel()
-            self.t.broadcast(self.flat, src=0)
+                o, n, _ = self.offsets[nme]
+                self.flats[0][o:o + n].copy_(p.detach().reshape(-1))
+            self.t.broadcast(self.flats[0], src=0)
+            self.flats[1].copy_(self.flats[0])
         self._bind()
-        # ---------------- owner state + shared buffers
+        # ---------------- owner shard: fp32 master + per-key-prefix updater segments
         self.share = _Shared(self.t, self.device)
         lo = me * L
-        self.master = self.flat[lo:lo + L].float().clone()
-        self.states = self.updater.new_states(self.master) if self.gpu else []
-        self.mbox = self.share.alloc((W, L), self.dtype)
+        self.master = self.flats[0][lo:lo + L].float().clone()
+        self.segs = self._segments(lo, lo + L)  # [(updater, a, z)] shard-local
+        self.states = [u.new_states(self.master[a:z]) for (u, a, z) in self.segs] if self.gpu else []
+        A = _native().async_ctl
+        self.MB = A.MBOX()
+        self.mbox = self.share.alloc((W * self.MB, L), self.dtype)
         self.pub = self.share.alloc((3, L), self.dtype)
         with torch.no_grad():
-            self.pub.copy_(self.flat[lo:lo + L].expand(3, L))
+            self.pub.copy_(self.flats[0][lo:lo + L].expand(3, L))
         # control block: rank 0 creates the shared segment, everyone maps it
-        A = _native().async_ctl
         name = self.t.all_gather_object(f"psamd_ctl_{uuid.uuid4().hex[:16]}" if me == 0 else None)[0]
         if me == 0:
             self._ctl = _ShmSeg(name, A.SIZE, create=True)
@@ -231,106 +263,203 @@ class AsyncPS:
         if self.gpu:
             from .. import _C  # type: ignore
 
-            h = self.updater.hyper(1)
-            st = self.states + [None] * (2 - len(self.states))
-            bias = _BIAS_MODE[self.updater.bias_correction] if isinstance(self.updater, AdamUpdater) else 0
-            self.server = _C.GpuAsyncServer(
-                self.ctl, me, self.updater.kind, self.master, st[0], st[1], [self.mbox[w] for w in range(W)],
-                [self.pub[s] for s in range(3)], h.get("lr", 0.01), h.get("beta1", 0.9), h.get("beta2", 0.999),
-                h.get("eps", 1e-8), h.get("wd", 0.0), h.get("momentum", 0.0), h.get("dampening", 0.0),
-                bool(h.get("nesterov", False)), bool(h.get("adamw", False)), bias, h.get("l1", 0.0), h.get("l2", 0.0),
-                h.get("fbeta", 1.0), int(h.get("ftrl_mode", 0)), self.gscale)
+            self._C = _C
+            self.server = _C.GpuAsyncServer(self.ctl, me, self.master, [self.mbox[i] for i in range(W * self.MB)],
+                                            [self.pub[s] for s in range(3)], self.gscale)
+            for (u, a, z), st in zip(self.segs, self.states):
+                h = _o._hp(u.hyper(1))
+                bias = _BIAS_MODE[u.bias_correction] if isinstance(u, AdamUpdater) else 0
+                st2 = list(st) + [None] * (2 - len(st))
+                self.server.add_segment(u.kind, a, z, st2[0], st2[1], [float(h[k]) for k in _HYPER], bias)
             self.notifier = _C.GpuNotifier(self.ctl)
             self.push_stream = side_stream(self.device)
+            self.pull_stream = torch.cuda.Stream(device=self.device)
+            self._done_ev: List[Optional[torch.cuda.Event]] = [None, None]
         else:
-            if self.dtype != torch.float32:
-                raise ValueError("CPU AsyncPS shards are fp32")
             self.server = _native().CpuAsyncServer(
-                self.ctl, me, self.updater.name, L, self.master.data_ptr(), [self.mbox[w].data_ptr() for w in range(W)],
+                self.ctl, me, L, self.master.data_ptr(), [self.mbox[i].data_ptr() for i in range(W * self.MB)],
                 [self.pub[s].data_ptr() for s in range(3)], self.gscale)
+            for u, a, z in self.segs:
+                self.server.add_segment(u.name, a, z)
             self.notifier = None
         self.t.barrier()
         self.server.start()
         self.clock = 0
         self.round = 0
         self.accumulating = False
-        self.stats = {"gate_waits": 0}
+        self.stats = {"gate_waits": 0, "bucket_pushes": 0}
+        self._pending = [len(ks) for ks in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._landing: List[Dict[str, torch.Tensor]] = [dict() for _ in self.buckets]
+        self._step_open = False
+        self._hooks = ([p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
+                       if overlap else [])
+
+    def _segments(self, lo: int, hi: int) -> List[tuple]:
+        """Updater segments of the shard [lo, hi): exact key -> longest prefix -> default per key
+        (store/KVStore.java:242-252), adjacent runs merged, padding given to its neighbours."""
+        segs: List[tuple] = []
+        for nme, (o, n, _) in sorted(self.offsets.items(), key=lambda kv: kv[1][0]):
+            a, z = max(o, lo), min(o + n, hi)
+            if a >= z:
+                continue
+            u = resolve_updater(nme, self.umap)
+            if segs and segs[-1][0] is u:
+                segs[-1] = (u, segs[-1][1], z - lo)
+            else:
+                if segs:  # a gap (bucket padding) belongs to the previous segment
+                    segs[-1] = (segs[-1][0], segs[-1][1], a - lo)
+                segs.append((u, a - lo, z - lo))
+        if not segs:  # pure padding shard
+            return [(resolve_updater(next(iter(self.offsets)), self.umap), 0, hi - lo)]
+        segs[0] = (segs[0][0], 0, segs[0][2])
+        segs[-1] = (segs[-1][0], segs[-1][1], hi - lo)
+        return segs
 
     # ------------------------------------------------------------------ views
     def _bind(self) -> None:
+        fl = self.flats[self.cur]
         for nme, p in self.params.items():
             off, n, shape = self.offsets[nme]
-            p.data = self.flat[off:off + n].view(shape)
+            p.data = fl[off:off + n].view(shape)
             p.grad = None
 
     def weight(self, name: str) -> torch.Tensor:
         off, n, shape = self.offsets[name]
-        return self.flat[off:off + n].view(shape)
+        return self.flats[self.cur][off:off + n].view(shape)
 
-    # ------------------------------------------------------------------ step
-    def _land(self) -> None:
+    @property
+    def flat(self) -> torch.Tensor:
+        return self.flats[self.cur]
+
+    # ------------------------------------------------------------------ push path
+    def _on_ready(self, name: str, p: torch.Tensor) -> None:
+        if self.accumulating:
+            return
+        b = self._key_bucket[name]
+        if name not in self._landing[b]:
+            self._pending[b] -= 1
+        self._landing[b][name] = p.grad
+        if self._pending[b] == 0:
+            self._push_bucket(b)
+
+    def _open_step(self) -> None:
+        """Before the first bucket of push ``clock`` leaves: the mailbox slot it lands in
+        (clock % 2) must be free on every owner -- push clock - 2 applied, i.e. ack >= clock - 1
+        (we gate on our OWN push count: seq lags behind on GPU).  The previous push's copies
+        must have read gflat before it is overwritten."""
+        if self._step_open:
+            return
+        self._step_open = True
+        if self.clock >= 2:
+            for r in range(self.world):
+                self.A.wait_ack(self.ctl, r, self.rank, self.clock - 1, self.timeout_s)
+        if self.gpu:
+            torch.cuda.current_stream(self.device).wait_stream(self.push_stream)
+
+    def _push_bucket(self, b: int) -> None:
+        if self._launched[b]:
+            return
+        self._launched[b] = True
+        self._open_step()
+        parked = self._landing[b]
         dst, src = [], []
-        for nme, p in self.params.items():
+        for nme in self.buckets[b]:
             off, n, _ = self.offsets[nme]
             v = self.gflat[off:off + n]
-            if p.grad is None:
+            g = parked.get(nme)
+            if g is None:
                 v.zero_()
             else:
                 dst.append(v)
-                src.append(p.grad.reshape(-1))
-            p.grad = None
+                src.append(g.reshape(-1))
+            self.params[nme].grad = None
         if dst:
             torch._foreach_copy_(dst, src)
+        self._landing[b] = {}
+        lo, hi = self.bucket_range[b]
+        L, MB, me = self.L, self.MB, self.rank
+        slot = self.clock % MB
+        pieces = []
+        for r in range(self.world):
+            a, z = max(lo, r * L), min(hi, (r + 1) * L)
+            if a < z:
+                pieces.append((r, a, z))
+        if self.gpu:
+            self.push_stream.wait_stream(torch.cuda.current_stream(self.device))
+            es = self.gflat.element_size()
+            segs = [(self.gflat.data_ptr() + a * es,
+                     self.peer_mbox[r][me * MB + slot].data_ptr() + (a - r * L) * es, (z - a) * es)
+                    for r, a, z in pieces]
+            with torch.cuda.stream(self.push_stream):
+                self._C.plane.copy_many(segs, self.push_stream.cuda_stream, self.device.index)
+        else:
+            for r, a, z in pieces:
+                self.peer_mbox[r][me * MB + slot][a - r * L:z - r * L].copy_(self.gflat[a:z])
+        self.stats["bucket_pushes"] += 1
 
     def finish_step(self) -> None:
-        """Push this step's gradient to every owner (asynchronously), advance the clock, and
-        pull the newest weights the staleness bound allows."""
+        """Close this step's push (buckets the hooks did not send leave now; the owners see it
+        once every copy landed), advance the clock, and pull the newest weights the staleness
+        bound allows into the back buffer."""
         if self.accumulating:
             return
         with _trace.range(f"async_ps.step.c{self.clock}"):
             self._finish_step()
 
     def _finish_step(self) -> None:
-        W, me, L, A = self.world, self.rank, self.L, self.A
+        W, me, A = self.world, self.rank, self.A
+        if not self.overlap:  # gradients were accumulated into p.grad: park them all now
+            for nme, p in self.params.items():
+                b = self._key_bucket[nme]
+                self._landing[b][nme] = p.grad
+        for b in range(len(self.buckets)):
+            self._push_bucket(b)
         if self.gpu:
-            torch.cuda.current_stream(self.device).wait_stream(self.push_stream)  # gflat free again
-        self._land()
-        # each owner must have APPLIED every earlier push of ours before the next copy lands in the
-        # 1-deep mailbox: gate on our own push count (seq lags behind on GPU -- it is bumped by
-        # the completion thread after the copy finished -- so "ack == seq" could pass while the
-        # previous copy is still queued, and the owner would read a mailbox being overwritten)
-        for r in range(W):
-            A.wait_ack(self.ctl, r, me, self.clock, self.timeout_s)
-        if self.gpu:
-            cur = torch.cuda.current_stream(self.device)
-            self.push_stream.wait_stream(cur)
-            with torch.cuda.stream(self.push_stream):
-                for r in range(W):
-                    self.peer_mbox[r][me].copy_(self.gflat[r * L:(r + 1) * L], non_blocking=True)
-                self.notifier.after(self.push_stream.cuda_stream, self.device.index, list(range(W)), me, True, [])
+            self.notifier.after(self.push_stream.cuda_stream, self.device.index, list(range(W)), me, True, [])
         else:
             for r in range(W):
-                self.peer_mbox[r][me].copy_(self.gflat[r * L:(r + 1) * L])
                 A.bump_seq(self.ctl, r, me)
             A.bump_clock(self.ctl, me)
         self.clock += 1
         self.round += 1
+        self._pending = [len(ks) for ks in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._step_open = False
         self._pull()
 
-    def _pull(self) -> None:
+    def _pull(self, gate: bool = True) -> None:
+        """Copy every owner's current published slot (pinned: never overwritten while read) into
+        the BACK replica buffer with one kernel, then make it the front buffer: the compute stream
+        waits on the copy, the host does not."""
         W, L, A = self.world, self.L, self.A
-        if self.staleness is not None:
+        if gate and self.staleness is not None:
             A.wait_min_ack(self.ctl, self.clock - int(self.staleness), self.timeout_s)
         pins = [(r, A.pin(self.ctl, r)) for r in range(W)]
-        with torch.no_grad():
-            for r, s in pins:
-                self.flat[r * L:(r + 1) * L].copy_(self.peer_pub[r][s], non_blocking=True)
+        back = 1 - self.cur
+        dst = self.flats[back]
         if self.gpu:
-            self.notifier.after(torch.cuda.current_stream(self.device).cuda_stream, self.device.index, [],
-                                self.rank, False, pins)
+            comp = torch.cuda.current_stream(self.device)
+            ev = self._done_ev[back]
+            if ev is not None:  # the step that last read the back buffer is done with it
+                self.pull_stream.wait_event(ev)
+            es = dst.element_size()
+            segs = [(self.peer_pub[r][s].data_ptr(), dst.data_ptr() + r * L * es, L * es) for r, s in pins]
+            with torch.cuda.stream(self.pull_stream):
+                self._C.plane.copy_many(segs, self.pull_stream.cuda_stream, self.device.index)
+            self.notifier.after(self.pull_stream.cuda_stream, self.device.index, [], self.rank, False, pins)
+            done = torch.cuda.Event()
+            done.record(comp)  # everything issued so far on the front buffer
+            self._done_ev[self.cur] = done
+            comp.wait_stream(self.pull_stream)
         else:
+            with torch.no_grad():
+                for r, s in pins:
+                    dst[r * L:(r + 1) * L].copy_(self.peer_pub[r][s])
             for r, s in pins:
                 A.unpin(self.ctl, r, s)
+        self.cur = back
+        self._bind()
 
     # ------------------------------------------------------------------ control
     def snapshot(self) -> dict:
@@ -340,6 +469,7 @@ class AsyncPS:
         """Wait until every push of THIS worker has been applied by every owner, then pull."""
         if self.gpu:
             torch.cuda.current_stream(self.device).synchronize()
+            self.push_stream.synchronize()
             self.notifier.drain()
         import time
 
@@ -357,16 +487,22 @@ class AsyncPS:
             self.notifier.drain()
 
     # ------------------------------------------------------------------ checkpoint
+    def _state_list(self) -> List[torch.Tensor]:
+        if self.gpu:
+            return [s for st in self.states for s in st]
+        return [torch.from_numpy(a) for a in self.server.states()]
+
     def shard_state(self) -> dict:
-        """This owner's shard (fp32 master, optimizer state, version) at a QUIESCENT point: every
-        rank calls it at the same step boundary; after the barrier no push is in flight."""
+        """This owner's shard (fp32 master, optimizer state per updater segment, update count)
+        at a QUIESCENT point: every rank calls it at the same step boundary; after the barrier no
+        push is in flight."""
         self.synchronize()
         self.t.barrier()
-        st = self.states if self.gpu else [torch.from_numpy(a) for a in self.server.states()]
         version = int(self.A.snapshot(self.ctl)["version"][self.rank])
         snap = {"rank": self.rank, "world": self.world, "round": self.round, "clock": self.clock, "version": version,
                 "master": self.master.detach().to("cpu", copy=True),
-                "states": [s.detach().to("cpu", copy=True) for s in st], "staleness": self.staleness}
+                "states": [s.detach().to("cpu", copy=True) for s in self._state_list()],
+                "segments": [(u.name, a, z) for u, a, z in self.segs], "staleness": self.staleness}
         self.t.barrier()
         return snap
 
@@ -378,7 +514,7 @@ class AsyncPS:
         with torch.no_grad():
             self.master.copy_(st["master"].to(self.master.device))
             if self.gpu:
-                for s, src in zip(self.states, st["states"]):
+                for s, src in zip([s for sts in self.states for s in sts], st["states"]):
                     s.copy_(src.to(s.device))
             else:
                 self.server.set_states([x.numpy() for x in st["states"]])
@@ -394,14 +530,7 @@ class AsyncPS:
 
     def refresh(self) -> None:
         """Pull the newest published weights (no staleness gate), e.g. after a final barrier."""
-        self._pull_latest()
-
-    def _pull_latest(self) -> None:
-        s, self.staleness = self.staleness, None
-        try:
-            self._pull()
-        finally:
-            self.staleness = s
+        self._pull(gate=False)
         if self.gpu:
             torch.cuda.current_stream(self.device).synchronize()
             self.notifier.drain()
@@ -410,6 +539,9 @@ class AsyncPS:
         """Stop the progress thread (after every rank is done) and release shared memory."""
         if getattr(self, "server", None) is None:
             return
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
         self.synchronize()
         self.t.barrier()
         self.server.stop()
@@ -422,3 +554,7 @@ class AsyncPS:
         self._ctl.close()
         if self.rank == 0:
             self._ctl.unlink()
+
+
+_HYPER = ("lr", "beta1", "beta2", "eps", "wd", "momentum", "dampening", "nesterov", "adamw", "bc1", "bc2", "l1", "l2",
+          "fbeta", "ftrl_mode", "gscale")

@@ -1,0 +1,320 @@
+"""Asynchronous sparse rows: embedding / wide rows under ASP and SSP without lockstep traffic.
+
+Reference: every embedding row and every wide weight is its own PS key, pulled per batch with
+``getList`` (store/KVStore.java:74-127, layer/EmbeddingField.java:57-64, layer/LRLayer.java:62-70)
+and pushed through the same fire-and-forget ``push`` as the dense keys; an async server
+applies each push on arrival (net/PServer.java:164-184).  The collective sparse exchange of
+``ShardedSparseTable`` (all-to-alls) keeps every rank in lockstep; here, as for the dense keys
+of ``AsyncPS``, no rank ever waits for another rank to reach a matching call:
+
+* rows are owned by ``mix64(key) % W`` (the sharded table's rule); each owner keeps its shard in
+  a ``RowShard`` (device hash map, fp32 rows, lazy-init flags, optimizer state) that ONLY its
+  own row-service thread touches;
+* pull  = the worker writes its unique keys for owner o into o's request mailbox (IPC-mapped
+  memory), bumps ``req[o][me]`` and waits for ``resp[o][me]`` -- i.e. for owner o's service
+  thread, never for another worker -- then reads the rows out of o's response buffer;
+* push  = the worker writes (keys, summed row gradients) into o's push mailbox (2 deep: push k
+  lands in slot k % 2) and bumps ``pseq[o][me]``; it waits only if its push k-2 is still
+  unapplied.  The owner applies the row optimizer (gradient / W) on arrival;
+* SSP(s): before its pull at round c a worker waits until every owner applied every worker's
+  first c - s row pushes (the dense gate of ``AsyncPS`` for the rows); ASP: no gate.
+
+The owner side is a native thread (csrc/runtime/bindings_native.cpp ``rows.Service``) polling
+the control words in POSIX shared memory and calling back into Python for the row work, which
+runs on the owner's own stream (HIP hash map / lazy init / gather / sparse optimizer on GPU,
+the same ops' torch oracles on CPU).
+"""
+from __future__ import annotations
+
+import uuid
+from typing import Optional, Sequence, Tuple, Union
+
+import torch
+
+from .async_ps import _addr, _native, _Shared, _ShmSeg
+from .sparse_table import RowShard, TcpSparseTable, _mix64
+from .transport import Transport
+from .updaters import Updater
+
+_MAGIC_WORDS = 4
+
+
+class _RowCtl:
+    """Word addresses of one table's control block (layout: csrc/runtime/bindings_native.cpp)."""
+
+    def __init__(self, base: int, W: int, mb: int):
+        self.base, self.W, self.mb = base, W, mb
+
+    def _w(self, k: int, o: int, w: int) -> int:
+        return self.base + 8 * (_MAGIC_WORDS + k * self.W * self.W + o * self.W + w)
+
+    def req(self, o, w):
+        return self._w(0, o, w)
+
+    def resp(self, o, w):
+        return self._w(1, o, w)
+
+    def nreq(self, o, w):
+        return self._w(2, o, w)
+
+    def pseq(self, o, w):
+        return self._w(3, o, w)
+
+    def pack(self, o, w):
+        return self._w(4, o, w)
+
+    def npush(self, o, w, m):
+        return self.base + 8 * (_MAGIC_WORDS + 5 * self.W * self.W + (o * self.W + w) * self.mb + m)
+
+    @property
+    def stop(self):
+        return self.base + 16
+
+
+class _AsyncRowClient:
+    """The ``row_pull`` / ``row_push`` of ``TcpSparseTable`` over owner mailboxes."""
+
+    def __init__(self, table: "AsyncRowTable"):
+        self.tb = table
+
+    def row_pull(self, name, dim, ukeys: torch.Tensor, lo, hi, seed) -> torch.Tensor:
+        return self.tb._pull(ukeys)
+
+    def row_push(self, name, dim, ukeys: torch.Tensor, grads: torch.Tensor, spec: str) -> None:
+        self.tb._push(ukeys, grads)
+
+
+class AsyncRowTable(TcpSparseTable):
+    """A sparse table whose rows live on the co-located owners, reached one-sidedly (module
+    docstring).  ``staleness=None`` is ASP, an int s is SSP(s).  ``capacity``: max unique keys
+    one worker sends one owner per pull / push; ``rows_per_owner``: owner shard capacity."""
+
+    def __init__(self, name: str, dim: int, rows: Union[int, Sequence[int]], transport: Transport,
+                 updater: Optional[Updater] = None, *, init: Tuple[float, float] = (0.0, 0.0), id_mode: str = "map",
+                 seed: int = 0, fields: int = 1, device=None, staleness: Optional[int] = None,
+                 capacity: int = 1 << 15, rows_per_owner: Optional[int] = None, timeout_s: float = 600.0):
+        self.t = transport
+        self.W, self.me = transport.world, transport.rank
+        super().__init__(name, dim, rows, _AsyncRowClient(self), updater, init=init, id_mode=id_mode, seed=seed,
+                         fields=fields, device=device)
+        self.staleness = staleness
+        self.C = int(capacity)
+        self.timeout_s = timeout_s
+        self.gpu = self.device.type == "cuda"
+        total = sum(self.field_rows)
+        cap = rows_per_owner or max(1024, 2 * total // self.W + 1024)
+        self.shard = RowShard(self.dim, cap, "map", 0, self.seed, self.init, self.device, updater)
+        W, MB = self.W, None
+        N = _native()
+        MB = N.async_ctl.MBOX()
+        self.MB = MB
+        # owner-side mailboxes (shared): request keys, response rows, push keys / gradients
+        self.share = _Shared(transport, self.device)
+        C, D = self.C, self.dim
+        self.rq = self.share.alloc((W, C), torch.int64)
+        self.rs = self.share.alloc((W, C, D), torch.float32)
+        self.pk = self.share.alloc((W, MB, C), torch.int64)
+        self.pg = self.share.alloc((W, MB, C, D), torch.float32)
+        self.peer_rq = self.share.exchange(self.rq)
+        self.peer_rs = self.share.exchange(self.rs)
+        self.peer_pk = self.share.exchange(self.pk)
+        self.peer_pg = self.share.exchange(self.pg)
+        # control block: rank 0 creates it
+        R = N.rows
+        cname = transport.all_gather_object(f"psamd_rows_{uuid.uuid4().hex[:16]}" if self.me == 0 else None)[0]
+        if self.me == 0:
+            self._ctl = _ShmSeg(cname, R.ctl_size(W), create=True)
+            R.ctl_init(_addr(self._ctl), W)
+        transport.barrier()
+        if self.me != 0:
+            self._ctl = _ShmSeg(cname)
+        self.ctl = _RowCtl(_addr(self._ctl), W, MB)
+        self.shm = N.shm
+        self.pulls = 0
+        self.pushes = 0
+        self.applied = 0
+        # the owner's row work and the worker's mailbox copies run on streams of their own: a
+        # copy never waits behind the compute stream's queued kernels
+        self._svc_stream = torch.cuda.Stream(device=self.device) if self.gpu else None
+        self._io_stream = torch.cuda.Stream(device=self.device) if self.gpu else None
+        self.service = R.Service(self.ctl.base, self.me, self._serve)
+        transport.barrier()
+        self.service.start()
+
+    # ------------------------------------------------------------------ config
+    def set_updater(self, u: Updater) -> None:
+        self.updater = u
+        self.shard.updater = u
+        self.shard.alloc_states()
+
+    @property
+    def init(self):
+        return self._init
+
+    @init.setter
+    def init(self, v):
+        self._init = tuple(v)
+        if getattr(self, "shard", None) is not None:
+            self.shard.init = self._init
+
+    # ------------------------------------------------------------------ worker side
+    def _owner(self, keys: torch.Tensor) -> torch.Tensor:
+        return torch.remainder(_mix64(keys), self.W) if self.W > 1 else torch.zeros_like(keys)
+
+    def _check_cap(self, n: int) -> None:
+        if n > self.C:
+            raise RuntimeError(f"async row table {self.name}: {n} keys for one owner exceed capacity {self.C}")
+
+    def _pull(self, ukeys: torch.Tensor) -> torch.Tensor:
+        """Rows of the unique ``ukeys`` (CPU int64) -> [n, dim] fp32 on CPU."""
+        W, me, c = self.W, self.me, self.ctl
+        if self.staleness is not None and self.W > 1:  # SSP gate over every (owner, worker)
+            target = self.pushes - int(self.staleness)  # this worker's clock = rounds pushed
+            if target > 0:
+                self.shm.wait_ge([c.pack(o, w) for o in range(W) for w in range(W)], target, c.stop, self.timeout_s)
+        own = self._owner(ukeys)
+        parts = []
+        with self._io():
+            for o in range(W):
+                ko = ukeys[own == o]
+                self._check_cap(ko.numel())
+                if ko.numel():
+                    self.peer_rq[o][me][:ko.numel()].copy_(ko)
+                parts.append(ko)
+            self._io_sync()  # the keys are in the owners' memory before the requests go up
+        for o in range(W):
+            self.shm.st(c.nreq(o, me), parts[o].numel())
+        self.pulls += 1
+        for o in range(W):
+            self.shm.add(c.req(o, me), 1)
+        self.shm.wait_ge([c.resp(o, me) for o in range(W)], self.pulls, c.stop, self.timeout_s)
+        out = torch.empty(ukeys.numel(), self.dim, dtype=torch.float32)
+        with self._io():
+            for o, ko in enumerate(parts):
+                if ko.numel():
+                    out[own == o] = self.peer_rs[o][me][:ko.numel()].to("cpu")
+        return out
+
+    def _io(self):
+        return torch.cuda.stream(self._io_stream) if self.gpu else _Null()
+
+    def _io_sync(self) -> None:
+        if self.gpu:
+            self._io_stream.synchronize()
+
+    def _push(self, ukeys: torch.Tensor, grads: torch.Tensor) -> None:
+        W, me, c = self.W, self.me, self.ctl
+        k = self.pushes
+        slot = k % self.MB
+        if k >= 2:  # mailbox slot k % 2 is free once push k - 2 was applied
+            self.shm.wait_ge([c.pack(o, me) for o in range(W)], k - 1, c.stop, self.timeout_s)
+        own = self._owner(ukeys)
+        g = grads.float().cpu()
+        ns = []
+        with self._io():
+            for o in range(W):
+                sel = own == o
+                ko = ukeys[sel]
+                self._check_cap(ko.numel())
+                if ko.numel():
+                    self.peer_pk[o][me][slot][:ko.numel()].copy_(ko)
+                    self.peer_pg[o][me][slot][:ko.numel()].copy_(g[sel])
+                ns.append(ko.numel())
+            self._io_sync()
+        for o in range(W):
+            self.shm.st(c.npush(o, me, slot), ns[o])
+        for o in range(W):
+            self.shm.add(c.pseq(o, me), 1)
+        self.pushes += 1
+
+    def push_pending(self) -> int:
+        """Every round pushes (possibly nothing): the owners' applied counts are the clocks of
+        the SSP gate."""
+        n = super().push_pending()
+        if n == 0 and not self.accumulating:
+            self._push(torch.empty(0, dtype=torch.int64), torch.empty(0, self.dim))
+            self.round += 1
+        return n
+
+    # ------------------------------------------------------------------ owner side
+    def _serve(self, op: str, worker: int, n: int, m: int) -> None:
+        """Row-service callback (native thread, GIL held): the owner's work for one request."""
+        ctx = torch.cuda.stream(self._svc_stream) if self.gpu else _Null()
+        with ctx, torch.no_grad():
+            if op == "pull":
+                if n:
+                    keys = self.rq[worker][:n]
+                    slots = self.shard.slots(keys, insert=True)
+                    self.rs[worker][:n].copy_(self.shard.read(slots, keys))
+            elif op == "push":
+                if n:
+                    keys = self.pk[worker][m][:n]
+                    slots = self.shard.slots(keys, insert=True)
+                    self.shard.apply(slots, self.pg[worker][m][:n], 1.0 / self.W, self.applied + 1, sorted_runs=False)
+                self.applied += 1
+            else:
+                raise ValueError(op)
+            if self.gpu:
+                self._svc_stream.synchronize()
+                self.shard.check()
+
+    def clocks(self):
+        """Row pushes deposited by every worker (its row clock)."""
+        return [self.shm.ld(self.ctl.pseq(0, w)) for w in range(self.W)]
+
+    # ------------------------------------------------------------------ lifecycle
+    def synchronize(self) -> None:
+        """Wait until every owner applied every row push of this worker."""
+        c = self.ctl
+        self.shm.wait_ge([c.pack(o, self.me) for o in range(self.W)], self.pushes, c.stop, self.timeout_s)
+
+    def state_dict(self) -> dict:
+        self.synchronize()
+        self.t.barrier()
+        d = self.shard.state_dict()
+        d["applied"] = self.applied
+        self.t.barrier()
+        return d
+
+    def load_state_dict(self, d: dict) -> None:
+        self.synchronize()
+        self.t.barrier()
+        self.shard.load_state_dict(d)
+        self.applied = int(d.get("applied", 0))
+        self.t.barrier()
+
+    def close(self) -> None:
+        if getattr(self, "service", None) is None:
+            return
+        self.synchronize()
+        self.t.barrier()
+        self.service.stop()
+        err = self.service.error()
+        self.service = None
+        self.t.barrier()
+        self.share.close(unlink=not self.share.threads)
+        self._ctl.close()
+        if self.me == 0:
+            self._ctl.unlink()
+        if err:
+            raise RuntimeError(f"async row table {self.name}: {err}")
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def async_table_factory(transport: Transport, device=None, seed: int = 0, staleness: Optional[int] = None,
+                        capacity: int = 1 << 15):
+    """Tables for the reference models under -Dconsistency=asp|ssp on the co-located servers."""
+    from .sparse_table import stable_seed
+
+    def make(name, dim, rows, init, mode=None, fields=1):
+        return AsyncRowTable(name, dim, rows, transport, init=init, seed=stable_seed(name, seed), fields=fields,
+                             device=device, staleness=staleness, capacity=capacity)
+
+    return make

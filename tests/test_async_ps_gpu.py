@@ -123,3 +123,60 @@ def test_asp_slow_server_applies_every_push_exactly_once(monkeypatch):
     want = 1.0 - 0.25 / 2 * steps * (1.0 + 2.0)
     for r in range(2):
         assert torch.equal(res[r], torch.full((16, 64), want)), res[r].unique()
+
+
+def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0):
+    import time
+
+    from ps_amd.context import ctx
+    from ps_amd.parallel.async_rows import async_table_factory
+    from ps_amd.train.trainer import CollectiveEngine, Trainer
+    from tests.test_sparse_ps_cpu import _batches, _build
+
+    torch.cuda.set_device(0)
+    ctx.init()
+    s = None if consistency == "asp" else staleness
+    m = _build(True, async_table_factory(tp, DEV, seed=7, staleness=s)).to(DEV)
+    eng = CollectiveEngine(m, tp, consistency=consistency, staleness=staleness or 0)
+    tr = Trainer(m, eng, device=DEV)
+    n = 64
+    lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
+    fixed = _batches(1, n, True)[0]
+    losses, dlead, rlead = [], [], []
+    for _ in range(steps):
+        if tp.rank == delay_rank:
+            time.sleep(delay_s)
+        losses.append(tr.train([{k: v[lo:hi] for k, v in fixed.items()}]))
+        c = eng.ps.snapshot()["clock"]
+        dlead.append(c[tp.rank] - min(c))
+        rc = m.tables()["emF"].clocks()
+        rlead.append(rc[tp.rank] - min(rc))
+    eng.ps.synchronize()
+    for t in m.tables().values():
+        t.synchronize()
+    tp.barrier()
+    eng.ps.refresh()
+    dense = {k: v.detach().float().cpu().clone() for k, v in m.named_parameters()}
+    probe = m.tables()["emF"].pull(torch.arange(40).repeat(4, 1).t().contiguous()).cpu()
+    eng.ps.close()
+    for t in m.tables().values():
+        t.close()
+    return {"losses": losses, "dlead": dlead, "rlead": rlead, "dense": dense, "probe": probe}
+
+
+@pytest.mark.parametrize("consistency,staleness", [("asp", None), ("ssp", 1)])
+def test_widedeep_async_two_processes_gpu(consistency, staleness):
+    """WideDeepNN (FTRL wide.bias + Adam segments on the owners' HIP fused
+    optimizer, embedding and wide ROWS on the owners' row services) under ASP / SSP(1) with 2
+    processes on cuda:0 -- no collective anywhere in the step."""
+    res = dist_util.run(_wide_gpu_body, 2, (consistency, staleness, 25))
+    for r in res:
+        assert sum(r["losses"][-5:]) / 5 < 0.8 * sum(r["losses"][:5]) / 5, r["losses"]
+    for k in res[0]["dense"]:
+        assert torch.equal(res[0]["dense"][k], res[1]["dense"][k])
+    assert torch.equal(res[0]["probe"], res[1]["probe"])
+
+
+def test_ssp1_straggler_bound_dense_and_rows_gpu():
+    res = dist_util.run(_wide_gpu_body, 2, ("ssp", 1, 10, 1, 0.15))
+    assert max(res[0]["dlead"]) <= 2 and max(res[0]["rlead"]) <= 2, (res[0]["dlead"], res[0]["rlead"])
