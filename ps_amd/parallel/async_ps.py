@@ -363,30 +363,45 @@ class AsyncPS:
         self._launched[b] = True
         self._open_step()
         parked = self._landing[b]
+        lo, hi = self.bucket_range[b]
+        L, MB, me = self.L, self.MB, self.rank
+        slot = self.clock % MB
+        own_lo, own_hi = me * L, (me + 1) * L
+        own_box = self.mbox[me * MB + slot]
         dst, src = [], []
+
+        def land(view_off, n, g):
+            # the piece this rank owns lands straight in its own mailbox slot (no copy); the
+            # rest in the gradient flat, from where one kernel sends it to the other owners
+            for a, z in ((view_off, min(view_off + n, own_lo)), (max(view_off, own_lo), min(view_off + n, own_hi)),
+                         (max(view_off, own_hi), view_off + n)):
+                if a >= z:
+                    continue
+                v = own_box[a - own_lo:z - own_lo] if own_lo <= a < own_hi else self.gflat[a:z]
+                if g is None:
+                    v.zero_()
+                else:
+                    dst.append(v)
+                    src.append(g[a - view_off:z - view_off])
+
         for nme in self.buckets[b]:
             off, n, _ = self.offsets[nme]
-            v = self.gflat[off:off + n]
             g = parked.get(nme)
-            if g is None:
-                v.zero_()
-            else:
-                dst.append(v)
-                src.append(g.reshape(-1))
+            land(off, n, None if g is None else g.reshape(-1))
             self.params[nme].grad = None
         if dst:
             torch._foreach_copy_(dst, src)
         self._landing[b] = {}
-        lo, hi = self.bucket_range[b]
-        L, MB, me = self.L, self.MB, self.rank
-        slot = self.clock % MB
         pieces = []
         for r in range(self.world):
             a, z = max(lo, r * L), min(hi, (r + 1) * L)
-            if a < z:
+            if a < z and r != me:
                 pieces.append((r, a, z))
         if self.gpu:
             self.push_stream.wait_stream(torch.cuda.current_stream(self.device))
+            if not pieces:
+                self.stats["bucket_pushes"] += 1
+                return
             es = self.gflat.element_size()
             segs = [(self.gflat.data_ptr() + a * es,
                      self.peer_mbox[r][me * MB + slot].data_ptr() + (a - r * L) * es, (z - a) * es)
