@@ -744,10 +744,9 @@ std::vector<Tensor> fa_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout
   const c10::DeviceGuard guard(q.device());
   auto fopt = q.options().dtype(torch::kFloat32);
   auto dsum = torch::empty({B, H, S}, fopt);
-  auto dkp = torch::empty({B, H, S, 128}, fopt), dvp = torch::empty({B, H, S, 128}, fopt);
   auto dq = torch::empty_like(q), dk = torch::empty_like(k), dv = torch::empty_like(v);
   psamd::launch_fa_bwd(u16(q), u16(k), u16(v), u16(out), u16(dout), lse.data_ptr<float>(), dsum.data_ptr<float>(),
-                       dkp.data_ptr<float>(), dvp.data_ptr<float>(), u16m(dq), u16m(dk), u16m(dv),
+                       u16m(dq), u16m(dk), u16m(dv),
                        static_cast<int>(B), static_cast<int>(S), static_cast<int>(H), static_cast<int>(KV),
                        1.f / std::sqrt(128.f), cur_stream(q));
   return {dq, dk, dv};

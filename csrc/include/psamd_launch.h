@@ -316,12 +316,12 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      int B, int S, int H, float scale, float p, uint64_t seed, hipStream_t s);
 void launch_attn_dropout_mask(uint8_t* mask, int64_t n, float p, uint64_t seed, hipStream_t s);
 // Causal GQA flash attention (flash_attn.hip): q [B, H, S, 128], k / v [B, KV, S, 128] bf16,
-// out [B, S, H * 128], lse / dsum [B, H, S] fp32, dkp / dvp [B, H, S, 128] fp32 scratch; S % 128 == 0
+// out [B, S, H * 128], lse / dsum [B, H, S] fp32; S % 128 == 0
 void launch_fa_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, float* lse, int B, int S,
                    int H, int KV, float scale, hipStream_t s);
 void launch_fa_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* out, const uint16_t* dout,
-                   const float* lse, float* dsum, float* dkp, float* dvp, uint16_t* dq, uint16_t* dk, uint16_t* dv,
-                   int B, int S, int H, int KV, float scale, hipStream_t s);
+                   const float* lse, float* dsum, uint16_t* dq, uint16_t* dk, uint16_t* dv, int B, int S, int H,
+                   int KV, float scale, hipStream_t s);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s);
 // BN helpers for the fused bottleneck (bn_act.hip): y = act(x*scale + shift [+ res [* rscale + rshift]])
 // mbits (nullable): also write the ReLU mask of y, 1 bit per element

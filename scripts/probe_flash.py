@@ -26,7 +26,8 @@ def bench(fn, it=10):
 
 
 def main():
-    B, H, KV, S, D = 1, 32, 8, 4096, 128
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    H, KV, S, D = 32, 8, 4096, 128
     q = torch.randn(B, H, S, D, device="cuda").bfloat16()
     k = torch.randn(B, KV, S, D, device="cuda").bfloat16()
     v = torch.randn(B, KV, S, D, device="cuda").bfloat16()
