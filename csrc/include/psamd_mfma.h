@@ -96,18 +96,31 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return static_cast<uint32_t>(f32_to_bf16(a)) | (static_cast<uint32_t>(f32_to_bf16(b)) << 16);
 }
 
+// v_permlane32_swap(x, y): x's upper 32 lanes <-> y's lower 32 lanes (a VALU op: no LDS queue,
+// no lgkmcnt wait behind in-flight fragment reads, unlike a ds_bpermute shuffle).
+__device__ __forceinline__ float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // same two addends on both halves
+}
+
 // B operand (k = rows 16 (s & 1) + 8 hl + e of a 32-row accumulator block, n = lane column)
 // from that block held in the accumulator layout: half hl holds rows (q & 3) + 8 (q >> 2) + 4 hl;
 // half 0 needs rows 0..7 of the 16-row step = its own 4 + the partner half's 4, half 1 rows
-// 8..15 = the partner's 4 + its own 4: one xor-32 exchange of two packed bf16 pairs.
+// 8..15 = the partner's 4 + its own 4.  With x = own rows 0..3 and y = own rows 4..7 packed,
+// swap(x, y) leaves {x', y'} = {own x, partner x} on half 0 and {partner y, own y} on half 1:
+// exactly the four pairs each half needs, in order, with no per-half select.
 __device__ __forceinline__ bf16x8_t acc_to_b(const f32x16& blk, int s, int hl) {
+  (void)hl;
   const int qb = 8 * (s & 1);
   const uint32_t lo0 = pack2(blk[qb + 0], blk[qb + 1]), lo1 = pack2(blk[qb + 2], blk[qb + 3]);
   const uint32_t hi0 = pack2(blk[qb + 4], blk[qb + 5]), hi1 = pack2(blk[qb + 6], blk[qb + 7]);
-  const uint32_t s0 = hl ? lo0 : hi0, s1 = hl ? lo1 : hi1;
-  const uint32_t r0 = __shfl_xor(s0, 32, 64), r1 = __shfl_xor(s1, 32, 64);
-  const u32x4 v = hl == 0 ? u32x4{lo0, lo1, r0, r1} : u32x4{r0, r1, hi0, hi1};
-  return __builtin_bit_cast(bf16x8_t, v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+  return __builtin_bit_cast(bf16x8_t, u32x4{a[0], b[0], a[1], b[1]});
 }
 
 __device__ __forceinline__ f32x16 mma(bf16x8_t a, bf16x8_t b, f32x16 c) {

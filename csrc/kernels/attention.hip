@@ -98,10 +98,12 @@ __device__ __forceinline__ bf16x8_t p_operand(const f32x16& blk, int s, int hl) 
   // pack own values as bf16 pairs: lo = keys qb..qb+3, hi = qb+4..qb+7 (in register order)
   const uint32_t lo0 = pack2(blk[qb + 0], blk[qb + 1]), lo1 = pack2(blk[qb + 2], blk[qb + 3]);
   const uint32_t hi0 = pack2(blk[qb + 4], blk[qb + 5]), hi1 = pack2(blk[qb + 6], blk[qb + 7]);
-  const uint32_t s0 = hl ? lo0 : hi0, s1 = hl ? lo1 : hi1;  // what the partner half needs
-  const uint32_t r0 = __shfl_xor(s0, 32, 64), r1 = __shfl_xor(s1, 32, 64);
-  const u32x4 v = hl == 0 ? u32x4{lo0, lo1, r0, r1} : u32x4{r0, r1, hi0, hi1};
-  return __builtin_bit_cast(bf16x8_t, v);
+  // one permlane32_swap per pair (VALU, no LDS queue): {own lo, partner lo} on half 0,
+  // {partner hi, own hi} on half 1 -- see mfma::acc_to_b (psamd_mfma.h)
+  (void)hl;
+  const auto a = __builtin_amdgcn_permlane32_swap(lo0, hi0, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(lo1, hi1, false, false);
+  return __builtin_bit_cast(bf16x8_t, u32x4{a[0], b[0], a[1], b[1]});
 }
 
 // stage rows [0, S) of one head's 64-wide slice (row stride rs elements) into a [128][64] tile;
@@ -156,7 +158,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
     if (kb < nkb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) m = fmaxf(m, st[kb][e]);
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    m = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
   const float k2 = scale * kLog2e;
   float sum = 0.f;
 #pragma unroll
@@ -167,7 +172,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       st[kb][e] = p;
       sum += p;
     }
-  sum += __shfl_xor(sum, 32, 64);
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false);
+    sum = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
   const float inv = 1.f / sum;
   const int q = q0 + c;
   if (hl == 0) lse[static_cast<int64_t>(bh) * S + q] = m * scale + __logf(sum);

@@ -1,21 +1,23 @@
 // Causal grouped-query flash attention (Llama-3: head dim 128, S a multiple of 128), forward and
-// backward on v_mfma_f32_32x32x16_bf16 -- replaces SDPA's library kernels, whose backward ran
-// at ~180 TF/s on the Llama-3-8B bench shape (profiles/r2_llama_rocprof_kernel_stats.txt).
+// backward on v_mfma_f32_32x32x16_bf16 -- the default attention of the Llama family; on the
+// Llama-3-8B bench shape it runs ahead of SDPA's library kernels forward and backward
+// (profiles/r3_flash_v3_probe.jsonl).
 //
-// Forward / dQ (grid: query blocks of 128 x heads x batch, 4 waves of 32 queries): the block's
-// keys stream through LDS 64 at a time; S^T = K Q^T is held in registers with ONE query per lane
-// column, so the online softmax (running max / sum) is in-register plus one cross-half
-// shuffle, P^T goes straight from the accumulators into the O^T = V^T P^T MFMAs (acc_to_b), and
-// O leaves as 8-B row pieces in the [B, S, H, D] layout the output projection reads.  The dQ
-// kernel recomputes P^T from the forward's log-sum-exp, forms dS^T = P^T (dO V^T - D), and
-// accumulates dQ^T = K^T dS^T; it also stores D = rowsum(dO * O).
+// Forward / dQ (grid: query blocks of 256 (8 waves x 32 queries) x heads x batch): the block's
+// keys stream through a double-buffered LDS image 64 at a time, prefetched into registers two
+// tiles ahead (one barrier per tile); S^T = K Q^T is held in registers with ONE query per lane
+// column, so the online softmax (deferred reference max, running sum) is in-register plus one
+// cross-half permlane32_swap, P^T goes straight from the accumulators into the O^T = V^T P^T
+// MFMAs (acc_to_b), and O leaves as 8-B row pieces in the [B, S, H, D] layout the output
+// projection reads.  The dQ kernel recomputes P^T from the forward's log-sum-exp, forms
+// dS^T = P^T (dO V^T - D), and accumulates dQ^T = K^T dS^T; it also stores D = rowsum(dO * O).
 // dK / dV (grid: key blocks of 128 x KV heads x batch, 4 waves of 32 keys): every query head
-// of the GQA group streams through LDS 64 queries at a time (prefetched one stage ahead); S =
+// of the GQA group streams through LDS 64 queries at a time (LDS-DMA, double buffer); S =
 // Q K^T and dP = dO V^T with ONE key per lane column, so P and dS feed dV^T += dO^T P and
 // dK^T += Q^T dS straight from the accumulators, which sum the whole group in registers -- the
 // backward is deterministic (no atomics, no partials).
-// Forward: 8 waves (256 queries) share each K / V tile, prefetched into registers one tile ahead;
-// forward and dQ grids run their heaviest (latest) query blocks first.
+// Forward and dQ grids run their heaviest (latest) query blocks first, dK / dV its heaviest
+// (earliest) key blocks first.
 #include "psamd_launch.h"
 #include "psamd_mfma.h"
 
@@ -90,11 +92,18 @@ __device__ __forceinline__ void pv_block(const uint16_t* T, const f32x16 (&pt)[2
   }
 }
 
-// NW waves x 32 queries per block share each 64-key K / V tile; the tiles are prefetched into
-// registers one tile ahead (issued right after the tile in LDS is published, written to LDS
-// after the next barrier), so the global loads overlap the whole QK^T / softmax / PV of the
-// current tile.  Query blocks run latest-first: under the causal mask the last blocks carry the
-// most keys, and starting them first keeps the tail short.
+// NW waves x 32 queries per block share each 64-key K / V tile.  The tiles are double-buffered in
+// LDS and prefetched into registers two tiles ahead: tile kb + 1 is written (from registers)
+// into the idle buffer right after tile kb's math, and tile kb + 2's global loads are issued
+// behind it, so ONE barrier per tile publishes the next buffer and the loads overlap a whole
+// QK^T / softmax / PV.  Cross-half reductions and the P^T -> B-operand relayout use
+// permlane32_swap (VALU) rather than LDS shuffles, which would wait behind the in-flight
+// fragment reads.  The online softmax keeps a deferred reference max (rescale only when the
+// running max grows by more than 2^8 in exp2 units): O and l are exact against that reference,
+// P stays <= 256.  Query blocks run latest-first: under the causal mask the last blocks carry
+// the most keys, and starting them first keeps the tail short.
+constexpr float kRescale = 8.f;
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
                                                          const uint16_t* __restrict__ v, uint16_t* __restrict__ out,
@@ -102,17 +111,14 @@ __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restr
   constexpr int BQ = NW * 32, NT = NW * 64;
   constexpr int CH = kBK * 16 / NT;  // 16-B chunks per thread per tensor per tile
   static_assert(CH >= 1 && kBK * 16 % NT == 0, "tile / block shape");
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kBK * kD];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[kBK * kD];
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kBK * kD];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kBK * kD];
   const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z, kvh = h / (H / KV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const uint16_t* qp = q + static_cast<int64_t>(b * H + h) * S * kD;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const uint16_t* vp = v + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const int q0 = qb * BQ + w * 32, qi = q0 + c;
-  bf16x8_t qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + static_cast<int64_t>(qi) * kD + 16 * s + 8 * hl);
   const int nkb = (qb * BQ + BQ - 1) / kBK + 1;
   const float k2 = scale * kLog2e;
   u16x8 kr[CH], vr[CH];
@@ -125,83 +131,103 @@ __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restr
       vr[i] = *reinterpret_cast<const u16x8*>(vp + o);
     }
   };
-  auto swrite = [&]() {
+  auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int id = threadIdx.x + i * NT, r = id >> 4, ch = id & 15;
-      *reinterpret_cast<u16x8*>(Ks + off<128>(r, ch * 8)) = kr[i];
-      *reinterpret_cast<u16x8*>(Vs + off<128>(r, ch * 8)) = vr[i];
+      *reinterpret_cast<u16x8*>(Ks[buf] + off<128>(r, ch * 8)) = kr[i];
+      *reinterpret_cast<u16x8*>(Vs[buf] + off<128>(r, ch * 8)) = vr[i];
     }
   };
-  float m = kNeg, l = 0.f;
+  gload(0);
+  bf16x8_t qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + static_cast<int64_t>(qi) * kD + 16 * s + 8 * hl);
+  swrite(0);
+  if (nkb > 1) gload(1);
+  float m2 = -INFINITY, l = 0.f;  // reference max in exp2 units (scores * scale * log2 e)
   f32x16 o[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) zero(o[db]);
-  gload(0);
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();  // the previous tile is read out
-    swrite();
-    __syncthreads();
-    if (kb + 1 < nkb) gload(kb + 1);  // in flight behind this tile's math
-    if (kb * kBK > q0 + 31) continue;  // wave-uniform: every key is in this wave's future
-    f32x16 st[2];
+    __syncthreads();  // tile kb is in LDS; every wave is done with tile kb - 1's buffer
+    const uint16_t* K = Ks[kb & 1];
+    const uint16_t* V = Vs[kb & 1];
+    if (kb * kBK <= q0 + 31) {  // wave-uniform: skip tiles wholly in this wave's future
+      f32x16 st[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      zero(st[ks]);
+      for (int ks = 0; ks < 2; ++ks) {
+        zero(st[ks]);
 #pragma unroll
-      for (int s = 0; s < 8; ++s) st[ks] = mma(frag<128>(Ks, ks * 32 + c, 2 * s + hl), qf[s], st[ks]);
-    }
-    float mb = kNeg;
-    if (kb * kBK + kBK - 1 > q0) {  // the diagonal tile: mask the future keys
+        for (int s = 0; s < 8; ++s) st[ks] = mma(frag<128>(K, ks * 32 + c, 2 * s + hl), qf[s], st[ks]);
+      }
+      if (kb * kBK + kBK - 1 > q0) {  // the diagonal tile: mask the future keys
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int key = kb * kBK + ks * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
+            if (key > qi) st[ks][e] = -INFINITY;
+          }
+      }
+      float mb = st[0][0];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mb = fmaxf(mb, st[ks][e]);
+      mb = xhalf_max(mb) * k2;  // every processed tile holds >= 1 visible key per query
+      if (!__all(mb - m2 <= kRescale)) {
+        const float mn = fmaxf(m2, mb);
+        const float alpha = exp2f(m2 - mn);
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
+        m2 = mn;
+      }
+      float ls = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int key = kb * kBK + ks * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-          if (key > qi) st[ks][e] = kNeg;
+          const float p = exp2f(st[ks][e] * k2 - m2);
+          st[ks][e] = p;
+          ls += p;
         }
-    }
+      l += xhalf_sum(ls);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8_t pb = acc_to_b(st[s >> 1], s, hl);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) mb = fmaxf(mb, st[ks][e]);
-    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
-    const float mn = fmaxf(m, mb);
-    const float alpha = exp2f((m - mn) * k2);
-    const float mk = mn * k2;
-    float ls = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float p = exp2f(st[ks][e] * k2 - mk);
-        st[ks][e] = p;
-        ls += p;
+        for (int db = 0; db < 4; ++db) o[db] = mma(tfrag<128>(V, s, db * 32, lane), pb, o[db]);
       }
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8_t pb = acc_to_b(st[s >> 1], s, hl);
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[db] = mma(tfrag<128>(Vs, s, db * 32, lane), pb, o[db]);
+    }
+    if (kb + 1 < nkb) {
+      swrite((kb + 1) & 1);             // write-late: the loads had a whole tile to land
+      if (kb + 2 < nkb) gload(kb + 2);  // in flight behind the next tile's math
     }
   }
   store_t(o, out + (static_cast<int64_t>(b) * S + qi) * H * kD + h * kD, 1.f / l, hl);
-  if (hl == 0) lse[static_cast<int64_t>(b * H + h) * S + qi] = m * scale + __logf(l);
+  if (hl == 0) lse[static_cast<int64_t>(b * H + h) * S + qi] = m2 * 0.6931471805599453f + __logf(l);
 }
 
 // ------------------------------------------------------------------------------ backward: dQ (+ D)
-__global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
-                                                        const uint16_t* __restrict__ v, const uint16_t* __restrict__ o,
-                                                        const uint16_t* __restrict__ dout,
-                                                        const float* __restrict__ lse, float* __restrict__ dsum,
-                                                        uint16_t* __restrict__ dq, int S, int H, int KV, float scale) {
+// The forward's structure (NW waves x 32 queries sharing double-buffered K / V tiles prefetched
+// two tiles ahead, one barrier per tile), with each 64-key tile taken as two 32-key halves so S^T,
+// dP^T and dS^T of only one half are live: at 8 waves the kernel fits two waves per SIMD.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void fa_bwd_dq_kernel(const uint16_t* __restrict__ q,
+                                                            const uint16_t* __restrict__ k,
+                                                            const uint16_t* __restrict__ v,
+                                                            const uint16_t* __restrict__ o,
+                                                            const uint16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse, float* __restrict__ dsum,
+                                                            uint16_t* __restrict__ dq, int S, int H, int KV,
+                                                            float scale) {
+  constexpr int BQ = NW * 32, NT = NW * 64;
+  constexpr int CH = kBK * 16 / NT;
+  static_assert(CH >= 1 && kBK * 16 % NT == 0, "tile / block shape");
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kBK * kD];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kBK * kD];
   const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z, kvh = h / (H / KV);
@@ -209,13 +235,27 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const uint16_t* __restri
   const uint16_t* qp = q + static_cast<int64_t>(b * H + h) * S * kD;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const uint16_t* vp = v + static_cast<int64_t>(b * KV + kvh) * S * kD;
-  const int q0 = qb * kBQ + w * 32, qi = q0 + c;
-  const int nkb = (qb * kBQ + kBQ - 1) / kBK + 1;
-  auto issue = [&](int kb) {
-    dma_tile128(Ks[kb & 1], kp + static_cast<int64_t>(kb) * kBK * kD, kD, kBK, w, 4, lane);
-    dma_tile128(Vs[kb & 1], vp + static_cast<int64_t>(kb) * kBK * kD, kD, kBK, w, 4, lane);
+  const int q0 = qb * BQ + w * 32, qi = q0 + c;
+  const int nkb = (qb * BQ + BQ - 1) / kBK + 1;
+  u16x8 kr[CH], vr[CH];
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int id = threadIdx.x + i * NT, r = id >> 4, ch = id & 15;
+      const int64_t off_ = static_cast<int64_t>(kb * kBK + r) * kD + ch * 8;
+      kr[i] = *reinterpret_cast<const u16x8*>(kp + off_);
+      vr[i] = *reinterpret_cast<const u16x8*>(vp + off_);
+    }
   };
-  issue(0);
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int id = threadIdx.x + i * NT, r = id >> 4, ch = id & 15;
+      *reinterpret_cast<u16x8*>(Ks[buf] + off<128>(r, ch * 8)) = kr[i];
+      *reinterpret_cast<u16x8*>(Vs[buf] + off<128>(r, ch * 8)) = vr[i];
+    }
+  };
+  gload(0);
   const int64_t orow = (static_cast<int64_t>(b) * S + qi) * H * kD + h * kD;
   bf16x8_t qf[8], df[8];
   float dd = 0.f;
@@ -228,30 +268,51 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const uint16_t* __restri
 #pragma unroll
     for (int e = 0; e < 8; ++e) dd += bf16_to_f32(ov[e]) * bf16_to_f32(dv[e]);
   }
-  dd += __shfl_xor(dd, 32, 64);
+  dd = xhalf_sum(dd);
   const int64_t li = static_cast<int64_t>(b * H + h) * S + qi;
   if (hl == 0) dsum[li] = dd;
   const float l2 = lse[li] * kLog2e, k2 = scale * kLog2e;
+  swrite(0);
+  if (nkb > 1) gload(1);
   f32x16 acc[4];
 #pragma unroll
   for (int db = 0; db < 4; ++db) zero(acc[db]);
   for (int kb = 0; kb < nkb; ++kb) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kb + 1 < nkb) issue(kb + 1);
-    if (kb * kBK > q0 + 31) continue;
-    f32x16 st[2], dp[2];
-    st_block(Ks[kb & 1], qf, c, hl, st);
-    st_block(Vs[kb & 1], df, c, hl, dp);  // dP^T = V dO^T: same shape as S^T = K Q^T
+    const uint16_t* K = Ks[kb & 1];
+    const uint16_t* V = Vs[kb & 1];
+    if (kb * kBK <= q0 + 31) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kk0 = kb * kBK + ks * 32;
+        if (kk0 > q0 + 31) continue;  // wave-uniform: this half is wholly in the future
+        f32x16 st, dp;
+        zero(st);
+        zero(dp);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int key = kb * kBK + ks * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-        const float p = key > qi ? 0.f : exp2f(st[ks][e] * k2 - l2);
-        st[ks][e] = p * (dp[ks][e] - dd);  // dS^T
+        for (int s = 0; s < 8; ++s) {
+          st = mma(frag<128>(K, ks * 32 + c, 2 * s + hl), qf[s], st);
+          dp = mma(frag<128>(V, ks * 32 + c, 2 * s + hl), df[s], dp);  // dP^T = V dO^T
+        }
+        const bool diag = kk0 + 31 > q0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float p = exp2f(st[e] * k2 - l2);
+          if (diag && kk0 + (e & 3) + 8 * (e >> 2) + 4 * hl > qi) p = 0.f;
+          st[e] = p * (dp[e] - dd);  // dS^T
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8_t sb = acc_to_b(st, s2, hl);
+#pragma unroll
+          for (int db = 0; db < 4; ++db) acc[db] = mma(tfrag<128>(K, ks * 2 + s2, db * 32, lane), sb, acc[db]);
+        }
       }
-    pv_block(Ks[kb & 1], st, lane, hl, acc);  // dQ^T += K^T dS^T
+    }
+    if (kb + 1 < nkb) {
+      swrite((kb + 1) & 1);
+      if (kb + 2 < nkb) gload(kb + 2);
+    }
   }
   store_t(acc, dq + static_cast<int64_t>(b * H + h) * S * kD + static_cast<int64_t>(qi) * kD, scale, hl);
 }
@@ -259,9 +320,24 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const uint16_t* __restri
 // ------------------------------------------------------------------------------ backward: dK / dV
 // One block per (128-key block, KV head): the block sweeps EVERY query head of its GQA group, so
 // dK / dV of its keys accumulate over the group in registers and leave once, in bf16 (no per-q-
-// head fp32 partials, no group-sum pass).  Queries stream through LDS 64 at a time, prefetched
-// into registers one stage ahead.  Key blocks with the most queries (the first ones) run first.
+// head fp32 partials, no group-sum pass).  Key blocks with the most queries (the first ones) run
+// first.  dK / dV take 128 accumulator registers, so the kernel runs one wave per SIMD and hides
+// latency inside the wave: query stages of 64 rows arrive by LDS-DMA into a double buffer (one
+// barrier per stage), and per 32-query slice every LDS read is issued a phase ahead of the MFMAs
+// that consume it -- L / D and the Q fragments, then the dO fragments behind the S chain, then
+// all transposed dO / Q fragments behind the dP chain and under the softmax VALU work.
 constexpr int kBQS = 64;  // queries per dK / dV stage
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ f32x4 lds_f4(const float* p) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(reinterpret_cast<const uint16_t*>(p))) : "memory");
+  return v;
+}
+__device__ __forceinline__ void tie4(f32x4& v) { asm volatile("" : "+v"(v)); }
 
 __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __restrict__ q,
                                                           const uint16_t* __restrict__ k,
@@ -270,15 +346,27 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __rest
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ dsum, uint16_t* __restrict__ dko,
                                                           uint16_t* __restrict__ dvo, int S, int H, int KV, float scale) {
-  constexpr int CH = kBQS * 16 / 256;  // 16-B chunks per thread per tensor per stage
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[kBQS * kD];
-  __shared__ __attribute__((aligned(16))) uint16_t dOs[kBQS * kD];
-  __shared__ float Ls[kBQS], Ds[kBQS];
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[2][kBQS * kD];
+  __shared__ __attribute__((aligned(16))) uint16_t dOs[2][kBQS * kD];
+  __shared__ __attribute__((aligned(16))) float Ls[2][kBQS];
+  __shared__ __attribute__((aligned(16))) float Ds[2][kBQS];
   const int kblk = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z, G = H / KV;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const uint16_t* vp = v + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const int k0 = kblk * kBQ + w * 32, key = k0 + c;
+  // stages: (q head g, query stage qs) for qs from this key block's first query on
+  const int qs0 = kblk * kBQ / kBQS, nqs = S / kBQS, per = nqs - qs0, nst = G * per;
+  auto issue = [&](int st) {
+    const int g = st / per, qs = qs0 + st % per, h = kvh * G + g, buf = st & 1;
+    const int64_t li = static_cast<int64_t>(b * H + h) * S + qs * kBQS;
+    dma_tile128(Qs[buf], q + li * kD, kD, kBQS, w, 4, lane);
+    dma_tile128(dOs[buf], dout + (static_cast<int64_t>(b) * S + qs * kBQS) * H * kD + h * kD, static_cast<int64_t>(H) * kD,
+                kBQS, w, 4, lane);
+    if (w == 0) __builtin_amdgcn_global_load_lds((gptr_t*)(lse + li + lane), (lptr_t*)Ls[buf], 4, 0, 0);
+    if (w == 1) __builtin_amdgcn_global_load_lds((gptr_t*)(dsum + li + lane), (lptr_t*)Ds[buf], 4, 0, 0);
+  };
+  issue(0);
   bf16x8_t kf[8], vf[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -292,71 +380,77 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __rest
     zero(dk[db]);
     zero(dv[db]);
   }
-  // stages: (q head g, query stage qs) for qs from this key block's first query on
-  const int qs0 = kblk * kBQ / kBQS, nqs = S / kBQS, per = nqs - qs0, nst = G * per;
-  u16x8 qr[CH], dr[CH];
-  float lr = 0.f, dsr = 0.f;
-  auto gload = [&](int st) {
-    const int g = st / per, qs = qs0 + st % per, h = kvh * G + g;
-    const uint16_t* qp = q + (static_cast<int64_t>(b * H + h) * S + qs * kBQS) * kD;
-    const uint16_t* dp = dout + (static_cast<int64_t>(b) * S + qs * kBQS) * H * kD + h * kD;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int id = threadIdx.x + i * 256, r = id >> 4, ch = id & 15;
-      qr[i] = *reinterpret_cast<const u16x8*>(qp + static_cast<int64_t>(r) * kD + ch * 8);
-      dr[i] = *reinterpret_cast<const u16x8*>(dp + static_cast<int64_t>(r) * H * kD + ch * 8);
-    }
-    if (threadIdx.x < kBQS) {
-      const int64_t li = static_cast<int64_t>(b * H + h) * S + qs * kBQS + threadIdx.x;
-      lr = lse[li] * kLog2e;
-      dsr = dsum[li];
-    }
-  };
-  auto swrite = [&]() {
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int id = threadIdx.x + i * 256, r = id >> 4, ch = id & 15;
-      *reinterpret_cast<u16x8*>(Qs + off<128>(r, ch * 8)) = qr[i];
-      *reinterpret_cast<u16x8*>(dOs + off<128>(r, ch * 8)) = dr[i];
-    }
-    if (threadIdx.x < kBQS) {
-      Ls[threadIdx.x] = lr;
-      Ds[threadIdx.x] = dsr;
-    }
-  };
-  gload(0);
   for (int st = 0; st < nst; ++st) {
-    const int qbase = (qs0 + st % per) * kBQS;
-    __syncthreads();  // the previous stage is read out
-    swrite();
-    __syncthreads();
-    if (st + 1 < nst) gload(st + 1);  // in flight behind this stage's math
+    const int qbase = (qs0 + st % per) * kBQS, buf = st & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed everywhere; stage st - 1's buffer is read out
+    if (st + 1 < nst) issue(st + 1);
+    const uint16_t* Q = Qs[buf];
+    const uint16_t* dO = dOs[buf];
 #pragma unroll
     for (int sl = 0; sl < kBQS / 32; ++sl) {
       const int qr0 = qbase + sl * 32;
       if (qr0 + 31 < k0) continue;  // wave-uniform: every query precedes every key of this wave
+      f32x4 lv[4], dv4[4];
+      bf16x8_t qa[8], da[8];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lv[g] = lds_f4(Ls[buf] + sl * 32 + 8 * g + 4 * hl);
+        dv4[g] = lds_f4(Ds[buf] + sl * 32 + 8 * g + 4 * hl);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) qa[s] = frag_a<128>(Q, sl * 32 + c, 2 * s + hl);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) da[s] = frag_a<128>(dO, sl * 32 + c, 2 * s + hl);
+      lgkm_wait<8>();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        tie4(lv[g]);
+        tie4(dv4[g]);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) tie(qa[s]);
       f32x16 sa, dp;
       zero(sa);
       zero(dp);
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sa = mma(frag<128>(Qs, sl * 32 + c, 2 * s + hl), kf[s], sa);
-        dp = mma(frag<128>(dOs, sl * 32 + c, 2 * s + hl), vf[s], dp);
-      }
+      for (int s = 0; s < 8; ++s) sa = mma(qa[s], kf[s], sa);
+      lgkm_wait<0>();
+#pragma unroll
+      for (int s = 0; s < 8; ++s) tie(da[s]);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) dp = mma(da[s], vf[s], dp);
+      bf16x8_t ta[2][4], tq[2][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          ta[s2][db] = tfrag_a<128>(dO, sl * 2 + s2, db * 32, lane);
+          tq[s2][db] = tfrag_a<128>(Q, sl * 2 + s2, db * 32, lane);
+        }
+      const bool diag = k0 + 31 > qr0;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int qr = sl * 32 + (e & 3) + 8 * (e >> 2) + 4 * hl;
-        const float p = key > qbase + qr ? 0.f : exp2f(sa[e] * k2 - Ls[qr]);
+        float p = exp2f(sa[e] * k2 - lv[e >> 2][e & 3] * kLog2e);
+        if (diag && key > qr0 + (e & 3) + 8 * (e >> 2) + 4 * hl) p = 0.f;
         sa[e] = p;
-        dp[e] = p * (dp[e] - Ds[qr]);  // dS
+        dp[e] = p * (dp[e] - dv4[e >> 2][e & 3]);  // dS
       }
+      lgkm_wait<0>();
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          tie(ta[s2][db]);
+          tie(tq[s2][db]);
+        }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bf16x8_t pb = acc_to_b(sa, s2, hl), sb = acc_to_b(dp, s2, hl);
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
-          dv[db] = mma(tfrag<128>(dOs, sl * 2 + s2, db * 32, lane), pb, dv[db]);
-          dk[db] = mma(tfrag<128>(Qs, sl * 2 + s2, db * 32, lane), sb, dk[db]);
+          dv[db] = mma(ta[s2][db], pb, dv[db]);
+          dk[db] = mma(tq[s2][db], sb, dk[db]);
         }
       }
     }
@@ -390,8 +484,12 @@ void launch_fa_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint
 void launch_fa_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* out, const uint16_t* dout,
                    const float* lse, float* dsum, uint16_t* dq, uint16_t* dk, uint16_t* dv, int B, int S, int H,
                    int KV, float scale, hipStream_t s) {
-  hipLaunchKernelGGL(fa_bwd_dq_kernel, dim3(S / kBQ, H, B), dim3(256), 0, s, q, k, v, out, dout, lse, dsum, dq, S, H,
-                     KV, scale);
+  if (S % 256 == 0)
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<8>, dim3(S / 256, H, B), dim3(512), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
+                       H, KV, scale);
+  else
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<4>, dim3(S / kBQ, H, B), dim3(256), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
+                       H, KV, scale);
   hipLaunchKernelGGL(fa_bwd_dkdv_kernel, dim3(S / kBQ, KV, B), dim3(256), 0, s, q, k, v, dout, lse, dsum, dk, dv, S,
                      H, KV, scale);
 }

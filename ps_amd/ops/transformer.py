@@ -209,10 +209,11 @@ def attention_qkv(qkv: torch.Tensor, heads: int, p: float = 0.0, mask: Optional[
 
 # ------------------------------------------------------------------------------ causal GQA flash attention
 def flash_ok(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> bool:
-    """Opt-in (PS_AMD_FLASH_ATTN=1): correct and GPU-tested, but on the Llama-3-8B shape it still
-    runs behind SDPA's kernels (profiles/r2_flash_probe.jsonl), so SDPA stays the default."""
+    """The in-house causal GQA flash kernels are the default for head dim 128 (PS_AMD_FLASH_ATTN=0
+    falls back to SDPA): on the Llama-3-8B shape they beat SDPA's library kernels forward and
+    backward (profiles/r3_flash_v3_probe.jsonl) and end to end (profiles/r3_llama_flash_vs_sdpa.jsonl)."""
     return (_hip(q, k, v) and q.dim() == 4 and q.shape[3] == 128 and k.shape == v.shape and q.shape[2] % 128 == 0
-            and q.shape[1] % k.shape[1] == 0 and os.environ.get("PS_AMD_FLASH_ATTN", "0") == "1")
+            and q.shape[1] % k.shape[1] == 0 and os.environ.get("PS_AMD_FLASH_ATTN", "1") != "0")
 
 
 class _FlashCausal(torch.autograd.Function):

@@ -55,7 +55,7 @@ def test_llama_block_flash_matches_sdpa(monkeypatch):
     wl = torch.randn(2, 256, 512, device=DEV)
     cs = rope_table(256, 128, c.rope_theta, x.device)
     outs = []
-    for flag in ("1", "0"):  # flash kernel (opt-in) vs SDPA
+    for flag in ("1", "0"):  # flash kernel (the default) vs SDPA
         monkeypatch.setenv("PS_AMD_FLASH_ATTN", flag)
         blk.zero_grad()
         xi = x.clone().requires_grad_()
