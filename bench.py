@@ -174,6 +174,8 @@ def main():
               f"(includes MIOpen find/compile for new conv shapes)", file=sys.stderr, flush=True)
     tp.barrier()
     sync()
+    if bench.stats is not None:
+        bench.stats()  # zero the counters at the start of the timed region
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -185,6 +187,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
+    timed_stats = bench.stats() if bench.stats is not None else None
     value = bench.samples_per_step * world * args.steps / elapsed
     # after the timed region: per-phase PS timing (default 3 steps at world > 1, so the driver's
     # multi-GPU lines show how much of the push / pull the backward hides) and the collective
@@ -245,6 +248,8 @@ def main():
             cfg["data_plane"] = bench.engine.plane_kind
         cfg["final_loss"] = round(float(loss.item()), 4)
         cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        if timed_stats:
+            cfg.update(timed_stats)
         if tsum:
             cfg["ps_phase_ms_per_step"] = tsum  # measured after the timed region
         if comm:

@@ -486,7 +486,18 @@ __global__ __launch_bounds__(256) void sparse_opt_vec_kernel(float* __restrict__
       if (perm == nullptr) {
         g = load4(grad, r * dim + c);
       } else {
-        for (int64_t j = r; j < nrows && rows[j] == row; ++j) g += load4(grad, perm[j] * dim + c);
+        // the run's next row id and this entry's perm are independent loads: issue both, then
+        // the gradient row; runs are short (one entry per pushing worker / micro-batch)
+        int64_t j = r;
+        int64_t pj = perm[j];
+        int64_t nx = j + 1 < nrows ? rows[j + 1] : -1;
+        g = load4(grad, pj * dim + c);
+        while (nx == row) {
+          ++j;
+          pj = perm[j];
+          nx = j + 1 < nrows ? rows[j + 1] : -1;
+          g += load4(grad, pj * dim + c);
+        }
       }
       g *= scale;
     }

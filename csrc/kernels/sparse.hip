@@ -317,6 +317,13 @@ void launch_sparse_lr_fwd(const float* w, const int64_t* ids, int64_t batch, int
   hipLaunchKernelGGL(sparse_lr_fwd_kernel, dim3(grid), dim3(256), 0, s, w, ids, batch, fields, hash_size, bias, out);
 }
 
+__device__ __forceinline__ int vec_lanes_log2_dev(int dim) {  // lanes per row: dim = 4 * 2^lg <= 256
+  if (dim % 4 != 0 || dim > 256) return -1;
+  const int l = dim / 4;
+  if ((l & (l - 1)) != 0) return -1;
+  return __builtin_ctz(l);
+}
+
 // rows: owner-local indices (negative = unresolved, skipped).  The RNG is keyed by the row's
 // GLOBAL key -- keys[r] when given (hash-mapped tables: the raw id), else row + row_base (range
 // partitioned tables: the global row) -- so a row's initial value does not depend on which rank
@@ -330,8 +337,12 @@ __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__
   const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
   const float span = hi - lo;
   // 64 rows per wave step: every lane checks one row's flag, the rows still to be created are
-  // ballotted and then initialised one after the other by the whole wave (steady state: almost
-  // every row exists, so the kernel is one coalesced flag probe per 64 rows)
+  // ballotted and then initialised P = 64 / L at a time, L = dim / 4 lanes per row when dim is
+  // 4 * 2^k <= 256 (each lane one Philox call -> one 16-B store), else one row at a time by the
+  // whole wave.  Steady state: almost every row exists, so the kernel is one coalesced flag probe
+  // per 64 rows; a fresh batch keeps every lane busy.
+  const int lg = vec_lanes_log2_dev(dim);
+  const int L = lg >= 0 ? (1 << lg) : 64, P = 64 / L, sub = lane / L, ql = lane % L;
   for (int64_t base = wave * 64; base < nrows; base += nwaves * 64) {
     const int64_t r = base + lane;
     const int64_t row = r < nrows ? rows[r] : -1;
@@ -339,13 +350,16 @@ __global__ __launch_bounds__(256) void lazy_init_rows_kernel(float* __restrict__
     const int64_t key = need ? (keys ? keys[r] : row + row_base) : 0;
     uint64_t todo = __ballot(need);
     while (todo) {
-      const int l = __ffsll(static_cast<unsigned long long>(todo)) - 1;
-      todo &= todo - 1;
+      uint64_t t = todo;  // this lane group's row: the sub-th remaining set bit
+      for (int k = 0; k < sub; ++k) t &= t - 1;
+      for (int k = 0; k < P; ++k) todo &= todo - 1;
+      const int l = t ? __ffsll(static_cast<unsigned long long>(t)) - 1 : 0;
       const int64_t rr = __shfl(row, l, 64);
       const uint64_t grow = static_cast<uint64_t>(__shfl(key, l, 64));
+      if (!t) continue;
       // one Philox call yields the 4 values of elements 4q .. 4q+3: 128-bit counter (q, key), so
       // map-mode keys (field << 44 | id) keep their field bits and every field gets its own rows
-      for (int q = lane; q * 4 < dim; q += 64) {
+      for (int q = ql; q * 4 < dim; q += L) {
         uint32_t rnd[4];
         Philox::gen(seed, static_cast<uint64_t>(q), rnd, grow);
         float* dst = table + rr * dim + q * 4;
@@ -413,7 +427,7 @@ __global__ __launch_bounds__(256) void hash_slots_kernel(unsigned long long* __r
       }
     }
     out[i] = slot;
-    if (slot < 0 && (insert || ids[i] < 0)) status[0] = 1;
+    if (slot < 0 && insert && ids[i] >= 0) status[0] = 1;  // negative ids = pad keys (no row)
   }
 }
 

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Callable, Dict
+from typing import Callable, Dict, Optional
 
 import torch
 import torch.nn.functional as F
@@ -37,6 +37,7 @@ class Bench:
     unit: str
     config: Dict = field(default_factory=dict)
     engine: object = None
+    stats: Optional[Callable[[], Dict]] = None  # extra counters for the JSON line (read after timing)
 
 
 def setup_resnet50(args, tp, dev) -> Bench:
@@ -123,19 +124,31 @@ def setup_dlrm(args, tp, dev) -> Bench:
     # exchange are measured on fresh data rather than on one memorised batch
     pool = [dlrm_batch(B, rows, seed=tp.rank * 1000 + i, device=dev) for i in range(4 * POOL)]
     it = _cycle(pool)
+    cur = [next(it)]
 
     def step():
-        dense, sparse, y = next(it)
+        dense, sparse, y = cur[0]
+        cur[0] = nxt = next(it)
+        model.prefetch(nxt[1])  # next batch's id routing runs ahead: its lookup needs no host wait
         loss = F.binary_cross_entropy_with_logits(model(dense, sparse).float(), y)
         loss.backward()  # row gradients leave from the embedding leaf's hook (side stream)
         model.push_sparse()  # flush (no-op when the hook already pushed)
         ps.finish_step()
         return loss
 
+    tbl = model.emb.table
+    s0 = {"host_syncs": 0, "pulls": 0}
+
+    def stats():  # host waits of the sparse exchange per timed step (0 = sync-free)
+        st = tbl.stats
+        d = {"sparse_host_syncs_per_pull": round((st["host_syncs"] - s0["host_syncs"]) / max(1, st["pulls"] - s0["pulls"]), 3)}
+        s0.update(host_syncs=st["host_syncs"], pulls=st["pulls"])
+        return d
+
     return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",
                  {"model": "DLRM-26x128", "global_batch": B * tp.world, "seq_len": None,
                   "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}",
-                  "sparse_push_overlap": overlap}, ps)
+                  "sparse_push_overlap": overlap}, ps, stats)
 
 
 def setup_llama_onebit(args, tp, dev) -> Bench:

@@ -84,6 +84,10 @@ class DLRM(nn.Module):
     def push_sparse(self) -> int:
         return self.emb.push_sparse()
 
+    def prefetch(self, sparse: torch.Tensor) -> None:
+        """Route the next batch's ids ahead of time (no host wait on its lookup at W > 1)."""
+        self.emb.table.prefetch(sparse)
+
     def pull_weights(self) -> None:
         self.emb.clear()
 

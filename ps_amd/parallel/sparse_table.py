@@ -15,12 +15,16 @@ exchange instead of one getList per field:
            map:    field << 44 | id, exact id -> slot on the owner (unbounded ids, Q17: int64)
 * owner    direct/hash: key // ceil(total_rows / W);  map: mix64(key) mod W
 * pull     (worker) sort keys by (owner, key) -> run heads = unique keys, per-owner counts
-           -> ONE device->host copy of the W send + W receive counts (the only host sync of
-           the step for this table) -> all_to_all(keys) -> (owner) slot lookup (HIP hash map
-           for map mode: no host round trip), deterministic lazy init keyed by the global key
-           (HIP), gather -> all_to_all(rows) back.  The pulled rows are an autograd leaf;
-           outputs gather through the inverse index (HIP), backward is a deterministic
-           segment sum per unique key (HIP).
+           -> count exchange -> async device->host copy of the W send + W receive counts ->
+           all_to_all(keys) -> (owner) slot lookup (HIP hash map for map mode: no host round
+           trip), deterministic lazy init keyed by the global key (HIP), gather ->
+           all_to_all(rows) back.  The pulled rows are an autograd leaf; outputs gather
+           through the inverse index (HIP), backward is a deterministic segment sum per unique
+           key (HIP).  Host syncs: none at W = 1 on the GPU (every buffer is sized by the
+           host-known n, pad keys -1 resolve to slot -1 = zero row / skipped update, the id
+           range check is deferred to ``synchronize``); at W > 1 the split sizes must reach
+           the host, and ``prefetch(next_ids)`` routes the next batch a step ahead so the
+           copy has landed by the time its lookup runs (``stats["host_syncs"]`` counts waits).
 * push     the leaf's gradient goes back along the SAME splits (no second count exchange);
            the owner sorts the received slots (several workers may push one row) and the
            HIP sparse optimizer sums each run and applies ONE update per row.  With
@@ -227,7 +231,23 @@ class _Plan:
 
     @property
     def counts(self) -> torch.Tensor:
-        return self.seg_off[1:] - self.seg_off[:-1]
+        """Occurrences per unique key (>= 1; the empty pad segments of a sync-free plan read 1)."""
+        return (self.seg_off[1:] - self.seg_off[:-1]).clamp(min=1)
+
+
+@dataclass
+class _Route:
+    """Device-side routing of one lookup (sizes n / n + 1; nu and the splits live in ``counts``
+    = [W send counts, #bad ids, W receive counts], copied to ``host`` asynchronously)."""
+    n: int
+    inv: torch.Tensor
+    perm: torch.Tensor
+    seg_full: torch.Tensor
+    ubuf: torch.Tensor
+    counts: torch.Tensor
+    nbad: torch.Tensor
+    host: Optional[torch.Tensor] = None
+    event: Optional[object] = None
 
 
 class ShardedSparseTable:
@@ -276,6 +296,9 @@ class ShardedSparseTable:
         self._acc: List[Tuple[torch.Tensor, torch.Tensor]] = []
         self._push_done: Optional[torch.cuda.Event] = None
         self.stats = {"pulls": 0, "pushes": 0, "rows_pulled": 0, "rows_pushed": 0, "host_syncs": 0}
+        self._pf: dict = {}  # ids signature -> (keys, route) of prefetched lookups
+        self._nbad: Optional[torch.Tensor] = None  # deferred out-of-range id count (sync-free path)
+        self._rows_dev = torch.zeros((), dtype=torch.int64, device=self.device)  # sync-free rows pulled
 
     # ------------------------------------------------------------------ compat accessors
     @property
@@ -340,9 +363,10 @@ class ShardedSparseTable:
             torch.cuda.current_stream(self.device).wait_event(self._push_done)
             self._push_done = None
 
-    def _route(self, keys: torch.Tensor, nbad: torch.Tensor):
-        """Dedupe + owner sort on device, exchange counts, ONE host read.  Returns
-        (plan pieces, unique keys)."""
+    def _route(self, keys: torch.Tensor, nbad: torch.Tensor) -> "_Route":
+        """Device half of the routing: dedupe + owner sort, per-owner unique counts and the count
+        exchange, then (GPU) an ASYNC device->host copy of the counts.  No host sync here:
+        ``_counts`` reads them when the key exchange needs its split sizes."""
         n = keys.numel()
         W = self.world
         owner = self._owner(keys)
@@ -352,17 +376,18 @@ class ShardedSparseTable:
             head[1:] = srt[1:] != srt[:-1]
         cum = torch.cumsum(head.long(), 0)
         uidx = cum - 1
-        ubuf = torch.empty(n, dtype=torch.int64, device=self.device)
-        seg_full = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        # outputs sized n / n + 1: unique key u < nu at ubuf[u], pad keys -1 behind it (no row);
+        # segment u's occurrences at seg[u] .. seg[u + 1], empty pad segments [n, n)
+        ubuf = torch.full((n,), -1, dtype=torch.int64, device=self.device)
+        seg_full = torch.full((n + 1,), n, dtype=torch.int64, device=self.device)
         if n == 0:
-            seg_full.zero_()
+            pass
         elif self.gpu:  # one HIP pass: unique keys + segment starts (no atomics, no host size)
             from ..ops._ext import native
 
             native().unique_runs(srt, uidx, KEY_MASK, ubuf, seg_full)
         else:
             ubuf.scatter_(0, uidx, srt & KEY_MASK)  # duplicates write identical values
-            seg_full.fill_(n)
             seg_full.scatter_reduce_(0, uidx, torch.arange(n, device=self.device), reduce="amin", include_self=True)
         # per-owner unique counts from the owner-major sort order (binary search, no atomics)
         bounds = torch.searchsorted(srt, torch.arange(W + 1, device=self.device, dtype=torch.int64) << OWNER_SHIFT)
@@ -373,21 +398,51 @@ class ShardedSparseTable:
         if W > 1:
             recv = torch.empty(W, dtype=torch.int64, device=self.device)
             self.t.all_to_all(recv, meta[:W].contiguous())
-            host = torch.cat([meta, recv]).cpu()
+            counts = torch.cat([meta, recv])
         else:
-            host = torch.cat([meta, meta[:1]]).cpu()
-        self.stats["host_syncs"] += 1
-        h = host.tolist()
-        if h[W]:
-            raise IndexError(f"{self.name}: {h[W]} ids out of range for id_mode={self.id_mode!r}")
-        send, recv_l = h[:W], h[W + 1:]
-        nu = sum(send)
+            counts = torch.cat([meta, meta[:1]])
         inv = torch.empty(n, dtype=torch.int64, device=self.device)
         inv[perm] = uidx
-        seg_off = seg_full[:nu + 1]
-        if not self.gpu:
-            seg_off[nu] = n
-        return n, nu, inv, perm, seg_off, send, recv_l, ubuf[:nu]
+        r = _Route(n, inv, perm, seg_full, ubuf, counts, nbad)
+        if self.gpu:
+            r.host = torch.empty(counts.numel(), dtype=torch.int64, pin_memory=True)
+            r.host.copy_(counts, non_blocking=True)
+            r.event = torch.cuda.Event()
+            r.event.record()
+        return r
+
+    def _counts(self, r: "_Route") -> List[int]:
+        """The route's counts on the host.  A host sync only if the copy has not landed yet --
+        a route made by ``prefetch`` a step earlier has (stats["host_syncs"] counts the waits)."""
+        if r.event is not None:
+            if not r.event.query():
+                self.stats["host_syncs"] += 1
+                r.event.synchronize()
+            return r.host.tolist()
+        return r.counts.tolist()
+
+    def prefetch(self, ids: torch.Tensor) -> None:
+        """Route the NEXT batch's ids now (its device work and count exchange run ahead of this
+        step's compute), so the lookup of ``ids`` finds its split sizes already on the host.
+        Only useful at W > 1: at W = 1 the GPU lookup needs no counts at all."""
+        if self.world == 1 and self.gpu:
+            return
+        keys, nbad = self.keys_of(ids)
+        if len(self._pf) >= 4:  # stale prefetches (ids never looked up): drop the oldest
+            self._pf.pop(next(iter(self._pf)))
+        self._pf[self._ids_sig(ids)] = (keys, self._route(keys, nbad))
+
+    @staticmethod
+    def _ids_sig(ids: torch.Tensor):
+        return ids.data_ptr(), tuple(ids.shape), ids._version, ids.dtype
+
+    def check_ids(self) -> None:
+        """Raise if a sync-free (W = 1, GPU) lookup saw ids out of range since the last check."""
+        if self._nbad is not None:
+            nb = int(self._nbad.item())
+            self._nbad = None
+            if nb:
+                raise IndexError(f"{self.name}: {nb} ids out of range for id_mode={self.id_mode!r}")
 
     def _serve_keys(self, ukeys: torch.Tensor, send: List[int], recv: List[int]):
         """Ship unique keys to their owners; owners resolve slots.  -> (received keys, slots)"""
@@ -405,20 +460,41 @@ class ShardedSparseTable:
         self.t.all_to_all(back, rows.contiguous(), send, recv)
         return back
 
-    def _plan(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool = True):
+    def _plan(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool = True, route=None):
         with _trace.range(f"sparse.pull.{self.name}"):
-            return self._plan_impl(keys, nbad, fetch)
+            return self._plan_impl(keys, nbad, fetch, route)
 
-    def _plan_impl(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool):
+    def _plan_impl(self, keys: torch.Tensor, nbad: torch.Tensor, fetch: bool, route=None):
         self._wait_push()
-        n, nu, inv, perm, seg_off, send, recv, ukeys = self._route(keys, nbad)
+        r = route if route is not None else self._route(keys, nbad)
+        n = r.n
+        if self.world == 1 and self.gpu:
+            # sync-free: every buffer sized n (pad keys -1 -> slot -1 -> zero row, skipped by
+            # the optimizer), the id check deferred to check_ids / synchronize
+            self._nbad = r.nbad.clone() if self._nbad is None else self._nbad + r.nbad
+            nu, send, recv = n, [n], [n]
+            ukeys, seg_off = r.ubuf, r.seg_full
+            self._rows_dev = self._rows_dev + r.counts[0]
+        else:
+            h = self._counts(r)
+            W = self.world
+            if h[W]:
+                raise IndexError(f"{self.name}: {h[W]} ids out of range for id_mode={self.id_mode!r}")
+            send, recv = h[:W], h[W + 1:]
+            nu = sum(send)
+            ukeys, seg_off = r.ubuf[:nu], r.seg_full[:nu + 1]
+            self.stats["rows_pulled"] += nu
         rkeys, rslots = self._serve_keys(ukeys, send, recv)
         rows = None
         if fetch:
             rows = self._rows_back(self.shard.read(rslots, rkeys), nu, send, recv)
             self.stats["pulls"] += 1
-            self.stats["rows_pulled"] += nu
-        return _Plan(n, nu, inv, perm, seg_off, send, recv, rslots), rows
+        return _Plan(n, nu, r.inv, r.perm, seg_off, send, recv, rslots), rows
+
+    def _take_prefetch(self, ids: torch.Tensor):
+        if not self._pf:
+            return None
+        return self._pf.pop(self._ids_sig(ids), None)
 
     # ------------------------------------------------------------------ worker API
     def lookup(self, ids: torch.Tensor, out_dtype=None, grad_fn: Optional[Callable] = None) -> torch.Tensor:
@@ -426,8 +502,13 @@ class ShardedSparseTable:
         flows to the pulled rows; their gradient is pushed by ``push_pending`` (or by the
         leaf hook when ``overlap``).  ``grad_fn(grad_unique, plan)`` may rewrite the pushed
         gradient (reference gradient modes)."""
-        keys, nbad = self.keys_of(ids)
-        plan, rows = self._plan(keys, nbad)
+        pf = self._take_prefetch(ids)
+        if pf is not None:
+            keys, route = pf
+            plan, rows = self._plan(keys, route.nbad, route=route)
+        else:
+            keys, nbad = self.keys_of(ids)
+            plan, rows = self._plan(keys, nbad)
         want_grad = torch.is_grad_enabled()
         leaf = rows.detach().requires_grad_(want_grad)
         out = _sp.gather_unique(leaf, plan.inv, plan.perm, plan.seg_off, out_dtype)
@@ -471,7 +552,8 @@ class ShardedSparseTable:
         self._acc.append((plan.rslots, rg))
         plan.pushed = True
         self.stats["pushes"] += 1
-        self.stats["rows_pushed"] += plan.nu
+        if not (self.world == 1 and self.gpu):
+            self.stats["rows_pushed"] += plan.nu
 
     def _apply_acc(self, gscale: Optional[float] = None, average: Optional[bool] = None) -> None:
         if not self._acc:
@@ -552,6 +634,14 @@ class ShardedSparseTable:
     def synchronize(self) -> None:
         self._wait_push()
         self.shard.check()
+        self.check_ids()
+
+    def row_stats(self) -> dict:
+        """``stats`` with the sync-free path's device-side unique-row count read back (a sync)."""
+        d = dict(self.stats)
+        if self.world == 1 and self.gpu:
+            d["rows_pulled"] = int(self._rows_dev.item())
+        return d
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:

@@ -109,3 +109,37 @@ def test_sparse_table_gpu_matches_cpu(mode):
 
     for a, b in zip(run("cpu"), run(DEV)):
         torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["map", "direct"])
+def test_sparse_table_gpu_world1_is_host_sync_free(mode):
+    """W = 1 on the GPU: lookups / pushes never read a count back to the host (buffers sized by
+    the host-known n, pad keys -> slot -1), and the deferred id check still fires."""
+    from ps_amd.parallel.sparse_table import SparseTable
+    from ps_amd.parallel.updaters import AdagradUpdater
+
+    t = SparseTable("t", 16, [3000] * 4, AdagradUpdater(0.05, 1e-8, rowwise=True), init=(-0.1, 0.1),
+                    id_mode=mode, seed=5, device=DEV, fields=4)
+    g = torch.Generator().manual_seed(2)
+    for _ in range(5):
+        ids = torch.randint(0, 200, (128, 4), generator=g).to(DEV)  # heavy duplication
+        rows = t.lookup(ids)
+        (rows.float().pow(2).sum() * 0.01).backward()
+        t.push_pending()
+    assert t.stats["host_syncs"] == 0
+    t.synchronize()
+    st = t.row_stats()
+    assert 0 < st["rows_pulled"] <= 5 * 4 * 200
+    assert int(t.shard.status.item()) == 0  # pad keys never flag the hash map
+    if mode == "direct":
+        t.lookup(torch.full((4, 4), 5000, device=DEV))  # out of range: deferred, raised at the check
+        with pytest.raises(IndexError):
+            t.synchronize()
+
+
+def test_hash_slots_pad_keys_are_silent():
+    hk = torch.full((256,), -1, dtype=torch.int64, device=DEV)
+    st = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = S.hash_slots(hk, torch.tensor([-1, 5, -1, 7], device=DEV), True, st).cpu()
+    assert s[0].item() == -1 and s[2].item() == -1 and (s[[1, 3]] >= 0).all()
+    assert int(st.item()) == 0

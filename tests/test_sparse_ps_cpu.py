@@ -232,3 +232,36 @@ def test_lazy_init_fields_with_same_id_get_independent_rows():
     for i in range(len(keys)):
         for j in range(i + 1, len(keys)):
             assert not torch.allclose(rows[i], rows[j])
+
+
+def _prefetch_body(tp, use_prefetch):
+    from ps_amd.parallel.sparse_table import ShardedSparseTable
+    from ps_amd.parallel.updaters import AdagradUpdater
+
+    t = ShardedSparseTable("emb", 8, [500] * 3, tp, AdagradUpdater(0.05, 1e-8, rowwise=True), init=(-0.1, 0.1),
+                           seed=4, fields=3)
+    g = torch.Generator().manual_seed(10 + tp.rank)
+    batches = [torch.randint(0, 500, (32, 3), generator=g) for _ in range(5)]
+    outs = []
+    if use_prefetch:
+        t.prefetch(batches[0])
+    for i, ids in enumerate(batches):
+        if use_prefetch and i + 1 < len(batches):
+            t.prefetch(batches[i + 1])  # routed a step ahead (counts exchanged now)
+        rows = t.lookup(ids)
+        (rows.pow(2).sum() * 0.01).backward()
+        t.push_pending()
+        outs.append(rows.detach().clone())
+    t.synchronize()
+    left = len(t._pf)
+    return outs, t.pull(torch.arange(500).repeat(3, 1).t().contiguous()), left
+
+
+def test_prefetched_routing_matches_inline_routing_gloo_world2():
+    a = dist_util.run(_prefetch_body, 2, (False,))
+    b = dist_util.run(_prefetch_body, 2, (True,))
+    for (oa, ta, _), (ob, tb, left) in zip(a, b):
+        assert left == 0  # every prefetched route was consumed by its lookup
+        for x, y in zip(oa, ob):
+            assert torch.equal(x, y)
+        assert torch.equal(ta, tb)
