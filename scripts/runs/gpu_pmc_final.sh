@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM bytes per kernel over ResNet-50 steps (FETCH_SIZE / WRITE_SIZE passes, kernel-trace only) +
 # a clean kernel trace for durations -> gpurun_out/pmcstep/summary.txt
-bash scripts/gpu_pmc_step.sh || exit $?
+bash scripts/runs/gpu_pmc_step.sh || exit $?
 R=$PWD
 mkdir -p gpurun_out/pmcstep/clean
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/pmcstep/clean -o run --output-format csv -- python3 $R/bench.py --steps 6 --warmup 2 > $R/gpurun_out/pmcstep/clean.log 2>&1 || exit $?
