@@ -61,7 +61,7 @@ def parse():
                     help="MIOpen find (exhaustive) for each conv shape during warm-up")
     ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
                     help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
-                         "ResNet-50: 32.7 vs 31.6 ms, profiles/r1_graph_vs_eager.txt)")
+                         "ResNet-50: 32.7 vs 31.6 ms, profiles/archive/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--comm-probe", type=int, default=1,

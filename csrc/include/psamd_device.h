@@ -121,8 +121,10 @@ __host__ inline int stream_grid(int64_t work_items, int block) {
 struct Philox {
   __device__ __forceinline__ static void round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-    uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
-    uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    // one 32x32->64 multiply (v_mad_u64_u32) per product instead of separate hi / lo multiplies
+    const uint64_t p0 = static_cast<uint64_t>(M0) * c[0], p1 = static_cast<uint64_t>(M1) * c[2];
+    const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32), lo0 = static_cast<uint32_t>(p0);
+    const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32), lo1 = static_cast<uint32_t>(p1);
     uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
     c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
   }

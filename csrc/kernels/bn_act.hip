@@ -1,7 +1,7 @@
 // Fused BatchNorm (+ residual add) + activation for NHWC (channels_last) activations.
 //
 // ResNet-50 under MIOpen spends ~37 % of its step in BatchNorm and another ~17 % in the
-// separate ReLU / residual-add / ReLU-backward passes (profiles/r1_resnet50_ps_kernel_breakdown.txt).
+// separate ReLU / residual-add / ReLU-backward passes (profiles/archive/r1_resnet50_ps_kernel_breakdown.txt).
 // All of them are HBM-bound, so the lever is passes over memory:
 //
 //   forward   MIOpen: stats(read x) + norm(read x, write z) + [add(read z,r write s)] + relu(read, write)
@@ -60,7 +60,7 @@ int bn_red_blocks(int64_t R, int C) {
 
 // Elementwise BN passes: ~2 vectors per thread (one trip of the 2-vector loop), not a
 // 2048-block grid-stride sweep -- the short-lived waves keep more loads in flight per CU
-// (stage-1 block output + residual + bits: 519 -> 436 us, profiles/r1_stream_probe.jsonl).
+// (stage-1 block output + residual + bits: 519 -> 436 us, profiles/archive/r1_stream_probe.jsonl).
 inline int apply_grid(int64_t nvec) {
   int64_t g = (nvec + 511) / 512;
   if (g < 1) g = 1;

@@ -1,5 +1,5 @@
 """1x1 stride-1 convolution on channels_last bf16 activations, routed per direction to the
-faster backend measured on MI355X (scripts/probe_convs.py, profiles/r1_conv_probe_b512.jsonl).
+faster backend measured on MI355X (scripts/probe_convs.py, profiles/archive/r1_conv_probe_b512.jsonl).
 
 A 1x1 conv over NHWC is a plain GEMM on the [N*H*W, C] view.  At ResNet-50 shapes (batch
 512) hipBLASLt beats MIOpen's solvers for the forward when C_in >= 1024 (e.g. 14x14

@@ -5,7 +5,7 @@ MIOpen's find for every convolution shape), the step -- every forward/backward k
 bucket hooks' comm-stream work and the fused optimizer kernels -- is captured once with
 ``torch.cuda.graph`` and replayed with a single launch per step.  This removes the CPU
 launch gaps that otherwise leave the GPU idle in the short-kernel tail of backward
-(measured: ~9 % idle per ResNet-50 step, profiles/r1_*).
+(measured: ~9 % idle per ResNet-50 step, profiles/archive/r1_*).
 
 Graph-safety rules the PS engine follows (parallel/colocated.py): static input/output
 tensors, no host synchronisation inside the step, buffer bindings that do not change
