@@ -14,7 +14,9 @@
 // Tiles: 256 threads = 4 waves, C tile 64x64, reduction 32 per stage, each wave a 32x32 quarter
 // = 2x2 16x16 MFMA tiles; bf16 operands use v_mfma_f32_16x16x32_bf16 (one 16-B LDS read per
 // operand per MFMA), fp32 operands v_mfma_f32_16x16x4_f32 (fp32 end to end for the
-// reference-parity fp32 models).  Next stage's global loads are issued before the MFMAs.
+// reference-parity fp32 models).  Operand pieces move as 16-B vector loads (8 contiguous
+// elements per thread, in either staging layout) into registers one stage ahead, and land in a
+// double-buffered LDS tile after the current stage's MFMAs (one barrier per stage).
 // Activation codes as dense.hip: 0 none, 1 relu, 2 leaky 0.01, 3 reference clipped sigmoid
 // (backward dy * y * (1 - y) on the clipped output, Sigmoid.java).
 #include "psamd_device.h"
@@ -54,45 +56,70 @@ __device__ __forceinline__ void lds_put<uint16_t>(uint16_t* lds, int row, int co
   lds[row * (kR + kPad) + col] = f32_to_bf16(v);
 }
 
-// Stage one 64 x 32 operand tile of C-rows [r0, r0+64) x reduction [k0, k0+32) into LDS as
-// lds[row][k].  TRANS: element (row, k) lives at src[k * ld + row] (reduction = slow index);
-// else at src[row * ld + k].  With ACT >= 0, the value is act'(y) * src (y laid out like src)
-// and -- DB -- the per-row sums of that value are accumulated into dbacc (TRANS layout only).
-template <typename T, bool TRANS, bool GRAD, bool DB>
-__device__ __forceinline__ void stage(const T* __restrict__ src, const T* __restrict__ y, int64_t ld, int rows,
-                                      int kdim, int r0, int k0, int act, T* lds, float (&dbacc)[8]) {
-  const int t = threadIdx.x;
-  if constexpr (TRANS) {
-    const int k = t >> 3, rc = (t & 7) * 8;  // 32 reduction rows x 8 chunks of 8 C-rows
-    const int gk = k0 + k;
+// One thread's share of a 64 x 32 operand stage: 8 consecutive elements of ONE memory row -- 8
+// reduction elements of one C-row (k contiguous) or, TRANS (element (row, k) at src[k * ld +
+// row]), 8 C-rows of one reduction row.  Either way they are contiguous in memory, so an aligned
+// in-range piece is one 16-B load (bf16) or two (fp32); tails and odd strides go element-wise.
+// GRAD also loads y at the same offsets for the act' prologue.
+template <typename T>
+__device__ __forceinline__ void load8(const T* __restrict__ p, int64_t o, int nvalid, bool vec, float (&v)[8]) {
+  if (vec) {
+    if constexpr (sizeof(T) == 2) {
+      const u16x8 q = *reinterpret_cast<const u16x8*>(p + o);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = r0 + rc + j;
-      float v = 0.f;
-      if (gk < kdim && row < rows) {
-        const int64_t o = static_cast<int64_t>(gk) * ld + row;
-        v = Ld<T>::get(src, o);
-        if constexpr (GRAD) v = act_grad(v, Ld<T>::get(y, o), act);
-      }
-      if constexpr (DB) dbacc[j] += v;
-      lds_put<T>(lds, rc + j, k, v);
+      for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(q[j]);
+    } else {
+      const f32x4v a = *reinterpret_cast<const f32x4v*>(p + o), b = *reinterpret_cast<const f32x4v*>(p + o + 4);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+      v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
     }
   } else {
-    const int row = t >> 2, kc = (t & 3) * 8;  // 64 C-rows x 4 chunks of 8 reduction elements
-    const int grow = r0 + row;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int gk = k0 + kc + j;
-      float v = 0.f;
-      if (grow < rows && gk < kdim) {
-        const int64_t o = static_cast<int64_t>(grow) * ld + gk;
-        v = Ld<T>::get(src, o);
-        if constexpr (GRAD) v = act_grad(v, Ld<T>::get(y, o), act);
-      }
-      lds_put<T>(lds, row, kc + j, v);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = j < nvalid ? Ld<T>::get(p, o + j) : 0.f;
   }
 }
+
+template <typename T, bool TRANS, bool GRAD>
+struct StageRegs8 {
+  float v[8];
+  float y[GRAD ? 8 : 1];
+  // global -> registers (issued a stage ahead of its use)
+  __device__ __forceinline__ void load(const T* __restrict__ src, const T* __restrict__ ysrc, int64_t ld, int rows,
+                                       int kdim, int r0, int k0) {
+    const int t = threadIdx.x;
+    int64_t o;
+    int nvalid;
+    if constexpr (TRANS) {
+      const int gk = k0 + (t >> 3), row = r0 + (t & 7) * 8;  // 32 reduction rows x 8 chunks of 8 C-rows
+      nvalid = gk < kdim ? min(8, rows - row) : 0;
+      o = static_cast<int64_t>(gk) * ld + row;
+    } else {
+      const int grow = r0 + (t >> 2), gk = k0 + (t & 3) * 8;  // 64 C-rows x 4 chunks of 8 reduction elements
+      nvalid = grow < rows ? min(8, kdim - gk) : 0;
+      o = static_cast<int64_t>(grow) * ld + gk;
+    }
+    nvalid = nvalid < 0 ? 0 : nvalid;
+    const bool vec = nvalid == 8 && (o & (16 / sizeof(T) - 1)) == 0;
+    load8<T>(src, o, nvalid, vec, v);
+    if constexpr (GRAD) load8<T>(ysrc, o, nvalid, vec, y);
+  }
+  // registers -> LDS (lds[row][k]); act' applied, bias-gradient partials accumulated (DB)
+  template <bool DB>
+  __device__ __forceinline__ void store(T* lds, int act, float (&dbacc)[8]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = v[j];
+      if constexpr (GRAD) x = act_grad(x, y[j], act);
+      if constexpr (TRANS) {
+        if constexpr (DB) dbacc[j] += x;
+        lds_put<T>(lds, (t & 7) * 8 + j, t >> 3, x);
+      } else {
+        lds_put<T>(lds, t >> 2, (t & 3) * 8 + j, x);
+      }
+    }
+  }
+};
 
 template <typename T>
 __device__ __forceinline__ void mma_stage(const T* la, const T* lb, int wm, int wn, int lane, f32x4v (&acc)[2][2]);
@@ -139,7 +166,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const T* __restrict__ a, co
                                                      const T* __restrict__ b, int64_t ldb, T* __restrict__ c,
                                                      int64_t ldc, float* __restrict__ dbias, int R, int Cc, int K,
                                                      int act) {
-  __shared__ __attribute__((aligned(16))) T lds[2][kT * (kR + kPad)];
+  __shared__ __attribute__((aligned(16))) T lds[2][2][kT * (kR + kPad)];  // [buffer][operand]
   __shared__ float dbl[256][9];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
@@ -151,15 +178,24 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const T* __restrict__ a, co
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
   float dbacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // register-staged double buffer: stage q + 1's global loads are in flight during stage q's
+  // MFMAs, written to the idle LDS buffer after them -- one barrier per stage
+  StageRegs8<T, TA, true> ra;
+  StageRegs8<T, TB, false> rb;
+  ra.load(a, ay, lda, R, K, r0, 0);
+  rb.load(b, nullptr, ldb, Cc, K, c0, 0);
+  int buf = 0;
   for (int k0 = 0; k0 < K; k0 += kR) {
-    if (db_here)
-      stage<T, TA, true, TA>(a, ay, lda, R, K, r0, k0, act, lds[0], dbacc);
-    else
-      stage<T, TA, true, false>(a, ay, lda, R, K, r0, k0, act, lds[0], dbacc);
-    stage<T, TB, false, false>(b, nullptr, ldb, Cc, K, c0, k0, 0, lds[1], dbacc);
+    if (db_here) ra.template store<TA>(lds[buf][0], act, dbacc);
+    else ra.template store<false>(lds[buf][0], act, dbacc);
+    rb.template store<false>(lds[buf][1], 0, dbacc);
     __syncthreads();
-    mma_stage<T>(lds[0], lds[1], wm, wn, lane, acc);
-    __syncthreads();
+    if (k0 + kR < K) {
+      ra.load(a, ay, lda, R, K, r0, k0 + kR);
+      rb.load(b, nullptr, ldb, Cc, K, c0, k0 + kR);
+    }
+    mma_stage<T>(lds[buf][0], lds[buf][1], wm, wn, lane, acc);
+    buf ^= 1;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -219,7 +255,7 @@ void launch_fc(const void* dy, const void* y, const void* x, const void* w, void
 __global__ __launch_bounds__(256) void fc_fwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias, float* __restrict__ y, int M,
                                                           int N, int K, int act) {
-  __shared__ __attribute__((aligned(16))) float lds[2][kT * (kR + kPad)];
+  __shared__ __attribute__((aligned(16))) float lds[2][2][kT * (kR + kPad)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   const int r0 = blockIdx.y * kT, c0 = blockIdx.x * kT;
@@ -229,12 +265,20 @@ __global__ __launch_bounds__(256) void fc_fwd_f32_kernel(const float* __restrict
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
   float unused[8];
+  StageRegs8<float, false, false> ra, rb;
+  ra.load(x, nullptr, K, M, K, r0, 0);
+  rb.load(w, nullptr, K, N, K, c0, 0);
+  int buf = 0;
   for (int k0 = 0; k0 < K; k0 += kR) {
-    stage<float, false, false, false>(x, nullptr, K, M, K, r0, k0, 0, lds[0], unused);
-    stage<float, false, false, false>(w, nullptr, K, N, K, c0, k0, 0, lds[1], unused);
+    ra.template store<false>(lds[buf][0], 0, unused);
+    rb.template store<false>(lds[buf][1], 0, unused);
     __syncthreads();
-    mma_stage<float>(lds[0], lds[1], wm, wn, lane, acc);
-    __syncthreads();
+    if (k0 + kR < K) {
+      ra.load(x, nullptr, K, M, K, r0, k0 + kR);
+      rb.load(w, nullptr, K, N, K, c0, k0 + kR);
+    }
+    mma_stage<float>(lds[buf][0], lds[buf][1], wm, wn, lane, acc);
+    buf ^= 1;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)

@@ -1,5 +1,5 @@
 // ThreadSanitizer stress of the asynchronous-PS control protocol (csrc/include/async_ctl.h):
-// W owner threads run serve_loop, W worker threads push into 1-deep mailboxes, bump clocks, and
+// W owner threads run serve_loop, W worker threads push into kMbox-deep mailboxes, bump clocks, and
 // pin / copy / unpin published slots under an SSP(s) gate.  The "GPU" is plain host memory
 // here, written and read with ordinary loads/stores, so TSan checks that the acquire/release
 // hand-offs order every mailbox and slot access (a missing fence is a reported data race).
@@ -26,8 +26,8 @@ int main(int argc, char** argv) {
   const int L = 64;  // shard length
   AsyncCtl* c = new AsyncCtl;
   init(c, W);
-  // per owner: W mailboxes of L floats, 3 slots of L floats + a version stamp per slot
-  std::vector<std::vector<float>> mbox(W * W, std::vector<float>(L, 0.f));
+  // per owner: W x kMbox mailboxes of L floats, 3 slots of L floats + a version stamp per slot
+  std::vector<std::vector<float>> mbox(W * W * kMbox, std::vector<float>(L, 0.f));
   std::vector<std::vector<float>> slot(W * kSlots, std::vector<float>(L, 0.f));
   std::vector<int64_t> stamp(W * kSlots, 0);
   std::vector<float> master(W * L, 0.f);
@@ -36,8 +36,8 @@ int main(int argc, char** argv) {
   std::vector<std::thread> th;
   for (int o = 0; o < W; ++o)
     th.emplace_back([&, o] {
-      serve_loop(c, o, &stop, [&](int w, int sl, int64_t step) {
-        for (int i = 0; i < L; ++i) master[o * L + i] += mbox[o * W + w][i];
+      serve_loop(c, o, &stop, [&](int w, int ms, int sl, int64_t step) {
+        for (int i = 0; i < L; ++i) master[o * L + i] += mbox[(o * W + w) * kMbox + ms][i];
         for (int i = 0; i < L; ++i) slot[o * kSlots + sl][i] = master[o * L + i];
         stamp[o * kSlots + sl] = step;
         applied[o] += 1;
@@ -51,8 +51,9 @@ int main(int argc, char** argv) {
       for (int t = 0; t < steps; ++t) {
         for (int o = 0; o < W; ++o) {
           Backoff bo;
-          while (ld(&c->ack[o][w]) < ld(&c->seq[o][w])) bo();
-          for (int i = 0; i < L; ++i) mbox[o * W + w][i] = 1.f;  // gradient of 1 per element
+          const int64_t k = ld(&c->seq[o][w]);  // this worker's push number (only it bumps seq)
+          while (ld(&c->ack[o][w]) + kMbox <= k) bo();  // mailbox slot k % kMbox still unapplied
+          for (int i = 0; i < L; ++i) mbox[(o * W + w) * kMbox + k % kMbox][i] = 1.f;  // gradient of 1
           add(&c->seq[o][w], 1);
         }
         const int64_t clk = add(&c->clock[w], 1);

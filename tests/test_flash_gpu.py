@@ -25,7 +25,7 @@ def _ref(q, k, v):
     return o.transpose(1, 2).reshape(B, S, H * D), lse
 
 
-@pytest.mark.parametrize("B,H,KV,S", [(1, 4, 1, 128), (2, 4, 2, 256), (1, 8, 2, 384), (1, 8, 2, 2048)])
+@pytest.mark.parametrize("B,H,KV,S", [(1, 4, 1, 128), (2, 4, 2, 256), (1, 8, 2, 384), (1, 8, 2, 2048), (1, 4, 1, 4096)])
 def test_flash_causal_gqa(B, H, KV, S):
     g = torch.Generator().manual_seed(B * 100 + H * 10 + S)
     q = torch.randn(B, H, S, 128, generator=g).bfloat16().to(DEV)
