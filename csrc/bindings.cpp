@@ -360,9 +360,14 @@ void fc_bwd(Tensor dy, Tensor y, Tensor x, Tensor w, c10::optional<Tensor> dw, c
     pdx = dx->data_ptr();
   }
   const c10::DeviceGuard guard(dy.device());
+  const int64_t nws = pdw != nullptr ? psamd::fc_bwd_ws_floats(static_cast<int>(M), static_cast<int>(N),
+                                                               static_cast<int>(K))
+                                     : 0;
+  Tensor ws;  // split-reduction dW slabs (stream-ordered caching allocator: freed after the launch)
+  if (nws > 0) ws = torch::empty({nws}, dy.options().dtype(torch::kFloat32));
   psamd::launch_fc_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), w.data_ptr(), pdw, pdb, pdx, code,
                        static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(act),
-                       cur_stream(dy));
+                       nws > 0 ? ws.data_ptr<float>() : nullptr, cur_stream(dy));
 }
 
 void fc_fwd_f32(Tensor x, Tensor w, c10::optional<Tensor> b, Tensor y, int64_t act) {

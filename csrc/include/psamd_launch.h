@@ -127,7 +127,9 @@ void launch_hash_slots(int64_t* hkeys, int64_t capacity, const int64_t* ids, int
 // fused FC backward: dW = (act'(y) * dy)^T x (+ db = column sums), dX = (act'(y) * dy) W;
 // dtype 0 fp32 / 1 bf16 for every operand; dw / db / dx nullable
 void launch_fc_bwd(const void* dy, const void* y, const void* x, const void* w, void* dw, float* db, void* dx,
-                   int dtype, int M, int N, int K, int act, hipStream_t s);
+                   int dtype, int M, int N, int K, int act, float* ws, hipStream_t s);
+// fp32 workspace (floats) of the split-reduction dW path, 0 = unsplit
+int64_t fc_bwd_ws_floats(int M, int N, int K);
 void launch_fc_fwd_f32(const float* x, const float* w, const float* b, float* y, int M, int N, int K, int act,
                        hipStream_t s);
 
