@@ -53,6 +53,22 @@ __device__ __forceinline__ void store_t(const f32x16 (&acc)[4], uint16_t* row, f
 }
 
 // ------------------------------------------------------------------------------ forward
+// XCD-aware 1-D block order.  The hardware deals consecutive block ids round-robin over the 8
+// XCDs, each with its own L2; a "unit" is every block that reads one (batch, KV head)'s K / V
+// (forward, dQ) or Q / dO (dK / dV), so each XCD is given whole units -- block L runs on XCD
+// L mod 8 and takes the (L / 8) mod per -th item of unit (L mod 8) + 8 ((L / 8) / per).  Needs
+// units % 8 == 0 (else plain order).  Items run heaviest first within a unit.
+__device__ __forceinline__ void xcd_unit(int L, int per, int units, int& unit, int& r) {
+  if ((units & 7) == 0) {
+    const int x = L & 7, j = L >> 3;
+    unit = x + 8 * (j / per);
+    r = j % per;
+  } else {
+    unit = L / per;
+    r = L % per;
+  }
+}
+
 // S^T for one 64-key block from the LDS tile (asm reads: a DMA into the other buffer is in flight)
 __device__ __forceinline__ void st_block(const uint16_t* Ks, const bf16x8_t (&qf)[8], int c, int hl, f32x16 (&st)[2]) {
   zero(st[0]);
@@ -113,7 +129,10 @@ __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restr
   static_assert(CH >= 1 && kBK * 16 % NT == 0, "tile / block shape");
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kBK * kD];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kBK * kD];
-  const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z, kvh = h / (H / KV);
+  const int G = H / KV, nqb = S / BQ;
+  int unit, rr;
+  xcd_unit(blockIdx.x, G * nqb, static_cast<int>(gridDim.x) / (G * nqb), unit, rr);
+  const int b = unit / KV, kvh = unit % KV, qb = nqb - 1 - rr / G, h = kvh * G + rr % G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const uint16_t* qp = q + static_cast<int64_t>(b * H + h) * S * kD;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
@@ -230,7 +249,10 @@ __global__ __launch_bounds__(NW * 64) void fa_bwd_dq_kernel(const uint16_t* __re
   static_assert(CH >= 1 && kBK * 16 % NT == 0, "tile / block shape");
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][kBK * kD];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[2][kBK * kD];
-  const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z, kvh = h / (H / KV);
+  const int G = H / KV, nqb = S / BQ;
+  int unit, rr;
+  xcd_unit(blockIdx.x, G * nqb, static_cast<int>(gridDim.x) / (G * nqb), unit, rr);
+  const int b = unit / KV, kvh = unit % KV, qb = nqb - 1 - rr / G, h = kvh * G + rr % G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const uint16_t* qp = q + static_cast<int64_t>(b * H + h) * S * kD;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
@@ -350,7 +372,10 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __rest
   __shared__ __attribute__((aligned(16))) uint16_t dOs[2][kBQS * kD];
   __shared__ __attribute__((aligned(16))) float Ls[2][kBQS];
   __shared__ __attribute__((aligned(16))) float Ds[2][kBQS];
-  const int kblk = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z, G = H / KV;
+  const int G = H / KV, nkb = S / kBQ;
+  int unit, kblk;
+  xcd_unit(blockIdx.x, nkb, static_cast<int>(gridDim.x) / nkb, unit, kblk);
+  const int b = unit / KV, kvh = unit % KV;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const uint16_t* kp = k + static_cast<int64_t>(b * KV + kvh) * S * kD;
   const uint16_t* vp = v + static_cast<int64_t>(b * KV + kvh) * S * kD;
@@ -476,21 +501,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __rest
 void launch_fa_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, float* lse, int B, int S,
                    int H, int KV, float scale, hipStream_t s) {
   if (S % 256 == 0)
-    hipLaunchKernelGGL(fa_fwd_kernel<8>, dim3(S / 256, H, B), dim3(512), 0, s, q, k, v, out, lse, S, H, KV, scale);
+    hipLaunchKernelGGL(fa_fwd_kernel<8>, dim3(S / 256 * H * B), dim3(512), 0, s, q, k, v, out, lse, S, H, KV, scale);
   else
-    hipLaunchKernelGGL(fa_fwd_kernel<4>, dim3(S / kBQ, H, B), dim3(256), 0, s, q, k, v, out, lse, S, H, KV, scale);
+    hipLaunchKernelGGL(fa_fwd_kernel<4>, dim3(S / kBQ * H * B), dim3(256), 0, s, q, k, v, out, lse, S, H, KV, scale);
 }
 
 void launch_fa_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* out, const uint16_t* dout,
                    const float* lse, float* dsum, uint16_t* dq, uint16_t* dk, uint16_t* dv, int B, int S, int H,
                    int KV, float scale, hipStream_t s) {
   if (S % 256 == 0)
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<8>, dim3(S / 256, H, B), dim3(512), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<8>, dim3(S / 256 * H * B), dim3(512), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
                        H, KV, scale);
   else
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<4>, dim3(S / kBQ, H, B), dim3(256), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<4>, dim3(S / kBQ * H * B), dim3(256), 0, s, q, k, v, out, dout, lse, dsum, dq, S,
                        H, KV, scale);
-  hipLaunchKernelGGL(fa_bwd_dkdv_kernel, dim3(S / kBQ, KV, B), dim3(256), 0, s, q, k, v, dout, lse, dsum, dk, dv, S,
+  hipLaunchKernelGGL(fa_bwd_dkdv_kernel, dim3(S / kBQ * KV * B), dim3(256), 0, s, q, k, v, dout, lse, dsum, dk, dv, S,
                      H, KV, scale);
 }
 

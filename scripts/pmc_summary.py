@@ -13,7 +13,7 @@ from collections import defaultdict
 
 def short(name: str) -> str:
     if "psamd::" in name:
-        return name.replace("void ", "").split("(")[0][:120]
+        return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:120]
     return name[:60]
 
 
