@@ -807,7 +807,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int TN, int TK, int WN, int WK, bool PRO, bool DB = false>
+template <int TN, int TK, int WN, int WK, bool PRO, bool DB = false, bool LIN = false>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgradArgs p, int rows_per_split) {
   constexpr int BNO = WN * 32 * TN, BKO = WK * 32 * TK;
   static_assert(WN * WK == 8, "8 waves");
@@ -846,23 +846,41 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
     xkh[i] = tap / g.ks;
     xkw[i] = tap - xkh[i] * g.ks;
   }
+  // Loop-invariant per-lane parts of the DMA sources; a stage adds its (block-uniform, scalar)
+  // row base.  1x1 stride-1 pad-0 geometry (every linear layer, most ResNet 1x1 layers): X row m is
+  // pixel m, so a source is one 64-bit add -- the general path's two divisions and bounds tests per
+  // instruction per stage had made the kernel VALU-bound (~14 VALU per MFMA).
+  int64_t goff[GI], xoff[XI];
+#pragma unroll
+  for (int i = 0; i < GI; ++i) goff[i] = static_cast<int64_t>(grow[i]) * p.N + gcol[i];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) xoff[i] = static_cast<int64_t>(xrow[i]) * g.C + xcc[i];
   auto issue = [&](int st, int buf) {
     const int mc = mb + st * kWP;
     uint16_t* Gs = lds + buf * STAGE;
     uint16_t* Xs = Gs + kWP * BNO;
+    const uint16_t* gb = p.dz + static_cast<int64_t>(mc) * p.N;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int m = mc + grow[i];
-      const uint16_t* src = m < me ? p.dz + static_cast<int64_t>(m) * p.N + gcol[i] : kZeroPage;
+      const uint16_t* src = mc + grow[i] < me ? gb + goff[i] : kZeroPage;
       __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Gs + (wave * GI + i) * 512), 16, 0, 0);
     }
+    if constexpr (LIN) {
+      const uint16_t* xb = p.x + static_cast<int64_t>(mc) * g.C;
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int m = mc + xrow[i];
-      const PixSrc ps = pix_src(m < me ? m : p.M, p.M, g);
-      const int64_t o = tap_off(ps, xkh[i], xkw[i], xcc[i], g);
-      const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
-      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
+      for (int i = 0; i < XI; ++i) {
+        const uint16_t* src = mc + xrow[i] < me ? xb + xoff[i] : kZeroPage;
+        __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int m = mc + xrow[i];
+        const PixSrc ps = pix_src(m < me ? m : p.M, p.M, g);
+        const int64_t o = tap_off(ps, xkh[i], xkw[i], xcc[i], g);
+        const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
+        __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
+      }
     }
   };
 
@@ -1172,12 +1190,17 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const WPlan w = wplan(a.M, a.N, a.K, a.g.C, a.pro != nullptr);
   const int nblk = w.tiles * w.nsplit;
-#define PSAMD_CWW(TN, TK, WN, WK)                                                                                   \
-  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true>), dim3(nblk), dim3(512), 0, s, a,   \
-                                w.rows);                                                                          \
-  else if (a.db) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, true>), dim3(nblk), dim3(512), \
-                                    0, s, a, w.rows);                                                             \
-  else hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false>), dim3(nblk), dim3(512), 0, s, a, w.rows)
+  // LIN: 1x1 stride-1 pad-0 geometry (X row m = pixel m), DMA sources without the pixel decode
+  const bool lin = a.g.ks == 1 && a.g.stride == 1 && a.g.pad == 0;
+#define PSAMD_CWW3(TN, TK, WN, WK, L)                                                                             \
+  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true, false, L>), dim3(nblk), dim3(512), \
+                                0, s, a, w.rows);                                                               \
+  else if (a.db) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, true, L>), dim3(nblk),        \
+                                    dim3(512), 0, s, a, w.rows);                                                \
+  else hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, false, L>), dim3(nblk), dim3(512), 0, s, \
+                          a, w.rows)
+#define PSAMD_CWW(TN, TK, WN, WK) \
+  if (lin) { PSAMD_CWW3(TN, TK, WN, WK, true); } else { PSAMD_CWW3(TN, TK, WN, WK, false); }
 #define PSAMD_CW(TN, TK, PRO, GL) \
   hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, PRO, GL>), dim3(nblk), dim3(256), 0, s, a, w.rows)
   // without the prologue both operands are plain row slices: LDS-DMA staging
@@ -1197,6 +1220,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
     if (w.tko == 2) { PSAMD_CWP(1, 2) } else { PSAMD_CWP(1, 1) }
   }
 #undef PSAMD_CWW
+#undef PSAMD_CWW3
 #undef PSAMD_CWP
 #undef PSAMD_CW
   if (w.wide && a.db != nullptr && a.pro == nullptr)  // bias gradient: fold the per-split column sums
