@@ -1,4 +1,5 @@
-"""Causal GQA flash attention (csrc/kernels/flash_attn.hip) vs a plain-torch fp32 reference:
+"""Causal GQA flash attention (csrc/kernels/flash_attn.hip) vs a plain-torch fp32 reference (B * KV a
+multiple of 8 takes the XCD-aware block order, other shapes the plain one):
 output, log-sum-exp, dq / dk / dv (the GQA dk / dv sum over the q heads of each KV group)."""
 import pytest
 import torch
@@ -25,7 +26,7 @@ def _ref(q, k, v):
     return o.transpose(1, 2).reshape(B, S, H * D), lse
 
 
-@pytest.mark.parametrize("B,H,KV,S", [(1, 4, 1, 128), (2, 4, 2, 256), (1, 8, 2, 384), (1, 8, 2, 2048), (1, 4, 1, 4096)])
+@pytest.mark.parametrize("B,H,KV,S", [(1, 4, 1, 128), (2, 4, 2, 256), (1, 8, 2, 384), (1, 8, 2, 2048), (1, 4, 1, 4096), (1, 16, 8, 256), (2, 8, 8, 512)])
 def test_flash_causal_gqa(B, H, KV, S):
     g = torch.Generator().manual_seed(B * 100 + H * 10 + S)
     q = torch.randn(B, H, S, 128, generator=g).bfloat16().to(DEV)
