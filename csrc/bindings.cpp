@@ -726,6 +726,36 @@ static void check_fa(const Tensor& q, const Tensor& k, const Tensor& v) {
   TORCH_CHECK(q.size(2) % 128 == 0 && q.size(2) > 0, "sequence length a multiple of 128");
 }
 
+// fused cross-entropy over bf16 logits [R, V] with int64 labels (ignore_index rows contribute 0)
+std::vector<Tensor> xent_fwd(Tensor x, Tensor lab, int64_t ignore) {
+  check_gpu(x, "x");
+  check_gpu(lab, "labels");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == torch::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 [R, V]");
+  TORCH_CHECK(lab.scalar_type() == torch::kInt64 && lab.numel() == x.size(0) && lab.is_contiguous(), "labels [R] int64");
+  TORCH_CHECK(x.size(1) < (int64_t(1) << 31), "vocab");
+  const c10::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(torch::kFloat32);
+  auto lse = torch::empty({x.size(0)}, fopt), loss = torch::empty({x.size(0)}, fopt);
+  psamd::launch_xent_fwd(u16(x), lab.data_ptr<int64_t>(), x.size(0), static_cast<int>(x.size(1)), ignore,
+                         lse.data_ptr<float>(), loss.data_ptr<float>(), cur_stream(x));
+  return {lse, loss};
+}
+
+Tensor xent_bwd(Tensor x, Tensor lab, Tensor lse, Tensor go, Tensor count, int64_t ignore) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == torch::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 [R, V]");
+  TORCH_CHECK(lab.scalar_type() == torch::kInt64 && lab.numel() == x.size(0), "labels [R] int64");
+  check_f32(lse, "lse");
+  check_f32(go, "go");
+  check_f32(count, "count");
+  TORCH_CHECK(lse.numel() == x.size(0) && go.numel() == 1 && count.numel() == 1, "lse [R], go / count scalars");
+  const c10::DeviceGuard guard(x.device());
+  auto dx = torch::empty_like(x);
+  psamd::launch_xent_bwd(u16(x), lab.data_ptr<int64_t>(), lse.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)),
+                         ignore, go.data_ptr<float>(), count.data_ptr<float>(), u16m(dx), cur_stream(x));
+  return dx;
+}
+
 std::vector<Tensor> fa_fwd(Tensor q, Tensor k, Tensor v) {
   check_fa(q, k, v);
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
@@ -1406,6 +1436,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("xent_fwd", &xent_fwd, py::arg("x"), py::arg("labels"), py::arg("ignore_index"));
+  m.def("xent_bwd", &xent_bwd, py::arg("x"), py::arg("labels"), py::arg("lse"), py::arg("go"), py::arg("count"),
+        py::arg("ignore_index"));
   m.def("fa_fwd", &fa_fwd);
   m.def("fa_bwd", &fa_bwd);
   m.def("attn_bwd", &attn_bwd);

@@ -319,6 +319,12 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
 void launch_attn_dropout_mask(uint8_t* mask, int64_t n, float p, uint64_t seed, hipStream_t s);
 // Causal GQA flash attention (flash_attn.hip): q [B, H, S, 128], k / v [B, KV, S, 128] bf16,
 // out [B, S, H * 128], lse / dsum [B, H, S] fp32; S % 128 == 0
+// Fused softmax cross-entropy over bf16 logits [R, V] (xent.hip): forward lse / per-row loss,
+// backward dx = (softmax - onehot) * go / count (go, count: device scalars); ignored rows -> 0
+void launch_xent_fwd(const uint16_t* x, const int64_t* lab, int64_t R, int V, int64_t ignore, float* lse, float* loss,
+                     hipStream_t s);
+void launch_xent_bwd(const uint16_t* x, const int64_t* lab, const float* lse, int64_t R, int V, int64_t ignore,
+                     const float* go, const float* count, uint16_t* dx, hipStream_t s);
 void launch_fa_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* out, float* lse, int B, int S,
                    int H, int KV, float scale, hipStream_t s);
 void launch_fa_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* out, const uint16_t* dout,

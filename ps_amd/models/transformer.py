@@ -20,7 +20,8 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.dense import SplitKLinear
-from ..ops.transformer import attention_causal_gqa, attention_qkv, layer_norm_residual, rms_norm, rope_split, rope_table, swiglu
+from ..ops.transformer import (attention_causal_gqa, attention_qkv, cross_entropy, layer_norm_residual, rms_norm, rope_split,
+                              rope_table, swiglu)
 
 
 # ------------------------------------------------------------------------------------ BERT
@@ -102,7 +103,7 @@ class BertForMLM(nn.Module):
         logits = h @ self.word.weight.t() + self.head_bias
         if labels is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, self.c.vocab), labels.reshape(-1), ignore_index=-100)
+        return cross_entropy(logits.view(-1, self.c.vocab), labels.reshape(-1), ignore_index=-100)
 
 
 def mlm_batch(batch: int, seq: int, vocab: int = 30522, mask_prob: float = 0.15, seed: int = 0, device=None,
@@ -215,7 +216,9 @@ class LlamaForCausalLM(nn.Module):
         logits = self.lm_head(h)
         if labels is None:
             return logits
-        return F.cross_entropy(logits[:, :-1].float().reshape(-1, self.c.vocab), labels[:, 1:].reshape(-1))
+        # next-token targets; the last position has none (ignored) -- no sliced copy of the logits
+        tgt = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], -100)], dim=1)
+        return cross_entropy(logits, tgt, ignore_index=-100)
 
 
 def param_count(m: nn.Module) -> int:

@@ -238,3 +238,33 @@ def attention_causal_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> t
     b, _, s, _ = q.shape
     a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
     return a.transpose(1, 2).reshape(b, s, -1)
+
+
+# ------------------------------------------------------------------------------ fused LM-head cross-entropy
+class _FusedXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, labels, ignore):
+        lse, rows = native().xent_fwd(x, labels, int(ignore))
+        count = (labels != ignore).sum().float().reshape(1)
+        ctx.save_for_backward(x, labels, lse, count)
+        ctx.ignore = int(ignore)
+        return (rows.sum() / count.clamp(min=1.0)).reshape(())
+
+    @staticmethod
+    def backward(ctx, go):
+        x, labels, lse, count = ctx.saved_tensors
+        dx = native().xent_bwd(x, labels, lse, go.float().reshape(1).contiguous(), count, ctx.ignore)
+        return dx, None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """Mean softmax cross-entropy of ``logits`` [..., V] against ``labels`` [...] (ignore_index rows
+    excluded), as F.cross_entropy.  GPU bf16 logits take the fused HIP kernels (csrc/kernels/xent.hip):
+    the forward reads the logits once (per-row log-sum-exp), the backward reads them once and writes
+    the bf16 gradient -- no fp32 copy of the vocab-sized activations.  PS_AMD_FUSED_XENT=0 falls back."""
+    V = logits.shape[-1]
+    if _hip(logits) and logits.dtype == torch.bfloat16 and os.environ.get("PS_AMD_FUSED_XENT", "1") != "0":
+        x = logits.reshape(-1, V)
+        x = x if x.is_contiguous() else x.contiguous()
+        return _FusedXent.apply(x, labels.reshape(-1).long().contiguous(), int(ignore_index))
+    return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1), ignore_index=ignore_index)

@@ -69,3 +69,25 @@ def test_bert_layer_fused_attention_matches_sdpa(monkeypatch):
         outs.append((y.detach(), xi.grad.clone(), layer.qkv.weight.grad.clone()))
     for a, b in zip(outs[0], outs[1]):
         assert _rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("R,V,ign", [(300, 30522, 7), (64, 1000, 0), (33, 517, 5)])
+def test_fused_cross_entropy_matches_fp32(R, V, ign):
+    """LM-head cross-entropy on bf16 logits (csrc/kernels/xent.hip) vs F.cross_entropy in fp32:
+    loss and gradient, with ignored rows (label -100) and a non-multiple-of-8 vocab."""
+    from ps_amd.ops.transformer import cross_entropy
+
+    torch.manual_seed(R + V)
+    x = (torch.randn(R, V, device="cuda") * 3).bfloat16()
+    lab = torch.randint(0, V, (R,), device="cuda")
+    lab[torch.randperm(R, device="cuda")[:ign]] = -100
+    xf = x.float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(xf, lab, ignore_index=-100)
+    (ref * 0.7).backward()
+    xg = x.clone().requires_grad_()
+    loss = cross_entropy(xg, lab)
+    (loss * 0.7).backward()
+    torch.testing.assert_close(loss.float(), ref.detach(), rtol=1e-4, atol=1e-4)
+    rel = ((xg.grad.float() - xf.grad).norm() / xf.grad.norm()).item()
+    assert rel < 1e-2, rel
+    assert bool((xg.grad[lab == -100] == 0).all())
