@@ -79,9 +79,13 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// one 32-bit hash per PAIR of elements (2j, 2j + 1): a 16-bit draw each, kept if >= p * 2^16
+// one 32-bit hash per PAIR of elements (2j, 2j + 1): a 16-bit draw each, kept if >= p * 2^16.
+// The 64-bit seed folds into one 32-bit key (uniform: scalar ALU), so a pair costs ONE avalanche
+// finalizer (bijective in the pair index): the dropout hash had been the largest VALU item of the
+// fused attention kernels (two finalizers per pair, ~85 VALU per MFMA in the forward).
 __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, uint32_t pair) {
-  return mix32(mix32(pair ^ static_cast<uint32_t>(seed)) + static_cast<uint32_t>(seed >> 32));
+  const uint32_t k = static_cast<uint32_t>(seed) ^ (static_cast<uint32_t>(seed >> 32) * 0x9E3779B9u);
+  return mix32(pair ^ k);
 }
 __device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t thr) { return (h & 0xffffu) >= thr; }
 __device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
