@@ -46,6 +46,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import side_stream as _side
 from ._ext import native
 
 
@@ -228,6 +229,8 @@ class _BottleneckFn(torch.autograd.Function):
         n, h, w, s, oh, ow = ctx.dims
         gi, go = geo(h, w), geo(oh, ow)
         d2 = rows(dout)
+        # weight gradients run on the side stream, overlapped with this data-gradient chain
+        sd = _side.Fork(d2.device, (w1, w2, w3, wd))
         lk = ctx.link_out
         if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
                 and d2._version == lk.dx_version):
@@ -242,8 +245,9 @@ class _BottleneckFn(torch.autograd.Function):
             lk.part = lk.dx_keep = None
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
+        sd.fork()
+        dw3 = sd.run(lambda: nat.conv_wgrad(dz3, z2r, go, cf2), dz3, z2r, cf2, like=w3)
         gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
-        dw3 = nat.conv_wgrad(dz3, z2r, go, cf2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
         c1 = w2.shape[1]
         ours_dgrad = _conv3x3_enabled() and (s == 1 or (s == 2 and h % 2 == 0 and w % 2 == 0
@@ -252,12 +256,18 @@ class _BottleneckFn(torch.autograd.Function):
         # MIOpen there; at 64 / 128 channels MIOpen's is faster: profiles/r2_wgrad_probe.jsonl)
         ours_wgrad = _conv3x3_enabled() and c1 >= WGRAD3X3_MIN_C
         dy1 = dw2 = None
-        if not (ours_dgrad and ours_wgrad):
-            dy1, dw2, _ = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
-                                                              [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                              [not ours_dgrad, not ours_wgrad, False])
+        sd.fork()
         if ours_wgrad:
-            dw2 = nat.conv_wgrad(dz2, y1, geo(h, w, 3, s, 1)).view(w2.shape[0], 3, 3, c1).permute(0, 3, 1, 2)
+            dw2 = sd.run(lambda: nat.conv_wgrad(dz2, y1, geo(h, w, 3, s, 1)).view(w2.shape[0], 3, 3, c1)
+                         .permute(0, 3, 1, 2), dz2, y1, like=w2)
+        else:
+            dw2 = sd.run(lambda: torch.ops.aten.convolution_backward(
+                image(dz2, n, oh, ow), image(y1, n, h, w), w2, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                [False, True, False])[1], dz2, y1, like=w2)
+        if not ours_dgrad:
+            dy1 = torch.ops.aten.convolution_backward(image(dz2, n, oh, ow), image(y1, n, h, w), w2, None,
+                                                      [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                      [True, False, False])[0]
         if ours_dgrad:
             # data grad = the forward GEMM over dz2 with the flipped, transposed weight; its epilogue
             # applies bn1's ReLU mask and reduces bn1's backward sums (no separate reduce pass)
@@ -268,6 +278,8 @@ class _BottleneckFn(torch.autograd.Function):
             dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
             dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
+        sd.fork()
+        dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
         w1t = _mat(w1).t()
         dwd = dgd = dbd = None
         li = ctx.link_in
@@ -275,7 +287,8 @@ class _BottleneckFn(torch.autograd.Function):
         fkw = dict(mean=li.mean, invstd=li.invstd, aux2=li.z3, bits2=li.bits) if fold else {}
         if wd is not None:
             dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
-            dwd = nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)).view_as(wd)
+            sd.fork()
+            dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
             t = nat.conv_gemm(dzd, _mat(wd).t(), go)[0]
             epi = 4 if s == 2 else 2
             dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
@@ -286,8 +299,7 @@ class _BottleneckFn(torch.autograd.Function):
             # consumer's gradient into it in place (it would not bump the version): a summed
             # gradient always lands in a different buffer and fails the pointer check
             li.part, li.dx_ptr, li.dx_version, li.dx_keep = part, dx2.data_ptr(), dx2._version, dx2
-        dw1 = nat.conv_wgrad(dz1, x2, gi)
-        return (image(dx2, n, h, w), dw1.view_as(w1), dg1, db1, dw2, dg2, db2, dw3.view_as(w3), dg3, db3,
+        return (image(dx2, n, h, w), dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3,
                 dwd, dgd, dbd, None, None)
 
 

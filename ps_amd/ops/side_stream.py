@@ -1,0 +1,118 @@
+"""Weight gradients on a second HIP stream, overlapped with the data-gradient chain.
+
+In a ResNet backward the data gradients form one serial chain (block i's dx feeds block i-1),
+while every weight gradient is a leaf: nothing but the optimizer reads it.  The chain is mostly
+HBM-bound (BN applies, 1x1 data grads at 5+ TB/s), the weight gradients are MFMA-bound split-K
+GEMMs, so running them on their own stream lets the CU dispatcher fill the MFMA-idle cycles of
+the HBM-bound kernels with weight-gradient workgroups (two hardware queues feeding one chip).
+
+Protocol (``Fork``):
+  * ``fork()`` records an event on the compute stream after the operands of the next weight
+    gradients were enqueued; the side stream waits on it;
+  * ``run(fn, *inputs)`` enqueues ``fn`` on the side stream; every input tensor is
+    ``record_stream``-ed so the caching allocator does not hand its memory to the compute
+    stream before the side stream is done with it; outputs are allocated on the side stream
+    and laid out like their parameter (so AccumulateGrad adopts them without a copy kernel on
+    the compute stream);
+  * the first fork of each ``Fork`` queues an autograd end-of-backward callback that makes
+    the compute stream wait for the side stream -- whatever runs after ``loss.backward()``
+    (an optimizer, a checkpoint) sees finished gradients;
+  * consumers that read gradients DURING backward (the parameter-server bucket hooks,
+    parallel/colocated.py ``_launch``) call ``join(stream)`` before reading.
+
+Opt-in (``PS_AMD_WGRAD_STREAM=1``): measured on ResNet-50 bs1024 the streams overlap for 29 ms
+of the 77 ms step, but the compute stream's HBM-bound kernels stretch by about as much as the
+weight gradients hide (profiles/r3_wgrad_side_stream_ab.txt: -1.5 %), so one stream is the
+default.  Also off on CPU, under graph capture, and when a parameter already holds a gradient
+(micro-batch accumulation would make AccumulateGrad add on the compute stream).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Callable, Dict, Optional
+
+import torch
+
+_STREAMS: Dict[int, torch.cuda.Stream] = {}
+_lock = threading.Lock()
+
+
+def enabled() -> bool:
+    return os.environ.get("PS_AMD_WGRAD_STREAM", "0") == "1"
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    with _lock:
+        s = _STREAMS.get(idx)
+        if s is None:
+            s = _STREAMS[idx] = torch.cuda.Stream(device=idx)
+        return s
+
+
+def active(device: torch.device) -> Optional[torch.cuda.Stream]:
+    """The device's side stream if weight gradients were ever put on it, else None."""
+    if not _STREAMS or device.type != "cuda":
+        return None
+    return _STREAMS.get(device.index if device.index is not None else torch.cuda.current_device())
+
+
+def join(stream: Optional[torch.cuda.Stream] = None, device: Optional[torch.device] = None) -> None:
+    """Make ``stream`` (default: the current stream) wait for every weight gradient enqueued
+    on the side stream so far."""
+    if not _STREAMS:
+        return
+    stream = stream if stream is not None else torch.cuda.current_stream(device)
+    side = _STREAMS.get(stream.device_index)
+    if side is not None and side is not stream:
+        stream.wait_stream(side)
+
+
+def _match_layout(g: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """``g`` with ``like``'s strides (a copy on the current -- side -- stream if they differ)."""
+    if g.shape != like.shape:
+        g = g.reshape(like.shape) if g.is_contiguous() else g.contiguous().reshape(like.shape)
+    if all(gs == ls for gs, ls, n in zip(g.stride(), like.stride(), like.shape) if n != 1):
+        return g
+    out = torch.empty_strided(like.shape, like.stride(), dtype=g.dtype, device=g.device)
+    out.copy_(g)
+    return out
+
+
+class Fork:
+    """Per-backward helper (see module docstring)."""
+
+    def __init__(self, device: torch.device, params=()):
+        self.on = (enabled() and device.type == "cuda" and not torch.cuda.is_current_stream_capturing()
+                   and all(p is None or p.grad is None for p in params))
+        self.queued = False
+        if self.on:
+            self.main = torch.cuda.current_stream(device)
+            self.side = side_stream(device)
+
+    def fork(self) -> None:
+        if not self.on:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        if not self.queued:  # one end-of-backward join per Fork (no state across passes)
+            self.queued = True
+            main, side = self.main, self.side
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+
+    def run(self, fn: Callable, *inputs: torch.Tensor, like: Optional[torch.Tensor] = None):
+        """``fn()`` on the side stream (inputs protected from reuse); with ``like`` the result is
+        returned in ``like``'s layout."""
+        if not self.on:
+            out = fn()
+            return _match_layout(out, like) if like is not None else out
+        for t in inputs:
+            if t is not None:
+                t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            out = fn()
+            if like is not None:
+                out = _match_layout(out, like)
+        return out

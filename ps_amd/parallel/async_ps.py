@@ -48,6 +48,7 @@ import torch
 
 from ..obs import trace as _trace
 from ..ops import optim as _o
+from ..ops import side_stream as _side
 from .transport import Transport, side_stream
 from .updaters import AdamUpdater, Updater, resolve_updater
 
@@ -362,6 +363,8 @@ class AsyncPS:
             return
         self._launched[b] = True
         self._open_step()
+        if self.gpu:  # weight gradients still in flight on the side stream (ops/side_stream.py)
+            _side.join(device=self.device)
         parked = self._landing[b]
         lo, hi = self.bucket_range[b]
         L, MB, me = self.L, self.MB, self.rank

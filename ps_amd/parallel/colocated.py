@@ -52,6 +52,7 @@ import torch
 from ..obs import trace as _trace
 from ..ops import compress as _cmp
 from ..ops import reduce as _red
+from ..ops import side_stream as _side
 from .registry import Registry
 from .transport import Transport
 from .updaters import Updater, resolve_updater
@@ -287,6 +288,23 @@ class ColocatedPS:
         if self.launched[b]:
             return
         self.launched[b] = True
+        side = _side.active(self.device) if self.gpu else None
+        if side is not None:
+            # some of the bucket's gradients are weight gradients still in flight on the side
+            # stream (ops/side_stream.py): land and push from that stream, after the compute
+            # stream's part of the bucket, so the data-gradient chain never waits for them
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            side.wait_event(ev)
+            for g in self._landing[b].values():
+                if g is not None:
+                    g.record_stream(side)
+            with torch.cuda.stream(side):
+                self._launch_body(b)
+        else:
+            self._launch_body(b)
+
+    def _launch_body(self, b: int) -> None:
         self._land(b)
         if self.fault is not None:
             self.fault.before_push()
