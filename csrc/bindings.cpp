@@ -1120,7 +1120,8 @@ static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::v
 std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10::optional<Tensor> pro, int64_t epi,
                               c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
                               c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits,
-                              c10::optional<Tensor> aux2, c10::optional<Tensor> bits2) {
+                              c10::optional<Tensor> aux2, c10::optional<Tensor> bits2, c10::optional<Tensor> a2,
+                              c10::optional<Tensor> bwd) {
   check_rows(a, "a");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
@@ -1150,6 +1151,16 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     bitsp = bits->data_ptr<uint8_t>();
   }
   TORCH_CHECK(!(pro.has_value() && pro->defined()) || epi <= 1, "the BN prologue combines with epilogue 0 or 1 only");
+  const bool has_bwd = bwd.has_value() && bwd->defined();
+  if (has_bwd) {  // BN-backward prologue: A := ca * a + cb * a2 + cc, stored to a third output
+    TORCH_CHECK(epi == 3 && !(pro.has_value() && pro->defined()), "the BN-backward prologue combines with epi 3 only");
+    TORCH_CHECK(g.ks == 1 && g.stride == 1 && g.pad == 0, "the BN-backward prologue is for 1x1 stride-1 convs");
+    TORCH_CHECK(a2.has_value() && a2->defined(), "the BN-backward prologue needs a2");
+    check_rows(*a2, "a2");
+    TORCH_CHECK(a2->sizes() == a.sizes(), "a2 must match a");
+    check_f32(*bwd, "bwd");
+    TORCH_CHECK(bwd->numel() == 3 * g.C, "bwd must be [3C]");
+  }
   const uint16_t* aux2p = nullptr;
   const uint8_t* bits2p = nullptr;
   if (fold) {
@@ -1167,7 +1178,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
   const bool has_pro = pro.has_value() && pro->defined();
-  const int G = psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), has_pro).gm;
+  const int G =
+      psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), has_pro || has_bwd).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;
@@ -1191,7 +1203,15 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   p.mean = f32_opt(mean, N, "mean");
   p.invstd = f32_opt(invstd, N, "invstd");
   p.part = sums ? part.data_ptr<float>() : nullptr;
+  Tensor aout;
+  if (has_bwd) {
+    aout = torch::empty_like(a);
+    p.a2 = u16(*a2);
+    p.bwd = bwd->data_ptr<float>();
+    p.aout = u16m(aout);
+  }
   psamd::launch_conv_fwd(p, cur_stream(a));
+  if (has_bwd) return {c, part, aout};
   return {c, part};
 }
 
@@ -1267,8 +1287,8 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
   const c10::DeviceGuard guard(dz.device());
   const float* prop = f32_opt(pro, 2 * g.C, "pro");
-  auto ws = torch::empty({psamd::conv_wgrad_ws(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), g.C,
-                                               prop != nullptr)},
+  auto ws = torch::empty({psamd::conv_wgrad_ws_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), g,
+                                                   prop != nullptr)},
                          dz.options().dtype(torch::kFloat32));
   auto dw = torch::empty({N, K}, dz.options());
   psamd::ConvWgradArgs p{};
@@ -1343,6 +1363,25 @@ std::vector<Tensor> bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> r
   return {y, mb};
 }
 
+// BN backward coefficients only (dx = ca * g + cb * x + cc for a GEMM prologue to apply) from
+// producer partial sums part [2, G, C] over R rows -> [dgamma, dbeta, coef = ca | cb | cc]
+std::vector<Tensor> bn_bwd_coef(Tensor part, c10::optional<Tensor> gamma, Tensor mean, Tensor invstd, int64_t R) {
+  check_f32(part, "part");
+  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.is_contiguous(), "part [2, G, C]");
+  const int64_t C = part.size(2);
+  TORCH_CHECK(C % 8 == 0, "C % 8");
+  const c10::DeviceGuard guard(part.device());
+  auto fopt = part.options();
+  auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt), coef = torch::empty({3 * C}, fopt);
+  const Tensor fp = fold_partials(part, cur_stream(part));
+  const int64_t Gf = fp.size(1);
+  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + Gf * C, static_cast<int>(Gf), nullptr,
+                                nullptr, f32_opt(gamma, C, "gamma"), f32_opt(mean, C, "mean"), f32_opt(invstd, C, "invstd"),
+                                dg.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), nullptr, R,
+                                static_cast<int>(C), cur_stream(part));
+  return {dg, db, coef};
+}
+
 // BN backward from producer partial sums part [2, G, C] (conv_gemm epi 3); g = masked gradient
 std::vector<Tensor> bn_bwd_partials(Tensor g, Tensor x, Tensor part, c10::optional<Tensor> gamma, Tensor mean,
                                     Tensor invstd) {
@@ -1377,8 +1416,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_gemm", &conv_gemm, py::arg("a"), py::arg("b"), py::arg("geo"), py::arg("pro") = py::none(),
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
-        py::arg("aux2") = py::none(), py::arg("bits2") = py::none());
+        py::arg("aux2") = py::none(), py::arg("bits2") = py::none(), py::arg("a2") = py::none(),
+        py::arg("bwd") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
+  m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("dz"), py::arg("wph"), py::arg("H"), py::arg("W"),
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());

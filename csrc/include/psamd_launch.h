@@ -289,6 +289,12 @@ struct ConvGemmArgs {
   const float* mean;    // epi 3/6-8: [N]
   const float* invstd;  // epi 3/6-8: [N]
   float* part;          // epi 1/3/6-8: [2][conv_fwd_plan(M, N, K, pro).gm][N] block partial sums
+  // BN-backward prologue (1x1, epi 3 only; excludes pro): A := bf16(ca * a + cb * a2 + cc), the
+  // previous BN's data gradient from its output gradient a and input a2 (coefficients bwd =
+  // [ca | cb | cc], 3C); the A tile is also stored to aout [M, C] (by the channel-tile-0 blocks)
+  const uint16_t* a2;   // [M, C] BN input; nullable
+  const float* bwd;     // [3C]
+  uint16_t* aout;       // [M, C]
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
@@ -308,6 +314,8 @@ struct ConvWgradArgs {
   float* dbws;          // [conv_wgrad_splits(...)][N] fp32 scratch when db is set
 };
 int conv_wgrad_splits(int M, int N, int K, int C, bool pro);
+// workspace of launch_conv_wgrad for this geometry (the 3x3 patch kernel's plan where it applies)
+int64_t conv_wgrad_ws_geo(int M, int N, int K, const ConvGeo& g, bool pro);
 bool conv_wgrad_is_wide(int M, int N, int K, int C, bool pro);
 int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro);
 // Fused short-sequence attention (attention.hip): qkv [B, S, 3, H, 64] bf16 (Linear layout),

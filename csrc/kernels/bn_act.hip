@@ -690,7 +690,7 @@ void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint1
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, pd, px, G, C, R, gamma, mean, invstd,
                      dgamma, dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
-  if (nvec <= 0) return;
+  if (nvec <= 0 || dx == nullptr) return;  // dx null: coefficients only (a GEMM prologue applies them)
   const int grid = apply_grid(nvec);
   const bool fixed = (static_cast<int64_t>(grid) * 256) % (C / 8) == 0;
   const uint16_t* none = nullptr;

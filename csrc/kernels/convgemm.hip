@@ -166,17 +166,23 @@ __device__ __attribute__((aligned(16))) uint16_t kZeroPage[8] = {0, 0, 0, 0, 0, 
 // sequence of (tile, stage) steps through two LDS buffers and two register stage sets: the loads
 // of step q + 2 are issued before the MFMAs of step q, so two steps of work -- and at tile ends
 // the epilogue -- cover their latency (the HBM-bound 1x1 layers have a single stage per tile).
-template <int AR, int BCH>
+template <int AR, int BCH, int AR2>
 struct StageRegs {
   u16x8 a[AR];
+  u16x8 a2[AR2];  // BN-backward prologue: the BN input rows (AR2 = 1: unused)
   u16x8 b[BCH];
+  int mt;         // pixel tile of the stage (BN-backward prologue: where the A tile is stored)
   unsigned ok;  // valid-row bits of a[]
   int cc;       // channel offset of the stage inside its tap (prologue coefficients)
   bool wb;      // b[] loaded (to be staged)
 };
 
-template <int BM, int BN, bool PRO, int EPI, bool KS1, bool GLDS>
+// PRO: 0 none, 1 BN + ReLU of the A rows, 2 BN backward from two row sources (a, a2)
+template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
+  constexpr bool BWD = PRO == 2;
+  static_assert(!BWD || (KS1 && EPI == 3 && !GLDS), "the BN-backward prologue is a 1x1 data-gradient prologue");
+  constexpr int AR2 = BWD ? BM / 32 : 1;
   // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce
   constexpr bool FOLD = EPI >= 6;
   constexpr int BASE = EPI == 6 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // staging: thread t moves 16-B chunk (t & 7) of tile rows (t >> 3) + 32 i
   const int srow = t >> 3, sc = t & 7;
   const uint16_t* bptr = p.b + static_cast<int64_t>(n0 + srow) * p.K + sc * 8;
-  StageRegs<AR, BCH> S0, S1;
+  StageRegs<AR, BCH, AR2> S0, S1;
   // producer cursor (runs two steps ahead of the MFMAs): tile iteration pti, stage pkt and its
   // tap (pkh, pkw) / channel offset pcc, advanced incrementally (no divisions per stage);
   // per-tile row sources: offset of tap (0, 0) channel 0, its input coordinates, row valid
@@ -233,9 +239,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       rbase[i] = ((static_cast<int64_t>(ps.img > 0 ? ps.img : 0) * g.H + ps.ih0) * g.W + ps.iw0) * g.C + sc * 8;
     }
   };
-  auto gload = [&](StageRegs<AR, BCH>& R) {
+  auto gload = [&](StageRegs<AR, BCH, AR2>& R) {
     R.cc = pcc;
     R.ok = 0;
+    R.mt = mg + pti * GM;
     const int64_t toff = KS1 ? pcc : static_cast<int64_t>(pkh * g.W + pkw) * g.C + pcc;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
@@ -247,6 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       R.ok |= (v ? 1u : 0u) << i;
       // out-of-map taps / rows past M read element 0 (in bounds) and are zeroed in LDS
       R.a[i] = *reinterpret_cast<const u16x8*>(p.a + (v ? rbase[i] + toff : 0));
+      if constexpr (BWD) R.a2[i] = *reinterpret_cast<const u16x8*>(p.a2 + (v ? rbase[i] + toff : 0));
     }
     const int k0 = pkt * kBK;
     R.wb = lq++ < 2 || nk > 2;
@@ -269,21 +277,36 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       if (++pti < my_tiles) set_rows(mg + pti * GM);
     }
   };
-  auto swrite = [&](const StageRegs<AR, BCH>& R, int buf) {
+  auto swrite = [&](const StageRegs<AR, BCH, AR2>& R, int buf) {
     uint16_t* As = lds + buf * (BM * kBK);
     uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
-    float psc[8], psh[8];
-    if constexpr (PRO) {  // [scale | shift] of 8 channels: L1-resident
+    float psc[8], psh[8], pcf[8];
+    if constexpr (PRO == 1) {  // [scale | shift] of 8 channels: L1-resident
       load8(p.pro, R.cc + sc * 8, psc);
       load8(p.pro + g.C, R.cc + sc * 8, psh);
+    } else if constexpr (BWD) {  // [ca | cb | cc]
+      load8(p.bwd, R.cc + sc * 8, psc);
+      load8(p.bwd + g.C, R.cc + sc * 8, psh);
+      load8(p.bwd + 2 * g.C, R.cc + sc * 8, pcf);
     }
+    // BWD: the channel-tile-0 blocks also store the A tile (the BN data gradient) to aout
+    const bool store_a = BWD && p.aout != nullptr && n0 == 0;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       u16x8 v = R.a[i];
-      if constexpr (PRO) v = bn_relu8(v, psc, psh);
-      if (!((R.ok >> i) & 1u)) v = kZero8;
+      if constexpr (PRO == 1) v = bn_relu8(v, psc, psh);
+      if constexpr (BWD) {
+        const u16x8 x8 = R.a2[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = f32_to_bf16(psc[j] * bf16_to_f32(v[j]) + psh[j] * bf16_to_f32(x8[j]) + pcf[j]);
+      }
+      const bool ok = (R.ok >> i) & 1u;
+      if (!ok) v = kZero8;
       const int r = srow + 32 * i;
       *reinterpret_cast<u16x8*>(As + r * kBK + swz(r, sc) * 8) = v;
+      if (store_a && ok)
+        *reinterpret_cast<u16x8*>(p.aout + static_cast<int64_t>(R.mt * BM + r) * g.C + R.cc + sc * 8) = v;
     }
     if (R.wb) {
 #pragma unroll
@@ -463,7 +486,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
 
   // one step of the (tile, stage) sequence; SF: the free register set (held step q), SN: step q + 1
   int ckt = 0, cti = 0;  // consumer cursor
-  auto step = [&](StageRegs<AR, BCH>& SF, const StageRegs<AR, BCH>& SN, int q) {
+  auto step = [&](StageRegs<AR, BCH, AR2>& SF, const StageRegs<AR, BCH, AR2>& SN, int q) {
     if (q + 2 < nq) gload(SF);
     compute(q & 1);
     if (++ckt == nk) {  // tile done
@@ -997,6 +1020,168 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
       }
 }
 
+// ------------------------------------------------------------------------------ conv_wgrad (patch)
+// 3x3 / stride-1 / pad-1 weight gradient at 64-128 channels, where the output dW [N][9C] is small and
+// the im2col view re-reads every input pixel once per tap.  A stage is 112 output pixels = R = 112 / W
+// whole rows of one image; the block stages the dz rows [112][64 n] and the input PATCH those rows
+// touch -- (R + 2) x (W + 2) pixel slots x 64 channels, halo slots zero (out-of-map rows / columns
+// load the zero page) -- ONCE, and all nine taps read their B fragments from it at a shifted slot
+// (slot(m) + kh (W + 2) + kw): L2 -> LDS traffic per stage drops from 9 x 112 x 64 to
+// (R + 2)(W + 2) x 64 pixel-channels.
+// LDS layout: both tiles are split into two 32-channel PLANES of 64-B rows (dz: [n half][pixel][32],
+// patch: [c half][slot][32]).  A wave reads one plane, and the 4 rows of a ds_read_b64_tr_b16 lane
+// group are 4 consecutive pixels (slots) = 256 contiguous bytes = every bank once -- no swizzle, so
+// every fragment address is linear: a tap's kw and a k-step's pixel offset become instruction
+// immediates and the whole loop runs on 1 + 14 loop-invariant address registers (W % 4 == 0: a
+// 4-pixel group never straddles an output row).
+// 12 waves: (kh, n half, c half) -> 32 n x 3 taps x 32 c each, one dz fragment + three patch
+// fragments per three MFMAs.  Block = (n tile 64, c tile 64, pixel split); fp32 per-split slabs,
+// fixed-order reduction (deterministic) as the other weight-gradient kernels.
+constexpr int kPP = 112;  // pixels per stage
+constexpr int kPS = 3;    // LDS ring depth
+
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr_off(uint32_t a) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
+  return v;
+}
+
+template <int W>
+__global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgradArgs p, int stages_per_split) {
+  constexpr int R = kPP / W, PW = W + 2, PR = R + 2;
+  static_assert(kPP % W == 0 && W % 4 == 0, "a stage is whole rows; 4-pixel groups stay in a row");
+  constexpr int GPL = kPP * 64;                         // dz plane bytes (32 n per row)
+  constexpr int GB = 2 * GPL;                           // dz tile bytes
+  constexpr int PPL = PR * PW * 64;                     // patch plane bytes
+  constexpr int PB = ((2 * PPL + 1023) / 1024) * 1024;  // patch tile bytes (whole 1 KiB DMA pieces)
+  constexpr int GI = GB / 1024, PI = PB / 1024;         // DMA pieces
+  constexpr int NI = GI + PI;                           // per stage, dealt over the 12 waves
+  constexpr int STB = GB + PB;                          // stage bytes
+  constexpr int MAXW = (NI + 11) / 12;                  // pieces of the busiest wave
+  static_assert(GB % 1024 == 0 && MAXW <= 4 && kPS * STB <= 160 * 1024, "stage shape");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kPS * STB / 2];
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nct = g.C / 64, tiles = (p.N / 64) * nct;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, tile = L - split * tiles;
+  const int n0 = (tile / nct) * 64, c0 = (tile % nct) * 64;
+  const int rows_per_img = g.OH / R, total = p.M / kPP;
+  const int sb = split * stages_per_split;
+  const int se = min(total, sb + stages_per_split);
+  const int nst = se > sb ? se - sb : 0;  // block-uniform
+
+  // ---- DMA: piece i = wave + 12 j (dz pieces first, then patch pieces); lane-linear 16-B chunks,
+  // chunk ch of a plane = row ch / 4, 8 channels (ch % 4); sources recomputed per stage
+  const int myn = (NI - wave + 11) / 12;  // wave-uniform: MAXW or MAXW - 1
+  auto issue = [&](int st, int buf) {
+    const int q = sb + st, img = q / rows_per_img, oh0 = (q - img * rows_per_img) * R;
+    uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STB;
+    const uint16_t* gsrc = p.dz + static_cast<int64_t>(q) * kPP * p.N + n0;
+    const uint16_t* xsrc = p.x + (static_cast<int64_t>(img) * g.H + oh0 - 1) * g.W * g.C + c0;
+#pragma unroll
+    for (int j = 0; j < MAXW; ++j) {
+      if (j >= myn) break;  // wave-uniform
+      const int i = wave + 12 * j;
+      const uint16_t* src;
+      if (i < GI) {  // wave-uniform
+        const int ch = i * 64 + lane, pl = ch / (GPL / 16), r = ch - pl * (GPL / 16);
+        src = gsrc + static_cast<int64_t>(r >> 2) * p.N + pl * 32 + (r & 3) * 8;
+      } else {  // slot (pr, pc) = input pixel (oh0 - 1 + pr, pc - 1); halo / out-of-map / tail: zero page
+        const int ch = (i - GI) * 64 + lane, pl = ch / (PPL / 16), r = ch - pl * (PPL / 16), slot = r >> 2;
+        const int pr = slot / PW, pc = slot - pr * PW, ih = oh0 - 1 + pr;
+        const bool ok = pl < 2 && pc >= 1 && pc <= W && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H);
+        src = ok ? xsrc + (static_cast<int64_t>(pr) * W + (pc - 1)) * g.C + pl * 32 + (r & 3) * 8 : kZeroPage;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(base + i * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- fragment addresses (bytes inside a stage): lane reads pixel m = 16 s + 4 h + mrow, columns
+  // 16 (gi & 1) + 4 (i16 & 3) .. + 3 of its plane; s / h / kw are immediates except the patch slot
+  const int kh = wave % 3, nh = (wave / 3) & 1, chf = wave / 6;
+  const int gi = lane >> 4, i16 = lane & 15;
+  const int mrow = 8 * (gi >> 1) + (i16 >> 2), colb = (16 * (gi & 1) + 4 * (i16 & 3)) * 2;
+  const uint32_t ga = static_cast<uint32_t>(nh * GPL + mrow * 64 + colb);
+  uint32_t xa[7][2];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = 16 * s + 4 * h + mrow, oh = m / W, ow = m - oh * W;
+      xa[s][h] = static_cast<uint32_t>(GB + chf * PPL + ((oh + kh) * PW + ow) * 64 + colb);
+    }
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[k][q] = 0.f;
+  auto mma = [&](int buf) {
+    const uint32_t b0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const lds_s16x4*)lds)) + buf * STB;
+    const uint32_t gb = b0 + ga;
+#define PSAMD_PATCH_STEP(S)                                                                              \
+  {                                                                                                      \
+    s16x4 a0 = ds_tr_off<(16 * S) * 64>(gb), a1 = ds_tr_off<(16 * S + 4) * 64>(gb);                      \
+    const uint32_t x0 = b0 + xa[S][0], x1 = b0 + xa[S][1];                                               \
+    s16x4 p00 = ds_tr_off<0>(x0), p01 = ds_tr_off<0>(x1);                                                \
+    s16x4 p10 = ds_tr_off<64>(x0), p11 = ds_tr_off<64>(x1);                                              \
+    s16x4 p20 = ds_tr_off<128>(x0), p21 = ds_tr_off<128>(x1);                                            \
+    /* the reads land asynchronously: the wait redefines their registers, so no MFMA is scheduled  */   \
+    /* above it and no register is reused before it                                               */   \
+    asm volatile("s_waitcnt lgkmcnt(0)"                                                                  \
+                 : "+v"(a0), "+v"(a1), "+v"(p00), "+v"(p01), "+v"(p10), "+v"(p11), "+v"(p20), "+v"(p21)  \
+                 :                                                                                       \
+                 : "memory");                                                                            \
+    const bf16x8_t af = as_bf16x8(s16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]});        \
+    acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                                                    \
+        af, as_bf16x8(s16x8{p00[0], p00[1], p00[2], p00[3], p01[0], p01[1], p01[2], p01[3]}), acc[0], 0, 0, 0); \
+    acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                                                    \
+        af, as_bf16x8(s16x8{p10[0], p10[1], p10[2], p10[3], p11[0], p11[1], p11[2], p11[3]}), acc[1], 0, 0, 0); \
+    acc[2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                                                    \
+        af, as_bf16x8(s16x8{p20[0], p20[1], p20[2], p20[3], p21[0], p21[1], p21[2], p21[3]}), acc[2], 0, 0, 0); \
+  }
+    PSAMD_PATCH_STEP(0)
+    PSAMD_PATCH_STEP(1)
+    PSAMD_PATCH_STEP(2)
+    PSAMD_PATCH_STEP(3)
+    PSAMD_PATCH_STEP(4)
+    PSAMD_PATCH_STEP(5)
+    PSAMD_PATCH_STEP(6)
+#undef PSAMD_PATCH_STEP
+  };
+
+  const int pre = nst < kPS - 1 ? nst : kPS - 1;
+  for (int st = 0; st < pre; ++st) issue(st, st);
+  for (int st = 0; st < nst; ++st) {
+    // this wave's DMAs of stage st landed (the next stage's may stay in flight), then everyone's
+    if (st + 1 < nst) {
+      if (myn == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (myn == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (myn == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
+    if (st + kPS - 1 < nst) issue(st + kPS - 1, (st + kPS - 1) % kPS);
+    mma(st % kPS);
+  }
+  // slab[split][n][k], k = (kh * 3 + kw) * C + c
+  float* sl = p.ws + static_cast<int64_t>(split) * p.N * p.K;
+  const int h = lane >> 5, cl = lane & 31;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int n = n0 + nh * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const int k = (kh * 3 + kw) * g.C + c0 + chf * 32 + cl;
+      sl[static_cast<int64_t>(n) * p.K + k] = acc[kw][q];
+    }
+}
+
 // out[y][e] = sum_{b in [y*per, y*per + per)} in[b][e] in fixed order (bf16 or fp32 out)
 template <bool BF16>
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ in, int nslab, int per, int64_t E,
@@ -1060,12 +1245,13 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
 
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
-  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K, a.pro != nullptr);
+  const bool bwd = a.bwd != nullptr;
+  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K, a.pro != nullptr || bwd);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
   // deep K without the BN prologue: LDS-DMA staging (one tile per block)
-  const bool glds = !a.pro && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
+  const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
 #define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \
   if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, GL>), dim3(nblk), dim3(256), 0, s, a, GM); \
   else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, GL>), dim3(nblk), dim3(256), 0, s, a, GM)
@@ -1100,6 +1286,11 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
       default: PSAMD_CFT(0); break;
     }
 #undef PSAMD_CFT
+    return;
+  }
+  if (bwd) {  // 1x1 data gradient with the previous BN's backward in the prologue (epilogue 3)
+    if (pl.bn == 128) hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 2, 3, true, false>), dim3(nblk), dim3(256), 0, s, a, GM);
+    else hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 2, 3, true, false>), dim3(nblk), dim3(256), 0, s, a, GM);
     return;
   }
   // the BN prologue only appears on forward convolutions (epilogue 0 / 1)
@@ -1178,6 +1369,61 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
 }
 }  // namespace
 
+namespace {
+// The patch kernel's shapes: 3x3 / stride 1 / pad 1 maps 56 or 28 wide (the ResNet-50 64- and
+// 128-channel stages), channels up to PS_AMD_WGRAD_PATCH_MAX_C (default 128; 0 = never).
+int patch_max_c() {
+  static const int v = [] {
+    const char* e = std::getenv("PS_AMD_WGRAD_PATCH_MAX_C");
+    return e ? std::atoi(e) : 128;
+  }();
+  return v;
+}
+
+bool patch_ok(const ConvGeo& g, int M, int N, bool pro) {
+  return !pro && g.ks == 3 && (g.ksw == 0 || g.ksw == 3) && g.stride == 1 && g.pad == 1 && g.H == g.OH &&
+         g.W == g.OW && (g.W == 56 || g.W == 28) && g.OH % (kPP / g.W) == 0 && g.C % 64 == 0 && N % 64 == 0 &&
+         g.C <= patch_max_c() && M % kPP == 0 && g.RH == 0;
+}
+
+struct PPlan {
+  int tiles, nsplit, spp, groups;
+};
+
+PPlan pplan(const ConvGeo& g, int M, int N) {
+  PPlan w{};
+  w.tiles = (N / 64) * (g.C / 64);
+  const int stages = M / kPP;
+  const int ns = fill_rounds(w.tiles, 256, std::max(1, stages / 4));  // one 12-wave block per CU
+  w.spp = (stages + ns - 1) / ns;
+  w.nsplit = (stages + w.spp - 1) / w.spp;
+  w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;
+  return w;
+}
+
+void slab_reduce(const ConvWgradArgs& a, int nsplit, int groups, hipStream_t s) {
+  const int64_t E = static_cast<int64_t>(a.N) * a.K;
+  const unsigned eb = static_cast<unsigned>((E + 255) / 256);
+  void* dw = a.dw;
+  if (groups) {
+    float* mid = a.ws + static_cast<int64_t>(nsplit) * E;
+    void* midv = mid;
+    hipLaunchKernelGGL(slab_reduce_kernel<false>, dim3(eb, groups), dim3(256), 0, s, a.ws, nsplit, 16, E, midv);
+    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, mid, groups, groups, E, dw);
+  } else {
+    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, a.ws, nsplit, nsplit, E, dw);
+  }
+}
+}  // namespace
+
+int64_t conv_wgrad_ws_geo(int M, int N, int K, const ConvGeo& g, bool pro) {
+  if (patch_ok(g, M, N, pro)) {
+    const PPlan w = pplan(g, M, N);
+    return static_cast<int64_t>(w.nsplit + w.groups) * N * K;
+  }
+  return conv_wgrad_ws(M, N, K, g.C, pro);
+}
+
 int conv_wgrad_splits(int M, int N, int K, int C, bool pro) { return wplan(M, N, K, C, pro).nsplit; }
 bool conv_wgrad_is_wide(int M, int N, int K, int C, bool pro) { return wplan(M, N, K, C, pro).wide != 0; }
 
@@ -1188,6 +1434,14 @@ int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro) {
 
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
+  if (a.db == nullptr && patch_ok(a.g, a.M, a.N, a.pro != nullptr)) {
+    const PPlan w = pplan(a.g, a.M, a.N);
+    const int nblk = w.tiles * w.nsplit;
+    if (a.g.W == 56) hipLaunchKernelGGL(conv_wgrad_patch_kernel<56>, dim3(nblk), dim3(768), 0, s, a, w.spp);
+    else hipLaunchKernelGGL(conv_wgrad_patch_kernel<28>, dim3(nblk), dim3(768), 0, s, a, w.spp);
+    slab_reduce(a, w.nsplit, w.groups, s);
+    return;
+  }
   const WPlan w = wplan(a.M, a.N, a.K, a.g.C, a.pro != nullptr);
   const int nblk = w.tiles * w.nsplit;
   // LIN: 1x1 stride-1 pad-0 geometry (X row m = pixel m), DMA sources without the pixel decode
@@ -1226,17 +1480,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (w.wide && a.db != nullptr && a.pro == nullptr)  // bias gradient: fold the per-split column sums
     hipLaunchKernelGGL(slab_reduce_kernel<false>, dim3((a.N + 255) / 256), dim3(256), 0, s, a.dbws, w.nsplit,
                        w.nsplit, static_cast<int64_t>(a.N), static_cast<void*>(a.db));
-  const int64_t E = static_cast<int64_t>(a.N) * a.K;
-  const unsigned eb = static_cast<unsigned>((E + 255) / 256);
-  void* dw = a.dw;
-  if (w.groups) {
-    float* mid = a.ws + static_cast<int64_t>(w.nsplit) * E;
-    void* midv = mid;
-    hipLaunchKernelGGL(slab_reduce_kernel<false>, dim3(eb, w.groups), dim3(256), 0, s, a.ws, w.nsplit, 16, E, midv);
-    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, mid, w.groups, w.groups, E, dw);
-  } else {
-    hipLaunchKernelGGL(slab_reduce_kernel<true>, dim3(eb), dim3(256), 0, s, a.ws, w.nsplit, w.nsplit, E, dw);
-  }
+  slab_reduce(a, w.nsplit, w.groups, s);
 }
 
 }  // namespace psamd

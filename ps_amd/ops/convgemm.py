@@ -152,6 +152,13 @@ def _dgrad_s2_min_c() -> int:
 WGRAD3X3_MIN_C = 256
 
 
+def _patch_wgrad_ok(h: int, w: int, c1: int, c2: int) -> bool:
+    """The shapes csrc conv_wgrad_patch_kernel takes (mirrors convgemm.hip patch_ok): 3x3 stride 1
+    on 56- or 28-wide maps of whole 112-pixel stages, c1 <= PS_AMD_WGRAD_PATCH_MAX_C (128)."""
+    cap = int(os.environ.get("PS_AMD_WGRAD_PATCH_MAX_C", "128"))
+    return w in (56, 28) and h % (112 // w) == 0 and c1 % 64 == 0 and c2 % 64 == 0 and c1 <= cap
+
+
 def _conv3x3_enabled() -> bool:
     return os.environ.get("PS_AMD_CONV3X3", "1") != "0"
 
@@ -169,6 +176,16 @@ class _Link:
 
 
 FOLD_STATS = {"used": 0}  # bn3 backward passes that took the consumer's partials (tests)
+
+
+def _bwd_prologue_enabled(c3: int) -> bool:
+    """bn3 backward applied in the conv3 data-gradient prologue, up to PS_AMD_BN_BWD_PROLOGUE_MAX_C
+    bn3 channels (0: never, the separate apply pass).  The prologue stages A through registers
+    from TWO row sources: at 256 channels (4 K-stages, persistent grid) it replaces the apply pass
+    + the LDS-DMA GEMM (1.29 -> 1.05-1.08 ms per layer-1 block); at 512-2048 channels the
+    register-staged deep-K GEMM is 2-6x slower than apply + LDS-DMA GEMM
+    (profiles/r3_bn_bwd_prologue_ab.txt)."""
+    return c3 <= int(os.environ.get("PS_AMD_BN_BWD_PROLOGUE_MAX_C", "256"))
 
 
 def _fold_enabled() -> bool:
@@ -232,29 +249,40 @@ class _BottleneckFn(torch.autograd.Function):
         # weight gradients run on the side stream, overlapped with this data-gradient chain
         sd = _side.Fork(d2.device, (w1, w2, w3, wd))
         lk = ctx.link_out
+        dz3 = None
         if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
                 and d2._version == lk.dx_version):
             # the consumer block already masked dout and reduced bn3's backward sums
-            dz3, dg3, db3 = nat.bn_bwd_partials(d2, z3, lk.part, g3, m3, i3)
+            if _bwd_prologue_enabled(z3.shape[1]):
+                # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
+                # the weight gradient: no separate apply pass over the widest tensors
+                dg3, db3, cb3 = nat.bn_bwd_coef(lk.part, g3, m3, i3, d2.shape[0])
+                gy2, p2, dz3 = nat.conv_gemm(d2, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2, a2=z3, bwd=cb3)
+            else:
+                dz3, dg3, db3 = nat.bn_bwd_partials(d2, z3, lk.part, g3, m3, i3)
+                gy2 = None
             FOLD_STATS["used"] += 1
         else:
             # bn3 with the ReLU mask from the output bits; the masked gradient dout * relu' is
             # also the identity-branch gradient -- recomputed where needed, never stored
             dz3, _, dg3, db3 = nat.bn_act_bwd(d2, None, z3, g3, m3, i3, 3, False, True, None, obits)
+            gy2 = None
         if lk is not None:
             lk.part = lk.dx_keep = None
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
         sd.fork()
         dw3 = sd.run(lambda: nat.conv_wgrad(dz3, z2r, go, cf2), dz3, z2r, cf2, like=w3)
-        gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
+        if gy2 is None:
+            gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
-        c1 = w2.shape[1]
+        c1, c2 = w2.shape[1], w2.shape[0]
         ours_dgrad = _conv3x3_enabled() and (s == 1 or (s == 2 and h % 2 == 0 and w % 2 == 0
                                                          and w2.shape[1] >= _dgrad_s2_min_c()))
         # weight grad on the wide-tile kernel from 256 input channels up (on par with / faster than
-        # MIOpen there; at 64 / 128 channels MIOpen's is faster: profiles/r2_wgrad_probe.jsonl)
-        ours_wgrad = _conv3x3_enabled() and c1 >= WGRAD3X3_MIN_C
+        # MIOpen there: profiles/r2_wgrad_probe.jsonl), on the patch kernel at 64 / 128 channels,
+        # stride 1 (csrc conv_wgrad_patch_kernel); MIOpen for the one stride-2 128-channel layer
+        ours_wgrad = _conv3x3_enabled() and (c1 >= WGRAD3X3_MIN_C or (s == 1 and _patch_wgrad_ok(h, w, c1, c2)))
         dy1 = dw2 = None
         sd.fork()
         if ours_wgrad:

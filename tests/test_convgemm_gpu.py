@@ -103,6 +103,35 @@ def test_conv1x1_bn_backward_epilogue(M, K, N):
     torch.testing.assert_close(part[1].sum(0).cpu(), (cg * ((z - mean) * invstd)).sum(0), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("M,K,N", [(300, 256, 64), (1000, 512, 128), (4099, 256, 64), (517, 1024, 256)])
+def test_bn_backward_prologue_matches_apply_then_gemm(M, K, N):
+    """conv_gemm(a=d, a2=z, bwd=coef) == bn_bwd_partials(d, z) then conv_gemm on its output: the
+    data gradient of the previous BN computed while staging A (and stored as a third output),
+    then the GEMM with epilogue 3 (ReLU mask + the next BN's backward sums)."""
+    g = _gen(M + K)
+    d, z = _rnd(M, K, g=g), _rnd(M, K, g=g)
+    gamma, mean, invstd = torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1, torch.rand(K) + 0.5
+    xhat = (z - mean) * invstd
+    part = torch.stack([d.sum(0, keepdim=True), (d * xhat).sum(0, keepdim=True)]).to(DEV).contiguous()
+    b, z2 = _rnd(N, K, g=g, scale=K ** -0.5), _rnd(M, N, g=g)
+    mc = _coef(N, g)
+    m2, i2 = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+    args = (_bf(b), [M, 1, M, 1, 1, 1, 0], None, 3, _bf(z2), None, mc.to(DEV), m2.to(DEV), i2.to(DEV))
+    dz_ref, dg_ref, db_ref = native().bn_bwd_partials(_bf(d), _bf(z), part, gamma.to(DEV), mean.to(DEV), invstd.to(DEV))
+    c_ref, p_ref = native().conv_gemm(dz_ref, *args)
+    dg, db, coef = native().bn_bwd_coef(part, gamma.to(DEV), mean.to(DEV), invstd.to(DEV), M)
+    torch.testing.assert_close(dg, dg_ref)
+    torch.testing.assert_close(db, db_ref)
+    c, p, dz = native().conv_gemm(_bf(d), *args, a2=_bf(z), bwd=coef)
+    # same formula, FMA contraction may differ by one bf16 ulp
+    assert (dz != dz_ref).float().mean().item() < 1e-2
+    torch.testing.assert_close(dz.float(), dz_ref.float(), rtol=8e-3, atol=1e-3)
+    ref_dz = gamma * invstd * (d - d.mean(0) - xhat * (d * xhat).mean(0))
+    _close(dz, ref_dz)
+    _close(c, c_ref, tol=1e-2, amax=0.05)
+    torch.testing.assert_close(p.sum(1), p_ref.sum(1), rtol=2e-3, atol=2e-2)
+
+
 def test_conv1x1_stride2_gather_and_strided_residual():
     n, h, w, K, N = 3, 13, 11, 128, 64
     g = _gen(3)
@@ -118,6 +147,22 @@ def test_conv1x1_stride2_gather_and_strided_residual():
     ref = a2 @ b2.t()
     ref.view(n, h, w, K)[:, ::2, ::2] += t.view(n, oh, ow, K)
     _close(c2, ref)
+
+
+@pytest.mark.parametrize("n,cin,cout,hw", [(2, 64, 64, 56), (3, 128, 128, 28), (1, 128, 64, 28), (2, 64, 192, 56)])
+def test_conv3x3_patch_wgrad(n, cin, cout, hw):
+    """The 3x3 patch weight-gradient kernel (stride 1, 56- / 28-wide maps, <= 128 channels; the
+    image borders are the patch halo) vs fp32 autograd, and vs the im2col kernels it replaces
+    (PS_AMD_WGRAD_PATCH_MAX_C is read once per process, so the comparison goes through the
+    ResNet-wide shapes here and the generic 14-wide path above)."""
+    g = _gen(n + cin + cout + hw)
+    x = _rnd(n, hw, hw, cin, g=g)
+    dz = _rnd(n * hw * hw, cout, g=g)
+    wv = torch.zeros(cout, cin, 3, 3, requires_grad=True)
+    yr = F.conv2d(x.permute(0, 3, 1, 2), wv, None, 1, 1)
+    dw_ref = torch.autograd.grad(yr, wv, dz.view(n, hw, hw, cout).permute(0, 3, 1, 2))[0]
+    dw = native().conv_wgrad(_bf(dz), _bf(x.reshape(-1, cin)), geo(hw, hw, 3, 1, 1))
+    _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, 9 * cin))
 
 
 @pytest.mark.parametrize("cin,cout,hw,stride", [(64, 64, 14, 1), (128, 128, 9, 2), (64, 128, 7, 1)])
