@@ -1034,11 +1034,14 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
 // every fragment address is linear: a tap's kw and a k-step's pixel offset become instruction
 // immediates and the whole loop runs on 1 + 14 loop-invariant address registers (W % 4 == 0: a
 // 4-pixel group never straddles an output row).
+// Stride 2 (S = 2): the stage's R output rows touch 2R + 1 input rows; the patch columns are stored
+// split by parity ([column parity][row][column / 2]), so tap kw reads parity kw & 1 at column
+// ow + kw / 2 -- 4 consecutive output pixels are again 4 consecutive 64-B rows, and kw is again an
+// immediate (a two-stage ring: the 2x-wide patch fills the LDS).
 // 12 waves: (kh, n half, c half) -> 32 n x 3 taps x 32 c each, one dz fragment + three patch
 // fragments per three MFMAs.  Block = (n tile 64, c tile 64, pixel split); fp32 per-split slabs,
 // fixed-order reduction (deterministic) as the other weight-gradient kernels.
 constexpr int kPP = 112;  // pixels per stage
-constexpr int kPS = 3;    // LDS ring depth
 
 template <int OFF>
 __device__ __forceinline__ s16x4 ds_tr_off(uint32_t a) {
@@ -1047,20 +1050,22 @@ __device__ __forceinline__ s16x4 ds_tr_off(uint32_t a) {
   return v;
 }
 
-template <int W>
+template <int W, int S>
 __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgradArgs p, int stages_per_split) {
-  constexpr int R = kPP / W, PW = W + 2, PR = R + 2;
-  static_assert(kPP % W == 0 && W % 4 == 0, "a stage is whole rows; 4-pixel groups stay in a row");
+  constexpr int OW = W / S, R = kPP / OW, PR = S * (R - 1) + 3;  // output rows / input rows per stage
+  constexpr int PW = S == 1 ? W + 2 : (W + 2) / 2;            // slots per patch row (per column parity)
+  constexpr int KPS = S == 1 ? 3 : 2;                         // LDS ring depth
+  static_assert(kPP % OW == 0 && OW % 4 == 0 && W % S == 0, "a stage is whole rows; 4-pixel groups stay in a row");
   constexpr int GPL = kPP * 64;                         // dz plane bytes (32 n per row)
   constexpr int GB = 2 * GPL;                           // dz tile bytes
-  constexpr int PPL = PR * PW * 64;                     // patch plane bytes
+  constexpr int PPL = S * PR * PW * 64;                 // patch plane bytes
   constexpr int PB = ((2 * PPL + 1023) / 1024) * 1024;  // patch tile bytes (whole 1 KiB DMA pieces)
   constexpr int GI = GB / 1024, PI = PB / 1024;         // DMA pieces
   constexpr int NI = GI + PI;                           // per stage, dealt over the 12 waves
   constexpr int STB = GB + PB;                          // stage bytes
   constexpr int MAXW = (NI + 11) / 12;                  // pieces of the busiest wave
-  static_assert(GB % 1024 == 0 && MAXW <= 4 && kPS * STB <= 160 * 1024, "stage shape");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kPS * STB / 2];
+  static_assert(GB % 1024 == 0 && MAXW <= 8 && (KPS == 2 || MAXW <= 4) && KPS * STB <= 160 * 1024, "stage shape");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[KPS * STB / 2];
 
   const ConvGeo& g = p.g;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1077,10 +1082,10 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
   // chunk ch of a plane = row ch / 4, 8 channels (ch % 4); sources recomputed per stage
   const int myn = (NI - wave + 11) / 12;  // wave-uniform: MAXW or MAXW - 1
   auto issue = [&](int st, int buf) {
-    const int q = sb + st, img = q / rows_per_img, oh0 = (q - img * rows_per_img) * R;
+    const int q = sb + st, img = q / rows_per_img, ih0 = (q - img * rows_per_img) * R * S - 1;
     uint8_t* base = reinterpret_cast<uint8_t*>(lds) + buf * STB;
     const uint16_t* gsrc = p.dz + static_cast<int64_t>(q) * kPP * p.N + n0;
-    const uint16_t* xsrc = p.x + (static_cast<int64_t>(img) * g.H + oh0 - 1) * g.W * g.C + c0;
+    const uint16_t* xsrc = p.x + (static_cast<int64_t>(img) * g.H + ih0) * g.W * g.C + c0;
 #pragma unroll
     for (int j = 0; j < MAXW; ++j) {
       if (j >= myn) break;  // wave-uniform
@@ -1089,9 +1094,10 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
       if (i < GI) {  // wave-uniform
         const int ch = i * 64 + lane, pl = ch / (GPL / 16), r = ch - pl * (GPL / 16);
         src = gsrc + static_cast<int64_t>(r >> 2) * p.N + pl * 32 + (r & 3) * 8;
-      } else {  // slot (pr, pc) = input pixel (oh0 - 1 + pr, pc - 1); halo / out-of-map / tail: zero page
+      } else {  // slot (parity, pr, j): input pixel (ih0 + pr, S j + parity - 1); halo / out-of-map: zero
         const int ch = (i - GI) * 64 + lane, pl = ch / (PPL / 16), r = ch - pl * (PPL / 16), slot = r >> 2;
-        const int pr = slot / PW, pc = slot - pr * PW, ih = oh0 - 1 + pr;
+        const int par = slot / (PR * PW), rem = slot - par * (PR * PW), pr = rem / PW;
+        const int pc = S * (rem - pr * PW) + par, ih = ih0 + pr;
         const bool ok = pl < 2 && pc >= 1 && pc <= W && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H);
         src = ok ? xsrc + (static_cast<int64_t>(pr) * W + (pc - 1)) * g.C + pl * 32 + (r & 3) * 8 : kZeroPage;
       }
@@ -1110,8 +1116,8 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
   for (int s = 0; s < 7; ++s)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int m = 16 * s + 4 * h + mrow, oh = m / W, ow = m - oh * W;
-      xa[s][h] = static_cast<uint32_t>(GB + chf * PPL + ((oh + kh) * PW + ow) * 64 + colb);
+      const int m = 16 * s + 4 * h + mrow, oh = m / OW, ow = m - oh * OW;
+      xa[s][h] = static_cast<uint32_t>(GB + chf * PPL + ((S * oh + kh) * PW + ow) * 64 + colb);
     }
 
   f32x16 acc[3];
@@ -1122,13 +1128,16 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
   auto mma = [&](int buf) {
     const uint32_t b0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const lds_s16x4*)lds)) + buf * STB;
     const uint32_t gb = b0 + ga;
-#define PSAMD_PATCH_STEP(S)                                                                              \
+    // byte offsets of taps kw = 1, 2 from kw = 0: the next slot (stride 1); the odd-column parity
+    // block / the next even slot (stride 2)
+    constexpr int K1 = S == 1 ? 64 : PR * PW * 64, K2 = S == 1 ? 128 : 64;
+#define PSAMD_PATCH_STEP(Q)                                                                              \
   {                                                                                                      \
-    s16x4 a0 = ds_tr_off<(16 * S) * 64>(gb), a1 = ds_tr_off<(16 * S + 4) * 64>(gb);                      \
-    const uint32_t x0 = b0 + xa[S][0], x1 = b0 + xa[S][1];                                               \
+    s16x4 a0 = ds_tr_off<(16 * Q) * 64>(gb), a1 = ds_tr_off<(16 * Q + 4) * 64>(gb);                      \
+    const uint32_t x0 = b0 + xa[Q][0], x1 = b0 + xa[Q][1];                                               \
     s16x4 p00 = ds_tr_off<0>(x0), p01 = ds_tr_off<0>(x1);                                                \
-    s16x4 p10 = ds_tr_off<64>(x0), p11 = ds_tr_off<64>(x1);                                              \
-    s16x4 p20 = ds_tr_off<128>(x0), p21 = ds_tr_off<128>(x1);                                            \
+    s16x4 p10 = ds_tr_off<K1>(x0), p11 = ds_tr_off<K1>(x1);                                              \
+    s16x4 p20 = ds_tr_off<K2>(x0), p21 = ds_tr_off<K2>(x1);                                              \
     /* the reads land asynchronously: the wait redefines their registers, so no MFMA is scheduled  */   \
     /* above it and no register is reused before it                                               */   \
     asm volatile("s_waitcnt lgkmcnt(0)"                                                                  \
@@ -1153,11 +1162,11 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
 #undef PSAMD_PATCH_STEP
   };
 
-  const int pre = nst < kPS - 1 ? nst : kPS - 1;
+  const int pre = nst < KPS - 1 ? nst : KPS - 1;
   for (int st = 0; st < pre; ++st) issue(st, st);
   for (int st = 0; st < nst; ++st) {
     // this wave's DMAs of stage st landed (the next stage's may stay in flight), then everyone's
-    if (st + 1 < nst) {
+    if (KPS == 3 && st + 1 < nst) {
       if (myn == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else if (myn == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else if (myn == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -1166,8 +1175,8 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
-    if (st + kPS - 1 < nst) issue(st + kPS - 1, (st + kPS - 1) % kPS);
-    mma(st % kPS);
+    if (st + KPS - 1 < nst) issue(st + KPS - 1, (st + KPS - 1) % KPS);
+    mma(st % KPS);
   }
   // slab[split][n][k], k = (kh * 3 + kw) * C + c
   float* sl = p.ws + static_cast<int64_t>(split) * p.N * p.K;
@@ -1370,8 +1379,8 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
 }  // namespace
 
 namespace {
-// The patch kernel's shapes: 3x3 / stride 1 / pad 1 maps 56 or 28 wide (the ResNet-50 64- and
-// 128-channel stages), channels up to PS_AMD_WGRAD_PATCH_MAX_C (default 128; 0 = never).
+// The patch kernel's shapes: 3x3 / pad 1, stride 1 on 56- or 28-wide maps, stride 2 on a 56-wide map
+// (the ResNet-50 64- and 128-channel stages), channels up to PS_AMD_WGRAD_PATCH_MAX_C (default 128; 0 = never).
 int patch_max_c() {
   static const int v = [] {
     const char* e = std::getenv("PS_AMD_WGRAD_PATCH_MAX_C");
@@ -1381,9 +1390,13 @@ int patch_max_c() {
 }
 
 bool patch_ok(const ConvGeo& g, int M, int N, bool pro) {
-  return !pro && g.ks == 3 && (g.ksw == 0 || g.ksw == 3) && g.stride == 1 && g.pad == 1 && g.H == g.OH &&
-         g.W == g.OW && (g.W == 56 || g.W == 28) && g.OH % (kPP / g.W) == 0 && g.C % 64 == 0 && N % 64 == 0 &&
-         g.C <= patch_max_c() && M % kPP == 0 && g.RH == 0;
+  if (pro || g.ks != 3 || !(g.ksw == 0 || g.ksw == 3) || g.pad != 1 || g.C % 64 != 0 || N % 64 != 0 ||
+      g.C > patch_max_c() || M % kPP != 0 || g.RH != 0)
+    return false;
+  if (g.stride == 1)  // 56- / 28-wide maps
+    return g.H == g.OH && g.W == g.OW && (g.W == 56 || g.W == 28) && g.OH % (kPP / g.W) == 0;
+  // stride 2: the 56-wide map -> 28 x 28
+  return g.stride == 2 && g.W == 56 && g.H % 2 == 0 && g.OH == g.H / 2 && g.OW == 28 && g.OH % 4 == 0;
 }
 
 struct PPlan {
@@ -1437,8 +1450,9 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
   if (a.db == nullptr && patch_ok(a.g, a.M, a.N, a.pro != nullptr)) {
     const PPlan w = pplan(a.g, a.M, a.N);
     const int nblk = w.tiles * w.nsplit;
-    if (a.g.W == 56) hipLaunchKernelGGL(conv_wgrad_patch_kernel<56>, dim3(nblk), dim3(768), 0, s, a, w.spp);
-    else hipLaunchKernelGGL(conv_wgrad_patch_kernel<28>, dim3(nblk), dim3(768), 0, s, a, w.spp);
+    if (a.g.stride == 2) hipLaunchKernelGGL((conv_wgrad_patch_kernel<56, 2>), dim3(nblk), dim3(768), 0, s, a, w.spp);
+    else if (a.g.W == 56) hipLaunchKernelGGL((conv_wgrad_patch_kernel<56, 1>), dim3(nblk), dim3(768), 0, s, a, w.spp);
+    else hipLaunchKernelGGL((conv_wgrad_patch_kernel<28, 1>), dim3(nblk), dim3(768), 0, s, a, w.spp);
     slab_reduce(a, w.nsplit, w.groups, s);
     return;
   }

@@ -152,11 +152,16 @@ def _dgrad_s2_min_c() -> int:
 WGRAD3X3_MIN_C = 256
 
 
-def _patch_wgrad_ok(h: int, w: int, c1: int, c2: int) -> bool:
-    """The shapes csrc conv_wgrad_patch_kernel takes (mirrors convgemm.hip patch_ok): 3x3 stride 1
-    on 56- or 28-wide maps of whole 112-pixel stages, c1 <= PS_AMD_WGRAD_PATCH_MAX_C (128)."""
+def _patch_wgrad_ok(h: int, w: int, c1: int, c2: int, s: int) -> bool:
+    """The shapes csrc conv_wgrad_patch_kernel takes (mirrors convgemm.hip patch_ok): 3x3 / pad 1,
+    stride 1 on 56- or 28-wide input maps, stride 2 on a 56-wide one (whole 112-pixel stages),
+    c1 <= PS_AMD_WGRAD_PATCH_MAX_C (128)."""
     cap = int(os.environ.get("PS_AMD_WGRAD_PATCH_MAX_C", "128"))
-    return w in (56, 28) and h % (112 // w) == 0 and c1 % 64 == 0 and c2 % 64 == 0 and c1 <= cap
+    if not (c1 % 64 == 0 and c2 % 64 == 0 and c1 <= cap):
+        return False
+    if s == 1:
+        return w in (56, 28) and h % (112 // w) == 0
+    return s == 2 and w == 56 and h % 8 == 0
 
 
 def _conv3x3_enabled() -> bool:
@@ -280,9 +285,9 @@ class _BottleneckFn(torch.autograd.Function):
         ours_dgrad = _conv3x3_enabled() and (s == 1 or (s == 2 and h % 2 == 0 and w % 2 == 0
                                                          and w2.shape[1] >= _dgrad_s2_min_c()))
         # weight grad on the wide-tile kernel from 256 input channels up (on par with / faster than
-        # MIOpen there: profiles/r2_wgrad_probe.jsonl), on the patch kernel at 64 / 128 channels,
-        # stride 1 (csrc conv_wgrad_patch_kernel); MIOpen for the one stride-2 128-channel layer
-        ours_wgrad = _conv3x3_enabled() and (c1 >= WGRAD3X3_MIN_C or (s == 1 and _patch_wgrad_ok(h, w, c1, c2)))
+        # MIOpen there: profiles/r2_wgrad_probe.jsonl), on the patch kernel at 64 / 128 channels
+        # (csrc conv_wgrad_patch_kernel: 2.4x / 1.6x MIOpen, profiles/r3_wgrad_probe_patch.jsonl)
+        ours_wgrad = _conv3x3_enabled() and (c1 >= WGRAD3X3_MIN_C or _patch_wgrad_ok(h, w, c1, c2, s))
         dy1 = dw2 = None
         sd.fork()
         if ours_wgrad:

@@ -43,12 +43,16 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--it", type=int, default=5)
     ap.add_argument("--miopen", type=int, default=1)
+    ap.add_argument("--only", default="", help="comma list of shape substrings, e.g. '3x3 56x56,3x3 28x28'")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     nat = native()
     n = a.batch
     tot = {"ours": 0.0, "miopen": 0.0}
     for h, ci, co, ks, s, calls in SHAPES:
+        name = f"{ks}x{ks} {h}x{h} {ci}->{co} s{s}"
+        if a.only and not any(o in name for o in a.only.split(",")):
+            continue
         g = geo(h, h, ks, s, ks // 2)
         oh = g[2]
         M = n * oh * oh

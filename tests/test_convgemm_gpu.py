@@ -149,19 +149,21 @@ def test_conv1x1_stride2_gather_and_strided_residual():
     _close(c2, ref)
 
 
-@pytest.mark.parametrize("n,cin,cout,hw", [(2, 64, 64, 56), (3, 128, 128, 28), (1, 128, 64, 28), (2, 64, 192, 56)])
-def test_conv3x3_patch_wgrad(n, cin, cout, hw):
+@pytest.mark.parametrize("n,cin,cout,hw,stride", [(2, 64, 64, 56, 1), (3, 128, 128, 28, 1), (1, 128, 64, 28, 1),
+                                                  (2, 64, 192, 56, 1), (2, 128, 128, 56, 2), (1, 64, 128, 56, 2)])
+def test_conv3x3_patch_wgrad(n, cin, cout, hw, stride):
     """The 3x3 patch weight-gradient kernel (stride 1, 56- / 28-wide maps, <= 128 channels; the
     image borders are the patch halo) vs fp32 autograd, and vs the im2col kernels it replaces
     (PS_AMD_WGRAD_PATCH_MAX_C is read once per process, so the comparison goes through the
     ResNet-wide shapes here and the generic 14-wide path above)."""
     g = _gen(n + cin + cout + hw)
     x = _rnd(n, hw, hw, cin, g=g)
-    dz = _rnd(n * hw * hw, cout, g=g)
+    oh = hw // stride
+    dz = _rnd(n * oh * oh, cout, g=g)
     wv = torch.zeros(cout, cin, 3, 3, requires_grad=True)
-    yr = F.conv2d(x.permute(0, 3, 1, 2), wv, None, 1, 1)
-    dw_ref = torch.autograd.grad(yr, wv, dz.view(n, hw, hw, cout).permute(0, 3, 1, 2))[0]
-    dw = native().conv_wgrad(_bf(dz), _bf(x.reshape(-1, cin)), geo(hw, hw, 3, 1, 1))
+    yr = F.conv2d(x.permute(0, 3, 1, 2), wv, None, stride, 1)
+    dw_ref = torch.autograd.grad(yr, wv, dz.view(n, oh, oh, cout).permute(0, 3, 1, 2))[0]
+    dw = native().conv_wgrad(_bf(dz), _bf(x.reshape(-1, cin)), geo(hw, hw, 3, stride, 1))
     _close(dw, dw_ref.permute(0, 2, 3, 1).reshape(cout, 9 * cin))
 
 
