@@ -36,6 +36,8 @@ def bench(fn, it=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--variants", type=int, default=0,
+                    help="also time each shape without the statistics epilogue / without the BN prologue")
     a = ap.parse_args()
     nat = native()
     for h, ci, co, pro in SHAPES:
@@ -48,10 +50,15 @@ def main():
         tb = bench(lambda: x @ w.t())
         fl = 2.0 * M * ci * co
         by = 2.0 * M * (ci + co)
-        print(json.dumps({"shape": f"1x1 {h}x{h} {ci}->{co}" + (" +bn" if pro else ""), "us": round(t, 1),
-                          "tflops": round(fl / t / 1e6, 1), "tbps": round(by / t / 1e6, 2),
-                          "blas_us": round(tb, 1), "persist_nk_pro": os.environ.get("PS_AMD_PERSIST_NK_PRO", "2")}),
-              flush=True)
+        rec = {"shape": f"1x1 {h}x{h} {ci}->{co}" + (" +bn" if pro else ""), "us": round(t, 1),
+               "tflops": round(fl / t / 1e6, 1), "tbps": round(by / t / 1e6, 2),
+               "blas_us": round(tb, 1), "persist_nk_pro": os.environ.get("PS_AMD_PERSIST_NK_PRO", "4")}
+        if a.variants:
+            rec["no_stats_us"] = round(bench(lambda: nat.conv_gemm(x, w, geo(h, h), coef, 0)), 1)
+            if pro:
+                rec["no_pro_us"] = round(bench(lambda: nat.conv_gemm(x, w, geo(h, h), None, 1, None, ks)), 1)
+                rec["no_pro_no_stats_us"] = round(bench(lambda: nat.conv_gemm(x, w, geo(h, h), None, 0)), 1)
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
