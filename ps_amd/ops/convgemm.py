@@ -17,13 +17,15 @@ MFMA GEMMs with the neighbouring BatchNorm passes folded into them:
             conv3 data grad -> ReLU mask + bn2 backward sums (GEMM epilogue), conv3 weight grad
             with relu(bn2(z2)) recomputed in the GEMM prologue, bn2 apply
             conv2 data grad -> ReLU mask + bn1 backward sums (GEMM epilogue; stride 2 as four
-            phase GEMMs), weight grad (C >= 256; MIOpen below)
+            phase GEMMs), weight grad (wide split-K kernel from 256 channels, the patch kernel
+            at 64 / 128: no MIOpen solver left)
             conv1 data grad + identity (dout masked by the bits) / downsample gradient (GEMM
             epilogue), weight grads.
 
 Across blocks: block i's conv1 data-grad epilogue also runs block i-1's bn3 backward reduce
 (epilogues 6/7/8: mask by block i-1's output bits, sums against its z3), so block i-1's bn3
-backward is one apply pass.  The hand-off is a ``_Link`` set up in forward when block i's input
+backward is one apply pass -- or, at 256 channels, no pass at all: block i-1's conv3 data-grad GEMM
+applies it while staging its A tile from (gradient, z3) and stores dz3 for the weight gradient.  The hand-off is a ``_Link`` set up in forward when block i's input
 IS block i-1's output; block i-1 uses the partials only if the gradient it receives is exactly
 the tensor block i produced (same storage, same version) -- any other consumer of the block
 output makes autograd sum into a different tensor and the plain reduce runs instead.
