@@ -1212,6 +1212,56 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   else static_cast<float*>(out)[blockIdx.y * E + e] = v;
 }
 
+// ------------------------------------------------------------------------------ weight_prep
+// The data-gradient GEMMs read every bottleneck weight in a second layout: the 1x1 weights
+// transposed, the stride-1 3x3 weight flipped and channel-transposed, the stride-2 3x3 weight
+// gathered into its four phase matrices.  Built per weight these were ~70 tiny copy / flip /
+// gather kernels per ResNet-50 step (0.64 ms); here ONE launch builds all of them, one job per
+// blockIdx.y, at the start of the forward (the weights are final for the step by then).
+// Destination-major iteration: coalesced writes, gathered reads (every weight is L2-resident).
+struct WPrepJob {
+  const uint16_t* src;  // channels_last weight [A][ks][ks][B] (A = output channels, B = input)
+  uint16_t* dst;
+  int kind;             // 0: 1x1 [A][B] -> [B][A]; 1: 3x3 -> [B][3][3][A] flipped; 2: 3x3 -> 4 phases
+  int A, B;
+};
+
+__global__ __launch_bounds__(256) void weight_prep_kernel(const WPrepJob* __restrict__ jobs) {
+  const WPrepJob jb = jobs[blockIdx.y];
+  const int A = jb.A, B = jb.B;
+  const int64_t E = (jb.kind == 0 ? 1 : 9) * static_cast<int64_t>(A) * B;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < E; e += static_cast<int64_t>(gridDim.x) * 256) {
+    int64_t so;
+    if (jb.kind == 0) {  // dst[b][a] = src[a][b]
+      const int64_t b = e / A, a = e - b * A;
+      so = a * B + b;
+    } else if (jb.kind == 1) {  // dst[c][kh][kw][n] = src[n][2 - kh][2 - kw][c]
+      const int64_t c = e / (9 * A);
+      const int r = static_cast<int>(e - c * 9 * A), kh = r / (3 * A), kw = (r / A) % 3, n = r % A;
+      so = ((static_cast<int64_t>(n) * 3 + (2 - kh)) * 3 + (2 - kw)) * B + c;
+    } else {  // phases (a, b) = (0,0), (0,1), (1,0), (1,1): [B][nh][nw][A], taps 1 (even) or {2, 0} (odd)
+      const int64_t AB = static_cast<int64_t>(A) * B;
+      int ph;
+      int64_t q;
+      if (e < AB) { ph = 0; q = e; }
+      else if (e < 3 * AB) { ph = 1; q = e - AB; }
+      else if (e < 5 * AB) { ph = 2; q = e - 3 * AB; }
+      else { ph = 3; q = e - 5 * AB; }
+      const int pa = ph >> 1, pb = ph & 1, nh = pa ? 2 : 1, nw = pb ? 2 : 1;
+      const int64_t c1 = q / (nh * nw * A);
+      const int r = static_cast<int>(q - c1 * nh * nw * A), dh = r / (nw * A), dw = (r / A) % nw, c2 = r % A;
+      const int kh = pa ? (dh ? 0 : 2) : 1, kw = pb ? (dw ? 0 : 2) : 1;
+      so = ((static_cast<int64_t>(c2) * 3 + kh) * 3 + kw) * B + c1;
+    }
+    jb.dst[e] = jb.src[so];
+  }
+}
+
+void launch_weight_prep(const void* jobs, int njobs, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(64, njobs), dim3(256), 0, s, static_cast<const WPrepJob*>(jobs));
+}
+
 // ------------------------------------------------------------------------------ launchers
 // Forward tile plan.  HBM-bound shallow-K layers (<= 2 stages; <= 4 with the BN prologue, whose
 // register staging gains most from the cross-tile prefetch: scripts/probe_conv_fwd.py) run a

@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
-from ..ops.convgemm import deferred_bn_counters, fused_block_ok, fused_bottleneck
+from ..ops.convgemm import deferred_bn_counters, fused_block_ok, fused_bottleneck, prepare_backward_weights
 from ..ops.pool import MaxPool2d, global_avg_pool
 
 
@@ -84,6 +84,9 @@ class ResNet(nn.Module):
                 if isinstance(m, Bottleneck):
                     nn.init.zeros_(m.bn3.weight)
 
+    def _blocks(self):
+        return [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+
     def _make_layer(self, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
         downsample = None
         if stride != 1 or self.inplanes != planes * 4:
@@ -101,6 +104,8 @@ class ResNet(nn.Module):
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         with deferred_bn_counters():
+            if self.fused_bn and self.training and x.is_cuda:
+                prepare_backward_weights(self._blocks())  # all data-grad weight layouts, one kernel
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.fused_bn:
             x = global_avg_pool(x)  # NHWC gradient straight into the last block's backward

@@ -241,6 +241,7 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, obits, zd,
                               m1, i1, cf1, m2, i2, cf2, m3, i3, md, idd)
         ctx.dims = (n, h, w, s, oh, ow)
+        ctx.prep = _prep_for(blk, w1, w2, w3)  # backward weight layouts built for this forward
         ctx.link_in = link_in  # block i-1's bn3: its reduce runs in our conv1 data-grad epilogue
         ctx.link_out = _Link(z3, obits, m3, i3) if _fold_enabled() else None
         return image(out, n, oh, ow)
@@ -255,6 +256,8 @@ class _BottleneckFn(torch.autograd.Function):
         d2 = rows(dout)
         # weight gradients run on the side stream, overlapped with this data-gradient chain
         sd = _side.Fork(d2.device, (w1, w2, w3, wd))
+        pw = ctx.prep
+        w3t = pw[1] if pw else _mat(w3).t()
         lk = ctx.link_out
         dz3 = None
         if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
@@ -264,7 +267,7 @@ class _BottleneckFn(torch.autograd.Function):
                 # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
                 # the weight gradient: no separate apply pass over the widest tensors
                 dg3, db3, cb3 = nat.bn_bwd_coef(lk.part, g3, m3, i3, d2.shape[0])
-                gy2, p2, dz3 = nat.conv_gemm(d2, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2, a2=z3, bwd=cb3)
+                gy2, p2, dz3 = nat.conv_gemm(d2, w3t, go, None, 3, z2r, None, cf2, m2, i2, a2=z3, bwd=cb3)
             else:
                 dz3, dg3, db3 = nat.bn_bwd_partials(d2, z3, lk.part, g3, m3, i3)
                 gy2 = None
@@ -281,7 +284,7 @@ class _BottleneckFn(torch.autograd.Function):
         sd.fork()
         dw3 = sd.run(lambda: nat.conv_wgrad(dz3, z2r, go, cf2), dz3, z2r, cf2, like=w3)
         if gy2 is None:
-            gy2, p2 = nat.conv_gemm(dz3, _mat(w3).t(), go, None, 3, z2r, None, cf2, m2, i2)
+            gy2, p2 = nat.conv_gemm(dz3, w3t, go, None, 3, z2r, None, cf2, m2, i2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)
         c1, c2 = w2.shape[1], w2.shape[0]
         ours_dgrad = _conv3x3_enabled() and (s == 1 or (s == 2 and h % 2 == 0 and w % 2 == 0
@@ -307,15 +310,16 @@ class _BottleneckFn(torch.autograd.Function):
             # data grad = the forward GEMM over dz2 with the flipped, transposed weight; its epilogue
             # applies bn1's ReLU mask and reduces bn1's backward sums (no separate reduce pass)
             if s == 1:
-                gy1, p1b = nat.conv_gemm(dz2, _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1, None, cf1, m1, i1)
+                gy1, p1b = nat.conv_gemm(dz2, pw[2] if pw else _mat3_dgrad(w2), geo(oh, ow, 3, 1, 1), None, 3, z1,
+                                         None, cf1, m1, i1)
             else:  # four stride-1 phase GEMMs, each writing every other dx row (no zero fill)
-                gy1, p1b = nat.conv_dgrad_s2(dz2, _phase_weights(w2), h, w, 3, z1, cf1, m1, i1)
+                gy1, p1b = nat.conv_dgrad_s2(dz2, pw[2] if pw else _phase_weights(w2), h, w, 3, z1, cf1, m1, i1)
             dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
             dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
         sd.fork()
         dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
-        w1t = _mat(w1).t()
+        w1t = pw[0] if pw else _mat(w1).t()
         dwd = dgd = dbd = None
         li = ctx.link_in
         fold = li is not None and _fold_enabled()
@@ -324,7 +328,7 @@ class _BottleneckFn(torch.autograd.Function):
             dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
             sd.fork()
             dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
-            t = nat.conv_gemm(dzd, _mat(wd).t(), go)[0]
+            t = nat.conv_gemm(dzd, pw[3] if pw else _mat(wd).t(), go)[0]
             epi = 4 if s == 2 else 2
             dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
         else:
@@ -372,6 +376,77 @@ def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
 
 _tls = threading.local()
 
+# Backward weight layouts (transposed 1x1, flipped / phase-split 3x3) of every fused block, built
+# in ONE kernel per forward (csrc weight_prep) instead of ~70 copy / flip / gather kernels per step.
+# Cache: weight storage pointers -> (job table, per-block output tensors); the PS binds weights to
+# fixed slot views, so the table is built once per slot.
+_PREP_CACHE: "dict" = {}
+
+
+def _prep_ok(blk: nn.Module) -> bool:
+    ws = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight] + (
+        [blk.downsample[0].weight] if blk.downsample is not None else [])
+    return (getattr(blk, "fuse_block", False) and all(w.is_cuda and w.dtype == torch.bfloat16 for w in ws)
+            and blk.conv2.weight.is_contiguous(memory_format=torch.channels_last)
+            and all(w.is_contiguous() for w in [blk.conv1.weight, blk.conv3.weight] + ws[3:]))
+
+
+def prepare_backward_weights(blocks) -> None:
+    """Build the backward weight layouts of ``blocks`` (the fused bottlenecks of one forward) in
+    one launch; _BottleneckFn picks them up through the thread-local set (cleared when the
+    enclosing ``deferred_bn_counters`` context ends)."""
+    if os.environ.get("PS_AMD_WEIGHT_PREP", "1") == "0":
+        return
+    blks = [b for b in blocks if _prep_ok(b)]
+    if not blks:
+        return
+    key = tuple((id(b), b.conv1.weight.data_ptr(), b.conv2.weight.data_ptr(), b.conv3.weight.data_ptr(),
+                 b.downsample[0].weight.data_ptr() if b.downsample is not None else 0) for b in blks)
+    ent = _PREP_CACHE.get(key)
+    if ent is None:
+        rows, outs = [], {}
+        dev = blks[0].conv1.weight.device
+
+        def job(src, kind, a, b):
+            n = (1 if kind == 0 else 9) * a * b
+            dst = torch.empty(n, dtype=torch.bfloat16, device=dev)
+            rows.append([src.data_ptr(), dst.data_ptr(), kind | (a << 32), b])
+            return dst
+
+        for b in blks:
+            w1, w2, w3 = b.conv1.weight, b.conv2.weight, b.conv3.weight
+            c2, c1 = w2.shape[0], w2.shape[1]
+            w1t = job(w1, 0, w1.shape[0], w1.shape[1]).view(w1.shape[1], w1.shape[0])
+            w3t = job(w3, 0, w3.shape[0], w3.shape[1]).view(w3.shape[1], w3.shape[0])
+            if b.conv2.stride[0] == 1:
+                w2d = job(w2, 1, c2, c1).view(c1, 9 * c2)
+            else:
+                flat = job(w2, 2, c2, c1)
+                w2d, o = [], 0
+                for nh, nw in ((1, 1), (1, 2), (2, 1), (2, 2)):
+                    k = nh * nw * c2
+                    w2d.append(flat[o:o + c1 * k].view(c1, k))
+                    o += c1 * k
+            wdt = None
+            if b.downsample is not None:
+                wd = b.downsample[0].weight
+                wdt = job(wd, 0, wd.shape[0], wd.shape[1]).view(wd.shape[1], wd.shape[0])
+            outs[id(b)] = (w1t, w3t, w2d, wdt, (w1.data_ptr(), w2.data_ptr(), w3.data_ptr()))
+        ent = (torch.tensor(rows, dtype=torch.int64).to(dev), outs)
+        if len(_PREP_CACHE) >= 4:
+            _PREP_CACHE.pop(next(iter(_PREP_CACHE)))
+        _PREP_CACHE[key] = ent
+    native().weight_prep(ent[0])
+    _tls.prep = ent[1]
+
+
+def _prep_for(blk, w1, w2, w3):
+    prep = getattr(_tls, "prep", None)
+    ent = prep.get(id(blk)) if prep else None
+    if ent is None or ent[4] != (w1.data_ptr(), w2.data_ptr(), w3.data_ptr()):
+        return None
+    return ent
+
 
 @contextlib.contextmanager
 def deferred_bn_counters():
@@ -384,6 +459,7 @@ def deferred_bn_counters():
         yield
     finally:
         _tls.last = None
+        _tls.prep = None
         pending, _tls.pending = _tls.pending, prev
         if pending:
             torch._foreach_add_(pending, 1)

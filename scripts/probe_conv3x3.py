@@ -38,6 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--it", type=int, default=10)
+    ap.add_argument("--miopen", type=int, default=1)
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True  # as bench.py: MIOpen find picks its best solver
     nat = native()
@@ -52,11 +53,14 @@ def main():
         w = (torch.randn(c, c, 3, 3, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
         dz = torch.randn(n, c, oh, oh, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         rec = {"shape": f"3x3 {h}x{h} {c} s{s}", "M": M}
-        rec["miopen_fwd_us"] = bench(lambda: F.conv2d(x, w, None, s, 1), a.it)
-        rec["miopen_dgrad_us"] = bench(lambda: torch.ops.aten.convolution_backward(
-            dz, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]), a.it)
-        rec["miopen_wgrad_us"] = bench(lambda: torch.ops.aten.convolution_backward(
-            dz, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]), a.it)
+        if a.miopen:
+            rec["miopen_fwd_us"] = bench(lambda: F.conv2d(x, w, None, s, 1), a.it)
+            rec["miopen_dgrad_us"] = bench(lambda: torch.ops.aten.convolution_backward(
+                dz, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]), a.it)
+            rec["miopen_wgrad_us"] = bench(lambda: torch.ops.aten.convolution_backward(
+                dz, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]), a.it)
+        else:
+            rec["miopen_fwd_us"] = rec["miopen_dgrad_us"] = rec["miopen_wgrad_us"] = 0.0
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)
         dz2 = dz.permute(0, 2, 3, 1).reshape(-1, c)
         wm = w.permute(0, 2, 3, 1).reshape(c, 9 * c)
@@ -76,7 +80,7 @@ def main():
             if k.endswith("_us"):
                 rec[k] = round(rec[k], 1)
                 d = k.split("_")[1]
-                rec[k.replace("_us", "_tf")] = round(flops / rec[k] / 1e6, 1)
+                rec[k.replace("_us", "_tf")] = round(flops / rec[k] / 1e6, 1) if rec[k] > 0 else None
         tot["miopen"] += rec["miopen_fwd_us"] + rec["miopen_dgrad_us"] + rec["miopen_wgrad_us"]
         tot["ours"] += rec["ours_fwd_us"] + rec.get("ours_dgrad_us", rec["miopen_dgrad_us"]) + rec["ours_wgrad_us"]
         print(json.dumps(rec), flush=True)

@@ -530,3 +530,40 @@ def test_conv3x3_stride2_data_grad_phases(n, h, w, C1, C2, epi):
     xhat = (z1 - mean) * invstd
     torch.testing.assert_close(part[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=2e-2)
     torch.testing.assert_close(part[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=2e-2)
+
+
+def test_weight_prep_matches_reference_layouts(monkeypatch):
+    """csrc weight_prep (one launch for every fused block) == the per-weight torch layouts the data
+    gradients used before; and a ResNet-tiny backward is bitwise the same with and without it."""
+    from ps_amd.models.resnet import prepare_for_mi355x, resnet_tiny
+    from ps_amd.ops import convgemm as cg
+
+    torch.manual_seed(3)
+    m = prepare_for_mi355x(resnet_tiny(num_classes=10).cuda())
+    blocks = m._blocks()
+    cg.prepare_backward_weights(blocks)
+    prep = cg._tls.prep
+    cg._tls.prep = None
+    for b in blocks:
+        w1t, w3t, w2d, wdt, _ = prep[id(b)]
+        assert torch.equal(w1t, cg._mat(b.conv1.weight).t())
+        assert torch.equal(w3t, cg._mat(b.conv3.weight).t())
+        if b.conv2.stride[0] == 1:
+            assert torch.equal(w2d, cg._mat3_dgrad(b.conv2.weight))
+        else:
+            for u, v in zip(w2d, cg._phase_weights(b.conv2.weight)):
+                assert torch.equal(u, v)
+        if b.downsample is not None:
+            assert torch.equal(wdt, cg._mat(b.downsample[0].weight).t())
+    monkeypatch.setattr(cg, "WGRAD3X3_MIN_C", 64)  # in-house weight gradients: deterministic
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(8, 3, 64, 64, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=DEV, generator=g)
+    grads = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PS_AMD_WEIGHT_PREP", flag)
+        mm = copy.deepcopy(m)
+        F.cross_entropy(mm(x).float(), y).backward()
+        grads[flag] = {n: p.grad.clone() for n, p in mm.named_parameters()}
+    for n, gr in grads["0"].items():
+        assert torch.equal(grads["1"][n], gr), n
