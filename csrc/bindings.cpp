@@ -1178,8 +1178,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
   const bool has_pro = pro.has_value() && pro->defined();
-  const int G =
-      psamd::conv_fwd_plan(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), has_pro || has_bwd).gm;
+  const int G = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
+                                        has_pro || has_bwd, g).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;

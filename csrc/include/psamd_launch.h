@@ -300,6 +300,8 @@ struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
+// the plan launch_conv_fwd uses for this geometry (the 3x3 patch-staged tiles where they apply)
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)

@@ -178,7 +178,16 @@ struct StageRegs {
 };
 
 // PRO: 0 none, 1 BN + ReLU of the A rows, 2 BN backward from two row sources (a, a2)
-template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS>
+// PATCH (3x3 / stride 1 / pad 1, LDS-DMA path): the tile's input rows -- a PATCH of whole rows with
+// zero halo rows / columns, at most two images -- are staged ONCE per 64-channel chunk and the nine
+// taps read their A fragments from it at a shifted slot; a K stage then moves only its weight tile.
+// The im2col staging moved 9 copies of every input pixel through L2 (52 FLOP per staged byte on
+// the 64-channel layers: L2-bandwidth bound).  Patch layout: eight 16-B channel planes of
+// [rows][W + 2] slots, so 16 consecutive pixels of a b128 fragment read hit 16 distinct rows.
+template <int BN>
+constexpr int patch_bytes() { return BN == 64 ? 65536 : 40960; }  // 8 channel planes of 8 / 5 KiB
+
+template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, bool PATCH = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr bool BWD = PRO == 2;
   static_assert(!BWD || (KS1 && EPI == 3 && !GLDS), "the BN-backward prologue is a 1x1 data-gradient prologue");
@@ -195,13 +204,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   constexpr int TM = TALL ? 2 : BM / 64;        // 32-pixel MFMA blocks per wave
   constexpr int AR = BM / 32;              // A-tile chunks per thread per stage
   constexpr int BCH = BN / 32;             // B-tile chunks per thread per stage
+  constexpr int BI_P = BN / 32;            // PATCH: weight LDS-DMA instructions per wave per stage
   // output tile row stride (bf16): 2 dwords mod 32 banks, so the 16 rows of a ds_write_b64 lane
   // group hit distinct bank pairs (BN + 8 made them 2-way); rows are 8-B aligned -> b64 readback
   constexpr int CS = BN + 4;
   // LDS: [A0 | A1] overlaid by the output tile + statistics scratch, then [B0 | B1] (never
   // overlaid, so a resident weight tile survives the epilogues)
   constexpr int EPI_ELEMS = BM * CS + 8 * BN * 2;
-  constexpr int B_BASE = ((2 * BM * kBK > EPI_ELEMS ? 2 * BM * kBK : EPI_ELEMS) + 7) & ~7;
+  constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : 2 * BM * kBK;
+  constexpr int B_BASE = ((A_ELEMS > EPI_ELEMS ? A_ELEMS : EPI_ELEMS) + 7) & ~7;
   constexpr int LDS_ELEMS = B_BASE + 2 * BN * kBK;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
@@ -503,7 +514,113 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   };
 
   zero_acc();
-  if constexpr (GLDS) {
+  if constexpr (PATCH) {
+    static_assert(GLDS && !KS1 && !PRO && BM == 128, "patch staging: 3x3 LDS-DMA path");
+    if (mg < mtiles) {  // block-uniform
+      const int PW = g.W + 2, ohw = g.OH * g.OW;
+      // the tile's rows: image part A (rows oh0 - 1 .. ), optional part B (next image, rows -1 .. )
+      const int m0 = mg * BM, mlast = min(m0 + BM, p.M) - 1;
+      const int img0 = m0 / ohw, oh0 = (m0 - img0 * ohw) / g.OW;
+      const int img1 = mlast / ohw, oh1 = (mlast - img1 * ohw) / g.OW;
+      const int nA = img1 == img0 ? oh1 - oh0 + 3 : g.OH - oh0 + 2;
+      const int R = img1 == img0 ? nA : nA + oh1 + 3;
+      constexpr int PLB = patch_bytes<BN>() / 8;  // bytes per 16-B channel plane (fixed: immediates)
+      // A-fragment rows of this lane: byte offset of tap (0, 0) in its plane (rows past M: slot 0)
+      uint32_t abase[TM];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm + 32 * j + fr;
+        int sl = 0;
+        if (m < p.M) {
+          const int im = m / ohw, r = m - im * ohw, oh = r / g.OW, ow = r - oh * g.OW;
+          sl = (im == img0 ? oh - oh0 : nA + oh) * PW + ow;
+        }
+        abase[j] = static_cast<uint32_t>(fh * PLB + sl * 16);  // bytes from the LDS base
+      }
+      const uint16_t* gb[BI_P];
+      const int lrow = lane >> 3, lch = lane & 7;
+#pragma unroll
+      for (int i = 0; i < BI_P; ++i) {
+        const int r = (wave * BI_P + i) * 8 + lrow;
+        gb[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + swz(r, lch) * 8;
+      }
+      auto issue_b = [&](int tap, int cc, int buf) {
+        uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
+        const int k0 = tap * g.C + cc * kBK;
+#pragma unroll
+        for (int i = 0; i < BI_P; ++i)
+          __builtin_amdgcn_global_load_lds((gptr_t*)(gb[i] + k0), (lptr_t*)(Bs + (wave * BI_P + i) * 8 * kBK), 16, 0,
+                                           0);
+      };
+      // patch of channel chunk cc: plane pl, piece k of the plane (1 KiB, lane-linear slots); the
+      // plane's tail past R x PW slots loads the zero page
+      const int nsl = R * PW, ppp = (nsl + 63) / 64, npiece = 8 * ppp;
+      auto issue_patch = [&](int cc) {
+        for (int pc = wave; pc < npiece; pc += 4) {  // wave-uniform trip count
+          const int pl = pc / ppp, sl = (pc - pl * ppp) * 64 + lane, prow = sl / PW, pcol = sl - prow * PW;
+          const int im = prow < nA ? img0 : img1, ih = prow < nA ? oh0 - 1 + prow : prow - nA - 1, iw = pcol - 1;
+          const bool ok = sl < nsl && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                          static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
+          const uint16_t* src =
+              ok ? p.a + ((static_cast<int64_t>(im) * g.H + ih) * g.W + iw) * g.C + cc * kBK + pl * 8 : kZeroPage;
+          __builtin_amdgcn_global_load_lds((gptr_t*)src,
+                                           (lptr_t*)(reinterpret_cast<uint8_t*>(lds) + pl * PLB + (pc - pl * ppp) * 1024),
+                                           16, 0, 0);
+        }
+      };
+      auto compute_patch = [&](int buf, int tapoff) {
+        const uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
+        uint32_t aa[TM];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) aa[j] = abase[j] + tapoff * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int ch = 2 * s2 + fh;
+          bf16x8_t xa[TM], wb[TN];
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            xa[j] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const uint8_t*>(lds) + aa[j] + 2 * s2 * PLB);
+#pragma unroll
+          for (int i = 0; i < TN; ++i) {
+            const int r = wn + 32 * i + fr;
+            wb[i] = *reinterpret_cast<const bf16x8_t*>(Bs + r * kBK + swz(r, ch) * 8);
+          }
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[i], xa[j], acc[i][j], 0, 0, 0);
+        }
+      };
+      const int ncc = g.C / kBK;
+      issue_patch(0);
+      issue_b(0, 0, 0);
+      int st = 0;
+      for (int cc = 0; cc < ncc; ++cc) {
+        for (int kh = 0; kh < 3; ++kh)
+          for (int kw = 0; kw < 3; ++kw, ++st) {
+            const int tap = kh * 3 + kw;
+            const bool next_same = tap < 8;  // the next stage reuses this patch
+            if (next_same) {
+              issue_b(tap + 1, cc, (st + 1) & 1);
+              if constexpr (BI_P == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            lds_barrier();  // every wave's stage DMAs (and the patch) landed
+            compute_patch(st & 1, kh * PW + kw);
+            lds_barrier();  // stage read out before its buffers are refilled
+            if (!next_same && cc + 1 < ncc) {  // next channel chunk: new patch + its first weight stage
+              issue_patch(cc + 1);
+              issue_b(0, cc + 1, (st + 1) & 1);
+            }
+          }
+      }
+      epi_load(mg);
+      epilogue(mg);
+    }
+  } else if constexpr (GLDS) {
     // Deep-K tile, one per block: both operands go global -> LDS by LDS-DMA (global_load_lds,
     // 16 B per lane), no staging registers and no ds_write.  One wave instruction fills 8 rows x
     // 128 B lane-linearly, so the chunk swizzle moves to the SOURCE address (linear destination +
@@ -1283,6 +1400,40 @@ bool tall_enabled() {
   return on;
 }
 
+bool patch_fwd_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_PATCH");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// 3x3 / stride 1 / pad 1 forward (or data gradient) whose 128-pixel tiles' patch fits the LDS
+// budget and spans at most two images
+bool patch_fwd_ok(const ConvGeo& g, int N, bool pro) {
+  if (pro || !patch_fwd_enabled() || g.ks != 3 || (g.ksw != 0 && g.ksw != 3) || g.stride != 1 || g.pad != 1 ||
+      g.RH != 0 || g.OH != g.H || g.OW != g.W || g.C % 64 != 0 || g.OH * g.OW < 128)
+    return false;
+  // 64-channel outputs keep the tall 256 x 64 im2col tile: the 128 x 64 patch tile (64 x 32 per
+  // wave, 1.5 fragment reads per MFMA) measured 9-14 % slower there (profiles/r3_conv_patch_fwd_ab.txt)
+  if (N % 128 != 0 && std::getenv("PS_AMD_CONV_PATCH64") == nullptr) return false;
+  const int bn = N % 128 == 0 ? 128 : 64;
+  const int span = (g.OW - 1 + 128 + g.OW - 1) / g.OW, rmax = span + 4;
+  const int plane = (rmax * (g.W + 2) * 16 + 1023) / 1024 * 1024;  // one 16-B channel plane, whole pieces
+  return 8 * plane <= (bn == 64 ? patch_bytes<64>() : patch_bytes<128>());
+}
+
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g) {
+  if (patch_fwd_ok(g, N, pro)) {  // one 128-pixel tile per block (LDS-DMA path)
+    ConvFwdPlan pl;
+    pl.bm = 128;
+    pl.bn = N % 128 == 0 ? 128 : 64;
+    pl.gm = (M + 127) / 128;
+    return pl;
+  }
+  return conv_fwd_plan(M, N, K, pro);
+}
+
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   ConvFwdPlan pl;
   if (!pro && N == 64 && K / kBK >= 8 && tall_enabled()) {  // 64-channel 3x3 (K = 576): 256 x 64 tiles
@@ -1305,9 +1456,20 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const bool bwd = a.bwd != nullptr;
-  const ConvFwdPlan pl = conv_fwd_plan(a.M, a.N, a.K, a.pro != nullptr || bwd);
+  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
+  if (!bwd && patch_fwd_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
+#define PSAMD_CFP(BN, EPI) \
+  hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 0, EPI, false, true, true>), dim3(nblk), dim3(256), 0, s, a, GM)
+    if (pl.bn == 128) {
+      if (a.epi == 1) { PSAMD_CFP(128, 1); } else if (a.epi == 3) { PSAMD_CFP(128, 3); } else { PSAMD_CFP(128, 0); }
+    } else {
+      if (a.epi == 1) { PSAMD_CFP(64, 1); } else if (a.epi == 3) { PSAMD_CFP(64, 3); } else { PSAMD_CFP(64, 0); }
+    }
+#undef PSAMD_CFP
+    return;
+  }
   const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
   // deep K without the BN prologue: LDS-DMA staging (one tile per block)
   const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;

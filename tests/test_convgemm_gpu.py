@@ -567,3 +567,38 @@ def test_weight_prep_matches_reference_layouts(monkeypatch):
         grads[flag] = {n: p.grad.clone() for n, p in mm.named_parameters()}
     for n, gr in grads["0"].items():
         assert torch.equal(grads["1"][n], gr), n
+
+
+@pytest.mark.parametrize("n,hw,cin,cout", [(2, 56, 64, 64), (3, 28, 128, 128), (2, 14, 256, 256), (2, 28, 64, 128)])
+def test_conv3x3_patch_forward_statistics_and_data_grad(n, hw, cin, cout):
+    """3x3 stride-1 forward on the patch-staged tiles (PS_AMD_CONV_PATCH, default on: the tile's
+    input rows staged once per 64-channel chunk, tiles straddling two images) with the BN
+    statistics epilogue, and the data gradient (flipped weight) with epilogue 3 -- vs fp32 torch."""
+    from ps_amd.ops.convgemm import _mat3_dgrad
+
+    g = _gen(n * hw + cin + cout)
+    x = _rnd(n, hw, hw, cin, g=g)
+    wt = _rnd(cout, cin, 3, 3, g=g, scale=(9 * cin) ** -0.5)
+    ref = F.conv2d(x.permute(0, 3, 1, 2), wt, None, 1, 1).permute(0, 2, 3, 1).reshape(-1, cout)
+    ks = torch.randn(cout, generator=g) * 0.1
+    c, part = native().conv_gemm(_bf(x.reshape(-1, cin)), _bf(wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin)),
+                                 geo(hw, hw, 3, 1, 1), None, 1, None, ks.to(DEV))
+    _close(c, ref)
+    cf = c.float().cpu()
+    torch.testing.assert_close(part[0].sum(0).cpu(), (cf - ks).sum(0), rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(part[1].sum(0).cpu(), ((cf - ks) ** 2).sum(0), rtol=1e-4, atol=5e-2)
+    # data gradient: dz [n, hw, hw, cout] -> dy [.., cin], ReLU mask + bn sums over z1
+    dz = _rnd(n, hw, hw, cout, g=g)
+    z1 = _rnd(n, hw, hw, cin, g=g)
+    coef = _coef(cin, g)
+    mean, invstd = torch.randn(cin, generator=g) * 0.1, torch.rand(cin, generator=g) + 0.5
+    dy = torch.nn.grad.conv2d_input((n, cin, hw, hw), wt, dz.permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    on = (z1 * coef[:cin] + coef[cin:]) > 0
+    gref = (dy.bfloat16().float() * on).reshape(-1, cin)
+    c2, p2 = native().conv_gemm(_bf(dz).reshape(-1, cout), _mat3_dgrad(_bf(wt)), geo(hw, hw, 3, 1, 1), None, 3,
+                                _bf(z1).reshape(-1, cin), None, coef.to(DEV), mean.to(DEV), invstd.to(DEV))
+    _close(c2, gref)
+    gc = c2.float().cpu()
+    xhat = (z1.reshape(-1, cin) - mean) * invstd
+    torch.testing.assert_close(p2[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(p2[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=5e-2)
