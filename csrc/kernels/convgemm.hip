@@ -423,10 +423,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       }
     }
   };
-  // epilogue(mt) consumes what epi_load(mt) read
-  auto epilogue = [&](int mt) {
-    // accumulators -> bf16 output tile [BM][CS]: register q of lane l is channel
-    // (q & 3) + 8 (q >> 2) + 4 (l >> 5), pixel l & 31 -> 4 consecutive channels per 8-B store
+  // accumulators -> bf16 output tile [BM][CS]: register q of lane l is channel
+  // (q & 3) + 8 (q >> 2) + 4 (l >> 5), pixel l & 31 -> 4 consecutive channels per 8-B store
+  auto acc_to_lds = [&]() {
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
@@ -438,7 +437,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
                            f32_to_bf16(acc[i][j][4 * q4 + 2]), f32_to_bf16(acc[i][j][4 * q4 + 3])};
           *reinterpret_cast<u16x4*>(Cs + ml * CS + nl) = v;
         }
-    lds_barrier();
+  };
+  // epilogue_rows(mt) consumes what epi_load(mt) read, from the output tile acc_to_lds() wrote
+  auto epilogue_rows = [&](int mt) {
     const int m0 = mt * BM;
 #pragma unroll
     for (int i = 0; i < NPASS; ++i) {
@@ -494,6 +495,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       *reinterpret_cast<u16x8*>(p.c + o) = v;
     }
   };
+  auto epilogue = [&](int mt) {
+    acc_to_lds();
+    lds_barrier();
+    epilogue_rows(mt);
+  };
 
   // one step of the (tile, stage) sequence; SF: the free register set (held step q), SN: step q + 1
   int ckt = 0, cti = 0;  // consumer cursor
@@ -501,9 +507,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     if (q + 2 < nq) gload(SF);
     compute(q & 1);
     if (++ckt == nk) {  // tile done
-      epi_load(mg + cti * GM);
+      // The epilogue row reads are issued after the accumulators went to LDS: both staging sets
+      // are live here, and acc + staging + 2-4 row streams of NPASS rows overran the 256-VGPR
+      // budget of 2 waves / SIMD (the folded data-gradient epilogues spilled 150-290 B / lane).
       lds_barrier();    // all waves are done with the stage buffers (the output tile overlaps)
-      epilogue(mg + cti * GM);
+      acc_to_lds();
+      epi_load(mg + cti * GM);
+      lds_barrier();
+      epilogue_rows(mg + cti * GM);
       zero_acc();
       ckt = 0;
       ++cti;
