@@ -209,6 +209,56 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_bwd_kernel(const uint16_t* _
   }
 }
 
+// k = 3, s = 2, p = 1 over even H, W (the ResNet stem pool): the dx pixel quad (2a + dh, 2b + dw)
+// is covered by windows (a + i, b + j), i, j in {0, 1} only -- one thread reads those four
+// (idx, dy) vectors once and writes the four dx vectors (the per-pixel form read 16 for 4).
+// Window (i, j) reaches row dh iff i <= dh (tap row dh + 1 - 2i) and column dw iff j <= dw;
+// contributions are summed in the (oh, ow) order of the per-pixel kernel (bitwise equal).
+template <typename IDX>
+__global__ __launch_bounds__(256) void maxpool_s2k3_bwd_quad_kernel(const uint16_t* __restrict__ dy,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    uint16_t* __restrict__ dx, int N, int H, int W,
+                                                                    int C, int OH, int OW) {
+  const int cv = C / 8, QH = H / 2, QW = W / 2;
+  const IDX total = static_cast<IDX>(N) * QH * QW * cv;
+  const IDX stride = static_cast<IDX>(gridDim.x) * blockDim.x;
+  for (IDX v = static_cast<IDX>(blockIdx.x) * blockDim.x + threadIdx.x; v < total; v += stride) {
+    const int c8 = static_cast<int>(v % cv);
+    IDX r = v / cv;
+    const int b = static_cast<int>(r % QW);
+    r /= QW;
+    const int a = static_cast<int>(r % QH);
+    const int n = static_cast<int>(r / QH);
+    uint64_t pk[4];
+    u16x8 gv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // windows past the map are clamped in bounds and never used
+      const int oh = min(a + (q >> 1), OH - 1), ow = min(b + (q & 1), OW - 1);
+      const int64_t o = ((static_cast<int64_t>(n) * OH + oh) * OW + ow) * C + c8 * 8;
+      pk[q] = *reinterpret_cast<const uint64_t*>(idx + o);
+      gv[q] = *reinterpret_cast<const u16x8*>(dy + o);
+    }
+    const bool ih = a + 1 < OH, iw = b + 1 < OW;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = q >> 1, j = q & 1;
+          if (i > dh || j > dw) continue;  // compile-time after unrolling
+          if ((i && !ih) || (j && !iw)) continue;
+          const uint8_t code = static_cast<uint8_t>((dh + 1 - 2 * i) * 3 + (dw + 1 - 2 * j));
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (static_cast<uint8_t>(pk[q] >> (8 * e)) == code) acc[e] += bf16_to_f32(gv[q][e]);
+        }
+        store8(dx, ((static_cast<int64_t>(n) * H + 2 * a + dh) * W + 2 * b + dw) * C + c8 * 8, acc);
+      }
+  }
+}
+
 // log2(C / 8) when the row mapping applies (C / 8 a power of two, rows of >= 64 elements so a
 // block's threads stay busy, row indices in int range), else -1 (generic flat mapping)
 static int row_lcv(int C, int width, int64_t rows) {
@@ -243,6 +293,17 @@ void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* d
                              int OW, int k, int s, int p, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(N) * H * W * (C / 8);
   if (total <= 0) return;
+  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
+    const int64_t quads = total / 4;
+    const int qgrid = stream_grid(quads, 256);
+    if (quads < (int64_t(1) << 31) - 2 * static_cast<int64_t>(qgrid) * 256)
+      hipLaunchKernelGGL((maxpool_s2k3_bwd_quad_kernel<uint32_t>), dim3(qgrid), dim3(256), 0, st, dy, idx, dx, N, H,
+                         W, C, OH, OW);
+    else
+      hipLaunchKernelGGL((maxpool_s2k3_bwd_quad_kernel<int64_t>), dim3(qgrid), dim3(256), 0, st, dy, idx, dx, N, H,
+                         W, C, OH, OW);
+    return;
+  }
   const int lcv = row_lcv(C, W, static_cast<int64_t>(N) * H);
   const int grid = lcv >= 0 ? static_cast<int>(std::min<int64_t>(static_cast<int64_t>(N) * H, 1 << 20))
                             : stream_grid(total, 256);

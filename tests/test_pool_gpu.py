@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("N,C,H,W,k,s,p", [(2, 64, 112, 112, 3, 2, 1), (3, 16, 9, 7, 2, 2, 0),
-                                           (1, 24, 10, 10, 3, 1, 1), (2, 8, 15, 15, 3, 2, 1)])
+                                           (1, 24, 10, 10, 3, 1, 1), (2, 8, 15, 15, 3, 2, 1),
+                                           (1, 32, 8, 12, 3, 2, 1), (2, 8, 6, 4, 3, 2, 1)])
 def test_maxpool_nhwc_fwd_bwd(N, C, H, W, k, s, p):
     torch.manual_seed(0)
     x = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
