@@ -195,8 +195,9 @@ class PlaneEngine {
     j.t_submit = j.since = Clock::now();
     if (gpu_) {
       hip_ok(hipSetDevice(dev_), "hipSetDevice");
-      // default event flags keep the system-scope release: peers on other GPUs read this data
-      hip_ok(hipEventCreateWithFlags(&j.land, hipEventDisableTiming), "hipEventCreate");
+      // default event flags keep the system-scope release: peers on other GPUs read this data;
+      // timing enabled: land -> serve start is the device-side wait for the slowest push
+      hip_ok(hipEventCreateWithFlags(&j.land, hipEventDefault), "hipEventCreate");
       hip_ok(hipEventRecord(j.land, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord");
     }
     {
@@ -261,9 +262,18 @@ class PlaneEngine {
     for (auto& kv : sums_) d[py::str(kv.first)] = kv.second / n;
     d["rounds"] = rounds_done_;
     d["jobs"] = jobs_done_;
+    // link throughput of the two one-sided phases: bytes each rank's kernels moved / their
+    // device time (serve reads W pushes of its chunk, pull reads W-1 owners' chunks)
+    auto rate = [&](const char* bytes, const char* ms) {
+      auto b = sums_.find(bytes), t = sums_.find(ms);
+      return (b == sums_.end() || t == sums_.end() || t->second <= 0.0) ? 0.0 : b->second / (t->second * 1e6);
+    };
+    d["serve_GBps"] = rate("serve_bytes", "serve_ms");
+    d["pull_GBps"] = rate("pull_bytes", "pull_ms");
     if (reset) {
       sums_.clear();
       rounds_done_ = 0;
+      jobs_done_ = 0;
     }
     return d;
   }
@@ -271,6 +281,25 @@ class PlaneEngine {
   std::string error() {
     std::lock_guard<std::mutex> g(mu_);
     return err_;
+  }
+
+  // checkpoint restore at PS clock ``round`` (rounds 0 .. round-1 are complete): this rank's
+  // control words say so, as if it had run them -- the peers' waits (ready / served / the clip
+  // phase's fdone gate) are monotonic, so a fresh control block would stall the first round
+  // after a resume at round >= 2 (e.g. fdone >= round - 1 for clipping) -- and wait_pulled of
+  // an earlier round returns at once
+  void restore_round(int64_t round) {
+    TORCH_CHECK(round >= 0, "round");
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(incoming_.empty(), "restore_round with rounds in flight");
+    for (int b = 0; b < NB_; ++b) {
+      store_max(ctl_.ready(me_, b), round);
+      store_max(ctl_.served(me_, b), round);
+    }
+    store_max(ctl_.sqready(me_), round);
+    store_max(ctl_.fdone(me_), round);
+    if (round - 1 > done_round_) done_round_ = round - 1;
+    restored_round_ = round;
   }
 
  private:
@@ -417,7 +446,7 @@ class PlaneEngine {
     for (;;) {
       if (static_cast<int>(j.stage) >= limit) break;
       const Stage before = j.stage;
-      step(j);
+      step(j, limit);
       if (j.stage == before) break;
       moved = true;
       j.since = Clock::now();
@@ -425,13 +454,12 @@ class PlaneEngine {
     return moved;
   }
 
-  void step(Job& j) {
+  void step(Job& j, int limit) {
     auto& bk = buckets_[static_cast<size_t>(j.b)];
     const int64_t want = j.round + 1;
     switch (j.stage) {
       case LAND:
         if (!done(j.land)) return;
-        destroy(j.land);
         store_max(ctl_.ready(me_, j.b), want);
         j.t_ready = Clock::now();
         j.stage = READY;
@@ -449,6 +477,12 @@ class PlaneEngine {
           }
           ClipRound& cr = it->second;
           if (cr.stage < 1) return;  // norm slot not zeroed yet
+          // the reduced gradient (bk.gshard) and the factor have ONE buffer per bucket: round r+1
+          // may reduce only once round r's clipped serve of this bucket is enqueued (same
+          // stream, so the serve reads round r's values before the reduce overwrites them).
+          // Without the gate SSP (staleness >= 1) let round r+1 reduce while round r waited
+          // for its factor.  ``limit`` is the previous job's stage (DONE + 1 when none).
+          if (limit < static_cast<int>(SERVING)) return;
           j.t_allready = Clock::now();
           if (gpu_) launch_reduce(bk, j, serve_s_);
           else callback("reduce", j);
@@ -530,15 +564,25 @@ class PlaneEngine {
   }
 
   void account(const Job& j) {
-    float serve_ms = 0.f, pull_ms = 0.f;
+    float serve_ms = 0.f, pull_ms = 0.f, land_to_serve_ms = 0.f, serve_to_pull_ms = 0.f;
     if (gpu_) {
       hipEventElapsedTime(&serve_ms, j.s0, j.s1);
       hipEventElapsedTime(&pull_ms, j.p0, j.p1);
+      // device clock: own push landed -> serve kernel starts (the wait for the slowest peer's
+      // push + engine latency), own serve done -> pull starts (the wait for the other owners)
+      if (j.land) hipEventElapsedTime(&land_to_serve_ms, j.land, j.s0);
+      hipEventElapsedTime(&serve_to_pull_ms, j.s1, j.p0);
     }
+    const auto& bk = buckets_[static_cast<size_t>(j.b)];
+    const double push_bytes = (j.flags & 1) ? static_cast<double>(bk.chunk) / 8.0 + bk.chunk / psamd::kOnebitChunk * 4.0
+                                            : static_cast<double>(bk.chunk * bk.esize);
     std::lock_guard<std::mutex> g(mu_);
     sums_["serve_ms"] += serve_ms;
     sums_["pull_ms"] += pull_ms;
-    sums_["land_ms"] += ms_between(j.t_submit, j.t_ready);
+    sums_["land_to_serve_ms"] += land_to_serve_ms;
+    sums_["serve_to_pull_ms"] += serve_to_pull_ms;
+    sums_["serve_bytes"] += push_bytes * W_;
+    sums_["pull_bytes"] += static_cast<double>(bk.chunk * bk.esize) * (W_ - 1);
     sums_["peer_push_wait_ms"] += ms_between(j.t_ready, j.t_allready);
     sums_["peer_serve_wait_ms"] += ms_between(j.t_served, j.t_allserved);
     jobs_done_ += 1;
@@ -722,6 +766,7 @@ class PlaneEngine {
   std::map<std::string, double> sums_;
   int64_t rounds_done_ = 0, jobs_done_ = 0;
   int64_t done_round_ = -1;  // rounds <= this one have every pull enqueued
+  int64_t restored_round_ = 0;
 
   // engine-thread state
   std::thread th_;
@@ -844,7 +889,8 @@ void register_plane(pybind11::module& m) {
       .def("copy_peer", &PlaneEngine::copy_peer)
       .def("gather_now", &PlaneEngine::gather_now)
       .def("stats", &PlaneEngine::stats, py::arg("reset") = false)
-      .def("error", &PlaneEngine::error);
+      .def("error", &PlaneEngine::error)
+      .def("restore_round", &PlaneEngine::restore_round);
   py::class_<Arena>(pm, "Arena")
       .def(py::init<int64_t, int64_t>())
       .def("tensor", &Arena::tensor)

@@ -175,6 +175,20 @@ class Client {
     return rd.u64();
   }
 
+  uint64_t rendezvous(uint32_t worker) {
+    Writer w;
+    w.u32(worker);
+    std::vector<uint8_t> resp;
+    uint16_t st;
+    {
+      py::gil_scoped_release r;
+      st = c_.call(OP_RENDEZVOUS, w, &resp);
+    }
+    check(st, resp, "rendezvous");
+    Reader rd(resp.data(), resp.size());
+    return rd.u64();
+  }
+
   uint64_t clock(uint32_t worker, uint64_t c) {
     Writer w;
     w.u32(worker);
@@ -498,6 +512,7 @@ PYBIND11_MODULE(_native, m) {
       .def("push", &Client::push, py::arg("keys"), py::arg("grads"), py::arg("spec"), py::arg("async_flag") = 0)
       .def("barrier", &Client::barrier, py::arg("worker") = 0)
       .def("clock", &Client::clock)
+      .def("rendezvous", &Client::rendezvous, py::arg("worker") = 0)
       .def("row_pull", &Client::row_pull, py::arg("table"), py::arg("dim"), py::arg("keys"), py::arg("lo"),
            py::arg("hi"), py::arg("seed"))
       .def("row_push", &Client::row_push, py::arg("table"), py::arg("dim"), py::arg("keys"), py::arg("grads"),

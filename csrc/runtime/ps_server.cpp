@@ -284,6 +284,28 @@ uint16_t PSServer::handle(Op op, Reader& in, Writer& out) {
       out.u64(generation_.load());
       return ST_OK;
     }
+    case OP_RENDEZVOUS: {
+      // every worker meets here in any consistency mode (Trainer.resume: all present -> worker
+      // 0 reloads the store -> all present again, so nobody pulls or pushes across the reload)
+      in.u32();
+      std::unique_lock<std::mutex> g(barrier_mu_);
+      const uint64_t gen = rv_gen_;
+      rv_arrived_ += 1;
+      if (rv_arrived_ == workers_) {
+        rv_arrived_ = 0;
+        rv_gen_ += 1;
+        barrier_cv_.notify_all();
+      } else {
+        const bool ok = barrier_cv_.wait_for(g, std::chrono::duration<double>(barrier_timeout_s_),
+                                             [&] { return rv_gen_ != gen || !running_.load(); });
+        if (!ok) {
+          rv_arrived_ -= 1;
+          return ST_TIMEOUT;
+        }
+      }
+      out.u64(rv_gen_);
+      return ST_OK;
+    }
     case OP_CLOCK: {
       const uint32_t worker = in.u32();
       const uint64_t c = in.u64();

@@ -85,6 +85,8 @@ class PSServer {
   std::mutex barrier_mu_;
   std::condition_variable barrier_cv_;
   int arrived_ = 0;
+  int rv_arrived_ = 0;     // OP_RENDEZVOUS: its own count and generation, so a load() that
+  uint64_t rv_gen_ = 0;   // restores generation_ cannot release a waiter early
   std::atomic<uint64_t> generation_{0};
   std::vector<uint64_t> clocks_;
   std::mutex stop_mu_;

@@ -42,6 +42,7 @@ enum Op : uint8_t {
   OP_CLOCK = 13,
   OP_ROW_PULL = 14,  // sparse row tables: pull (lazy deterministic create) of many int64 keys
   OP_ROW_PUSH = 15,  // sparse row tables: push per-row gradients (BSP accumulate / apply)
+  OP_RENDEZVOUS = 16,  // mode-independent W-worker rendezvous (resume hand-off; never touches the BSP generation)
 };
 
 enum Status : uint16_t { ST_OK = 200, ST_NOT_FOUND = 204, ST_BAD = 400, ST_TIMEOUT = 408, ST_ERR = 500 };

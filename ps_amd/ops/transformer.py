@@ -245,7 +245,11 @@ class _FusedXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, labels, ignore):
         lse, rows = native().xent_fwd(x, labels, int(ignore))
-        count = (labels != ignore).sum().float().reshape(1)
+        # the kernels' rule for a scored row (xent.hip: y != ignore and 0 <= y < V): an out-of-range
+        # label scores 0 and is not in the mean's denominator either (F.cross_entropy raises on
+        # one; checking here would cost a host sync per step)
+        V = x.shape[1]
+        count = ((labels != ignore) & (labels >= 0) & (labels < V)).sum().float().reshape(1)
         ctx.save_for_backward(x, labels, lse, count)
         ctx.ignore = int(ignore)
         return (rows.sum() / count.clamp(min=1.0)).reshape(())

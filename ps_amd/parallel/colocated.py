@@ -580,6 +580,7 @@ class ColocatedPS:
             self.round = int(st["round"])
             # rebuild every replica slot by one pull of the restored masters
             if self.plane is not None:
+                self.plane.restore_round(self.round)
                 for b, bk in enumerate(self.reg.buckets):
                     lo, hi = bk.owner_range(self.rank)
                     for slot in range(self.nslots):

@@ -292,6 +292,11 @@ class XgmiPlane:
         stream = torch.cuda.current_stream(self.device).cuda_stream if self.gpu else 0
         self.engine.wait_pulled(rnd, stream)
 
+    def restore_round(self, rnd: int) -> None:
+        """After a checkpoint restore at PS clock ``rnd``: mark this rank's control words as if
+        rounds 0 .. rnd-1 had run here (csrc/plane.cpp restore_round)."""
+        self.engine.restore_round(int(rnd))
+
     def stats(self, reset: bool = False) -> dict:
         return dict(self.engine.stats(reset)) if self.engine is not None else {}
 

@@ -111,6 +111,10 @@ class PSClient:
     def clock(self, worker: int, c: int) -> int:
         return self._c.clock(worker, c)
 
+    def rendezvous(self, worker: int = 0) -> int:
+        """All W workers meet, in any consistency mode (independent of the BSP generation)."""
+        return self._c.rendezvous(worker)
+
     def register_updater(self, spec: str) -> None:
         self._c.register_updater(spec)
 
@@ -212,6 +216,11 @@ class PSRouterClient:
     def clock(self, worker: int, c: int) -> int:
         futs = [self.pool.submit(cl.clock, worker, c) for cl in self.clients]
         return min(f.result() for f in futs)
+
+    def rendezvous(self, worker: int = 0) -> int:
+        """Meet every worker on every shard (used around a store reload)."""
+        futs = [self.pool.submit(c.rendezvous, worker) for c in self.clients]
+        return max(f.result() for f in futs)
 
     def register_updater(self, spec: str) -> None:
         for c in self.clients:

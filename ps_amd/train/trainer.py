@@ -161,8 +161,9 @@ class Trainer:
     def resume(self) -> int:
         """Restore the newest committed checkpoint (if any); returns the step to continue from.
 
-        TCP topology: worker 0 has every server reload its store from the newest committed
-        ``tcp_step*`` directory; every worker continues from that step."""
+        TCP topology: all workers rendezvous on the servers, worker 0 has every server reload its
+        store from the newest committed ``tcp_step*`` directory, all rendezvous again, and every
+        worker continues from that step."""
         if self.ckpt is None:
             return 0
         if isinstance(self.engine, KVEngine):
@@ -171,8 +172,14 @@ class Trainer:
             d = self._tcp_latest()
             if d is None:
                 return 0
-            if self.engine.kv.client is not None and self.engine.kv.worker_id == 0:
-                self.engine.kv.client.load(os.path.join(d, "server"))
+            client = self.engine.kv.client
+            if client is not None:
+                # every worker is present before worker 0 reloads and waits until the reload is
+                # done: nobody pulls pre-restore weights or pushes a gradient the reload drops
+                client.rendezvous(self.engine.kv.worker_id)
+                if self.engine.kv.worker_id == 0:
+                    client.load(os.path.join(d, "server"))
+                client.rendezvous(self.engine.kv.worker_id)
             step = int(os.path.basename(d)[len("tcp_step"):])
             ctx.set_step(step)
             return step

@@ -91,3 +91,25 @@ def test_fused_cross_entropy_matches_fp32(R, V, ign):
     rel = ((xg.grad.float() - xf.grad).norm() / xf.grad.norm()).item()
     assert rel < 1e-2, rel
     assert bool((xg.grad[lab == -100] == 0).all())
+
+
+def test_fused_cross_entropy_out_of_range_labels_are_not_counted():
+    """a label outside [0, V) that is not ignore_index scores 0 in the kernels and is
+    left out of the mean's denominator too -- the loss equals F.cross_entropy over the in-range
+    rows only, and those rows get zero gradient."""
+    from ps_amd.ops.transformer import cross_entropy
+
+    torch.manual_seed(3)
+    R, V = 40, 517
+    x = (torch.randn(R, V, device="cuda") * 2).bfloat16()
+    lab = torch.randint(0, V, (R,), device="cuda")
+    lab[:3] = V + 4
+    lab[3:5] = -7
+    lab[5] = -100
+    ok = (lab >= 0) & (lab < V)
+    ref = torch.nn.functional.cross_entropy(x.float()[ok], lab[ok])
+    xg = x.clone().requires_grad_()
+    loss = cross_entropy(xg, lab)
+    loss.backward()
+    torch.testing.assert_close(loss.float(), ref, rtol=1e-4, atol=1e-4)
+    assert bool((xg.grad[~ok] == 0).all())

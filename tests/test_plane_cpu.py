@@ -141,14 +141,14 @@ def test_plane_straggler_still_bsp_exact():
         torch.testing.assert_close(res[0][0][k], v, rtol=1e-5, atol=1e-6)
 
 
-def _ckpt_body(tp, steps):
+def _ckpt_body(tp, steps, kw=None):
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import MomentumUpdater
 
     def make():
         m = _model(0)
         return m, ColocatedPS(m, MomentumUpdater(0.1, 0.9), tp, bucket_mb=0.001, last_bucket_mb=0.0005, plane="xgmi",
-                              timeout_s=60)
+                              timeout_s=20, **(kw or {}))
 
     x, y = _data()
     xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
@@ -178,3 +178,39 @@ def test_plane_checkpoint_restore_processes():
     for want, got in res:
         for k in want:
             assert torch.equal(want[k], got[k])
+
+
+def test_plane_checkpoint_restore_with_clipping_processes():
+    """a restore at round R >= 2 with global-norm clipping used to hang in the
+    first clip phase (fdone >= R - 1 on a fresh control block) and abort after timeout_s.  The
+    engine now marks its control words as of round R (plane.cpp restore_round)."""
+    res = dist_util.run(_ckpt_body, 2, (3, {"clip_norm": 0.05}))
+    for want, got in res:
+        for k in want:
+            assert torch.equal(want[k], got[k])
+
+
+def test_plane_clip_ssp1_straggler_matches_delayed_clipped_sgd():
+    """clipping + staleness 1 with a straggler.  Round r+1 must not reduce
+    into the bucket's one fp32 gradient buffer while round r still waits for its clip factor;
+    the result equals delayed SGD on the clipped averaged gradient."""
+    world, steps, lr, s, clip = 2, 6, 0.2, 1, 0.05
+    res = dist_util.run(_body, world, ({"staleness": s, "clip_norm": clip}, steps, "sgd", "xgmi", False,
+                                       (1, "delay_push:ms=60")))
+    ref = _model(0)
+    x, y = _data()
+    versions = [{n: p.detach().clone() for n, p in ref.named_parameters()}]
+    for t in range(steps):
+        probe = copy.deepcopy(ref)
+        with torch.no_grad():
+            for n, p in probe.named_parameters():
+                p.copy_(versions[max(0, t - s)][n])
+        loss = sum(F.cross_entropy(probe(x[r::world]), y[r::world]) for r in range(world)) / world
+        grads = torch.autograd.grad(loss, list(probe.parameters()))
+        tot = torch.sqrt(sum((g.double() ** 2).sum() for g in grads)).float()
+        f = min(1.0, clip / (float(tot) + 1e-6))
+        versions.append({n: versions[-1][n] - lr * f * g for (n, _), g in zip(probe.named_parameters(), grads)})
+    want = versions[max(0, steps - s)]
+    for k in want:
+        torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-6)
+        assert torch.equal(res[0][0][k], res[1][0][k])

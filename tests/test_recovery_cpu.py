@@ -116,7 +116,7 @@ def test_ctr_app_reference_dist_deployment(tmp_path):
             srv.kill()
 
 
-def _tcp_run(port, ckdir, steps, resume, x, y):
+def _tcp_run(port, ckdir, steps, resume, x, y, worker=0):
     from ps_amd.context import ctx
     from ps_amd.models.reference import FullConnectedNN
     from ps_amd.parallel.kvstore import KVStore
@@ -127,7 +127,7 @@ def _tcp_run(port, ckdir, steps, resume, x, y):
     m = FullConnectedNN.build_model(10, [8, 3], gen=torch.Generator().manual_seed(3), softmax_temp=1.0,
                                     reference_backward=False)
     client = PSRouterClient([f"127.0.0.1:{port}"])
-    tr = Trainer(m, KVEngine(m, KVStore(client, worker_id=0, consistency="bsp")), checkpoint_dir=ckdir)
+    tr = Trainer(m, KVEngine(m, KVStore(client, worker_id=worker, consistency="bsp")), checkpoint_dir=ckdir)
     start = tr.resume() if resume else 0
     for s in range(start, steps):
         tr.train([{"X": x, "Y": y}])
@@ -163,3 +163,36 @@ def test_tcp_topology_resumes_from_committed_server_checkpoint(tmp_path):
     assert start == 3
     for k in want:
         torch.testing.assert_close(got[k], want[k], rtol=1e-6, atol=1e-7)
+
+
+def test_tcp_resume_two_workers_rendezvous_around_reload(tmp_path):
+    """with 2 workers only worker 0 reloads the servers; worker 1 must neither pull
+    pre-restore weights nor push into the store the reload then overwrites.  Both workers
+    rendezvous on the servers before and after the reload (OP_RENDEZVOUS), so 3 steps + restart
+    with fresh servers + 3 steps equals 6 straight BSP steps for both workers."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from ps_amd.parallel.tcp import PServer
+
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(32, 10, generator=g) for _ in range(2)]
+    ys = [torch.arange(32) % 3, (torch.arange(32) + 1) % 3]
+
+    def job(ckdir, steps, resume, srv_kw=None):
+        srv = PServer(0, workers=2, mode="bsp", barrier_timeout_s=60.0).start()
+        try:
+            with ThreadPoolExecutor(2) as ex:
+                fs = [ex.submit(_tcp_run, srv.port, ckdir, steps, resume, xs[w], ys[w], w) for w in range(2)]
+                return [f.result(timeout=120) for f in fs]
+        finally:
+            srv.stop()
+
+    want = job(str(tmp_path / "a"), 6, False)
+    job(str(tmp_path / "b"), 3, False)
+    got = job(str(tmp_path / "b"), 6, True)
+    for w in range(2):
+        assert got[w][0] == 3
+        for k in want[w][1]:
+            torch.testing.assert_close(got[w][1][k], want[w][1][k], rtol=1e-6, atol=1e-7)
+    for k in want[0][1]:  # BSP: both workers end on the same weights
+        torch.testing.assert_close(got[0][1][k], got[1][1][k], rtol=0, atol=0)
