@@ -334,6 +334,22 @@ class AsyncPS:
         return self.flats[self.cur]
 
     # ------------------------------------------------------------------ push path
+    def push_key(self, name: str, grad: torch.Tensor) -> None:
+        """Key-level push (parallel/gpu_kvstore.py), as ColocatedPS.push_key."""
+        p = self.params[name]
+        b = self._key_bucket[name]
+        g = grad.detach().to(device=p.device, dtype=p.dtype).reshape(p.shape)
+        if name in self._landing[b]:
+            self._landing[b][name] = self._landing[b][name] + g
+            return
+        if self._launched[b]:
+            raise RuntimeError(f"key {name!r} was already pushed this round (its bucket has left)")
+        p.grad = g
+        if self.overlap:
+            self._on_ready(name, p)
+        else:
+            self._landing[b][name] = g
+
     def _on_ready(self, name: str, p: torch.Tensor) -> None:
         if self.accumulating:
             return

@@ -256,6 +256,21 @@ class ColocatedPS:
         return self._view(self.wbuf, self.wslot, name)
 
     # ------------------------------------------------------------------ push path
+    def push_key(self, name: str, grad: torch.Tensor) -> None:
+        """Key-level push (parallel/gpu_kvstore.py): park ``grad`` for key ``name`` as the
+        backward hook does; the key's bucket leaves once its last key arrived.  A second push of
+        a key in the same round adds to the parked gradient while its bucket has not left."""
+        p = self.params[name]
+        b = self._key_bucket[name]
+        g = grad.detach().to(device=p.device, dtype=p.dtype).reshape(p.shape)
+        if name in self._landing[b]:
+            self._landing[b][name] = self._landing[b][name] + g
+            return
+        if self.launched[b]:
+            raise RuntimeError(f"key {name!r} was already pushed this round (its bucket has left)")
+        p.grad = g
+        self._on_ready(name, p)
+
     def _on_ready(self, name: str, p: torch.Tensor) -> None:
         if self.accumulating:
             return

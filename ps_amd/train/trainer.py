@@ -85,9 +85,29 @@ class CollectiveEngine:
 
 
 class KVEngine:
-    def __init__(self, model, store: Optional[KVStore] = None):
+    """The reference's per-step KVStore protocol (train/Trainer.java:70-101): pull the weights,
+    train, ``sum`` every gradient, ``update`` (average + push + barrier), ``clear``.  ``store`` is
+    the CPU ``KVStore`` (standalone or TCP worker) or the GPU engines' ``GpuKVStore``
+    (parallel/gpu_kvstore.py), whose pulls bind the parameters to the replica and whose sums
+    stay on the device."""
+
+    def __init__(self, model, store=None):
         self.model = model
         self.kv = store or KVStore.ins()
+        if getattr(self.kv, "umap", "n/a") is None:  # GpuKVStore without updaters yet
+            self.kv.set_updaters(model.get_updater())
+
+    @property
+    def ps(self):
+        return getattr(self.kv, "ps", None)
+
+    @property
+    def t(self):
+        return getattr(self.kv, "t", None)
+
+    @property
+    def gpu_store(self) -> bool:
+        return not isinstance(self.kv, KVStore)
 
     def accumulate(self, on: bool) -> None:
         pass
@@ -105,7 +125,8 @@ class KVEngine:
         self.kv.clear()
 
     def synchronize(self) -> None:
-        pass
+        if self.gpu_store:
+            self.kv.synchronize()
 
 
 class Trainer:
@@ -133,7 +154,7 @@ class Trainer:
     def save(self, step: int, extra: Optional[dict] = None, blocking: bool = False) -> None:
         if self.ckpt is None:
             return
-        if isinstance(self.engine, KVEngine):
+        if isinstance(self.engine, KVEngine) and not self.engine.gpu_store:
             # dedicated TCP servers hold the whole model: worker 0 asks every server to write its
             # store, then marks the step COMMITTED (resume() only trusts committed steps)
             if self.engine.kv.client is not None and self.engine.kv.worker_id == 0:
@@ -166,7 +187,7 @@ class Trainer:
         worker continues from that step."""
         if self.ckpt is None:
             return 0
-        if isinstance(self.engine, KVEngine):
+        if isinstance(self.engine, KVEngine) and not self.engine.gpu_store:
             import os
 
             d = self._tcp_latest()
