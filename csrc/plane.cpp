@@ -833,6 +833,54 @@ class Arena {
   std::vector<void*> opened_;
 };
 
+// ------------------------------------------------------------------ IPC events
+// An event another process on the node can make its streams wait on (hipEventInterprocess):
+// the owner records it after a kernel, a peer that opened the handle enqueues
+// hipStreamWaitEvent -- the cross-process dependency lives on the device queues, the peer's
+// host only waits until the record was ENQUEUED (a flag in shared memory), never for it to run.
+class IpcEvent {
+ public:
+  explicit IpcEvent(int64_t device) : dev_(static_cast<int>(device)) {
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    hip_ok(hipEventCreateWithFlags(&ev_, hipEventInterprocess | hipEventDisableTiming), "hipEventCreate(ipc)");
+    own_ = true;
+  }
+  IpcEvent(py::bytes hb, int64_t device) : dev_(static_cast<int>(device)) {
+    std::string s = hb;
+    TORCH_CHECK(s.size() == sizeof(hipIpcEventHandle_t), "bad IPC event handle");
+    hipIpcEventHandle_t h;
+    std::memcpy(&h, s.data(), sizeof(h));
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    hip_ok(hipIpcOpenEventHandle(&ev_, h), "hipIpcOpenEventHandle");
+  }
+  ~IpcEvent() {
+    if (ev_ != nullptr) hipEventDestroy(ev_);
+  }
+  py::bytes handle() const {
+    TORCH_CHECK(own_, "only the creating process exports the handle");
+    hipIpcEventHandle_t h;
+    hip_ok(hipIpcGetEventHandle(&h, ev_), "hipIpcGetEventHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  void record(int64_t stream) { hip_ok(hipEventRecord(ev_, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord"); }
+  void wait(int64_t stream) {
+    hip_ok(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev_, 0), "hipStreamWaitEvent");
+  }
+  bool query() const {
+    const hipError_t e = hipEventQuery(ev_);
+    if (e == hipSuccess) return true;
+    TORCH_CHECK(e == hipErrorNotReady, "hipEventQuery: ", hipGetErrorString(e));
+    return false;
+  }
+  void synchronize() const { hip_ok(hipEventSynchronize(ev_), "hipEventSynchronize"); }
+  int64_t ptr() const { return reinterpret_cast<int64_t>(ev_); }
+
+ private:
+  int dev_;
+  hipEvent_t ev_ = nullptr;
+  bool own_ = false;
+};
+
 }  // namespace
 
 void register_plane(pybind11::module& m) {
@@ -891,6 +939,15 @@ void register_plane(pybind11::module& m) {
       .def("stats", &PlaneEngine::stats, py::arg("reset") = false)
       .def("error", &PlaneEngine::error)
       .def("restore_round", &PlaneEngine::restore_round);
+  py::class_<IpcEvent>(pm, "IpcEvent")
+      .def(py::init<int64_t>())
+      .def(py::init<py::bytes, int64_t>())
+      .def("handle", &IpcEvent::handle)
+      .def("record", &IpcEvent::record)
+      .def("wait", &IpcEvent::wait)
+      .def("query", &IpcEvent::query)
+      .def("synchronize", &IpcEvent::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("ptr", &IpcEvent::ptr);
   py::class_<Arena>(pm, "Arena")
       .def(py::init<int64_t, int64_t>())
       .def("tensor", &Arena::tensor)

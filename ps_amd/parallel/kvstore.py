@@ -7,14 +7,15 @@
   In LOSS_SURFACE_EVAL status ``get`` returns s*w_init + (1-s)*w (:153-155).
 * distributed worker (``client`` = PSClient / PSRouterClient over the native TCP server):
   ``get`` is a per-step cache in front of the servers; a missing key is created with
-  upsert(replace=False) so the first writer wins (:168-190); ``async_get``/``async_wait``
-  batch-prefetch many keys in ONE get_list + ONE upsert_list per shard on a background
-  thread (:74-127, 279-298); ``update`` pushes every summed key grouped by updater spec (one
+  upsert(replace=False) so the first writer wins (:168-190); ``async_get`` queues keys for a
+  prefetch thread (started on first use, :54-68, 279-298) that fetches everything queued in
+  ONE get_list + ONE upsert_list per shard while the caller goes on (:74-107), and
+  ``async_wait`` blocks until every key queued so far is in the cache (:113-127); ``update`` pushes every summed key grouped by updater spec (one
   request per shard per spec instead of one RPC per key) and then meets the servers at the
   consistency point (BSP barrier / SSP clock / nothing for ASP); ``clear`` drops the cache.
 
-The GPU hot path does not go through this class: it uses the co-located collective PS
-(colocated.py) and sharded sparse tables (sparse_table.py).
+The GPU engines have their own key-level store with the same API (gpu_kvstore.py: pulls
+are replica views, sums stay on the device).
 """
 from __future__ import annotations
 
@@ -53,6 +54,14 @@ class KVStore:
         self._cnt: Dict[str, int] = {}
         self._async: Dict[str, Init] = {}
         self._lock = threading.RLock()
+        # prefetch thread (reference KVStore.run, :279-298): queued batches -> one batched fetch
+        self._pf_cv = threading.Condition()
+        self._pf_queue: list = []
+        self._pf_done = 0
+        self._pf_sent = 0
+        self._pf_err: Optional[BaseException] = None
+        self._pf_thread: Optional[threading.Thread] = None
+        self.prefetch_batches = 0
         self.clock = 0
         self.round = 0
         self._fault = None  # lazily built FaultInjector (PS_AMD_FAULT); False = none configured
@@ -95,28 +104,69 @@ class KVStore:
 
     # ------------------------------------------------------------------ batch prefetch
     def async_get(self, key: str, init: Init) -> None:
+        """Queue ``key`` for the prefetch thread (store/KVStore.java:109-111); returns at once.
+        Keys queued before the next ``async_wait`` go out as one batch."""
         with self._lock:
-            self._async[key] = init
+            if key not in self.store:
+                self._async[key] = init
 
     def async_wait(self) -> None:
-        """Fetch every key registered with async_get in one batched round trip."""
+        """Hand the queued keys to the prefetch thread and wait until every key queued so far
+        is in the cache (store/KVStore.java:113-127)."""
         with self._lock:
             pending = {k: f for k, f in self._async.items() if k not in self.store}
             self._async.clear()
-        if not pending:
-            return
-        if not self.distributed:
+        if pending and not self.distributed:
             with self._lock:
                 for k, f in pending.items():
                     if k not in self.store:
                         self._create(k, f)
             return
-        got = self.client.get_list(list(pending))
-        missing = {k: pending[k]() for k, v in got.items() if v is None}
-        created = self.client.update_list(missing, replace=False) if missing else {}
-        with self._lock:
-            for k, v in got.items():
-                self.store[k] = v if v is not None else created[k]
+        if pending:
+            self.prefetch(pending)
+        with self._pf_cv:
+            target = self._pf_sent
+            while self._pf_done < target and self._pf_err is None:
+                self._pf_cv.wait(timeout=1.0)
+            if self._pf_err is not None:
+                err, self._pf_err = self._pf_err, None
+                raise RuntimeError("KVStore prefetch failed") from err
+
+    def prefetch(self, keys: Dict[str, Init]) -> None:
+        """Start fetching ``keys`` (key -> init) on the prefetch thread without waiting."""
+        if not self.distributed or not keys:
+            return
+        with self._pf_cv:
+            if self._pf_thread is None:
+                self._pf_thread = threading.Thread(target=self._prefetch_loop, name="kvstore-prefetch", daemon=True)
+                self._pf_thread.start()
+            self._pf_queue.append(dict(keys))
+            self._pf_sent += 1
+            self._pf_cv.notify_all()
+
+    def _prefetch_loop(self) -> None:
+        while True:
+            with self._pf_cv:
+                while not self._pf_queue:
+                    self._pf_cv.wait()
+                batch = self._pf_queue.pop(0)
+            try:
+                with self._lock:
+                    batch = {k: f for k, f in batch.items() if k not in self.store}
+                if batch:
+                    got = self.client.get_list(list(batch))
+                    missing = {k: batch[k]() for k, v in got.items() if v is None}
+                    created = self.client.update_list(missing, replace=False) if missing else {}
+                    with self._lock:
+                        for k, v in got.items():
+                            self.store[k] = v if v is not None else created[k]
+                self.prefetch_batches += 1
+            except BaseException as e:  # noqa: BLE001 -- surfaced by async_wait
+                with self._pf_cv:
+                    self._pf_err = e
+            with self._pf_cv:
+                self._pf_done += 1
+                self._pf_cv.notify_all()
 
     # ------------------------------------------------------------------ gradients
     def sum(self, key: str, g: torch.Tensor) -> None:
@@ -169,12 +219,18 @@ class KVStore:
         if self.distributed:
             self.client.barrier(self.worker_id)
 
-    def clear(self) -> None:
+    def clear(self, prefetch: bool = True) -> None:
+        """Drop the local sums and (worker) the per-step weight cache (store/KVStore.java:270-277).
+        A worker then starts re-fetching the keys it just dropped on the prefetch thread, so the
+        next step's pull finds them in flight or already cached (their values are post-barrier)."""
         with self._lock:
             self._sum.clear()
             self._cnt.clear()
+            dropped = list(self.store) if self.distributed else []
             if self.distributed:
                 self.store.clear()  # per-step worker cache: next step re-pulls (Q16)
+        if dropped and prefetch:
+            self.prefetch({k: _no_init(k) for k in dropped})
 
     # ------------------------------------------------------------------ model helpers
     def pull_into(self, model: torch.nn.Module, init: Optional[Dict[str, Init]] = None) -> None:
@@ -195,3 +251,9 @@ class KVStore:
         for n, p in model.named_parameters():
             if p.grad is not None:
                 self.sum(n, p.grad.cpu())
+
+
+def _no_init(key: str) -> Init:
+    def f():
+        raise KeyError(f"prefetched key {key!r} vanished from the servers")
+    return f

@@ -184,8 +184,56 @@ def _resnet_body(tp, steps):
         losses.append(loss.item())
     ps.synchronize()
     torch.cuda.synchronize()
+    out = {n: p.detach().float().cpu().clone() for n, p in net.named_parameters() if p.requires_grad}
     ps.close()
-    return losses
+    return losses, out
+
+
+def _bf16_oracle(world, steps, lr=0.05, mom=0.9):
+    """The same bf16 ResNet-tiny (same kernels, per-rank BN batches) in ONE process: every
+    rank's shard is run in turn, the bf16 gradients are summed in fp32 in rank order, scaled by
+    1/W, and momentum-SGD updates an fp32 master whose bf16 copy is the next replica -- the
+    plane's arithmetic without the plane (no arenas, no IPC, no owner chunks)."""
+    from ps_amd.models.resnet import prepare_for_mi355x, resnet_tiny
+
+    torch.manual_seed(0)
+    net = prepare_for_mi355x(resnet_tiny(num_classes=10, fused_bn=True).cuda())
+    params = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
+    master = {n: p.detach().float().clone() for n, p in params}
+    buf = {n: torch.zeros_like(v) for n, v in master.items()}
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    for _ in range(steps):
+        gsum = {n: torch.zeros_like(v) for n, v in master.items()}
+        for r in range(world):
+            for _, p in params:
+                p.grad = None
+            F.cross_entropy(net(x[r::world].bfloat16()).float(), y[r::world]).backward()
+            for n, p in params:
+                gsum[n] += p.grad.float()
+        with torch.no_grad():
+            for n, p in params:
+                buf[n] = mom * buf[n] + gsum[n] * (1.0 / world)
+                master[n] -= lr * buf[n]
+                p.copy_(master[n].to(p.dtype))
+    return {n: p.detach().float().cpu() for n, p in params}
+
+
+def _check_weights_tight(res, world, steps):
+    """every rank's final weights are bitwise equal, and equal to the
+    single-process bf16 oracle up to bf16 rounding of the replica (2 bf16 ulps of |w|, plus an
+    absolute floor for weights near 0): a wrong owner chunk or a stale pull moves a whole chunk
+    by a learning-rate-sized step and fails this."""
+    want = _bf16_oracle(world, steps)
+    w0 = res[0][1]
+    for r in range(1, world):
+        for k in w0:
+            assert torch.equal(w0[k], res[r][1][k]), (r, k)
+    for k, v in want.items():
+        err = (w0[k] - v).abs()
+        bound = 2.0 ** -7 * v.abs() + 2e-3
+        assert bool((err <= bound).all()), (k, err.max().item(), (err / (v.abs() + 1e-3)).max().item())
 
 
 def test_plane_processes_resnet_tiny_bf16_trajectory_vs_fp32():
@@ -210,10 +258,11 @@ def test_plane_processes_resnet_tiny_bf16_trajectory_vs_fp32():
         (sum(ls) / world).backward()
         opt.step()
         lref.append(ls[0].item())
-    la = res[0]
+    la = res[0][0]
     for a, b in zip(la, lref):
         assert abs(a - b) < 0.05 * max(1.0, abs(b)), (la, lref)
     assert la[-1] < la[0], la
+    _check_weights_tight(res, world, steps)
 
 
 def _resnet8_body(tp, steps):
@@ -239,8 +288,9 @@ def _resnet8_body(tp, steps):
         losses.append(loss.item())
     ps.synchronize()
     torch.cuda.synchronize()
+    out = {n: p.detach().float().cpu().clone() for n, p in net.named_parameters() if p.requires_grad}
     ps.close()
-    return losses
+    return losses, out
 
 
 def test_world8_processes_bf16_resnet_tiny_tracks_fp32_oracle():
@@ -267,9 +317,10 @@ def test_world8_processes_bf16_resnet_tiny_tracks_fp32_oracle():
         (sum(ls) / world).backward()
         opt.step()
         lref.append(ls[0].item())
-    la = res[0]
+    la = res[0][0]
     for a, b in zip(la, lref):
         assert abs(a - b) < 0.05 * max(1.0, abs(b)), (la, lref)
+    _check_weights_tight(res, world, steps)
 
 
 def _mlp8_body(tp, models, steps, reduce_fp32):

@@ -177,3 +177,56 @@ def test_tcp_router_checkpoint(tmp_path):
     finally:
         s1.stop()
         s2.stop()
+
+
+class _SlowClient:
+    """A PS client whose batched reads take ``delay`` seconds (a slow / remote server)."""
+
+    def __init__(self, delay):
+        import threading
+
+        self.delay, self.vals, self.calls = delay, {}, 0
+        self.mu = threading.Lock()
+
+    def get_list(self, keys):
+        import time
+
+        time.sleep(self.delay)
+        with self.mu:
+            self.calls += 1
+            return {k: (self.vals[k].clone() if k in self.vals else None) for k in keys}
+
+    def update_list(self, items, replace=False):
+        with self.mu:
+            for k, v in items.items():
+                self.vals.setdefault(k, v.clone())
+            return {k: self.vals[k].clone() for k in items}
+
+    def get(self, key):
+        return self.get_list([key])[key]
+
+
+def test_prefetch_thread_overlaps_a_slow_server():
+    """KVStore docstring: async_get queues keys for a real prefetch thread;
+    after update/clear a worker re-fetches its dropped keys in the background, so the next
+    step's pull overlaps the caller's work instead of paying the server latency again."""
+    import time
+
+    c = _SlowClient(0.3)
+    kv = KVStore(c, worker_id=0, consistency="asp")
+    for k in ("a", "b", "c"):
+        kv.async_get(k, lambda k=k: torch.full((2,), float(ord(k))))
+    t0 = time.perf_counter()
+    kv.async_wait()  # one batched round trip for the three keys
+    assert time.perf_counter() - t0 < 0.55 and c.calls == 1
+    assert torch.equal(kv.get("b"), torch.full((2,), 98.0))
+    c.vals["b"] = torch.full((2,), 5.0)  # the server moved on
+    kv.clear()  # drops the cache and starts re-fetching a, b, c in the background
+    time.sleep(0.4)  # the caller's compute
+    t1 = time.perf_counter()
+    for k in ("a", "b", "c"):
+        kv.async_get(k, lambda: torch.zeros(2))
+    kv.async_wait()
+    assert time.perf_counter() - t1 < 0.1  # already fetched while we computed
+    assert torch.equal(kv.get("b"), torch.full((2,), 5.0))
+    assert kv.prefetch_batches == 2
