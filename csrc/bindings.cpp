@@ -1001,6 +1001,37 @@ Tensor maxpool_nhwc_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, 
   return dx;
 }
 
+// stem: dz, dgamma, dbeta of z -> BN -> ReLU -> maxpool 3x3/2/1 from the pooled gradient (pool.hip)
+std::vector<Tensor> pool_bn_bwd(Tensor dy, Tensor idx, Tensor z, Tensor mask_coef, Tensor gamma, Tensor mean,
+                                Tensor invstd) {
+  check_gpu(dy, "dy");
+  check_gpu(z, "z");
+  TORCH_CHECK(dy.dim() == 4 && dy.scalar_type() == torch::kBFloat16 && dy.is_contiguous(), "dy: [N,OH,OW,C] bf16");
+  TORCH_CHECK(z.dim() == 4 && z.scalar_type() == torch::kBFloat16 && z.is_contiguous(), "z: [N,H,W,C] bf16");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == torch::kUInt8 && idx.is_contiguous(), "idx like dy");
+  const int64_t N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3);
+  TORCH_CHECK(dy.size(0) == N && dy.size(3) == C && H % 2 == 0 && W % 2 == 0 && dy.size(1) == H / 2 &&
+                  dy.size(2) == W / 2, "pool 3x3/2/1 over even H, W");
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "C / 8 must divide 256");
+  TORCH_CHECK(N * (H / 2) * (W / 2) * (C / 8) < (int64_t(1) << 31), "32-bit quad index");
+  for (const Tensor* t : {&mask_coef, &gamma, &mean, &invstd}) check_f32(*t, "bn vector");
+  TORCH_CHECK(mask_coef.numel() == 2 * C && gamma.numel() == C && mean.numel() == C && invstd.numel() == C, "bn sizes");
+  const c10::DeviceGuard guard(z.device());
+  auto fopt = z.options().dtype(torch::kFloat32);
+  const int G = psamd::pool_bn_bwd_blocks(N, static_cast<int>(H), static_cast<int>(W), static_cast<int>(C));
+  auto ws = torch::empty({2 * G * C + 3 * C}, fopt);
+  auto dz = torch::empty_like(z);
+  auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt);
+  psamd::launch_pool_bn_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                            reinterpret_cast<const uint16_t*>(z.data_ptr()), mask_coef.data_ptr<float>(),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                            ws.data_ptr<float>(), G, dg.data_ptr<float>(), db.data_ptr<float>(),
+                            reinterpret_cast<uint16_t*>(dz.data_ptr()), static_cast<int>(N), static_cast<int>(H),
+                            static_cast<int>(W), static_cast<int>(C), static_cast<int>(H / 2), static_cast<int>(W / 2),
+                            cur_stream(z));
+  return {dz, dg, db};
+}
+
 std::vector<Tensor> bn_act_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x, c10::optional<Tensor> gamma, Tensor mean,
                                Tensor invstd, int64_t act, bool want_dres, bool affine,
                                c10::optional<Tensor> mask_coef, c10::optional<Tensor> mbits) {
@@ -1121,7 +1152,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
                               c10::optional<Tensor> aux, c10::optional<Tensor> kshift, c10::optional<Tensor> mc,
                               c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits,
                               c10::optional<Tensor> aux2, c10::optional<Tensor> bits2, c10::optional<Tensor> a2,
-                              c10::optional<Tensor> bwd) {
+                              c10::optional<Tensor> bwd, c10::optional<Tensor> aux3, c10::optional<Tensor> mean2,
+                              c10::optional<Tensor> invstd2) {
   check_rows(a, "a");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
@@ -1129,8 +1161,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   const int64_t N = b.size(0), K = b.size(1);
   TORCH_CHECK(K == static_cast<int64_t>(g.ks) * g.ks * g.C, "b must be [N, ks*ks*C]");
   TORCH_CHECK(N % 64 == 0 && N <= 8192, "N must be a multiple of 64, <= 8192");
-  TORCH_CHECK(epi >= 0 && epi <= 8, "epi in 0..8");
-  const int base = epi == 6 ? 5 : epi == 7 ? 2 : epi == 8 ? 4 : static_cast<int>(epi);
+  TORCH_CHECK(epi >= 0 && epi <= 9, "epi in 0..9");
+  const int base = epi == 6 || epi == 9 ? 5 : epi == 7 ? 2 : epi == 8 ? 4 : static_cast<int>(epi);
   const bool fold = epi >= 6;
   const int64_t M = gi.second * g.OH * g.OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "pixel count");
@@ -1174,6 +1206,14 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     aux2p = u16(*aux2);
     bits2p = bits2->data_ptr<uint8_t>();
   }
+  const uint16_t* aux3p = nullptr;
+  if (epi == 9) {
+    TORCH_CHECK(aux3.has_value() && aux3->defined() && mean2.has_value() && invstd2.has_value(),
+                "epi 9 needs aux3, mean2, invstd2");
+    check_rows(*aux3, "aux3");
+    TORCH_CHECK(aux3->numel() == M * N, "aux3 must be [M, N]");
+    aux3p = u16(*aux3);
+  }
   const c10::DeviceGuard guard(a.device());
   auto c = torch::empty({M, N}, a.options());
   auto fopt = a.options().dtype(torch::kFloat32);
@@ -1183,7 +1223,10 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;
-  Tensor part = sums ? torch::empty({2, G, N}, fopt) : Tensor();
+  TORCH_CHECK(epi != 9 || psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
+                                                   has_pro || has_bwd, g).bm == 128,
+              "epi 9 runs on the 128-pixel tiles");
+  Tensor part = sums ? torch::empty({epi == 9 ? 3 : 2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};
   p.a = u16(a);
   p.b = u16(b);
@@ -1203,6 +1246,9 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   p.mean = f32_opt(mean, N, "mean");
   p.invstd = f32_opt(invstd, N, "invstd");
   p.part = sums ? part.data_ptr<float>() : nullptr;
+  p.aux3 = aux3p;
+  p.mean2 = epi == 9 ? f32_opt(mean2, N, "mean2") : nullptr;
+  p.invstd2 = epi == 9 ? f32_opt(invstd2, N, "invstd2") : nullptr;
   Tensor aout;
   if (has_bwd) {
     aout = torch::empty_like(a);
@@ -1428,7 +1474,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
         py::arg("aux2") = py::none(), py::arg("bits2") = py::none(), py::arg("a2") = py::none(),
-        py::arg("bwd") = py::none());
+        py::arg("bwd") = py::none(), py::arg("aux3") = py::none(), py::arg("mean2") = py::none(),
+        py::arg("invstd2") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("weight_prep", &weight_prep);
@@ -1502,6 +1549,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_split_bwd", &rope_split_bwd);
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
+  m.def("pool_bn_bwd", &pool_bn_bwd);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),
         py::arg("mask_coef") = py::none(), py::arg("mbits") = py::none());

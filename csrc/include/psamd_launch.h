@@ -183,6 +183,12 @@ void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, 
                              int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                              int OW, int k, int s, int p, hipStream_t st);
+// stem backward: maxpool 3x3/2/1 scatter fused into the BN(+ReLU) backward of its input z
+// (mc = the forward's [scale | shift]); ws: [2 G C + 3 C] fp32, G = pool_bn_bwd_blocks(...)
+int pool_bn_bwd_blocks(int64_t N, int H, int W, int C);
+void launch_pool_bn_bwd(const uint16_t* dy, const uint8_t* idx, const uint16_t* z, const float* mc, const float* mean,
+                        const float* invstd, const float* gamma, float* ws, int G, float* dgamma, float* dbeta,
+                        uint16_t* dz, int N, int H, int W, int C, int OH, int OW, hipStream_t st);
 
 // ---------------------------------------------------------------- stem.hip (ResNet 7x7/2 stem, MFMA)
 // x: [N, H, W, cin] bf16, cin 3 or 4 (channel 3 meets zero weights); wp: [64][224] packed
@@ -279,7 +285,8 @@ struct ConvGemmArgs {
                         // 4 + residual of the (OH+1)/2 x (OW+1)/2 map at even (h, w),
                         // 5 + residual masked by bits (aux * relu'(forward output)),
                         // 6/7/8 = 5/2/4 + the previous block's bn3 backward reduce (aux2, bits2,
-                        // mean, invstd): output masked by bits2, sums into part
+                        // mean, invstd): output masked by bits2, sums into part; 9 = 6 + the
+                        // previous block's downsample-BN sum (aux3, mean2, invstd2)
   const uint16_t* aux;  // epi 2/4/5: residual rows; epi 3: BN input z [M, N]
   const uint8_t* bits;  // epi 5/6: ReLU mask bits of aux's elements
   const uint16_t* aux2; // epi 6-8: previous block's bn3 input z3 [M, N]
@@ -289,6 +296,10 @@ struct ConvGemmArgs {
   const float* mean;    // epi 3/6-8: [N]
   const float* invstd;  // epi 3/6-8: [N]
   float* part;          // epi 1/3/6-8: [2][conv_fwd_plan(M, N, K, pro).gm][N] block partial sums
+                        // (epi 9: [3][gm][N], the third = the downsample BN's sum(g * xhat))
+  const uint16_t* aux3; // epi 9: the previous block's downsample-BN input zd [M, N]
+  const float* mean2;   // epi 9: [N] that BN's batch mean / inverse std
+  const float* invstd2;
   // BN-backward prologue (1x1, epi 3 only; excludes pro): A := bf16(ca * a + cb * a2 + cc), the
   // previous BN's data gradient from its output gradient a and input a2 (coefficients bwd =
   // [ca | cb | cc], 3C); the A tile is also stored to aout [M, C] (by the channel-tile-0 blocks)

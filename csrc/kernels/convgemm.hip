@@ -23,6 +23,9 @@
 //               6/7/8: epilogue 5/2/4, then the PREVIOUS block's bn3 backward reduce folded in:
 //                  g = v * relu'(previous block output) from its bits (stored masked) and the
 //                  sums sum(g), sum(g * (z3 - mean) * invstd) over that block's bn3 input z3
+//               9: epilogue 6 when the previous block has a downsample branch: its BN's backward
+//                  gets the same g, so a third sum sum(g * (zd - mean2) * invstd2) over the
+//                  downsample BN input zd replaces that BN's separate reduce pass
 //   conv_wgrad  dW[n, k] = sum_m dZ[m, n] f(A[src(m, k)]), split over m; both operands are read
 //               transposed from row-major LDS tiles (ds_read_b64_tr_b16); fp32 per-split slabs,
 //               fixed-order reduction (deterministic, no atomics).
@@ -192,9 +195,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   constexpr bool BWD = PRO == 2;
   static_assert(!BWD || (KS1 && EPI == 3 && !GLDS), "the BN-backward prologue is a 1x1 data-gradient prologue");
   constexpr int AR2 = BWD ? BM / 32 : 1;
-  // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce
+  // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce; 9 = 6 + the
+  // previous block's downsample-BN sum (third partial slab)
   constexpr bool FOLD = EPI >= 6;
-  constexpr int BASE = EPI == 6 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
+  constexpr bool FOLD_DS = EPI == 9;
+  constexpr int BASE = EPI == 6 || EPI == 9 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
+  constexpr int NSUM = FOLD_DS ? 3 : 2;
   // waves 2 x 2 over the tile; the tall 256 x 64 tile (LDS-DMA path only) stacks them 4 x 1 so
   // every wave still computes 64 x 64 (a 128 x 64 tile gave each wave 64 x 32: 1.5 fragment
   // reads per MFMA instead of 1, and half the weight-tile reuse)
@@ -210,7 +216,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   constexpr int CS = BN + 4;
   // LDS: [A0 | A1] overlaid by the output tile + statistics scratch, then [B0 | B1] (never
   // overlaid, so a resident weight tile survives the epilogues)
-  constexpr int EPI_ELEMS = BM * CS + 8 * BN * 2;
+  // EPI 9 keeps its third running sum in LDS (8 floats per thread past the output tile): in
+  // registers it pushed the register-staged variant from 20 to 76 B/lane of scratch
+  constexpr int RED_ELEMS = 4 * NSUM * BN * 2 > (FOLD_DS ? 256 * 8 * 2 : 0) ? 4 * NSUM * BN * 2 : 256 * 8 * 2;
+  constexpr int EPI_ELEMS = BM * CS + RED_ELEMS;
   constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : 2 * BM * kBK;
   constexpr int B_BASE = ((A_ELEMS > EPI_ELEMS ? A_ELEMS : EPI_ELEMS) + 7) & ~7;
   constexpr int LDS_ELEMS = B_BASE + 2 * BN * kBK;
@@ -371,6 +380,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   float s1[8], s2[8], e0[8], e1[8], e2[8], e3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = e0[j] = e1[j] = e2[j] = e3[j] = 0.f;
+  float* s3l = reinterpret_cast<float*>(lds + BM * CS) + t * 8;  // EPI 9: this thread's third sum
+  if constexpr (FOLD_DS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s3l[j] = 0.f;
+  }
   if constexpr (EPI == 1) {
     if (p.kshift) load8(p.kshift, nc, e0);
   } else if constexpr (EPI == 3) {
@@ -493,12 +507,52 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         }
       }
       *reinterpret_cast<u16x8*>(p.c + o) = v;
+      if constexpr (FOLD_DS) {  // the masked g back into this thread's own tile slots (epilogue_ds)
+        *reinterpret_cast<u16x4*>(Cs + rr * CS + cg * 8) = u16x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<u16x4*>(Cs + rr * CS + cg * 8 + 4) = u16x4{v[4], v[5], v[6], v[7]};
+      }
+    }
+  };
+  // EPI 9: second pass over the same rows once the first pass's row registers are dead (the
+  // register-staged variant sits at the 256-VGPR budget): the downsample BN input rows zd, then
+  // sum(g * (zd - mean2) * invstd2) with g read back from the thread's own tile slots
+  auto epilogue_ds = [&](int mt) {
+    if constexpr (FOLD_DS) {
+      float m2[8], i2[8], s3[8];
+      load8(p.mean2, nc, m2);
+      load8(p.invstd2, nc, i2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s3[j] = s3l[j];
+      const int m0 = mt * BM;
+      constexpr int HP = NPASS > 1 ? NPASS / 2 : 1;  // rows in flight per half (register budget)
+#pragma unroll
+      for (int h0 = 0; h0 < NPASS; h0 += HP) {
+        u16x8 zd[HP];
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int m = min(m0 + r0 + (h0 + i) * RPP, p.M - 1);
+          zd[i] = *reinterpret_cast<const u16x8*>(p.aux3 + orow(m) * p.N + nc);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int rr = r0 + (h0 + i) * RPP;
+          if (m0 + rr >= p.M) break;
+          const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8);
+          const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + cg * 8 + 4);
+          const u16x8 gv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s3[j] += bf16_to_f32(gv[j]) * ((bf16_to_f32(zd[i][j]) - m2[j]) * i2[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s3l[j] = s3[j];
     }
   };
   auto epilogue = [&](int mt) {
     acc_to_lds();
     lds_barrier();
     epilogue_rows(mt);
+    epilogue_ds(mt);
   };
 
   // one step of the (tile, stage) sequence; SF: the free register set (held step q), SN: step q + 1
@@ -515,6 +569,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       epi_load(mg + cti * GM);
       lds_barrier();
       epilogue_rows(mg + cti * GM);
+      epilogue_ds(mg + cti * GM);
       zero_acc();
       ckt = 0;
       ++cti;
@@ -723,6 +778,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   }
 
   if constexpr (EPI == 1 || EPI == 3 || FOLD) {
+    float s3[FOLD_DS ? 8 : 1];
+    if constexpr (FOLD_DS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s3[j] = s3l[j];
+      lds_barrier();  // every thread has its sum before the reduction scratch overwrites the slots
+    }
     // threads with equal cg: lanes l ^ CPR, l ^ 2 CPR, ... of a wave, then the 4 waves via LDS
 #pragma unroll
     for (int off = CPR; off < 64; off <<= 1)
@@ -730,6 +791,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       for (int j = 0; j < 8; ++j) {
         s1[j] += __shfl_xor(s1[j], off, 64);
         s2[j] += __shfl_xor(s2[j], off, 64);
+        if constexpr (FOLD_DS) s3[j] += __shfl_xor(s3[j], off, 64);
       }
     float* red = reinterpret_cast<float*>(lds + BM * CS);
     if (lane < CPR) {
@@ -737,6 +799,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       for (int j = 0; j < 8; ++j) {
         red[wave * BN + cg * 8 + j] = s1[j];
         red[(4 + wave) * BN + cg * 8 + j] = s2[j];
+        if constexpr (FOLD_DS) red[(8 + wave) * BN + cg * 8 + j] = s3[j];
       }
     }
     lds_barrier();
@@ -744,6 +807,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       p.part[mg * static_cast<int64_t>(p.N) + n0 + c] = (red[c] + red[BN + c]) + (red[2 * BN + c] + red[3 * BN + c]);
       p.part[(static_cast<int64_t>(GM) + mg) * p.N + n0 + c] =
           (red[4 * BN + c] + red[5 * BN + c]) + (red[6 * BN + c] + red[7 * BN + c]);
+      if constexpr (FOLD_DS)
+        p.part[(2 * static_cast<int64_t>(GM) + mg) * p.N + n0 + c] =
+            (red[8 * BN + c] + red[9 * BN + c]) + (red[10 * BN + c] + red[11 * BN + c]);
     }
   }
 }
@@ -1502,6 +1568,7 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
     case 6: PSAMD_CF(BN, PRO, 6); break; \
     case 7: PSAMD_CF(BN, PRO, 7); break; \
     case 8: PSAMD_CF(BN, PRO, 8); break; \
+    case 9: PSAMD_CF(BN, PRO, 9); break; \
     default: PSAMD_CF(BN, PRO, 0); break; \
   }
   if (pl.bm == 256) {  // LDS-DMA only (no prologue, deep K)

@@ -259,6 +259,145 @@ __global__ __launch_bounds__(256) void maxpool_s2k3_bwd_quad_kernel(const uint16
   }
 }
 
+// ResNet stem backward with the max-pool scatter fused into the BatchNorm backward passes
+// (k = 3, s = 2, p = 1, even H / W; the pool input was relu(z * scale + shift), never stored):
+// the pool's data gradient g is recomputed per 2x2 dx quad from the four covering windows'
+// (argmax, dy) -- pooled-size reads -- instead of being written at full resolution and read twice:
+//   REDUCE  per-channel partials sum(g'), sum(g' (z - mean) invstd) with g' = g * relu'(z sc + sh)
+//           -> [G][C] (then the shared bn_bwd_finalize_kernel: dgamma, dbeta, ca / cb / cc)
+//   APPLY   dz = ca g' + cb z + cc
+// (replacing pool-bwd write + reduce read + apply read of the full-resolution gradient: 3 of the
+// 7 full-size tensor passes of the stem backward).  g is rounded to bf16 exactly where the
+// unfused path stored it.  The grid stride is a multiple of C / 8 (launcher), so every thread
+// keeps one channel group and the partials stay in registers.
+template <bool APPLY>
+__global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx,
+                                                          const uint16_t* __restrict__ z,
+                                                          const float* __restrict__ mc,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ coef, float* __restrict__ pd,
+                                                          float* __restrict__ px, uint16_t* __restrict__ dz, int N,
+                                                          int H, int W, int C, int OH, int OW) {
+  const int cv = C / 8, QH = H / 2, QW = W / 2;
+  const uint32_t total = static_cast<uint32_t>(N) * QH * QW * cv;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t v0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = static_cast<int>(v0 % cv);
+  float sc[8], sh[8], mu[8], is[8], A[8], B[8], Cc[8];
+  load8(mc, c8 * 8, sc);
+  load8(mc + C, c8 * 8, sh);
+  if constexpr (APPLY) {
+    load8(coef, c8 * 8, A);
+    load8(coef + C, c8 * 8, B);
+    load8(coef + 2 * C, c8 * 8, Cc);
+  } else {
+    load8(mean, c8 * 8, mu);
+    load8(invstd, c8 * 8, is);
+  }
+  float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t v = v0; v < total; v += stride) {
+    uint32_t r = v / cv;
+    const int b = static_cast<int>(r % QW);
+    r /= QW;
+    const int a = static_cast<int>(r % QH);
+    const int n = static_cast<int>(r / QH);
+    uint64_t pk[4];
+    u16x8 gv[4], zv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // windows past the map are clamped in bounds and never used
+      const int oh = min(a + (q >> 1), OH - 1), ow = min(b + (q & 1), OW - 1);
+      const int64_t o = ((static_cast<int64_t>(n) * OH + oh) * OW + ow) * C + c8 * 8;
+      pk[q] = *reinterpret_cast<const uint64_t*>(idx + o);
+      gv[q] = *reinterpret_cast<const u16x8*>(dy + o);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      zv[q] = *reinterpret_cast<const u16x8*>(
+          z + ((static_cast<int64_t>(n) * H + 2 * a + (q >> 1)) * W + 2 * b + (q & 1)) * C + c8 * 8);
+    const bool ih = a + 1 < OH, iw = b + 1 < OW;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = q >> 1, j = q & 1;
+          if (i > dh || j > dw) continue;
+          if ((i && !ih) || (j && !iw)) continue;
+          const uint8_t code = static_cast<uint8_t>((dh + 1 - 2 * i) * 3 + (dw + 1 - 2 * j));
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (static_cast<uint8_t>(pk[q] >> (8 * e)) == code) acc[e] += bf16_to_f32(gv[q][e]);
+        }
+        const u16x8& zz = zv[dh * 2 + dw];
+        float out[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zf = bf16_to_f32(zz[e]);
+          const float g = zf * sc[e] + sh[e] > 0.f ? bf16_to_f32(f32_to_bf16(acc[e])) : 0.f;
+          if constexpr (APPLY) {
+            out[e] = A[e] * g + B[e] * zf + Cc[e];
+          } else {
+            sd[e] += g;
+            sx[e] += g * (zf - mu[e]) * is[e];
+          }
+        }
+        if constexpr (APPLY)
+          store8(dz, ((static_cast<int64_t>(n) * H + 2 * a + dh) * W + 2 * b + dw) * C + c8 * 8, out);
+      }
+  }
+  if constexpr (!APPLY) {
+    __shared__ float lds_d[256 * 8];
+    __shared__ float lds_x[256 * 8];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      lds_d[t * 8 + e] = sd[e];
+      lds_x[t * 8 + e] = sx[e];
+    }
+    __syncthreads();
+    if (t < cv) {  // fixed order over the threads of channel group t
+      for (int k = t + cv; k < static_cast<int>(blockDim.x); k += cv)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sd[e] += lds_d[k * 8 + e];
+          sx[e] += lds_x[k * 8 + e];
+        }
+      float* od = pd + static_cast<int64_t>(blockIdx.x) * C + t * 8;
+      float* ox = px + static_cast<int64_t>(blockIdx.x) * C + t * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        od[e] = sd[e];
+        ox[e] = sx[e];
+      }
+    }
+  }
+}
+
+// blocks of the fused stem backward: a multiple of 8 channel groups' worth of threads so each
+// thread keeps its channel group (C / 8 divides 256)
+int pool_bn_bwd_blocks(int64_t N, int H, int W, int C) {
+  const int64_t quads = N * (H / 2) * (W / 2) * (C / 8);
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(2048, (quads + 255) / 256)));
+}
+
+void launch_pool_bn_bwd(const uint16_t* dy, const uint8_t* idx, const uint16_t* z, const float* mc, const float* mean,
+                        const float* invstd, const float* gamma, float* ws, int G, float* dgamma, float* dbeta,
+                        uint16_t* dz, int N, int H, int W, int C, int OH, int OW, hipStream_t st) {
+  float* pd = ws;
+  float* px = ws + static_cast<int64_t>(G) * C;
+  float* coef = px + static_cast<int64_t>(G) * C;
+  hipLaunchKernelGGL((pool_bn_bwd_kernel<false>), dim3(G), dim3(256), 0, st, dy, idx, z, mc, mean, invstd, nullptr, pd,
+                     px, nullptr, N, H, W, C, OH, OW);
+  launch_bn_bwd_partials(pd, px, G, nullptr, nullptr, gamma, mean, invstd, dgamma, dbeta, coef, nullptr,
+                         static_cast<int64_t>(N) * H * W, C, st);
+  hipLaunchKernelGGL((pool_bn_bwd_kernel<true>), dim3(G), dim3(256), 0, st, dy, idx, z, mc, nullptr, nullptr, coef,
+                     nullptr, nullptr, dz, N, H, W, C, OH, OW);
+}
+
 // log2(C / 8) when the row mapping applies (C / 8 a power of two, rows of >= 64 elements so a
 // block's threads stay busy, row indices in int range), else -1 (generic flat mapping)
 static int row_lcv(int C, int width, int64_t rows) {

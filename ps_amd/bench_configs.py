@@ -165,8 +165,11 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
         model = LlamaForCausalLM(cfg, checkpointing=bool(int(os.environ.get("PS_AMD_LLAMA_CKPT", "0")))).to(
             torch.bfloat16)
     upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
+    # PS_AMD_OVERLAP=0: every bucket's serve after backward instead of overlapped with it -- the
+    # A/B that prices the serve's HBM traffic stretching backward (profiles/r4_llama_serve_overlap.txt)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
-                     compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None))
+                     compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None),
+                     overlap=os.environ.get("PS_AMD_OVERLAP", "1") == "1")
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)
     pool = [torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g) for _ in range(POOL)]

@@ -10,6 +10,8 @@ zero-fill / cast side kernels.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -166,9 +168,14 @@ class _StemBnReluMaxPool(torch.autograd.Function):
         n, oh, ow, c = z.shape
         dyn = dy.permute(0, 2, 3, 1)
         dyn = dyn if dyn.is_contiguous() else dyn.contiguous()
-        dpool = native().maxpool_nhwc_bwd(dyn, idx, oh, ow, 3, 2, 1)
-        dz, _, dg, db = native().bn_act_bwd(dpool.view(-1, c), None, z.view(-1, c), gamma, mean, invstd, 1, False,
-                                            True, coef)
+        if oh % 2 == 0 and ow % 2 == 0 and 256 % (c // 8) == 0 and os.environ.get("PS_AMD_POOL_BN_BWD", "1") != "0":
+            # pool scatter fused into both BN-backward passes: the full-resolution pool gradient
+            # is never written (csrc/kernels/pool.hip pool_bn_bwd_kernel)
+            dz, dg, db = native().pool_bn_bwd(dyn, idx, z, coef, gamma, mean, invstd)
+        else:
+            dpool = native().maxpool_nhwc_bwd(dyn, idx, oh, ow, 3, 2, 1)
+            dz, _, dg, db = native().bn_act_bwd(dpool.view(-1, c), None, z.view(-1, c), gamma, mean, invstd, 1, False,
+                                                True, coef)
         dw = unpack_stem_grad(native().stem_conv_wrw(xin, dz.view(n, oh, ow, c)), w.shape[1]).to(w.dtype)
         return None, dw, dg, db, None, None, None, None
 

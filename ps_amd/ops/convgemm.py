@@ -173,16 +173,20 @@ def _conv3x3_enabled() -> bool:
 class _Link:
     """bn3 backward hand-off from block i (consumer of this block's output) to this block."""
 
-    __slots__ = ("out_ref", "z3", "bits", "mean", "invstd", "part", "dx_ptr", "dx_version", "dx_keep")
+    __slots__ = ("out_ref", "z3", "bits", "mean", "invstd", "part", "dx_ptr", "dx_version", "dx_keep", "zd", "md",
+                 "idd")
 
-    def __init__(self, z3, bits, mean, invstd):
+    def __init__(self, z3, bits, mean, invstd, zd=None, md=None, idd=None):
         self.out_ref = None
         self.z3, self.bits, self.mean, self.invstd = z3, bits, mean, invstd
+        # a downsample block also hands its downsample BN (input zd, batch stats): the consumer's
+        # epilogue 9 reduces that BN's backward sum next to bn3's
+        self.zd, self.md, self.idd = zd, md, idd
         self.part = None
         self.dx_ptr = self.dx_version = self.dx_keep = None
 
 
-FOLD_STATS = {"used": 0}  # bn3 backward passes that took the consumer's partials (tests)
+FOLD_STATS = {"used": 0, "ds": 0}  # bn3 / downsample-BN backward passes that took the consumer's partials
 
 
 def _bwd_prologue_enabled(c3: int) -> bool:
@@ -197,6 +201,11 @@ def _bwd_prologue_enabled(c3: int) -> bool:
 
 def _fold_enabled() -> bool:
     return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
+
+
+def _fold_ds_enabled() -> bool:
+    """Downsample BN's backward reduce in the consumer block's conv1 data-gradient epilogue (9)."""
+    return os.environ.get("PS_AMD_FOLD_BN_DS", "1") != "0"
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -243,7 +252,8 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.dims = (n, h, w, s, oh, ow)
         ctx.prep = _prep_for(blk, w1, w2, w3)  # backward weight layouts built for this forward
         ctx.link_in = link_in  # block i-1's bn3: its reduce runs in our conv1 data-grad epilogue
-        ctx.link_out = _Link(z3, obits, m3, i3) if _fold_enabled() else None
+        ctx.link_out = (_Link(z3, obits, m3, i3, zd if _fold_ds_enabled() else None, md, idd)
+                        if _fold_enabled() else None)
         return image(out, n, oh, ow)
 
     @staticmethod
@@ -260,9 +270,14 @@ class _BottleneckFn(torch.autograd.Function):
         w3t = pw[1] if pw else _mat(w3).t()
         lk = ctx.link_out
         dz3 = None
+        ds_part = None  # [2, G, C] downsample-BN sums from the consumer's epilogue 9
         if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
                 and d2._version == lk.dx_version):
             # the consumer block already masked dout and reduced bn3's backward sums
+            if lk.part.shape[0] == 3:
+                ds_part = torch.stack([lk.part[0], lk.part[2]])
+                lk.part = lk.part[:2]
+                FOLD_STATS["ds"] += 1
             if _bwd_prologue_enabled(z3.shape[1]):
                 # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
                 # the weight gradient: no separate apply pass over the widest tensors
@@ -325,12 +340,18 @@ class _BottleneckFn(torch.autograd.Function):
         fold = li is not None and _fold_enabled()
         fkw = dict(mean=li.mean, invstd=li.invstd, aux2=li.z3, bits2=li.bits) if fold else {}
         if wd is not None:
-            dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
+            if ds_part is not None:  # d2 is masked already; sum(g), sum(g * xhat_d) came with it
+                dzd, dgd, dbd = nat.bn_bwd_partials(d2, zd, ds_part, gd, md, idd)
+            else:
+                dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
             sd.fork()
             dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
             t = nat.conv_gemm(dzd, pw[3] if pw else _mat(wd).t(), go)[0]
             epi = 4 if s == 2 else 2
             dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
+        elif fold and li.zd is not None:  # the producer has a downsample BN: its sum rides along
+            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, 9, d2, bits=obits, aux3=li.zd, mean2=li.md, invstd2=li.idd,
+                                      **fkw)
         else:
             dx2, part = nat.conv_gemm(dz1, w1t, gi, None, 6 if fold else 5, d2, bits=obits, **fkw)
         if fold:

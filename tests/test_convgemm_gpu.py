@@ -462,9 +462,17 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
         loss.backward()
         return xi.grad.clone(), {n: p.grad.clone() for n, p in a.named_parameters()}
 
-    before = cg.FOLD_STATS["used"]
+    before, before_ds = cg.FOLD_STATS["used"], cg.FOLD_STATS["ds"]
     ga, pa = run()
     assert cg.FOLD_STATS["used"] - before == (1 if extra_consumer else 2)
+    # the downsample block's BN sum rides in block 1's epilogue 9 unless y1 has a second consumer
+    assert cg.FOLD_STATS["ds"] - before_ds == (0 if extra_consumer else 1)
+    monkeypatch.setenv("PS_AMD_FOLD_BN_DS", "0")  # bn3 folded, the downsample BN reduced on its own
+    gc, pc = run()
+    _close(ga, gc, tol=1e-2, amax=0.05)
+    for n in pc:
+        _close(pa[n], pc[n], tol=1e-2, amax=0.05)
+    monkeypatch.delenv("PS_AMD_FOLD_BN_DS")
     monkeypatch.setenv("PS_AMD_FOLD_BN3", "0")
     before = cg.FOLD_STATS["used"]
     gb, pb = run()
@@ -602,3 +610,30 @@ def test_conv3x3_patch_forward_statistics_and_data_grad(n, hw, cin, cout):
     xhat = (z1.reshape(-1, cin) - mean) * invstd
     torch.testing.assert_close(p2[0].sum(0).cpu(), gc.sum(0), rtol=1e-4, atol=5e-2)
     torch.testing.assert_close(p2[1].sum(0).cpu(), (gc * xhat).sum(0), rtol=1e-4, atol=5e-2)
+
+
+@pytest.mark.parametrize("M,K,N", [(3000, 64, 256), (1000, 128, 512), (517, 512, 256)])
+def test_epilogue9_downsample_bn_sum(M, K, N):
+    """Epilogue 9 = epilogue 6 (+ residual masked by bits, output masked by the previous block's
+    bits, bn3 sums) + the third partial sum(g * (zd - mean2) * invstd2) of the previous block's
+    downsample BN: same output and first two slabs as epilogue 6, third slab vs fp32.  K = 64 / 128
+    run the persistent register-staged tiles (the third sum lives in LDS), K = 512 the LDS-DMA one."""
+    g = _gen(M + K + N)
+    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    r, z3, zd = _rnd(M, N, g=g), _rnd(M, N, g=g), _rnd(M, N, g=g)
+
+    def bits_of(keep):
+        return (keep.view(-1, 8).int() << torch.arange(8)).sum(1).to(torch.uint8).to(DEV)
+
+    k1, k2 = torch.rand(M, N, generator=g) > 0.5, torch.rand(M, N, generator=g) > 0.4
+    m3, i3 = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+    md, idd = torch.randn(N, generator=g) * 0.1, torch.rand(N, generator=g) + 0.5
+    common = dict(bits=bits_of(k1), aux2=_bf(z3), bits2=bits_of(k2), mean=m3.to(DEV), invstd=i3.to(DEV))
+    geo1 = [M, 1, M, 1, 1, 1, 0]
+    c6, p6 = native().conv_gemm(_bf(a), _bf(b), geo1, None, 6, _bf(r), **common)
+    c9, p9 = native().conv_gemm(_bf(a), _bf(b), geo1, None, 9, _bf(r), aux3=_bf(zd), mean2=md.to(DEV),
+                                invstd2=idd.to(DEV), **common)
+    assert p9.shape[0] == 3 and torch.equal(c6, c9)
+    torch.testing.assert_close(p9[:2], p6, rtol=0, atol=0)
+    gv = c9.float().cpu()
+    torch.testing.assert_close(p9[2].sum(0).cpu(), (gv * ((zd - md) * idd)).sum(0), rtol=1e-3, atol=1e-2)

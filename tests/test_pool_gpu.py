@@ -151,3 +151,33 @@ def test_fused_bn_pool_value_and_first_argmax_exact(H, k, s, p):
     ik = idx.view(N, OH, OH, C).permute(0, 3, 1, 2).long()
     assert torch.equal(yk, ref)
     assert torch.equal(ik, first)
+
+
+@pytest.mark.parametrize("N,H,C", [(2, 112, 64), (3, 16, 32)])
+def test_pool_bn_bwd_fused_matches_unfused(N, H, C):
+    """Stem backward with the pool scatter fused into both BN-backward passes (pool.hip
+    pool_bn_bwd_kernel) vs the unfused chain maxpool_nhwc_bwd -> bn_act_bwd (relu mask from z):
+    the same pool gradient (rounded to bf16 where the unfused path stores it), the same per-channel
+    sums up to fp32 summation order -> dz within one bf16 ulp, dgamma / dbeta to 1e-4."""
+    from ps_amd.ops import native
+
+    torch.manual_seed(2)
+    z = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    sc = torch.rand(C, device="cuda") + 0.5
+    sh = torch.randn(C, device="cuda") * 0.3
+    coef = torch.cat([sc, sh]).float().contiguous()
+    zf = z.float()
+    mean = zf.mean(dim=(0, 1, 2))
+    invstd = 1.0 / (zf.var(dim=(0, 1, 2), unbiased=False) + 1e-5).sqrt()
+    gamma = torch.rand(C, device="cuda") + 0.5
+    y, idx = native().maxpool_nhwc_fwd(z, coef, 3, 2, 1)
+    dy = torch.randn_like(y.float()).bfloat16()
+    dz, dg, db = native().pool_bn_bwd(dy, idx, z, coef, gamma, mean, invstd)
+    dpool = native().maxpool_nhwc_bwd(dy, idx, H, H, 3, 2, 1)
+    dz_ref, _, dg_ref, db_ref = native().bn_act_bwd(dpool.view(-1, C), None, z.view(-1, C), gamma, mean, invstd, 1,
+                                                    False, True, coef)
+    torch.testing.assert_close(dg, dg_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, db_ref, rtol=1e-4, atol=1e-4)
+    d = (dz.float() - dz_ref.view_as(dz).float()).abs()
+    ulp = dz_ref.view_as(dz).float().abs() * 2.0 ** -7 + 1e-6
+    assert bool((d <= ulp).all()), d.max().item()
