@@ -1001,6 +1001,77 @@ Tensor maxpool_nhwc_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, 
   return dx;
 }
 
+// ------------------------------------------------------------------ one-node row exchange
+static psamd::RowPeers row_peers(const std::vector<int64_t>& skeys, const std::vector<int64_t>& meta,
+                                 const std::vector<int64_t>& rows, const std::vector<int64_t>& grads) {
+  psamd::RowPeers P{};
+  const size_t W = std::max({skeys.size(), meta.size(), rows.size(), grads.size()});
+  TORCH_CHECK(W >= 1 && W <= static_cast<size_t>(psamd::kPlaneMaxSrc), "row plane: 1..", psamd::kPlaneMaxSrc, " ranks");
+  for (size_t w = 0; w < W; ++w) {
+    if (w < skeys.size()) P.skeys[w] = reinterpret_cast<const int64_t*>(skeys[w]);
+    if (w < meta.size()) P.meta[w] = reinterpret_cast<const int64_t*>(meta[w]);
+    if (w < rows.size()) P.rows[w] = reinterpret_cast<float*>(rows[w]);
+    if (w < grads.size()) P.grads[w] = reinterpret_cast<const float*>(grads[w]);
+  }
+  P.W = static_cast<int>(W);
+  return P;
+}
+
+static void check_i64_gpu(const Tensor& t, int64_t n, const char* what) {
+  check_gpu(t, what);
+  TORCH_CHECK(t.scalar_type() == torch::kInt64 && t.is_contiguous() && t.numel() == n, what, ": int64 [", n, "]");
+}
+
+// owner: rkeys[w * cap + j] = worker w's j-th key for this owner (-1 past its count); pmeta = the
+// W (offset, count) pairs
+void row_plane_recv(std::vector<int64_t> skeys, std::vector<int64_t> meta, int64_t me, int64_t cap, Tensor rkeys,
+                    Tensor pmeta) {
+  const auto P = row_peers(skeys, meta, {}, {});
+  TORCH_CHECK(skeys.size() == meta.size() && me >= 0 && me < P.W && cap > 0, "row plane recv args");
+  check_i64_gpu(rkeys, P.W * cap, "rkeys");
+  check_i64_gpu(pmeta, 2 * P.W, "pmeta");
+  const c10::DeviceGuard guard(rkeys.device());
+  psamd::launch_row_plane_recv(P, static_cast<int>(me), cap, rkeys.data_ptr<int64_t>(), pmeta.data_ptr<int64_t>(),
+                               cur_stream(rkeys));
+}
+
+// owner: rows of rslots -> every worker's arena rows at its offsets
+void row_plane_send(Tensor table, Tensor rslots, Tensor pmeta, std::vector<int64_t> rows, int64_t cap) {
+  const auto P = row_peers({}, {}, rows, {});
+  check_f32(table, "table");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous(), "table [rows, dim]");
+  check_i64_gpu(rslots, P.W * cap, "rslots");
+  check_i64_gpu(pmeta, 2 * P.W, "pmeta");
+  const int dim = static_cast<int>(table.size(1));
+  const int lpe = dim % 4 == 0 ? dim / 4 : dim;
+  TORCH_CHECK(cap % 256 == 0, "row plane capacity must be a multiple of 256");
+  TORCH_CHECK(dim % 4 != 0 || (reinterpret_cast<uintptr_t>(table.data_ptr()) & 15) == 0, "table 16-B aligned");
+  (void)lpe;
+  const c10::DeviceGuard guard(table.device());
+  psamd::launch_row_plane_send(table.data_ptr<float>(), rslots.data_ptr<int64_t>(), pmeta.data_ptr<int64_t>(), P, cap,
+                               dim, cur_stream(table));
+}
+
+// owner: the W workers' pushed rows -> acc, in rank order (tflag / tag / touched / tcount: the
+// round's touched-slot list)
+void row_plane_accum(std::vector<int64_t> grads, Tensor rslots, Tensor pmeta, Tensor acc, Tensor tflag, int64_t tag,
+                     Tensor touched, Tensor tcount, int64_t cap) {
+  const auto P = row_peers({}, {}, {}, grads);
+  check_f32(acc, "acc");
+  TORCH_CHECK(acc.dim() == 2 && acc.is_contiguous(), "acc [rows, dim]");
+  check_i64_gpu(rslots, P.W * cap, "rslots");
+  check_i64_gpu(pmeta, 2 * P.W, "pmeta");
+  check_i64_gpu(touched, P.W * cap, "touched");
+  check_gpu(tflag, "tflag");
+  check_gpu(tcount, "tcount");
+  TORCH_CHECK(tflag.scalar_type() == torch::kInt32 && tflag.numel() == acc.size(0), "tflag: int32 [rows]");
+  TORCH_CHECK(tcount.scalar_type() == torch::kInt32 && tcount.numel() == 1, "tcount: int32 [1]");
+  const c10::DeviceGuard guard(acc.device());
+  psamd::launch_row_plane_accum(P, rslots.data_ptr<int64_t>(), pmeta.data_ptr<int64_t>(), acc.data_ptr<float>(),
+                                tflag.data_ptr<int32_t>(), static_cast<int32_t>(tag), touched.data_ptr<int64_t>(),
+                                tcount.data_ptr<int32_t>(), cap, static_cast<int>(acc.size(1)), cur_stream(acc));
+}
+
 // stem: dz, dgamma, dbeta of z -> BN -> ReLU -> maxpool 3x3/2/1 from the pooled gradient (pool.hip)
 std::vector<Tensor> pool_bn_bwd(Tensor dy, Tensor idx, Tensor z, Tensor mask_coef, Tensor gamma, Tensor mean,
                                 Tensor invstd) {
@@ -1550,6 +1621,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dlrm_interact_bwd", &dlrm_interact_bwd);
   m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd);
   m.def("pool_bn_bwd", &pool_bn_bwd);
+  m.def("row_plane_recv", &row_plane_recv);
+  m.def("row_plane_send", &row_plane_send);
+  m.def("row_plane_accum", &row_plane_accum);
   m.def("bn_act_bwd", &bn_act_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("mean"),
         py::arg("invstd"), py::arg("act"), py::arg("want_dres"), py::arg("affine"),
         py::arg("mask_coef") = py::none(), py::arg("mbits") = py::none());

@@ -58,6 +58,19 @@ struct PlaneCopies {
 };
 // every segment ``nbytes`` long
 void launch_plane_gather(const PlaneCopies& c, int64_t nbytes, hipStream_t s);
+// one-node row exchange (sparse.hip, parallel/row_plane.py): every rank's arena pointers
+struct RowPeers {
+  const int64_t* skeys[kPlaneMaxSrc];  // unique keys sorted by owner
+  const int64_t* meta[kPlaneMaxSrc];   // [2W]: offset of owner o's segment, then its count
+  float* rows[kPlaneMaxSrc];           // [cap, dim] rows for skeys (written by the owners)
+  const float* grads[kPlaneMaxSrc];    // [cap, dim] pushed gradient rows for skeys
+  int W;
+};
+void launch_row_plane_recv(const RowPeers& P, int me, int64_t cap, int64_t* rkeys, int64_t* pmeta, hipStream_t s);
+void launch_row_plane_send(const float* table, const int64_t* rslots, const int64_t* pmeta, const RowPeers& P,
+                           int64_t cap, int dim, hipStream_t s);
+void launch_row_plane_accum(const RowPeers& P, const int64_t* rslots, const int64_t* pmeta, float* acc, int32_t* tflag,
+                            int32_t tag, int64_t* touched, int32_t* tcount, int64_t cap, int dim, hipStream_t s);
 // segment sizes from c.nbytes
 void launch_plane_copy(const PlaneCopies& c, hipStream_t s);
 // total = sum_r *(float*)c.src[r] (rank order); factor = min(1, max_norm / (sqrt(total) + 1e-6))

@@ -21,6 +21,8 @@
 //                       (store/KVStore.java:86-107, net/PServer.java:143-162)
 //  hash_slots           device-resident id -> slot map (open addressing, CAS insert) for
 //                       tables keyed by unbounded ids; no host round trip per lookup
+#include <algorithm>
+
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
@@ -461,6 +463,137 @@ void launch_unique_runs(const int64_t* srt, const int64_t* uidx, int64_t n, int6
                         int64_t* seg, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(unique_runs_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, s, srt, uidx, n, mask, ukeys, seg);
+}
+
+// ---------------------------------------------------------------------------------------
+// One-node row exchange over IPC-mapped arenas (parallel/row_plane.py): every rank publishes its
+// unique keys sorted by owner, with [offset | count] per owner, in its own arena; owners read
+// their segments straight from the peers' arenas and write the rows straight back; pushes are
+// read the same way.  Counts stay in device memory -- no split sizes on the host.  Entry e of
+// the owner's [W][cap] view is worker e / cap's key e % cap (pads: key -1 / slot -1).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void row_plane_recv_kernel(const RowPeers P, int me, int64_t cap,
+                                                             int64_t* __restrict__ rkeys, int64_t* __restrict__ pmeta) {
+  const int64_t total = static_cast<int64_t>(P.W) * cap;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int w = static_cast<int>(e / cap);
+    const int64_t j = e - w * cap;
+    const int64_t off = P.meta[w][me], cnt = P.meta[w][P.W + me];
+    rkeys[e] = j < cnt ? P.skeys[w][off + j] : -1;
+    if (j == 0) {
+      pmeta[2 * w] = off;
+      pmeta[2 * w + 1] = cnt;
+    }
+  }
+}
+
+// rows of the owner's slots -> worker w's arena rows at its offset (slot < 0: zero row).
+// Blocks never straddle two workers (cap % (entries per block) == 0) and skip pad blocks whole.
+template <int V>
+__global__ __launch_bounds__(256) void row_plane_send_kernel(const float* __restrict__ table,
+                                                             const int64_t* __restrict__ rslots,
+                                                             const int64_t* __restrict__ pmeta, const RowPeers P,
+                                                             int64_t cap, int dim, int lpe) {
+  // lpe lanes per entry (each V floats per step), 256 / lpe entries per block-step
+  const int epb = 256 / lpe;
+  const int64_t nblocks = static_cast<int64_t>(P.W) * cap / epb;
+  const int sub = threadIdx.x / lpe, ql = threadIdx.x % lpe;
+  for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const int64_t e0 = b * epb;
+    const int w = static_cast<int>(e0 / cap);
+    const int64_t j0 = e0 - w * cap;
+    const int64_t cnt = pmeta[2 * w + 1];
+    if (j0 >= cnt) continue;  // block-uniform: a block of pads
+    const int64_t j = j0 + sub;
+    if (j >= cnt) continue;
+    const int64_t slot = rslots[e0 + sub];
+    float* dst = P.rows[w] + (pmeta[2 * w] + j) * dim;
+    for (int c = ql * V; c < dim; c += lpe * V) {
+      if constexpr (V == 4) {
+        const f32x4 v = slot >= 0 ? load4(table, slot * dim + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        store4(dst, c, v);
+      } else {
+        dst[c] = slot >= 0 ? table[slot * dim + c] : 0.f;
+      }
+    }
+  }
+}
+
+// one worker's pushed rows into the owner's fp32 accumulator (pass w of W, launched in rank
+// order: deterministic sums, no atomics on the data).  A slot first seen this round (tflag !=
+// tag) is appended to the touched list and its accumulator row overwritten instead of added to.
+template <int V>
+__global__ __launch_bounds__(256) void row_plane_accum_kernel(const RowPeers P, int w, const int64_t* __restrict__ rslots,
+                                                              const int64_t* __restrict__ pmeta, float* __restrict__ acc,
+                                                              int32_t* __restrict__ tflag, int32_t tag,
+                                                              int64_t* __restrict__ touched, int32_t* __restrict__ tcount,
+                                                              int64_t cap, int dim, int lpe) {
+  const int epb = 256 / lpe;
+  const int64_t cnt = pmeta[2 * w + 1], off = pmeta[2 * w];
+  const int64_t nb = (cnt + epb - 1) / epb;
+  const int sub = threadIdx.x / lpe, ql = threadIdx.x % lpe;
+  const float* src = P.grads[w];
+  for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const int64_t j = b * epb + sub;
+    const int64_t slot = j < cnt ? rslots[static_cast<int64_t>(w) * cap + j] : -1;
+    // every lane of the entry reads the flag before its first lane writes it (one wave, in order)
+    const bool first = slot >= 0 && tflag[slot] != tag;
+    if (slot >= 0 && ql == 0 && first) {
+      tflag[slot] = tag;
+      touched[atomicAdd(tcount, 1)] = slot;
+    }
+    if (slot < 0) continue;
+    const float* g = src + (off + j) * dim;
+    float* a = acc + slot * dim;
+    for (int c = ql * V; c < dim; c += lpe * V) {
+      if constexpr (V == 4) {
+        f32x4 v = load4(g, c);
+        if (!first) v += load4(a, c);
+        store4(a, c, v);
+      } else {
+        a[c] = first ? g[c] : a[c] + g[c];
+      }
+    }
+  }
+}
+
+static int row_lanes(int dim, int V) {  // lanes per entry: a power of two <= 64 covering dim / V
+  int need = (dim + V - 1) / V, l = 1;
+  while (l < need && l < 64) l <<= 1;
+  return l;
+}
+
+void launch_row_plane_recv(const RowPeers& P, int me, int64_t cap, int64_t* rkeys, int64_t* pmeta, hipStream_t s) {
+  const int64_t total = static_cast<int64_t>(P.W) * cap;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(row_plane_recv_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, P, me, cap, rkeys, pmeta);
+}
+
+void launch_row_plane_send(const float* table, const int64_t* rslots, const int64_t* pmeta, const RowPeers& P,
+                           int64_t cap, int dim, hipStream_t s) {
+  const bool v4 = dim % 4 == 0;
+  const int lpe = row_lanes(dim, v4 ? 4 : 1);
+  const int64_t nblocks = static_cast<int64_t>(P.W) * cap / (256 / lpe);
+  if (nblocks <= 0) return;
+  const int grid = static_cast<int>(std::min<int64_t>(nblocks, 65536));
+  if (v4) hipLaunchKernelGGL(row_plane_send_kernel<4>, dim3(grid), dim3(256), 0, s, table, rslots, pmeta, P, cap, dim, lpe);
+  else hipLaunchKernelGGL(row_plane_send_kernel<1>, dim3(grid), dim3(256), 0, s, table, rslots, pmeta, P, cap, dim, lpe);
+}
+
+void launch_row_plane_accum(const RowPeers& P, const int64_t* rslots, const int64_t* pmeta, float* acc, int32_t* tflag,
+                            int32_t tag, int64_t* touched, int32_t* tcount, int64_t cap, int dim, hipStream_t s) {
+  const bool v4 = dim % 4 == 0;
+  const int lpe = row_lanes(dim, v4 ? 4 : 1);
+  const int grid = static_cast<int>(std::min<int64_t>(std::max<int64_t>(1, cap / (256 / lpe)), 16384));
+  for (int w = 0; w < P.W; ++w) {  // rank order
+    if (v4)
+      hipLaunchKernelGGL(row_plane_accum_kernel<4>, dim3(grid), dim3(256), 0, s, P, w, rslots, pmeta, acc, tflag, tag,
+                         touched, tcount, cap, dim, lpe);
+    else
+      hipLaunchKernelGGL(row_plane_accum_kernel<1>, dim3(grid), dim3(256), 0, s, P, w, rslots, pmeta, acc, tflag, tag,
+                         touched, tcount, cap, dim, lpe);
+  }
 }
 
 }  // namespace psamd

@@ -39,6 +39,7 @@ dedicated-server topology is ``TcpSparseTable`` (rows live in the native server'
 """
 from __future__ import annotations
 
+import os
 import zlib
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence, Tuple, Union
@@ -259,7 +260,7 @@ class ShardedSparseTable:
     def __init__(self, name: str, dim: int, rows: Union[int, Sequence[int]], transport: Optional[Transport] = None,
                  updater: Optional[Updater] = None, *, init: Tuple[float, float] = (0.0, 0.0),
                  id_mode: str = "direct", seed: int = 0, device=None, fields: int = 1, overlap: bool = False,
-                 average: bool = True):
+                 average: bool = True, exchange: Optional[str] = None):
         if id_mode not in ("direct", "hash", "map"):
             raise ValueError(id_mode)
         self.t = transport or Transport()
@@ -299,6 +300,22 @@ class ShardedSparseTable:
         self._pf: dict = {}  # ids signature -> (keys, route) of prefetched lookups
         self._nbad: Optional[torch.Tensor] = None  # deferred out-of-range id count (sync-free path)
         self._rows_dev = torch.zeros((), dtype=torch.int64, device=self.device)  # sync-free rows pulled
+        # W > 1 on one node: the IPC / shared-memory row plane (row_plane.py) instead of all-to-alls
+        # (``exchange`` "plane" | "collective"; default: PS_AMD_ROW_EXCHANGE, else auto)
+        self.plane = None
+        self._rowacc = None
+        if self.world > 1:
+            from . import row_plane as _rp
+
+            if exchange is not None:
+                os.environ.setdefault("PS_AMD_ROW_EXCHANGE", exchange)
+            want = (exchange == "plane") if exchange is not None else _rp.plane_rows_wanted(self.t, self.device)
+            if exchange == "plane":
+                _rp.plane_rows_wanted(self.t, self.device)  # same-host check
+            if want:
+                self.plane = _rp.RowPlane(self.t, self.dim, self.device)
+                self._rowacc = _rp.RowAccumulator(self.shard)
+        self.exchange = "plane" if self.plane is not None else ("collective" if self.world > 1 else "local")
 
     # ------------------------------------------------------------------ compat accessors
     @property
@@ -395,7 +412,7 @@ class ShardedSparseTable:
         meta = torch.empty(W + 1, dtype=torch.int64, device=self.device)
         meta[:W] = cum0[bounds[1:]] - cum0[bounds[:-1]]
         meta[W] = nbad
-        if W > 1:
+        if W > 1 and self.plane is None:
             recv = torch.empty(W, dtype=torch.int64, device=self.device)
             self.t.all_to_all(recv, meta[:W].contiguous())
             counts = torch.cat([meta, recv])
@@ -404,7 +421,7 @@ class ShardedSparseTable:
         inv = torch.empty(n, dtype=torch.int64, device=self.device)
         inv[perm] = uidx
         r = _Route(n, inv, perm, seg_full, ubuf, counts, nbad)
-        if self.gpu:
+        if self.gpu and self.plane is None:
             r.host = torch.empty(counts.numel(), dtype=torch.int64, pin_memory=True)
             r.host.copy_(counts, non_blocking=True)
             r.event = torch.cuda.Event()
@@ -425,8 +442,8 @@ class ShardedSparseTable:
         """Route the NEXT batch's ids now (its device work and count exchange run ahead of this
         step's compute), so the lookup of ``ids`` finds its split sizes already on the host.
         Only useful at W > 1: at W = 1 the GPU lookup needs no counts at all."""
-        if self.world == 1 and self.gpu:
-            return
+        if (self.world == 1 and self.gpu) or self.plane is not None:
+            return  # no host-side sizes to wait for
         keys, nbad = self.keys_of(ids)
         if len(self._pf) >= 4:  # stale prefetches (ids never looked up): drop the oldest
             self._pf.pop(next(iter(self._pf)))
@@ -468,6 +485,15 @@ class ShardedSparseTable:
         self._wait_push()
         r = route if route is not None else self._route(keys, nbad)
         n = r.n
+        if self.plane is not None:
+            # one-node IPC plane: counts stay on the device, the id check is deferred like W = 1
+            self._nbad = r.nbad.clone() if self._nbad is None else self._nbad + r.nbad
+            rows, st = self.plane.pull(r.ubuf, r.counts, n, self.shard, fetch)
+            plan = _Plan(n, n, r.inv, r.perm, r.seg_full, [n], [n], None)
+            plan.extra["plane"] = st
+            if fetch:
+                self.stats["pulls"] += 1
+            return plan, (rows if fetch else None)
         if self.world == 1 and self.gpu:
             # sync-free: every buffer sized n (pad keys -1 -> slot -1 -> zero row, skipped by
             # the optimizer), the id check deferred to check_ids / synchronize
@@ -544,6 +570,11 @@ class ShardedSparseTable:
 
     def _exchange_grads(self, plan: _Plan, g: torch.Tensor) -> None:
         _trace.mark(f"sparse.push.{self.name}")
+        if "plane" in plan.extra:
+            self.plane.push(g, plan.nu, plan.extra.pop("plane"), self.shard, self._rowacc)
+            plan.pushed = True
+            self.stats["pushes"] += 1
+            return
         if self.world > 1:
             rg = torch.empty(sum(plan.recv), self.dim, dtype=torch.float32, device=self.device)
             self.t.all_to_all(rg, g.contiguous(), plan.recv, plan.send)
@@ -556,10 +587,14 @@ class ShardedSparseTable:
             self.stats["rows_pushed"] += plan.nu
 
     def _apply_acc(self, gscale: Optional[float] = None, average: Optional[bool] = None) -> None:
-        if not self._acc:
-            return
         avg = self.average if average is None else average
         gs = gscale if gscale is not None else (1.0 / self.world if avg else 1.0)
+        if self._rowacc is not None and self._rowacc.open:
+            self._rowacc.apply(gs, self.round + 1)
+            self.round += 1
+            return
+        if not self._acc:
+            return
         if len(self._acc) == 1 and self.world == 1:
             slots, g = self._acc[0]  # unique slots already
             self.shard.apply(slots, g, gs, self.round + 1, sorted_runs=False)
@@ -616,7 +651,7 @@ class ShardedSparseTable:
                 n += plan.nu
         self._pending = []
         if not self.accumulating:
-            if self.overlap and self._acc:
+            if self.overlap and (self._acc or (self._rowacc is not None and self._rowacc.open)):
                 comm = side_stream(self.device)
                 comm.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(comm):
@@ -635,6 +670,12 @@ class ShardedSparseTable:
         self._wait_push()
         self.shard.check()
         self.check_ids()
+
+    def close(self) -> None:
+        """Release the row plane's shared memory (collective)."""
+        if self.plane is not None:
+            self.plane.close()
+            self.plane = None
 
     def row_stats(self) -> dict:
         """``stats`` with the sync-free path's device-side unique-row count read back (a sync)."""
