@@ -36,7 +36,7 @@ import torch
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default=os.environ.get("PS_AMD_BENCH_CONFIG", "resnet50"),
-                    choices=["resnet50", "bert-ssp", "dlrm", "llama-onebit", "mlp-tcp"])
+                    choices=["resnet50", "bert-ssp", "dlrm", "llama-onebit", "mlp-tcp", "ctr-async"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: contract dry run of the same code path on CPU tensors over gloo (tests only; "
@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--checkpoint-dir", type=str, default=os.environ.get("PS_AMD_CHECKPOINT_DIR", ""),
                     help="after the timed region: one sharded checkpoint of every rank's server shard (timed, "
                          "reported on stderr) -- utils/checkpoint.py")
+    ap.add_argument("--sync-audit", type=int, default=-1,
+                    help="after the timed region: N steps under torch.cuda.set_sync_debug_mode('warn'), "
+                         "reporting the host-synchronising torch ops per step (default 2 for the sparse "
+                         "configs, 0 otherwise)")
     ap.add_argument("--timing", type=int, default=0,
                     help="after the timed region: N more steps with per-phase device timing "
                          "(fwd+bwd / push / serve / pull / exposed comm) printed to stderr")
@@ -214,6 +218,24 @@ def main():
         eng.timing = False
         if rank == 0 and tsum:
             print("[bench-timing] " + json.dumps(tsum), file=sys.stderr, flush=True)
+    audit = None
+    n_audit = args.sync_audit if args.sync_audit >= 0 else (2 if args.config in ("dlrm", "ctr-async") else 0)
+    if n_audit and not cpu and not use_graph:
+        import warnings
+
+        try:
+            with warnings.catch_warnings(record=True) as ws:
+                warnings.simplefilter("always")
+                torch.cuda.set_sync_debug_mode("warn")
+                for _ in range(n_audit):
+                    step()
+                torch.cuda.set_sync_debug_mode(0)
+            sync()
+            hits = [str(w.message).split("\n")[0][:80] for w in ws if "synchroniz" in str(w.message)]
+            audit = {"host_syncs_per_step": round(len(hits) / n_audit, 2), "sync_ops": sorted(set(hits))[:4]}
+        except Exception as e:  # diagnostics only
+            torch.cuda.set_sync_debug_mode(0)
+            print(f"[bench-sync-audit] failed: {e!r}", file=sys.stderr, flush=True)
     if world > 1 and args.comm_probe:
         from ps_amd.parallel.comm_probe import probe
 
@@ -250,6 +272,8 @@ def main():
         cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         if timed_stats:
             cfg.update(timed_stats)
+        if audit is not None:
+            cfg["sync_audit"] = audit  # torch ops that synchronised the host, after the timed region
         if tsum:
             cfg["ps_phase_ms_per_step"] = tsum  # measured after the timed region
         if comm:
@@ -265,7 +289,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,  # the reference publishes no throughput number
-            "dtype": "bf16",
+            "dtype": bench.dtype,
             "data": f"synthetic: a pool of {BC.POOL if args.config != 'dlrm' else 4 * BC.POOL} distinct "
                     f"GPU-resident batches of the named shape, cycled; random-init weights",
             "config": cfg,

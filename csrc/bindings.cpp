@@ -1536,11 +1536,13 @@ std::vector<Tensor> bn_bwd_partials(Tensor g, Tensor x, Tensor part, c10::option
 
 void register_async_ps(pybind11::module& m);  // csrc/async_ps_gpu.cpp
 void register_plane(pybind11::module& m);      // csrc/plane.cpp
+void register_async_rows(pybind11::module& m); // csrc/async_rows_gpu.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "ps_amd HIP kernels for MI355X (gfx950)";
   register_async_ps(m);
   register_plane(m);
+  register_async_rows(m);
   m.def("conv_gemm", &conv_gemm, py::arg("a"), py::arg("b"), py::arg("geo"), py::arg("pro") = py::none(),
         py::arg("epi") = 0, py::arg("aux") = py::none(), py::arg("kshift") = py::none(), py::arg("mc") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),

@@ -66,6 +66,17 @@ struct RowPeers {
   const float* grads[kPlaneMaxSrc];    // [cap, dim] pushed gradient rows for skeys
   int W;
 };
+// worker <-> owner mailboxes of the asynchronous row tables: owner o's piece of a worker's
+// owner-sorted buffer is [meta[o], meta[o] + meta[W + o]); cnt[o] (nullable) receives the count
+struct PeerSegs {
+  void* ptr[kPlaneMaxSrc];
+  int64_t* cnt[kPlaneMaxSrc];
+  int W;
+};
+void launch_segs_peers(bool to_peers, const void* local, int esize, const int64_t* meta, const PeerSegs& P,
+                       int64_t width, int64_t cap, hipStream_t s);
+void launch_keys_to_rows(const int64_t* keys, int64_t n, int64_t base, int64_t* rows, hipStream_t s);
+void launch_system_acquire(hipStream_t s);
 void launch_row_plane_recv(const RowPeers& P, int me, int64_t cap, int64_t* rkeys, int64_t* pmeta, hipStream_t s);
 void launch_row_plane_send(const float* table, const int64_t* rslots, const int64_t* pmeta, const RowPeers& P,
                            int64_t cap, int dim, hipStream_t s);

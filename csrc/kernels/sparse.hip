@@ -474,6 +474,7 @@ void launch_unique_runs(const int64_t* srt, const int64_t* uidx, int64_t n, int6
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void row_plane_recv_kernel(const RowPeers P, int me, int64_t cap,
                                                              int64_t* __restrict__ rkeys, int64_t* __restrict__ pmeta) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' keys / counts: no stale lines (system scope)
   const int64_t total = static_cast<int64_t>(P.W) * cap;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < total; e += stride) {
@@ -529,6 +530,7 @@ __global__ __launch_bounds__(256) void row_plane_accum_kernel(const RowPeers P, 
                                                               int32_t* __restrict__ tflag, int32_t tag,
                                                               int64_t* __restrict__ touched, int32_t* __restrict__ tcount,
                                                               int64_t cap, int dim, int lpe) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // worker w's pushed rows (system scope)
   const int epb = 256 / lpe;
   const int64_t cnt = pmeta[2 * w + 1], off = pmeta[2 * w];
   const int64_t nb = (cnt + epb - 1) / epb;
@@ -594,6 +596,79 @@ void launch_row_plane_accum(const RowPeers& P, const int64_t* rslots, const int6
       hipLaunchKernelGGL(row_plane_accum_kernel<1>, dim3(grid), dim3(256), 0, s, P, w, rslots, pmeta, acc, tflag, tag,
                          touched, tcount, cap, dim, lpe);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Device-side segment moves between a worker and its owners' mailboxes (async rows,
+// parallel/async_rows.py): owner o's piece is [meta[o], meta[o] + meta[W + o]) of the worker's
+// owner-sorted buffer; counts stay in device memory (each mailbox carries its count in the word
+// after its cap entries).  blockIdx.y = owner; a block stride loop over that owner's piece only.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void segs_to_peers_kernel(const T* __restrict__ src, const int64_t* __restrict__ meta,
+                                                            const PeerSegs P, int64_t width) {
+  const int o = blockIdx.y;
+  const int64_t off = meta[o], cnt = meta[P.W + o];
+  T* dst = static_cast<T*>(P.ptr[o]);
+  const int64_t total = cnt * width;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    dst[i] = src[off * width + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && P.cnt[o] != nullptr) *P.cnt[o] = cnt;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void segs_from_peers_kernel(T* __restrict__ dst, const int64_t* __restrict__ meta,
+                                                              const PeerSegs P, int64_t width) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the owners' response rows (system scope)
+  const int o = blockIdx.y;
+  const int64_t off = meta[o], cnt = meta[P.W + o];
+  const T* src = static_cast<const T*>(P.ptr[o]);
+  const int64_t total = cnt * width;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    dst[off * width + i] = src[i];
+}
+
+void launch_segs_peers(bool to_peers, const void* local, int esize, const int64_t* meta, const PeerSegs& P,
+                       int64_t width, int64_t cap, hipStream_t s) {
+  if (P.W <= 0 || cap <= 0) return;
+  const int gx = static_cast<int>(std::min<int64_t>(std::max<int64_t>(1, (cap * width + 255) / 256), 1024));
+  const dim3 grid(gx, P.W);
+  if (esize == 8) {
+    if (to_peers)
+      hipLaunchKernelGGL(segs_to_peers_kernel<int64_t>, grid, dim3(256), 0, s, static_cast<const int64_t*>(local), meta, P,
+                         width);
+    else
+      hipLaunchKernelGGL(segs_from_peers_kernel<int64_t>, grid, dim3(256), 0, s,
+                         static_cast<int64_t*>(const_cast<void*>(local)), meta, P, width);
+  } else {
+    if (to_peers)
+      hipLaunchKernelGGL(segs_to_peers_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(local), meta, P,
+                         width);
+    else
+      hipLaunchKernelGGL(segs_from_peers_kernel<float>, grid, dim3(256), 0, s,
+                         static_cast<float*>(const_cast<void*>(local)), meta, P, width);
+  }
+}
+
+// owner-local rows of range-partitioned keys: rows[i] = keys[i] - base (negative keys stay negative)
+__global__ __launch_bounds__(256) void keys_to_rows_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t base,
+                                                           int64_t* __restrict__ rows) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    rows[i] = keys[i] < 0 ? -1 : keys[i] - base;
+}
+
+// a system-scope acquire on every CU (one block each): later kernels of the stream read memory
+// peers wrote (over xGMI, after the host saw their completion) without stale cached lines
+__global__ __launch_bounds__(64) void system_acquire_kernel() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
+void launch_system_acquire(hipStream_t s) { hipLaunchKernelGGL(system_acquire_kernel, dim3(256), dim3(64), 0, s); }
+
+void launch_keys_to_rows(const int64_t* keys, int64_t n, int64_t base, int64_t* rows, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(keys_to_rows_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, s, keys, n, base, rows);
 }
 
 }  // namespace psamd

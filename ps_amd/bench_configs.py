@@ -5,6 +5,9 @@
   dlrm          DLRM-style: 26 sharded embedding tables, sparse push/pull, row-wise
                 Adagrad on the owning server (HIP), dense MLPs on the co-located PS
   llama-onebit  Llama-3-8B bf16, 1-bit compressed gradient push with error feedback
+  ctr-async     the reference CTR Wide&Deep (23 fields x 10, 45 numeric, FC 150-10-1, wide hash
+                100000) on the asynchronous PS: dense keys through AsyncPS SSP(1), embedding and
+                wide rows through the device-resident asynchronous row tables
   mlp-tcp       2-layer MLP, 1 dedicated server + 2 workers on CPU/TCP loopback (plumbing)
 
 Each ``setup_*`` returns a Bench with ``step()`` (one full PS round: forward, backward,
@@ -38,6 +41,7 @@ class Bench:
     config: Dict = field(default_factory=dict)
     engine: object = None
     stats: Optional[Callable[[], Dict]] = None  # extra counters for the JSON line (read after timing)
+    dtype: str = "bf16"  # compute dtype reported in the JSON line
 
 
 def setup_resnet50(args, tp, dev) -> Bench:
@@ -148,7 +152,10 @@ def setup_dlrm(args, tp, dev) -> Bench:
     return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",
                  {"model": "DLRM-26x128", "global_batch": B * tp.world, "seq_len": None,
                   "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}",
-                  "sparse_push_overlap": overlap}, ps, stats)
+                  "sparse_push_overlap": overlap,
+                  # row exchange path at W > 1: "plane" (IPC arenas, parallel/row_plane.py) or
+                  # "collective" (RCCL all-to-alls); "local" at W = 1
+                  "sparse_exchange": tbl.exchange}, ps, stats)
 
 
 def setup_llama_onebit(args, tp, dev) -> Bench:
@@ -189,8 +196,54 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
                  ps)
 
 
+def setup_ctr_async(args, tp, dev) -> Bench:
+    """CTR.java:91 / WideDeepNN.java:105-161 shapes on the asynchronous PS (SSP(1) unless
+    --staleness says otherwise; rows: parallel/async_rows.py, dense: parallel/async_ps.py)."""
+    from .context import ctx
+    from .data.dataset import synthetic_ctr
+    from .models.reference import WideDeepNN
+    from .parallel.async_ps import AsyncPS
+    from .parallel.async_rows import async_table_factory
+
+    ctx.init()
+    stale = args.staleness if args.staleness else 1
+    tf = async_table_factory(tp, dev, seed=7, staleness=stale, capacity=max(1 << 15, args.batch_per_gpu * 24))
+    gen = torch.Generator().manual_seed(0)
+    model = WideDeepNN.build_model(23, 10, 45, [150, 10, 1], 100000, gen=gen, emb_rows=100000, table_factory=tf,
+                                   init_scale=0.2).to(dev)
+    ps = AsyncPS(model, model.get_updater(), tp, staleness=stale)
+    B = args.batch_per_gpu
+    pool = []
+    for i in range(POOL):
+        b = synthetic_ctr(B, fields=23, numeric=45, ids_per_field=100000, wide_k=23, wide_size=100000,
+                          seed=tp.rank * 1000 + i)
+        pool.append({k: v.to(dev) for k, v in b.items()})
+    it = _cycle(pool)
+
+    def step():
+        b = next(it)
+        loss = model.loss(model(b), b["Y"])
+        loss.backward()
+        model.push_sparse()
+        ps.finish_step()
+        model.pull_weights()
+        return loss
+
+    class _Engine:  # closes the row tables' services, then the dense async PS (collective)
+        def close(self):
+            for t in model.tables().values():
+                t.close()
+            ps.close()
+
+    return Bench(step, B, "samples/sec (whole node) CTR Wide&Deep on the asynchronous PS (SSP rows + dense)",
+                 "samples/s", {"model": "CTR-WideDeep-23x10", "global_batch": B * tp.world, "seq_len": None,
+                               "parallelism": f"ps-ssp{stale}-async-rows-dp{tp.world}",
+                               "row_tables": "device-resident (csrc/async_rows_gpu.cpp)" if dev.type == "cuda"
+                               else "host callbacks"}, _Engine(), dtype="fp32")
+
+
 SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_dlrm,
-          "llama-onebit": setup_llama_onebit}
+          "llama-onebit": setup_llama_onebit, "ctr-async": setup_ctr_async}
 
 DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not given
     "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "1024")), seq=0),
@@ -203,6 +256,7 @@ DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not giv
     # optimizer / PS cost amortises over 4x the tokens): 16.9K vs 15.7K (2 x 4096) and 14.0K tok/s
     # (1 x 4096), profiles/r2_llama_batch_sweep.txt
     "llama-onebit": dict(batch=4, seq=4096),
+    "ctr-async": dict(batch=1000, seq=0),  # CTR.java:83-87 training batch
 }
 
 

@@ -19,10 +19,16 @@ of ``AsyncPS``, no rank ever waits for another rank to reach a matching call:
 * SSP(s): before its pull at round c a worker waits until every owner applied every worker's
   first c - s row pushes (the dense gate of ``AsyncPS`` for the rows); ASP: no gate.
 
-The owner side is a native thread (csrc/runtime/bindings_native.cpp ``rows.Service``) polling
-the control words in POSIX shared memory and calling back into Python for the row work, which
-runs on the owner's own stream (HIP hash map / lazy init / gather / sparse optimizer on GPU,
-the same ops' torch oracles on CPU).
+GPU: device-resident end to end.  The worker dedupes and owner-sorts its keys on the device
+(counts never reach its host) and ONE segment kernel writes every owner's piece -- with its
+count -- into that owner's IPC-mapped mailbox; a completion thread bumps the request word once
+the copy landed (the training thread does not wait for it).  Each owner runs a NATIVE service
+thread (csrc/async_rows_gpu.cpp: no Python, no GIL) that reads the count on its own stream and
+launches the HIP hash lookup, lazy init, gather into its response mailbox, or the row optimizer
+for a push.  The worker copies its rows back out of the owners' response mailboxes with one
+kernel: keys, rows and gradients never pass through host memory.
+CPU: a native poller (csrc/runtime/bindings_native.cpp ``rows.Service``) calls back into Python
+for the row work (the same ops' torch oracles).
 """
 from __future__ import annotations
 
@@ -32,7 +38,8 @@ from typing import Optional, Sequence, Tuple, Union
 import torch
 
 from .async_ps import _addr, _native, _Shared, _ShmSeg
-from .sparse_table import RowShard, TcpSparseTable, _mix64
+from ..ops import sparse as _sp
+from .sparse_table import KEY_ID_BITS, KEY_MASK, OWNER_SHIFT, RowShard, TcpSparseTable, _mix64
 from .transport import Transport
 from .updaters import Updater
 
@@ -111,9 +118,10 @@ class AsyncRowTable(TcpSparseTable):
         # owner-side mailboxes (shared): request keys, response rows, push keys / gradients
         self.share = _Shared(transport, self.device)
         C, D = self.C, self.dim
-        self.rq = self.share.alloc((W, C), torch.int64)
+        # (GPU: the word after a mailbox's C keys carries the request's count, written on device)
+        self.rq = self.share.alloc((W, C + 1), torch.int64)
         self.rs = self.share.alloc((W, C, D), torch.float32)
-        self.pk = self.share.alloc((W, MB, C), torch.int64)
+        self.pk = self.share.alloc((W, MB, C + 1), torch.int64)
         self.pg = self.share.alloc((W, MB, C, D), torch.float32)
         self.peer_rq = self.share.exchange(self.rq)
         self.peer_rs = self.share.exchange(self.rs)
@@ -137,15 +145,46 @@ class AsyncRowTable(TcpSparseTable):
         # copy never waits behind the compute stream's queued kernels
         self._svc_stream = torch.cuda.Stream(device=self.device) if self.gpu else None
         self._io_stream = torch.cuda.Stream(device=self.device) if self.gpu else None
-        self.service = R.Service(self.ctl.base, self.me, self._serve)
+        if self.gpu:
+            from .. import _C  # type: ignore
+
+            self._R = _C.rows
+            self.service = self._R.Service(self.ctl.base, self.me, C, D)
+            self.service.set_mailboxes(self.rq, self.rs, self.pk, self.pg)
+            self._configure_native()
+            self._notify = self._R.Notifier()
+            self._nbad = None
+        else:
+            self.service = R.Service(self.ctl.base, self.me, self._serve)
         transport.barrier()
         self.service.start()
+
+    def _configure_native(self) -> None:
+        """Hand the shard (and the updater, once known) to the native GPU service."""
+        if not self.gpu or getattr(self, "service", None) is None:
+            return
+        sh = self.shard
+        st = list(sh.states) + [None] * (2 - len(sh.states))
+        lo, hi = sh.init
+        self.service.set_shard(sh.table, sh.flags, sh.hkeys, sh.row_base, sh.status, st[0], st[1], sh.seed,
+                               float(lo), float(hi))
+        u = self.updater
+        if u is not None:
+            from ..ops import optim as _o
+            from .async_ps import _BIAS_MODE, _HYPER
+            from .updaters import AdamUpdater
+
+            h = _o._hp(u.hyper(1))
+            bias = _BIAS_MODE[u.bias_correction] if isinstance(u, AdamUpdater) else 0
+            self.service.set_updater(u.kind, [float(h[k]) for k in _HYPER], bias, bool(getattr(u, "rowwise", False)),
+                                     getattr(u, "mode", "") == "reference", 1.0 / self.W)
 
     # ------------------------------------------------------------------ config
     def set_updater(self, u: Updater) -> None:
         self.updater = u
         self.shard.updater = u
         self.shard.alloc_states()
+        self._configure_native()
 
     @property
     def init(self):
@@ -156,6 +195,7 @@ class AsyncRowTable(TcpSparseTable):
         self._init = tuple(v)
         if getattr(self, "shard", None) is not None:
             self.shard.init = self._init
+            self._configure_native()
 
     # ------------------------------------------------------------------ worker side
     def _owner(self, keys: torch.Tensor) -> torch.Tensor:
@@ -230,11 +270,164 @@ class AsyncRowTable(TcpSparseTable):
     def push_pending(self) -> int:
         """Every round pushes (possibly nothing): the owners' applied counts are the clocks of
         the SSP gate."""
+        if self.gpu:
+            return self._push_pending_dev()
         n = super().push_pending()
         if n == 0 and not self.accumulating:
             self._push(torch.empty(0, dtype=torch.int64), torch.empty(0, self.dim))
             self.round += 1
         return n
+
+    # ------------------------------------------------------------------ worker side, GPU
+    # (device-resident: no key, row, gradient or count passes through host memory)
+    def _keys_dev(self, ids: torch.Tensor) -> torch.Tensor:
+        """Flat int64 keys on the device; out-of-range ids are clamped and counted for a deferred
+        check (synchronize), as the sync-free sharded table does."""
+        ids = ids.to(self.device).long()
+        if self.fields > 1:
+            if ids.shape[-1] != self.fields:
+                raise ValueError(f"{self.name}: ids last dim {ids.shape[-1]} != fields {self.fields}")
+            f = torch.arange(self.fields, device=self.device).expand_as(ids)
+        else:
+            f = torch.zeros_like(ids)
+        ids, f = ids.reshape(-1), f.reshape(-1)
+        if self.id_mode == "map":
+            bad = (ids < 0) | (ids >= (1 << KEY_ID_BITS))
+            keys = (f << KEY_ID_BITS) | ids.clamp(0, (1 << KEY_ID_BITS) - 1)
+        else:
+            rows_f = torch.tensor(self.field_rows, device=self.device)[f]
+            if self.id_mode == "hash":
+                ids = torch.remainder(ids, rows_f)
+            bad = (ids < 0) | (ids >= rows_f)
+            keys = torch.tensor(self.field_off, device=self.device)[f] + ids.clamp(min=0).minimum(rows_f - 1)
+        nb = bad.sum()
+        self._nbad = nb if self._nbad is None else self._nbad + nb
+        return keys
+
+    def _route_dev(self, keys: torch.Tensor) -> dict:
+        """Dedupe + owner-major sort on the device.  Negative keys (pads of a merged push) go to a
+        virtual owner W: they sort last and are in no owner's count, so they are never sent."""
+        from ..ops._ext import native
+
+        W, n = self.W, keys.numel()
+        own = torch.remainder(_mix64(keys), W) if W > 1 else torch.zeros_like(keys)
+        own = torch.where(keys < 0, torch.full_like(own, W), own)
+        srt, perm = torch.sort((own << OWNER_SHIFT) | (keys & KEY_MASK))
+        head = torch.ones(n, dtype=torch.bool, device=self.device)
+        if n > 1:
+            head[1:] = srt[1:] != srt[:-1]
+        cum = torch.cumsum(head.long(), 0)
+        uidx = cum - 1
+        ubuf = torch.full((n,), -1, dtype=torch.int64, device=self.device)
+        seg = torch.full((n + 1,), n, dtype=torch.int64, device=self.device)
+        if n:
+            native().unique_runs(srt, uidx, KEY_MASK, ubuf, seg)
+        bounds = torch.searchsorted(srt, torch.arange(W + 1, device=self.device, dtype=torch.int64) << OWNER_SHIFT)
+        cum0 = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device), cum])
+        cnt = cum0[bounds[1:]] - cum0[bounds[:-1]]
+        meta = torch.cat([torch.cumsum(cnt, 0) - cnt, cnt]).contiguous()
+        inv = torch.empty(n, dtype=torch.int64, device=self.device)
+        inv[perm] = uidx
+        return {"n": n, "ubuf": ubuf, "meta": meta, "inv": inv, "perm": perm, "seg": seg}
+
+    def _send(self, buf: torch.Tensor, meta: torch.Tensor, boxes, counted: bool, width: int) -> None:
+        """The owners' pieces of ``buf`` into their mailboxes ``boxes[o]`` (this worker's row of
+        each), on the io stream behind the compute stream."""
+        io = self._io_stream
+        io.wait_stream(torch.cuda.current_stream(self.device))
+        buf.record_stream(io)
+        meta.record_stream(io)
+        ptrs = [b.data_ptr() for b in boxes]
+        cnts = [b.data_ptr() + self.C * 8 for b in boxes] if counted else []
+        with torch.cuda.stream(io):
+            self._R.to_peers(buf, meta, ptrs, cnts, width, self.C)
+
+    def _pull_dev(self, plan: dict) -> torch.Tensor:
+        W, me, c = self.W, self.me, self.ctl
+        if self.staleness is not None and W > 1:  # SSP gate (host words, no device sync)
+            target = self.pushes - int(self.staleness)
+            if target > 0:
+                self.shm.wait_ge([c.pack(o, w) for o in range(W) for w in range(W)], target, c.stop, self.timeout_s)
+        self._check_cap(plan["n"])
+        self._send(plan["ubuf"], plan["meta"], [self.peer_rq[o][me] for o in range(W)], True, 1)
+        self._notify.after(self._io_stream.cuda_stream, self.device.index, [c.req(o, me) for o in range(W)])
+        self.pulls += 1
+        self.shm.wait_ge([c.resp(o, me) for o in range(W)], self.pulls, c.stop, self.timeout_s)
+        rows = torch.zeros(plan["n"], self.dim, dtype=torch.float32, device=self.device)
+        self._R.from_peers(rows, plan["meta"], [self.peer_rs[o][me].data_ptr() for o in range(W)], self.dim, self.C)
+        return rows
+
+    def _push_dev(self, plan: dict, ug: torch.Tensor) -> None:
+        W, me, c = self.W, self.me, self.ctl
+        k = self.pushes
+        slot = k % self.MB
+        if k >= 2:  # mailbox slot k % 2 is free once push k - 2 was applied
+            self.shm.wait_ge([c.pack(o, me) for o in range(W)], k - 1, c.stop, self.timeout_s)
+        self._check_cap(plan["n"])
+        self._send(plan["ubuf"], plan["meta"], [self.peer_pk[o][me][slot] for o in range(W)], True, 1)
+        self._send(ug.contiguous(), plan["meta"], [self.peer_pg[o][me][slot] for o in range(W)], False, self.dim)
+        self._notify.after(self._io_stream.cuda_stream, self.device.index, [c.pseq(o, me) for o in range(W)])
+        self.pushes += 1
+
+    def lookup(self, ids: torch.Tensor, out_dtype=None, grad_fn=None) -> torch.Tensor:
+        if not self.gpu:
+            return super().lookup(ids, out_dtype, grad_fn)
+        plan = self._route_dev(self._keys_dev(ids))
+        rows = self._pull_dev(plan)
+        want_grad = torch.is_grad_enabled()
+        leaf = rows.detach().requires_grad_(want_grad)
+        out = _sp.gather_unique(leaf, plan["inv"], plan["perm"], plan["seg"], out_dtype)
+        if want_grad:
+            self._pending.append({"dev": plan, "leaf": leaf, "grad_fn": grad_fn, "plan": _DevPlan(plan["seg"])})
+        return out.view(*ids.shape, self.dim)
+
+    def pull(self, ids: torch.Tensor) -> torch.Tensor:
+        if not self.gpu:
+            return super().pull(ids)
+        plan = self._route_dev(self._keys_dev(ids))
+        out = self._pull_dev(plan)[plan["inv"]]
+        return out if self.fields == 1 else out.view(*ids.shape, self.dim)
+
+    def push(self, ids: torch.Tensor, grads: torch.Tensor) -> None:
+        if not self.gpu:
+            return super().push(ids, grads)
+        plan = self._route_dev(self._keys_dev(ids))
+        ug = torch.zeros(plan["n"], self.dim, dtype=torch.float32, device=self.device)
+        _sp.segment_reduce_rows(grads.to(self.device).float().reshape(plan["n"], self.dim).contiguous(), plan["perm"],
+                                plan["seg"], ug, False)
+        self._push_dev(plan, ug)
+        self.round += 1
+
+    def _push_pending_dev(self) -> int:
+        items = []
+        for p in self._pending:
+            leaf = p["leaf"]
+            if leaf.grad is None:
+                continue
+            g = leaf.grad.detach().float()
+            if p["grad_fn"] is not None:
+                g = p["grad_fn"](g, p["plan"])
+            items.append((p["dev"], g))
+        self._pending = []
+        if self.accumulating:  # micro-batches: keep them for the round's one push
+            self._held = getattr(self, "_held", []) + items
+            return sum(d["n"] for d, _ in items)
+        items = getattr(self, "_held", []) + items
+        self._held = []
+        if len(items) == 1:
+            plan, ug = items[0]
+        elif items:  # several lookups this round: merge into ONE push (pads carry key -1)
+            keys = torch.cat([d["ubuf"] for d, _ in items])
+            g = torch.cat([x for _, x in items]).contiguous()
+            plan = self._route_dev(keys)
+            ug = torch.zeros(plan["n"], self.dim, dtype=torch.float32, device=self.device)
+            _sp.segment_reduce_rows(g, plan["perm"], plan["seg"], ug, False)
+        else:  # nothing looked up: an empty push still advances this worker's row clock
+            plan = self._route_dev(torch.empty(0, dtype=torch.int64, device=self.device))
+            ug = torch.zeros(0, self.dim, dtype=torch.float32, device=self.device)
+        self._push_dev(plan, ug)
+        self.round += 1
+        return sum(d["n"] for d, _ in items)
 
     # ------------------------------------------------------------------ owner side
     def _serve(self, op: str, worker: int, n: int, m: int) -> None:
@@ -264,15 +457,25 @@ class AsyncRowTable(TcpSparseTable):
 
     # ------------------------------------------------------------------ lifecycle
     def synchronize(self) -> None:
-        """Wait until every owner applied every row push of this worker."""
+        """Wait until every owner applied every row push of this worker (and, GPU, raise on ids
+        out of range since the last check)."""
         c = self.ctl
+        if self.gpu:
+            self._notify.drain()
         self.shm.wait_ge([c.pack(o, self.me) for o in range(self.W)], self.pushes, c.stop, self.timeout_s)
+        if self.gpu and self._nbad is not None:
+            nb = int(self._nbad.item())
+            self._nbad = None
+            if nb:
+                raise IndexError(f"{self.name}: {nb} ids out of range for id_mode={self.id_mode!r}")
 
     def state_dict(self) -> dict:
         self.synchronize()
         self.t.barrier()
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
         d = self.shard.state_dict()
-        d["applied"] = self.applied
+        d["applied"] = self.service.applied if self.gpu else self.applied
         self.t.barrier()
         return d
 
@@ -281,6 +484,9 @@ class AsyncRowTable(TcpSparseTable):
         self.t.barrier()
         self.shard.load_state_dict(d)
         self.applied = int(d.get("applied", 0))
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+            self.service.set_applied(self.applied)
         self.t.barrier()
 
     def close(self) -> None:
@@ -298,6 +504,17 @@ class AsyncRowTable(TcpSparseTable):
             self._ctl.unlink()
         if err:
             raise RuntimeError(f"async row table {self.name}: {err}")
+
+
+class _DevPlan:
+    """What a reference gradient mode needs of a device lookup: occurrences per unique key."""
+
+    def __init__(self, seg: torch.Tensor):
+        self._seg = seg
+
+    @property
+    def counts(self) -> torch.Tensor:
+        return (self._seg[1:] - self._seg[:-1]).clamp(min=1)
 
 
 class _Null:
