@@ -283,6 +283,46 @@ class PlaneEngine {
     return err_;
   }
 
+  // IPC serve events: create this rank's ring (R per bucket), export handles
+  std::vector<py::bytes> ipc_event_handles(int64_t ring) {
+    TORCH_CHECK(gpu_ && ring >= 1, "IPC events are the GPU-process path");
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(active_.empty() && incoming_.empty(), "set up IPC events before the first push");
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    ring_ = static_cast<int>(ring);
+    std::vector<py::bytes> out;
+    for (int i = 0; i < NB_ * ring_; ++i) {
+      hipEvent_t ev;
+      hip_ok(hipEventCreateWithFlags(&ev, hipEventInterprocess | hipEventDisableTiming), "hipEventCreate(ipc)");
+      own_ev_.push_back(ev);
+      hipIpcEventHandle_t h;
+      hip_ok(hipIpcGetEventHandle(&h, ev), "hipIpcGetEventHandle");
+      out.emplace_back(reinterpret_cast<const char*>(&h), sizeof(h));
+    }
+    return out;
+  }
+  // open every peer's ring (handles[r] from rank r; own entry ignored) and switch the round end
+  void enable_ipc_events(std::vector<std::vector<py::bytes>> handles) {
+    TORCH_CHECK(static_cast<int>(handles.size()) == W_ && ring_ > 0, "one handle list per rank");
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    peer_ev_.assign(static_cast<size_t>(W_), {});
+    for (int r = 0; r < W_; ++r) {
+      if (r == me_) continue;
+      TORCH_CHECK(static_cast<int>(handles[r].size()) == NB_ * ring_, "ring size mismatch");
+      for (auto& hb : handles[r]) {
+        std::string st = hb;
+        TORCH_CHECK(st.size() == sizeof(hipIpcEventHandle_t), "bad IPC event handle");
+        hipIpcEventHandle_t h;
+        std::memcpy(&h, st.data(), sizeof(h));
+        hipEvent_t ev;
+        hip_ok(hipIpcOpenEventHandle(&ev, h), "hipIpcOpenEventHandle");
+        peer_ev_[static_cast<size_t>(r)].push_back(ev);
+      }
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    ipc_ = true;
+  }
+
   // checkpoint restore at PS clock ``round`` (rounds 0 .. round-1 are complete): this rank's
   // control words say so, as if it had run them -- the peers' waits (ready / served / the clip
   // phase's fdone gate) are monotonic, so a fresh control block would stall the first round
@@ -363,6 +403,11 @@ class PlaneEngine {
       hipStreamDestroy(serve_s_);
       hipStreamDestroy(pull_s_);
     }
+    for (auto& v : peer_ev_)
+      for (auto ev : v) hipEventDestroy(ev);
+    peer_ev_.clear();
+    for (auto ev : own_ev_) hipEventDestroy(ev);
+    own_ev_.clear();
   }
 
   void fail(const std::string& what) {
@@ -499,6 +544,7 @@ class PlaneEngine {
           callback("serve", j);
         }
         j.stage = SERVING;
+        publish_enqueued(j);
         return;
       }
       case REDUCED: {
@@ -512,6 +558,7 @@ class PlaneEngine {
           callback("serve_clipped", j);
         }
         j.stage = SERVING;
+        publish_enqueued(j);
         return;
       }
       case SERVING:
@@ -527,6 +574,13 @@ class PlaneEngine {
         }
         j.t_allserved = Clock::now();
         if (gpu_) {
+          if (ipc_) {  // device-side: the pull runs after every owner's serve of this round
+            const size_t k = static_cast<size_t>(j.b * ring_ + j.round % ring_);
+            hip_ok(hipStreamWaitEvent(pull_s_, j.s1, 0), "hipStreamWaitEvent(own serve)");
+            for (int o = 0; o < W_; ++o)
+              if (o != me_) hip_ok(hipStreamWaitEvent(pull_s_, peer_ev_[static_cast<size_t>(o)][k], 0),
+                                   "hipStreamWaitEvent(peer serve)");
+          }
           j.p0 = record(pull_s_, true);
           launch_pull(bk, j.wslot, pull_s_);
           j.p1 = record(pull_s_, true);
@@ -545,6 +599,17 @@ class PlaneEngine {
       case DONE:
         return;
     }
+  }
+
+  // IPC mode: record this round's serve event of the bucket and publish served[me][b] now (the
+  // serve is enqueued; peers order their pulls after it on the device)
+  void publish_enqueued(Job& j) {
+    if (!ipc_ || !gpu_) return;
+    const size_t k = static_cast<size_t>(j.b * ring_ + j.round % ring_);
+    hip_ok(hipEventRecord(own_ev_[k], serve_s_), "hipEventRecord(ipc)");
+    store_max(ctl_.served(me_, j.b), j.round + 1);
+    j.t_served = Clock::now();
+    j.stage = SERVED;
   }
 
   void note_pull_enqueued(const Job& j) {
@@ -767,6 +832,13 @@ class PlaneEngine {
   int64_t rounds_done_ = 0, jobs_done_ = 0;
   int64_t done_round_ = -1;  // rounds <= this one have every pull enqueued
   int64_t restored_round_ = 0;
+  // IPC-event round end (enable_ipc_events): served[me][b] is published when the serve is
+  // ENQUEUED and the pulls wait on the owners' events on the device -- no rank's host waits for
+  // another rank's serve kernel to finish.  Ring of R events per bucket, slot = round % R.
+  bool ipc_ = false;
+  int ring_ = 0;
+  std::vector<hipEvent_t> own_ev_;
+  std::vector<std::vector<hipEvent_t>> peer_ev_;
 
   // engine-thread state
   std::thread th_;
@@ -938,7 +1010,9 @@ void register_plane(pybind11::module& m) {
       .def("gather_now", &PlaneEngine::gather_now)
       .def("stats", &PlaneEngine::stats, py::arg("reset") = false)
       .def("error", &PlaneEngine::error)
-      .def("restore_round", &PlaneEngine::restore_round);
+      .def("restore_round", &PlaneEngine::restore_round)
+      .def("ipc_event_handles", &PlaneEngine::ipc_event_handles)
+      .def("enable_ipc_events", &PlaneEngine::enable_ipc_events);
   py::class_<IpcEvent>(pm, "IpcEvent")
       .def(py::init<int64_t>())
       .def(py::init<py::bytes, int64_t>())

@@ -260,6 +260,14 @@ class XgmiPlane:
                 eng.set_norm(self.sq_off, self._total.data_ptr(), self._factor.data_ptr(), self._partial.data_ptr())
         if not self.gpu:
             eng.set_callback(self._callback)
+        # round end on the device (PS_AMD_PLANE_IPC_EVENTS=1, GPU processes): owners publish a
+        # serve as soon as it is enqueued and peers' pulls wait on its inter-process event, so no
+        # host waits for another rank's serve kernel to finish (csrc/plane.cpp enable_ipc_events)
+        self.ipc_events = (self.gpu and not self.threads and self.W > 1
+                           and os.environ.get("PS_AMD_PLANE_IPC_EVENTS", "0") == "1")
+        if self.ipc_events:
+            hs = eng.ipc_event_handles(self.nslots + 1)
+            eng.enable_ipc_events(self.t.all_gather_object(list(hs)))
         self.engine = eng
         self._tmp_engine = None
         eng.start()

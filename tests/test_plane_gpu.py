@@ -402,3 +402,18 @@ def test_tiny_llama_onebit_two_processes_on_the_plane():
         assert torch.equal(res[0][0][k], res[1][0][k])
     for _, losses in res:
         assert sum(losses[-5:]) / 5 < 0.8 * sum(losses[:5]) / 5, losses
+
+
+def test_plane_processes_ipc_event_round_end_matches_oracle(monkeypatch):
+    """PS_AMD_PLANE_IPC_EVENTS=1: owners publish a serve when it is ENQUEUED and every peer's pull
+    waits on the owner's inter-process event on the device (csrc/plane.cpp enable_ipc_events).
+    BSP at W = 2 and 4 and SSP(1) still match the fp32 oracles exactly as the host-observed
+    round end does."""
+    monkeypatch.setenv("PS_AMD_PLANE_IPC_EVENTS", "1")
+    for world in (2, 4):
+        res = dist_util.run(_body, world, ({}, 5))
+        ref = _oracle(world, 5, lambda p: torch.optim.SGD(p, lr=0.1, momentum=0.9, weight_decay=1e-4))
+        for k, v in ref.items():
+            torch.testing.assert_close(res[0][0][k], v, rtol=1e-5, atol=1e-5)
+            for r in range(1, world):
+                assert torch.equal(res[0][0][k], res[r][0][k])
