@@ -46,12 +46,15 @@ def local_table_factory(device=None, seed: int = 0, id_mode: str = "map"):
     return make
 
 
-def sharded_table_factory(transport, device=None, seed: int = 0, id_mode: str = "map", overlap: bool = True):
+def sharded_table_factory(transport, device=None, seed: int = 0, id_mode: str = "map", overlap: bool = True,
+                          exchange=None):
     """Rows partitioned over the co-located servers of ``transport`` (torchrun ranks); with
-    ``overlap`` (GPU) row gradients are pushed from backward hooks on a side stream."""
+    ``overlap`` (GPU) row gradients are pushed from backward hooks on a side stream.
+    ``exchange``: "plane" | "collective" | None (auto, see row_plane.plane_rows_wanted)."""
     def make(name, dim, rows, init, mode=None, fields=1):
         return ShardedSparseTable(name, dim, rows, transport, init=init, id_mode=mode or id_mode,
-                                  seed=stable_seed(name, seed), device=device, fields=fields, overlap=overlap)
+                                  seed=stable_seed(name, seed), device=device, fields=fields, overlap=overlap,
+                                  exchange=exchange)
 
     return make
 

@@ -369,10 +369,11 @@ class RowAccumulator:
         sh.apply(slots, g, gscale, step, sorted_runs=True)
 
 
-def plane_rows_wanted(transport: Transport, device) -> bool:
-    """Auto choice of the one-node row exchange: every rank on this host (the IPC / shared-memory
-    plane); PS_AMD_ROW_EXCHANGE=collective keeps the all-to-all path."""
-    req = os.environ.get("PS_AMD_ROW_EXCHANGE", "auto")
+def plane_rows_wanted(transport: Transport, device, req: Optional[str] = None) -> bool:
+    """Choice of the one-node row exchange.  ``req`` (default PS_AMD_ROW_EXCHANGE, else "auto"):
+    "auto" takes the IPC / shared-memory plane when every rank is on this host, "plane" insists
+    on it (raises across hosts), "collective" keeps the all-to-all path."""
+    req = req or os.environ.get("PS_AMD_ROW_EXCHANGE", "auto")
     if req == "collective" or transport.world <= 1:
         return False
     import socket

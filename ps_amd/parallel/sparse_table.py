@@ -307,12 +307,9 @@ class ShardedSparseTable:
         if self.world > 1:
             from . import row_plane as _rp
 
-            if exchange is not None:
-                os.environ.setdefault("PS_AMD_ROW_EXCHANGE", exchange)
-            want = (exchange == "plane") if exchange is not None else _rp.plane_rows_wanted(self.t, self.device)
-            if exchange == "plane":
-                _rp.plane_rows_wanted(self.t, self.device)  # same-host check
-            if want:
+            if exchange not in (None, "auto", "plane", "collective"):
+                raise ValueError(exchange)
+            if _rp.plane_rows_wanted(self.t, self.device, exchange):
                 self.plane = _rp.RowPlane(self.t, self.dim, self.device)
                 self._rowacc = _rp.RowAccumulator(self.shard)
         self.exchange = "plane" if self.plane is not None else ("collective" if self.world > 1 else "local")
