@@ -1061,7 +1061,7 @@ void row_plane_accum(std::vector<int64_t> grads, Tensor rslots, Tensor pmeta, Te
   TORCH_CHECK(acc.dim() == 2 && acc.is_contiguous(), "acc [rows, dim]");
   check_i64_gpu(rslots, P.W * cap, "rslots");
   check_i64_gpu(pmeta, 2 * P.W, "pmeta");
-  check_i64_gpu(touched, P.W * cap, "touched");
+  check_i64_gpu(touched, acc.size(0), "touched");  // at most one entry per slot
   check_gpu(tflag, "tflag");
   check_gpu(tcount, "tcount");
   TORCH_CHECK(tflag.scalar_type() == torch::kInt32 && tflag.numel() == acc.size(0), "tflag: int32 [rows]");
@@ -1224,7 +1224,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
                               c10::optional<Tensor> mean, c10::optional<Tensor> invstd, c10::optional<Tensor> bits,
                               c10::optional<Tensor> aux2, c10::optional<Tensor> bits2, c10::optional<Tensor> a2,
                               c10::optional<Tensor> bwd, c10::optional<Tensor> aux3, c10::optional<Tensor> mean2,
-                              c10::optional<Tensor> invstd2) {
+                              c10::optional<Tensor> invstd2, c10::optional<Tensor> pro2, c10::optional<Tensor> aout,
+                              c10::optional<Tensor> abits) {
   check_rows(a, "a");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
@@ -1264,6 +1265,26 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     check_f32(*bwd, "bwd");
     TORCH_CHECK(bwd->numel() == 3 * g.C, "bwd must be [3C]");
   }
+  // block-output prologue: A := relu(bn3(a) + r), r = a2 or the downsample BN of a2 (pro2); the
+  // block output and its ReLU bits land in the caller's aout / abits
+  const bool has_a2 = a2.has_value() && a2->defined();
+  const bool resp = has_a2 && !has_bwd;
+  if (resp) {
+    TORCH_CHECK(pro.has_value() && pro->defined(), "a2 without bwd is the block-output prologue: needs pro");
+    TORCH_CHECK(g.ks == 1 && g.stride == 1 && g.pad == 0, "the block-output prologue is for 1x1 stride-1 convs");
+    check_rows(*a2, "a2");
+    TORCH_CHECK(a2->sizes() == a.sizes(), "a2 must match a");
+    TORCH_CHECK(aout.has_value() && aout->defined() && abits.has_value() && abits->defined(),
+                "the block-output prologue needs aout and abits");
+    check_rows(*aout, "aout");
+    TORCH_CHECK(aout->sizes() == a.sizes(), "aout must match a");
+    check_gpu(*abits, "abits");
+    TORCH_CHECK(abits->scalar_type() == torch::kUInt8 && abits->is_contiguous() && abits->numel() * 8 == a.numel(),
+                "abits: uint8 [rows * C / 8]");
+  } else {
+    TORCH_CHECK(!(pro2.has_value() && pro2->defined()) && !(aout.has_value() && aout->defined()),
+                "pro2 / aout belong to the block-output prologue (pro + a2)");
+  }
   const uint16_t* aux2p = nullptr;
   const uint8_t* bits2p = nullptr;
   if (fold) {
@@ -1290,7 +1311,7 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto fopt = a.options().dtype(torch::kFloat32);
   const bool has_pro = pro.has_value() && pro->defined();
   const int G = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
-                                        has_pro || has_bwd, g).gm;
+                                        has_pro || has_bwd, g, resp).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;
@@ -1320,15 +1341,21 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   p.aux3 = aux3p;
   p.mean2 = epi == 9 ? f32_opt(mean2, N, "mean2") : nullptr;
   p.invstd2 = epi == 9 ? f32_opt(invstd2, N, "invstd2") : nullptr;
-  Tensor aout;
+  Tensor bwd_out;
   if (has_bwd) {
-    aout = torch::empty_like(a);
+    bwd_out = torch::empty_like(a);
     p.a2 = u16(*a2);
     p.bwd = bwd->data_ptr<float>();
-    p.aout = u16m(aout);
+    p.aout = u16m(bwd_out);
+  }
+  if (resp) {
+    p.a2 = u16(*a2);
+    p.pro2 = f32_opt(pro2, 2 * g.C, "pro2");
+    p.aout = u16m(*aout);
+    p.abits = abits->data_ptr<uint8_t>();
   }
   psamd::launch_conv_fwd(p, cur_stream(a));
-  if (has_bwd) return {c, part, aout};
+  if (has_bwd) return {c, part, bwd_out};
   return {c, part};
 }
 
@@ -1548,7 +1575,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("bits") = py::none(),
         py::arg("aux2") = py::none(), py::arg("bits2") = py::none(), py::arg("a2") = py::none(),
         py::arg("bwd") = py::none(), py::arg("aux3") = py::none(), py::arg("mean2") = py::none(),
-        py::arg("invstd2") = py::none());
+        py::arg("invstd2") = py::none(), py::arg("pro2") = py::none(), py::arg("aout") = py::none(),
+        py::arg("abits") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("weight_prep", &weight_prep);

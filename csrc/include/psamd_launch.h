@@ -330,13 +330,18 @@ struct ConvGemmArgs {
   const uint16_t* a2;   // [M, C] BN input; nullable
   const float* bwd;     // [3C]
   uint16_t* aout;       // [M, C]
+  // block-output prologue (1x1 forward, epi 0/1; pro and a2 set, bwd null): A := relu(a * sc + sh
+  // + r) with pro = [sc | sh] of bn3 and r = a2 (identity) or a2 * sc2 + sh2 (pro2 = the
+  // downsample BN's [sc2 | sh2]); the block output goes to aout, its ReLU bits to abits [M C / 8]
+  const float* pro2;    // [2C]; nullable
+  uint8_t* abits;
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
 // the plan launch_conv_fwd uses for this geometry (the 3x3 patch-staged tiles where they apply)
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g);
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, bool resp = false);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)

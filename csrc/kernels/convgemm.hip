@@ -180,7 +180,8 @@ struct StageRegs {
   bool wb;      // b[] loaded (to be staged)
 };
 
-// PRO: 0 none, 1 BN + ReLU of the A rows, 2 BN backward from two row sources (a, a2)
+// PRO: 0 none, 1 BN + ReLU of the A rows, 2 BN backward from two row sources (a, a2),
+// 3 the previous block's output relu(bn3(a) + r) with r = a2 (identity) or bnd(a2) (downsample)
 // PATCH (3x3 / stride 1 / pad 1, LDS-DMA path): the tile's input rows -- a PATCH of whole rows with
 // zero halo rows / columns, at most two images -- are staged ONCE per 64-channel chunk and the nine
 // taps read their A fragments from it at a shifted slot; a K stage then moves only its weight tile.
@@ -193,8 +194,10 @@ constexpr int patch_bytes() { return BN == 64 ? 65536 : 40960; }  // 8 channel p
 template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, bool PATCH = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr bool BWD = PRO == 2;
+  constexpr bool RESP = PRO == 3;
   static_assert(!BWD || (KS1 && EPI == 3 && !GLDS), "the BN-backward prologue is a 1x1 data-gradient prologue");
-  constexpr int AR2 = BWD ? BM / 32 : 1;
+  static_assert(!RESP || (KS1 && EPI <= 1 && !GLDS), "the block-output prologue is a 1x1 forward prologue");
+  constexpr int AR2 = BWD || RESP ? BM / 32 : 1;
   // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce; 9 = 6 + the
   // previous block's downsample-BN sum (third partial slab)
   constexpr bool FOLD = EPI >= 6;
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       R.ok |= (v ? 1u : 0u) << i;
       // out-of-map taps / rows past M read element 0 (in bounds) and are zeroed in LDS
       R.a[i] = *reinterpret_cast<const u16x8*>(p.a + (v ? rbase[i] + toff : 0));
-      if constexpr (BWD) R.a2[i] = *reinterpret_cast<const u16x8*>(p.a2 + (v ? rbase[i] + toff : 0));
+      if constexpr (BWD || RESP) R.a2[i] = *reinterpret_cast<const u16x8*>(p.a2 + (v ? rbase[i] + toff : 0));
     }
     const int k0 = pkt * kBK;
     R.wb = lq++ < 2 || nk > 2;
@@ -300,8 +303,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   auto swrite = [&](const StageRegs<AR, BCH, AR2>& R, int buf) {
     uint16_t* As = lds + buf * (BM * kBK);
     uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
-    float psc[8], psh[8], pcf[8];
-    if constexpr (PRO == 1) {  // [scale | shift] of 8 channels: L1-resident
+    float psc[8], psh[8], pcf[8], pdd[8];
+    if constexpr (PRO == 1 || RESP) {  // [scale | shift] of 8 channels: L1-resident
       load8(p.pro, R.cc + sc * 8, psc);
       load8(p.pro + g.C, R.cc + sc * 8, psh);
     } else if constexpr (BWD) {  // [ca | cb | cc]
@@ -309,8 +312,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       load8(p.bwd + g.C, R.cc + sc * 8, psh);
       load8(p.bwd + 2 * g.C, R.cc + sc * 8, pcf);
     }
-    // BWD: the channel-tile-0 blocks also store the A tile (the BN data gradient) to aout
-    const bool store_a = BWD && p.aout != nullptr && n0 == 0;
+    const bool dual = RESP && p.pro2 != nullptr;  // block-uniform
+    if (dual) {  // the downsample BN's [scale | shift]
+      load8(p.pro2, R.cc + sc * 8, pcf);
+      load8(p.pro2 + g.C, R.cc + sc * 8, pdd);
+    }
+    // BWD / RESP: the channel-tile-0 blocks also store the A tile (the BN data gradient / the
+    // block output, with its ReLU bits) to aout
+    const bool store_a = (BWD || RESP) && p.aout != nullptr && n0 == 0;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       u16x8 v = R.a[i];
@@ -321,12 +330,28 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         for (int j = 0; j < 8; ++j)
           v[j] = f32_to_bf16(psc[j] * bf16_to_f32(v[j]) + psh[j] * bf16_to_f32(x8[j]) + pcf[j]);
       }
+      unsigned obits = 0;
+      if constexpr (RESP) {  // the same arithmetic as bn_apply_kernel / bn_apply_dual_kernel
+        const u16x8 r8 = R.a2[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float o = bf16_to_f32(v[j]) * psc[j] + psh[j];
+          if (dual) o = o + (bf16_to_f32(r8[j]) * pcf[j] + pdd[j]);
+          else o += bf16_to_f32(r8[j]);
+          o = o > 0.f ? o : 0.f;
+          obits |= (o > 0.f ? 1u : 0u) << j;
+          v[j] = f32_to_bf16(o);
+        }
+      }
       const bool ok = (R.ok >> i) & 1u;
       if (!ok) v = kZero8;
       const int r = srow + 32 * i;
       *reinterpret_cast<u16x8*>(As + r * kBK + swz(r, sc) * 8) = v;
-      if (store_a && ok)
-        *reinterpret_cast<u16x8*>(p.aout + static_cast<int64_t>(R.mt * BM + r) * g.C + R.cc + sc * 8) = v;
+      if (store_a && ok) {
+        const int64_t e = static_cast<int64_t>(R.mt * BM + r) * g.C + R.cc + sc * 8;
+        *reinterpret_cast<u16x8*>(p.aout + e) = v;
+        if constexpr (RESP) p.abits[e >> 3] = static_cast<uint8_t>(obits);
+      }
     }
     if (R.wb) {
 #pragma unroll
@@ -1500,7 +1525,13 @@ bool patch_fwd_ok(const ConvGeo& g, int N, bool pro) {
   return 8 * plane <= (bn == 64 ? patch_bytes<64>() : patch_bytes<128>());
 }
 
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g) {
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, bool resp) {
+  if (resp) {  // block-output prologue: 64-channel tiles (128 x 128 with two row sources spilled)
+    ConvFwdPlan pl = conv_fwd_plan(M, N, K, true);
+    pl.bn = 64;
+    if (pl.gm != (M + 127) / 128) pl.gm = std::max(1, std::min((M + 127) / 128, 512 / (N / 64)));
+    return pl;
+  }
   if (patch_fwd_ok(g, N, pro)) {  // one 128-pixel tile per block (LDS-DMA path)
     ConvFwdPlan pl;
     pl.bm = 128;
@@ -1533,7 +1564,8 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const bool bwd = a.bwd != nullptr;
-  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g);
+  const bool resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
+  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, resp);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   if (!bwd && patch_fwd_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
@@ -1585,6 +1617,17 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
       default: PSAMD_CFT(0); break;
     }
 #undef PSAMD_CFT
+    return;
+  }
+  if (resp) {  // 1x1 forward over the previous block's output, applied while staging
+#define PSAMD_CFR(BN, EPI) \
+  hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 3, EPI, true, false>), dim3(nblk), dim3(256), 0, s, a, GM)
+    if (pl.bn == 128) {
+      if (a.epi == 1) { PSAMD_CFR(128, 1); } else { PSAMD_CFR(128, 0); }
+    } else {
+      if (a.epi == 1) { PSAMD_CFR(64, 1); } else { PSAMD_CFR(64, 0); }
+    }
+#undef PSAMD_CFR
     return;
   }
   if (bwd) {  // 1x1 data gradient with the previous BN's backward in the prologue (epilogue 3)

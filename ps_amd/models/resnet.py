@@ -11,12 +11,15 @@ the reference has no BN at all).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
-from ..ops.convgemm import deferred_bn_counters, fused_block_ok, fused_bottleneck, prepare_backward_weights
+from ..ops.convgemm import (deferred_bn_counters, flush_deferred, fused_block_ok, fused_bottleneck,
+                             prepare_backward_weights)
 from ..ops.pool import MaxPool2d, global_avg_pool
 
 
@@ -45,6 +48,7 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         if self.fuse_block and fused_block_ok(self, x):
             return fused_bottleneck(self, x)
+        flush_deferred()  # a deferred fused-block output (never on the fused ResNet path)
         identity = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
             # BN + ReLU fused; bn3 fuses the residual add and the final ReLU (ops/bn.py)
@@ -105,7 +109,11 @@ class ResNet(nn.Module):
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         with deferred_bn_counters():
             if self.fused_bn and self.training and x.is_cuda:
-                prepare_backward_weights(self._blocks())  # all data-grad weight layouts, one kernel
+                blks = self._blocks()
+                prepare_backward_weights(blks)  # all data-grad weight layouts, one kernel
+                # a block followed by a fused block leaves its output to that block's conv1 prologue
+                for a, b in zip(blks, blks[1:] + [None]):
+                    a._defer_out = b is not None and b.fuse_block and os.environ.get("PS_AMD_RESP", "1") != "0"
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.fused_bn:
             x = global_avg_pool(x)  # NHWC gradient straight into the last block's backward

@@ -186,7 +186,44 @@ class _Link:
         self.dx_ptr = self.dx_version = self.dx_keep = None
 
 
-FOLD_STATS = {"used": 0, "ds": 0}  # bn3 / downsample-BN backward passes that took the consumer's partials
+FOLD_STATS = {"used": 0, "ds": 0, "resp": 0}  # bn3 / downsample-BN backward passes that took the consumer's
+# partials; block outputs applied in the consumer's conv1 prologue ("resp")
+
+
+class _Deferred:
+    """A block output left unapplied: relu(bn3(z3) + r), r = the block input (identity) or the
+    downsample BN's output.  The next fused block's conv1 applies it while staging its A tile and
+    writes the output rows / ReLU bits into ``out`` / ``bits`` (block-output prologue, PRO 3):
+    the separate apply pass and conv1's re-read of the output are gone."""
+
+    __slots__ = ("out_ref", "z3", "cf3", "res", "cfd", "out", "bits")
+
+    def __init__(self, z3, cf3, res, cfd, out, bits):
+        self.out_ref = None
+        self.z3, self.cf3, self.res, self.cfd, self.out, self.bits = z3, cf3, res, cfd, out, bits
+
+    def flush(self) -> None:
+        """Materialise the output with the apply pass (a consumer that cannot take the prologue)."""
+        y, b = native().bn_apply_coef(self.z3, self.cf3, self.res, self.cfd, 1, True)
+        with torch.no_grad():
+            self.out.copy_(y)
+            self.bits.copy_(b)
+
+
+def _resp_enabled(c: int) -> bool:
+    """Block outputs of up to PS_AMD_RESP_MAX_C channels (0: never) are applied in the consumer's
+    conv1 prologue.  The prologue stages A through registers from two row sources, so it pays
+    where conv1's K is short (256 = the layer-1 outputs, 4 K-stages); deeper K keeps the apply
+    pass + the LDS-DMA GEMM."""
+    return c <= int(os.environ.get("PS_AMD_RESP_MAX_C", "256"))
+
+
+def flush_deferred() -> None:
+    """Apply a pending deferred block output now (a consumer outside the fused path)."""
+    pend = getattr(_tls, "pend", None)
+    _tls.pend = None
+    if pend is not None and pend.out_ref is not None and pend.out_ref() is not None:
+        pend.flush()
 
 
 def _bwd_prologue_enabled(c3: int) -> bool:
@@ -210,7 +247,7 @@ def _fold_ds_enabled() -> bool:
 
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, blk, link_in):
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, blk, link_in, pend_in):
         nat = native()
         n, cin, h, w = x.shape
         s = blk.conv2.stride[0]
@@ -221,7 +258,12 @@ class _BottleneckFn(torch.autograd.Function):
         # shift of the statistics sums (~ the batch mean): the running mean itself -- the finalize
         # kernel reads channel c's shift before it updates that channel's running mean
         k1 = bn1.running_mean
-        z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
+        if pend_in is not None:  # the previous block's output is applied (and stored) while staging
+            z1, p1 = nat.conv_gemm(pend_in.z3, _mat(w1), gi, pend_in.cf3, 1, None, k1, a2=pend_in.res,
+                                   pro2=pend_in.cfd, aout=x2, abits=pend_in.bits)
+            FOLD_STATS["resp"] += 1
+        else:
+            z1, p1 = nat.conv_gemm(x2, _mat(w1), gi, None, 1, None, k1)
         m1, i1, cf1 = _finalize(p1, k1, n * h * w, bn1)
         y1 = nat.bn_apply_coef(z1, cf1, None, None, 1)[0]
         if _conv3x3_enabled():
@@ -236,15 +278,23 @@ class _BottleneckFn(torch.autograd.Function):
         k3 = bn3.running_mean
         z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
         m3, i3, cf3 = _finalize(p3, k3, n * oh * ow, bn3)
+        cfd = None
         if wd is not None:
             bnd = blk.downsample[1]
             kd = bnd.running_mean
             zd, pd = nat.conv_gemm(x2, _mat(wd), geo(h, w, 1, s), None, 1, None, kd)
             md, idd, cfd = _finalize(pd, kd, n * oh * ow, bnd)
-            out, obits = nat.bn_apply_coef(z3, cf3, zd, cfd, 1, True)
         else:
             zd = md = idd = None
-            out, obits = nat.bn_apply_coef(z3, cf3, x2, None, 1, True)
+        if (getattr(blk, "_defer_out", False) and getattr(_tls, "pending", None) is not None
+                and _resp_enabled(z3.shape[1])):
+            # the next fused block applies this output in its conv1 prologue and fills out / obits
+            # (handed over through the thread-local, which also works under no_grad)
+            out = torch.empty_like(z3)
+            obits = torch.empty(z3.numel() // 8, dtype=torch.uint8, device=z3.device)
+            _tls.pend_new = _Deferred(z3, cf3, zd if wd is not None else x2, cfd, out, obits)
+        else:
+            out, obits = nat.bn_apply_coef(z3, cf3, zd if wd is not None else x2, cfd, 1, True)
         # the block output's ReLU mask is kept as 1 bit per element (the output itself is the
         # next block's input; the backward reads 1/16 of its bytes)
         ctx.save_for_backward(x2, w1, w2, w3, wd, g1, g2, g3, gd, z1, y1, z2r, z3, obits, zd,
@@ -360,7 +410,7 @@ class _BottleneckFn(torch.autograd.Function):
             # gradient always lands in a different buffer and fails the pointer check
             li.part, li.dx_ptr, li.dx_version, li.dx_keep = part, dx2.data_ptr(), dx2._version, dx2
         return (image(dx2, n, h, w), dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3,
-                dwd, dgd, dbd, None, None)
+                dwd, dgd, dbd, None, None, None)
 
 
 def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
@@ -476,9 +526,11 @@ def deferred_bn_counters():
     prev = getattr(_tls, "pending", None)
     _tls.pending = []
     _tls.last = None  # bn3 hand-off chain starts fresh every forward
+    _tls.pend = None
     try:
         yield
     finally:
+        flush_deferred()  # (a deferred output nobody consumed -- never on the ResNet path)
         _tls.last = None
         _tls.prep = None
         pending, _tls.pending = _tls.pending, prev
@@ -497,10 +549,26 @@ def fused_bottleneck(blk: nn.Module, x: torch.Tensor) -> torch.Tensor:
     wd, gd, bd = (ds[0].weight, ds[1].weight, ds[1].bias) if ds is not None else (None, None, None)
     last = getattr(_tls, "last", None)
     link_in = last if last is not None and last.out_ref is not None and last.out_ref() is x else None
+    _tls.pend_new = None
+    pend = getattr(_tls, "pend", None)
+    pend_in = None
+    if pend is not None:
+        if pend.out_ref is not None and pend.out_ref() is x:
+            pend_in = pend
+            _tls.pend = None
+        else:
+            flush_deferred()
     y = _BottleneckFn.apply(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
-                            blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk, link_in)
-    lk = y.grad_fn.link_out if y.grad_fn is not None and hasattr(y.grad_fn, "link_out") else None
+                            blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, wd, gd, bd, blk, link_in,
+                            pend_in)
+    gf = y.grad_fn
+    lk = gf.link_out if gf is not None and hasattr(gf, "link_out") else None
     if lk is not None and hasattr(_tls, "pending") and _tls.pending is not None:
         lk.out_ref = weakref.ref(y)
         _tls.last = lk
+    po = getattr(_tls, "pend_new", None)
+    _tls.pend_new = None
+    if po is not None:
+        po.out_ref = weakref.ref(y)
+        _tls.pend = po
     return y

@@ -449,9 +449,10 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
     gw1 = torch.randn(4, 256, 9, 9, device=DEV)
     state = copy.deepcopy(a.state_dict())
 
-    def run():
+    def run(defer=False):
         a.load_state_dict(state)
         a.zero_grad()
+        a[0]._defer_out = a[1]._defer_out = defer  # (set by ResNet.forward on the model path)
         xi = x.clone().requires_grad_()
         with cg.deferred_bn_counters():
             y1 = a[0](xi)
@@ -473,6 +474,14 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
     for n in pc:
         _close(pa[n], pc[n], tol=1e-2, amax=0.05)
     monkeypatch.delenv("PS_AMD_FOLD_BN_DS")
+    # block outputs applied in the next block's conv1 prologue (PRO 3): same gradients, and the
+    # forward outputs / ReLU bits they store equal the apply pass's
+    before = cg.FOLD_STATS["resp"]
+    gr, pr = run(defer=True)
+    assert cg.FOLD_STATS["resp"] - before == 2
+    _close(ga, gr, tol=1e-2, amax=0.05)
+    for n in pr:
+        _close(pa[n], pr[n], tol=1e-2, amax=0.05)
     monkeypatch.setenv("PS_AMD_FOLD_BN3", "0")
     before = cg.FOLD_STATS["used"]
     gb, pb = run()
@@ -637,3 +646,32 @@ def test_epilogue9_downsample_bn_sum(M, K, N):
     torch.testing.assert_close(p9[:2], p6, rtol=0, atol=0)
     gv = c9.float().cpu()
     torch.testing.assert_close(p9[2].sum(0).cpu(), (gv * ((zd - md) * idd)).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,C,N,dual", [(300, 256, 64, False), (4099, 256, 128, True), (1000, 64, 64, False),
+                                        (517, 512, 256, True)])
+def test_block_output_prologue_matches_apply_then_gemm(M, C, N, dual):
+    """conv_gemm(z3, pro=bn3 coef, a2=r[, pro2=downsample coef], aout, abits) == bn_apply_coef
+    (the block output relu(bn3(z3) + r) and its ReLU bits) then conv_gemm on that output with
+    the BN-statistics epilogue: the consumer block's conv1 applies the previous block's output
+    while staging A and stores it (rows + bits) for the residual and the backward."""
+    g = _gen(M + C + N)
+    z3, r = _rnd(M, C, g=g), _rnd(M, C, g=g)
+    cf3 = _coef(C, g).to(DEV)
+    cfd = _coef(C, g).to(DEV) if dual else None
+    b = _rnd(N, C, g=g, scale=C ** -0.5)
+    ks = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    geo = [M, 1, M, 1, 1, 1, 0]
+    y_ref, bits_ref = native().bn_apply_coef(_bf(z3), cf3, _bf(r), cfd, 1, True)
+    c_ref, p_ref = native().conv_gemm(y_ref, _bf(b), geo, None, 1, None, ks)
+    y = torch.full_like(y_ref, float("nan"))
+    bits = torch.zeros_like(bits_ref)
+    c, p = native().conv_gemm(_bf(z3), _bf(b), geo, cf3, 1, None, ks, a2=_bf(r), pro2=cfd, aout=y, abits=bits)
+    torch.cuda.synchronize()
+    # same arithmetic as the apply kernels; FMA contraction may move a value by one bf16 ulp
+    assert (y != y_ref).float().mean().item() < 1e-2
+    torch.testing.assert_close(y.float(), y_ref.float(), rtol=8e-3, atol=1e-3)
+    assert (bits != bits_ref).float().mean().item() < 1e-2
+    _close(c, c_ref, tol=1e-2, amax=0.05)
+    assert p.shape[0] == 2 and p.shape[2] == N
+    torch.testing.assert_close(p.sum(1), p_ref.sum(1), rtol=2e-3, atol=2e-2)

@@ -191,32 +191,45 @@ def _resnet_body(tp, steps):
 
 def _bf16_oracle(world, steps, lr=0.05, mom=0.9):
     """The same bf16 ResNet-tiny (same kernels, per-rank BN batches) in ONE process: every
-    rank's shard is run in turn, the bf16 gradients are summed in fp32 in rank order, scaled by
-    1/W, and momentum-SGD updates an fp32 master whose bf16 copy is the next replica -- the
-    plane's arithmetic without the plane (no arenas, no IPC, no owner chunks)."""
+    rank's shard is run in turn with THAT rank's BN buffers (the fused BN kernels shift their
+    statistic sums by the running mean, so sharing one set of buffers would perturb the batch
+    statistics at the rounding level), the bf16 gradients are summed in fp32 in rank order, and
+    the same fused momentum kernel the owners run (step_flat, gscale 1/W) updates an fp32 master
+    whose bf16 copy is the next replica -- the plane's arithmetic without the plane (no arenas,
+    no IPC, no owner chunks)."""
     from ps_amd.models.resnet import prepare_for_mi355x, resnet_tiny
+    from ps_amd.parallel.updaters import MomentumUpdater
 
     torch.manual_seed(0)
     net = prepare_for_mi355x(resnet_tiny(num_classes=10, fused_bn=True).cuda())
     params = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
     master = {n: p.detach().float().clone() for n, p in params}
-    buf = {n: torch.zeros_like(v) for n, v in master.items()}
+    u = MomentumUpdater(lr, mom, 0.0)
+    states = {n: u.new_states(v) for n, v in master.items()}
+    bufs = [{n: b.detach().clone() for n, b in net.named_buffers()} for _ in range(world)]
     g = torch.Generator(device="cuda").manual_seed(1)
     x = torch.randn(64, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (64,), device="cuda", generator=g)
-    for _ in range(steps):
+    for step in range(steps):
         gsum = {n: torch.zeros_like(v) for n, v in master.items()}
         for r in range(world):
+            with torch.no_grad():
+                for n, b in net.named_buffers():
+                    b.copy_(bufs[r][n])
             for _, p in params:
                 p.grad = None
             F.cross_entropy(net(x[r::world].bfloat16()).float(), y[r::world]).backward()
             for n, p in params:
                 gsum[n] += p.grad.float()
+            with torch.no_grad():
+                for n, b in net.named_buffers():
+                    bufs[r][n].copy_(b)
         with torch.no_grad():
             for n, p in params:
-                buf[n] = mom * buf[n] + gsum[n] * (1.0 / world)
-                master[n] -= lr * buf[n]
-                p.copy_(master[n].to(p.dtype))
+                out = torch.empty_like(p)
+                u.step_flat(master[n].view(-1), [s.view(-1) for s in states[n]], gsum[n].view(-1),
+                            wout=out.view(-1), gscale=1.0 / world, step=step + 1)
+                p.copy_(out)
     return {n: p.detach().float().cpu() for n, p in params}
 
 
