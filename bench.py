@@ -150,6 +150,10 @@ def main():
         local = 0
     if not cpu:
         torch.cuda.set_device(local)
+        if os.environ.get("PS_AMD_COMPUTE_PRIORITY", "normal") == "high":
+            # forward / backward on a high-priority stream: the PS's comm streams (normal priority)
+            # then only take the CUs the compute leaves idle (serve-overlap stretch A/B)
+            torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     tp = init_distributed(backend="gloo" if (cpu or one_gpu) else None)
     rank, world = tp.rank, tp.world
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)

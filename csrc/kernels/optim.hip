@@ -15,10 +15,25 @@
 //   FTRL         update/FtrlUpdater.java:51-76           reference ordering/sigma (Q6) -> ftrl_mode = 1;
 //                                                        canonical McMahan FTRL-proximal -> ftrl_mode = 0
 //   Adagrad      (north-star, DLRM tables)
+#include <cstdlib>
+
 #include "psamd_device.h"
 #include "psamd_launch.h"
 
 namespace psamd {
+
+// Dense optimizer grid: stream_grid capped by PS_AMD_OPT_MAX_BLOCKS (default 2048 = uncapped).  A
+// serve that overlaps a backward takes fewer CUs' worth of HBM bandwidth when capped; it runs
+// longer but stays hidden (profiles/r4_llama_serve_overlap.txt).
+static int opt_grid(int64_t work_items, int block) {
+  static const int cap = [] {
+    const char* e = std::getenv("PS_AMD_OPT_MAX_BLOCKS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
+  const int g = stream_grid(work_items, block);
+  return g < cap ? g : cap;
+}
 
 enum OptKind : int { kSGD = 0, kAdam = 1, kAdagrad = 2, kFtrl = 3 };
 
@@ -156,11 +171,11 @@ static void dispatch_vec(const FusedOptArgs& a, const OptParams& p, hipStream_t 
                        (sizeof(G) == 4 || (reinterpret_cast<uintptr_t>(a.g) & 15) == 0);
   const int block = 256;
   if (aligned) {
-    const int grid = stream_grid((a.n + 7) / 8, block);
+    const int grid = opt_grid((a.n + 7) / 8, block);
     hipLaunchKernelGGL((fused_opt_kernel<KIND, G, OUT, true>), dim3(grid), dim3(block), 0, s, a.w, a.st0, a.st1,
                        static_cast<const G*>(a.g), a.wout, a.n, p);
   } else {
-    const int grid = stream_grid(a.n, block);
+    const int grid = opt_grid(a.n, block);
     hipLaunchKernelGGL((fused_opt_kernel<KIND, G, OUT, false>), dim3(grid), dim3(block), 0, s, a.w, a.st0, a.st1,
                        static_cast<const G*>(a.g), a.wout, a.n, p);
   }
@@ -313,7 +328,7 @@ __global__ __launch_bounds__(256) void fused_opt_multi_kernel(float* __restrict_
 template <int KIND, int ONEBIT, typename G>
 static void launch_multi_out(const FusedOptArgs& a, const MultiGrad& m, const OptParams& p, int64_t head,
                              hipStream_t s) {
-  const int grid = stream_grid((a.n - head + 7) / 8, 256);
+  const int grid = opt_grid((a.n - head + 7) / 8, 256);
   if (a.wout == nullptr)
     hipLaunchKernelGGL((fused_opt_multi_kernel<KIND, ONEBIT, G, 0>), dim3(grid), dim3(256), 0, s, a.w, a.st0, a.st1,
                        m, a.wout, a.n, head, p);
@@ -377,7 +392,7 @@ void launch_reduce_multi(const MultiGrad& m, int g_bf16, int64_t n, float* out, 
   if (n <= 0) return;
   int64_t head = (8 - (m.off & 7)) & 7;
   if (head > n) head = n;
-  const int grid = stream_grid((n - head + 7) / 8, 256);
+  const int grid = opt_grid((n - head + 7) / 8, 256);
   if (m.onebit)
     hipLaunchKernelGGL((reduce_multi_kernel<1, float>), dim3(grid), dim3(256), 0, s, m, n, head, out);
   else if (g_bf16)

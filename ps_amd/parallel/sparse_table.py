@@ -625,7 +625,11 @@ class ShardedSparseTable:
             ev.record(cur)
             comm.wait_event(ev)
             g.record_stream(comm)
-            plan.rslots.record_stream(comm)
+            if plan.rslots is not None:
+                plan.rslots.record_stream(comm)
+            for v in plan.extra.get("plane", {}).values():  # the row plane's per-round index tensors
+                if isinstance(v, torch.Tensor) and v.is_cuda:
+                    v.record_stream(comm)
             with torch.cuda.stream(comm):
                 self._exchange_grads(plan, g)
                 if apply_now:

@@ -142,7 +142,7 @@ def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0
     n = 64
     lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
     fixed = _batches(1, n, True)[0]
-    losses, dlead, rlead = [], [], []
+    losses, dlead, rlead, skew = [], [], [], []
     for _ in range(steps):
         if tp.rank == delay_rank:
             time.sleep(delay_s)
@@ -151,6 +151,7 @@ def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0
         dlead.append(c[tp.rank] - min(c))
         rc = m.tables()["emF"].clocks()
         rlead.append(rc[tp.rank] - min(rc))
+        skew.append(min(c) - min(rc))  # dense vs row window seen by this worker's next forward
     eng.ps.synchronize()
     for t in m.tables().values():
         t.synchronize()
@@ -161,7 +162,7 @@ def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0
     eng.ps.close()
     for t in m.tables().values():
         t.close()
-    return {"losses": losses, "dlead": dlead, "rlead": rlead, "dense": dense, "probe": probe}
+    return {"losses": losses, "dlead": dlead, "rlead": rlead, "skew": skew, "dense": dense, "probe": probe}
 
 
 @pytest.mark.parametrize("consistency,staleness", [("asp", None), ("ssp", 1)])
@@ -180,3 +181,7 @@ def test_widedeep_async_two_processes_gpu(consistency, staleness):
 def test_ssp1_straggler_bound_dense_and_rows_gpu():
     res = dist_util.run(_wide_gpu_body, 2, ("ssp", 1, 10, 1, 0.15))
     assert max(res[0]["dlead"]) <= 2 and max(res[0]["rlead"]) <= 2, (res[0]["dlead"], res[0]["rlead"])
+    # the dense and the row gates are separate clocks, but both count this worker's steps: the
+    # slowest worker's dense and row clocks seen together never drift more than the bound apart
+    for r in res:
+        assert max(abs(k) for k in r["skew"]) <= 2, r["skew"]  # staleness 1 + one push in flight

@@ -203,7 +203,8 @@ def _bf16_oracle(world, steps, lr=0.05, mom=0.9):
     torch.manual_seed(0)
     net = prepare_for_mi355x(resnet_tiny(num_classes=10, fused_bn=True).cuda())
     params = [(n, p) for n, p in net.named_parameters() if p.requires_grad]
-    master = {n: p.detach().float().clone() for n, p in params}
+    # flat contiguous fp32 masters (conv weights are channels_last; the update is elementwise)
+    master = {n: p.detach().float().contiguous() for n, p in params}
     u = MomentumUpdater(lr, mom, 0.0)
     states = {n: u.new_states(v) for n, v in master.items()}
     bufs = [{n: b.detach().clone() for n, b in net.named_buffers()} for _ in range(world)]
@@ -226,7 +227,7 @@ def _bf16_oracle(world, steps, lr=0.05, mom=0.9):
                     bufs[r][n].copy_(b)
         with torch.no_grad():
             for n, p in params:
-                out = torch.empty_like(p)
+                out = torch.empty(p.shape, dtype=p.dtype, device=p.device)
                 u.step_flat(master[n].view(-1), [s.view(-1) for s in states[n]], gsum[n].view(-1),
                             wout=out.view(-1), gscale=1.0 / world, step=step + 1)
                 p.copy_(out)
