@@ -272,6 +272,8 @@ def main():
         cfg["hip_graph"] = bool(use_graph)
         if getattr(bench.engine, "plane_kind", None) is not None:
             cfg["data_plane"] = bench.engine.plane_kind
+        if getattr(getattr(bench.engine, "plane", None), "info", None) is not None:
+            cfg["plane_info"] = dict(bench.engine.plane.info)
         cfg["final_loss"] = round(float(loss.item()), 4)
         cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         if timed_stats:

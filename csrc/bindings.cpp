@@ -1311,7 +1311,7 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto fopt = a.options().dtype(torch::kFloat32);
   const bool has_pro = pro.has_value() && pro->defined();
   const int G = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
-                                        has_pro || has_bwd, g, resp).gm;
+                                        has_pro || has_bwd, g, resp ? 1 : has_bwd ? 2 : 0).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;

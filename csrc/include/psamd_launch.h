@@ -341,12 +341,25 @@ struct ConvFwdPlan {
 };
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
 // the plan launch_conv_fwd uses for this geometry (the 3x3 patch-staged tiles where they apply)
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, bool resp = false);
+// src2: the launch's two-source prologue (0 none, 1 block output, 2 BN backward)
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2 = 0);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, hipStream_t s);
 
+// n / d for 0 <= n < 2^31 as (umulhi(n, mul) + n) >> shift (d fixed per launch): the wide
+// weight-gradient kernel decodes pixel indices with it instead of two integer divisions per DMA
+// instruction per stage.
+struct FastDiv {
+  uint32_t mul, shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t sh = 0;
+  while (sh < 32 && (uint64_t(1) << sh) < d) ++sh;
+  const uint64_t one = 1;
+  return FastDiv{static_cast<uint32_t>(((one << 32) * ((one << sh) - d)) / d + 1), sh};
+}
 struct ConvWgradArgs {
   const uint16_t* dz;   // [M, N] output gradient rows
   const uint16_t* x;    // [images, H, W, C] input map
@@ -357,6 +370,7 @@ struct ConvWgradArgs {
   uint16_t* dw;         // [N, K] bf16
   float* db;            // nullable: [N] fp32 column sums of dz (a Linear's bias gradient; wide plan only)
   float* dbws;          // [conv_wgrad_splits(...)][N] fp32 scratch when db is set
+  FastDiv fd_ohw, fd_ow;  // set by launch_conv_wgrad (OH * OW, OW)
 };
 int conv_wgrad_splits(int M, int N, int K, int C, bool pro);
 // workspace of launch_conv_wgrad for this geometry (the 3x3 patch kernel's plan where it applies)

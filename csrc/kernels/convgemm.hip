@@ -38,6 +38,7 @@
 // and the BN finalize kernels sum only [2][blocks][N] partials in fixed order.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -82,6 +83,22 @@ __device__ __forceinline__ PixSrc pix_src(int m, int M, const ConvGeo& g) {
     const int ohw = g.OH * g.OW;
     s.img = m / ohw;
     const int r = m - s.img * ohw, oh = r / g.OW;
+    s.ih0 = oh * g.stride - g.pad;
+    s.iw0 = (r - oh * g.OW) * g.stride - g.pad;
+  }
+  return s;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
+
+// pix_src with the two divisions by invariant divisors done as multiply-high + shift
+__device__ __forceinline__ PixSrc pix_src_fd(int m, int M, const ConvGeo& g, const FastDiv& fohw,
+                                            const FastDiv& fow) {
+  PixSrc s{-1, 0, 0};
+  if (m < M) {
+    s.img = static_cast<int>(fdiv(static_cast<uint32_t>(m), fohw));
+    const int r = m - s.img * (g.OH * g.OW);
+    const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(r), fow));
     s.ih0 = oh * g.stride - g.pad;
     s.iw0 = (r - oh * g.OW) * g.stride - g.pad;
   }
@@ -142,6 +159,25 @@ __device__ __forceinline__ bf16x8_t tr_frag_asm(const uint16_t* T, int s, int c0
   return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
 }
 
+// tr_frag with the lane's address precomputed (tr_frag_base) and the k-step / half-row offsets as
+// instruction immediates: no per-fragment address arithmetic inside the MFMA loop.
+template <int RL>
+__device__ __forceinline__ uint32_t tr_frag_base(int c0, int lane) {
+  const int gi = lane >> 4, i16 = lane & 15;
+  const int r = 8 * (gi >> 1) + (i16 >> 2);
+  const int col = c0 + 16 * (gi & 1) + 4 * (i16 & 3);
+  return static_cast<uint32_t>(tr_off<RL>(r, col) * 2);
+}
+template <int RL, int S>
+__device__ __forceinline__ bf16x8_t tr_frag_imm(uint32_t addr) {
+  // rows 16 S + r and 16 S + r + 4 share the lane's swizzle (tr_swz looks at r & 3 / (r >> 1) & 1)
+  constexpr int o0 = S * 16 * RL * 2, o1 = o0 + 4 * RL * 2;
+  s16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "i"(o0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "i"(o1) : "memory");
+  return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+}
+
 __device__ __forceinline__ u16x8 bn_relu8(u16x8 v, const float (&sc)[8], const float (&sh)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -195,8 +231,12 @@ template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, bool PATCH = fa
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr bool BWD = PRO == 2;
   constexpr bool RESP = PRO == 3;
-  static_assert(!BWD || (KS1 && EPI == 3 && !GLDS), "the BN-backward prologue is a 1x1 data-gradient prologue");
-  static_assert(!RESP || (KS1 && EPI <= 1 && !GLDS), "the block-output prologue is a 1x1 forward prologue");
+  static_assert(!BWD || (KS1 && EPI == 3), "the BN-backward prologue is a 1x1 data-gradient prologue");
+  static_assert(!RESP || (KS1 && EPI <= 1), "the block-output prologue is a 1x1 forward prologue");
+  // two-source prologues on the LDS-DMA path: both row sources land in LDS by DMA and one pass
+  // over the stage tile applies the prologue in place (a single third buffer for the second
+  // source: it is refilled once the pass has read it)
+  constexpr bool TWO_GLDS = GLDS && (BWD || RESP);
   constexpr int AR2 = BWD || RESP ? BM / 32 : 1;
   // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce; 9 = 6 + the
   // previous block's downsample-BN sum (third partial slab)
@@ -223,7 +263,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // registers it pushed the register-staged variant from 20 to 76 B/lane of scratch
   constexpr int RED_ELEMS = 4 * NSUM * BN * 2 > (FOLD_DS ? 256 * 8 * 2 : 0) ? 4 * NSUM * BN * 2 : 256 * 8 * 2;
   constexpr int EPI_ELEMS = BM * CS + RED_ELEMS;
-  constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : 2 * BM * kBK;
+  constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : (TWO_GLDS ? 3 : 2) * BM * kBK;
+  constexpr int Z_BASE = 2 * BM * kBK;  // TWO_GLDS: the second source's stage tile
   constexpr int B_BASE = ((A_ELEMS > EPI_ELEMS ? A_ELEMS : EPI_ELEMS) + 7) & ~7;
   constexpr int LDS_ELEMS = B_BASE + 2 * BN * kBK;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
@@ -717,7 +758,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     // 128 B lane-linearly, so the chunk swizzle moves to the SOURCE address (linear destination +
     // swizzled source + swizzled read).  Out-of-map taps / rows past M load the zero page.  Two
     // buffers: issue stage t+1, counted vmcnt for stage t, barrier, MFMAs, barrier.
-    static_assert(!PRO, "the BN prologue needs register staging");
+    static_assert(!PRO || TWO_GLDS, "the one-source BN prologue needs register staging");
     constexpr int AI = BM / 32, BI = BN / 32;  // LDS-DMA instructions per wave per stage
     const int lrow = lane >> 3, lch = lane & 7;
     int64_t gbase[AI];
@@ -767,7 +808,85 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         }
       }
     };
-    if (mg < mtiles) {  // block-uniform
+    if constexpr (TWO_GLDS) {
+      // the second source (BN input z / block residual r) of stage kt into the single Z tile
+      auto issue_z = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          const uint16_t* src = ((gok >> i) & 1u) ? p.a2 + gbase[i] + kt * kBK : kZeroPage;
+          __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + Z_BASE + (wave * AI + i) * 8 * kBK), 16,
+                                           0, 0);
+        }
+      };
+      // one pass over stage kt's A tile: thread t owns LOGICAL chunk t & 7 (fixed channels, one
+      // coefficient load per stage) of rows (t >> 3) + 32 i, at physical chunk swz(r, chunk)
+      const int lc = t & 7, tr0 = t >> 3;
+      const bool store_a = p.aout != nullptr && n0 == 0;
+      auto transform = [&](int kt, int buf) {
+        uint16_t* As = lds + buf * (BM * kBK);
+        const uint16_t* Zs = lds + Z_BASE;
+        const int cc = kt * kBK + lc * 8;
+        float c0[8], c1[8], c2[8], c3[8];
+        if constexpr (BWD) {
+          load8(p.bwd, cc, c0);
+          load8(p.bwd + g.C, cc, c1);
+          load8(p.bwd + 2 * g.C, cc, c2);
+        } else {
+          load8(p.pro, cc, c0);
+          load8(p.pro + g.C, cc, c1);
+        }
+        const bool dual = RESP && p.pro2 != nullptr;  // block-uniform
+        if (dual) {
+          load8(p.pro2, cc, c2);
+          load8(p.pro2 + g.C, cc, c3);
+        }
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {
+          const int r = tr0 + 32 * i, m = mg * BM + r;
+          const int off = r * kBK + swz(r, lc) * 8;
+          u16x8 v = *reinterpret_cast<const u16x8*>(As + off);
+          const u16x8 z8 = *reinterpret_cast<const u16x8*>(Zs + off);
+          unsigned ob = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if constexpr (BWD) {
+              v[j] = f32_to_bf16(c0[j] * bf16_to_f32(v[j]) + c1[j] * bf16_to_f32(z8[j]) + c2[j]);
+            } else {  // the same arithmetic as bn_apply_kernel / bn_apply_dual_kernel
+              float o = bf16_to_f32(v[j]) * c0[j] + c1[j];
+              if (dual) o = o + (bf16_to_f32(z8[j]) * c2[j] + c3[j]);
+              else o += bf16_to_f32(z8[j]);
+              o = o > 0.f ? o : 0.f;
+              ob |= (o > 0.f ? 1u : 0u) << j;
+              v[j] = f32_to_bf16(o);
+            }
+          }
+          const bool ok = m < p.M;
+          if (!ok) v = kZero8;  // rows past M stay zero (the epilogue sums skip them anyway)
+          *reinterpret_cast<u16x8*>(As + off) = v;
+          if (store_a && ok) {
+            const int64_t e = static_cast<int64_t>(m) * g.C + cc;
+            *reinterpret_cast<u16x8*>(p.aout + e) = v;
+            if constexpr (RESP) p.abits[e >> 3] = static_cast<uint8_t>(ob);
+          }
+        }
+      };
+      if (mg < mtiles) {  // block-uniform
+        issue(0, 0);
+        issue_z(0);
+        for (int kt = 0; kt < nk; ++kt) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          lds_barrier();  // stage kt's A, B and Z landed; every wave is done with stage kt - 1
+          if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+          transform(kt, kt & 1);
+          lds_barrier();  // the A tile is transformed and Z is free
+          if (kt + 1 < nk) issue_z(kt + 1);
+          compute(kt & 1);
+        }
+        lds_barrier();  // the output tile overlays the stage buffers
+        epi_load(mg);
+        epilogue(mg);
+      }
+    } else if (mg < mtiles) {  // block-uniform
       issue(0, 0);
       for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) {
@@ -1118,7 +1237,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
 #pragma unroll
       for (int i = 0; i < XI; ++i) {
         const int m = mc + xrow[i];
-        const PixSrc ps = pix_src(m < me ? m : p.M, p.M, g);
+        const PixSrc ps = pix_src_fd(m < me ? m : p.M, p.M, g, p.fd_ohw, p.fd_ow);
         const int64_t o = tap_off(ps, xkh[i], xkw[i], xcc[i], g);
         const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
         __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
@@ -1143,16 +1262,23 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
     for (int j = 0; j < TK; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  auto mma = [&](int buf) {
-    const uint16_t* Gs = lds + buf * STAGE;
-    const uint16_t* Xs = Gs + kWP * BNO;
+  // per-lane fragment addresses (bytes from the stage base), computed once
+  uint32_t gfo[TN], xfo[TK];
 #pragma unroll
-    for (int s = 0; s < kWP / 16; ++s) {
+  for (int i = 0; i < TN; ++i) gfo[i] = tr_frag_base<BNO>(wn + 32 * i, lane);
+#pragma unroll
+  for (int j = 0; j < TK; ++j) xfo[j] = tr_frag_base<BKO>(wk + 32 * j, lane) + kWP * BNO * 2;
+  const uint32_t lds_u32 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lptr_t*)lds));
+  static_assert(kWP == 32, "two k-steps per stage");
+  auto mma = [&](int buf) {
+    const uint32_t sb = lds_u32 + static_cast<uint32_t>(buf * STAGE * 2);
+    auto kstep = [&](auto SC) {
+      constexpr int s = decltype(SC)::value;
       bf16x8_t ga[TN], xb[TK];
 #pragma unroll
-      for (int i = 0; i < TN; ++i) ga[i] = tr_frag_asm<BNO>(Gs, s, wn + 32 * i, lane);
+      for (int i = 0; i < TN; ++i) ga[i] = tr_frag_imm<BNO, s>(sb + gfo[i]);
 #pragma unroll
-      for (int j = 0; j < TK; ++j) xb[j] = tr_frag_asm<BKO>(Xs, s, wk + 32 * j, lane);
+      for (int j = 0; j < TK; ++j) xb[j] = tr_frag_imm<BKO, s>(sb + xfo[j]);
 #pragma unroll
       for (int i = 0; i < TN; ++i) asm volatile("" : "+v"(ga[i]));
 #pragma unroll
@@ -1179,7 +1305,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
 #pragma unroll
         for (int j = 0; j < TK; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i], xb[j], acc[i][j], 0, 0, 0);
-    }
+    };
+    kstep(std::integral_constant<int, 0>{});
+    kstep(std::integral_constant<int, 1>{});
   };
 
   // DB: the blocks of k-tile 0 also sum the staged dz tile's columns (bias gradient): thread t
@@ -1525,8 +1653,26 @@ bool patch_fwd_ok(const ConvGeo& g, int N, bool pro) {
   return 8 * plane <= (bn == 64 ? patch_bytes<64>() : patch_bytes<128>());
 }
 
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, bool resp) {
-  if (resp) {  // block-output prologue: 64-channel tiles (128 x 128 with two row sources spilled)
+int twosrc_glds_min_nk() {
+  static const int v = [] {
+    const char* e = std::getenv("PS_AMD_TWOSRC_GLDS_MIN_NK");
+    return e ? std::atoi(e) : 4;  // K >= 256 (profiles/r4_twosrc_probe.txt: LDS-DMA ahead at every K)
+  }();
+  return v;
+}
+
+// src2: two-source prologue of the launch (0 none, 1 block output, 2 BN backward)
+bool twosrc_glds(int K, int src2) { return src2 != 0 && K / kBK >= twosrc_glds_min_nk(); }
+
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2) {
+  if (twosrc_glds(K, src2)) {  // LDS-DMA two-source prologue: one 128-pixel tile per block
+    ConvFwdPlan pl;
+    pl.bm = 128;
+    pl.bn = N % 128 == 0 ? 128 : 64;
+    pl.gm = (M + 127) / 128;
+    return pl;
+  }
+  if (src2 == 1) {  // block-output prologue: 64-channel tiles (128 x 128 with two row sources spilled)
     ConvFwdPlan pl = conv_fwd_plan(M, N, K, true);
     pl.bn = 64;
     if (pl.gm != (M + 127) / 128) pl.gm = std::max(1, std::min((M + 127) / 128, 512 / (N / 64)));
@@ -1565,9 +1711,25 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const bool bwd = a.bwd != nullptr;
   const bool resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
-  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, resp);
+  const int src2 = resp ? 1 : bwd ? 2 : 0;
+  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
+  if (twosrc_glds(a.K, src2)) {  // (1x1: the binding checks)
+#define PSAMD_CF2S(BN, PRO, EPI) \
+  hipLaunchKernelGGL((conv_fwd_kernel<128, BN, PRO, EPI, true, true>), dim3(nblk), dim3(256), 0, s, a, GM)
+    if (resp) {
+      if (pl.bn == 128) {
+        if (a.epi == 1) { PSAMD_CF2S(128, 3, 1); } else { PSAMD_CF2S(128, 3, 0); }
+      } else {
+        if (a.epi == 1) { PSAMD_CF2S(64, 3, 1); } else { PSAMD_CF2S(64, 3, 0); }
+      }
+    } else {
+      if (pl.bn == 128) { PSAMD_CF2S(128, 2, 3); } else { PSAMD_CF2S(64, 2, 3); }
+    }
+#undef PSAMD_CF2S
+    return;
+  }
   if (!bwd && patch_fwd_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
 #define PSAMD_CFP(BN, EPI) \
   hipLaunchKernelGGL((conv_fwd_kernel<128, BN, 0, EPI, false, true, true>), dim3(nblk), dim3(256), 0, s, a, GM)
@@ -1778,8 +1940,11 @@ int64_t conv_wgrad_ws(int M, int N, int K, int C, bool pro) {
   return static_cast<int64_t>(w.nsplit + w.groups) * N * K;
 }
 
-void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t s) {
-  if (a.M <= 0) return;
+void launch_conv_wgrad(const ConvWgradArgs& a0, hipStream_t s) {
+  if (a0.M <= 0) return;
+  ConvWgradArgs a = a0;
+  a.fd_ohw = make_fastdiv(static_cast<uint32_t>(a.g.OH * a.g.OW));
+  a.fd_ow = make_fastdiv(static_cast<uint32_t>(a.g.OW));
   if (a.db == nullptr && patch_ok(a.g, a.M, a.N, a.pro != nullptr)) {
     const PPlan w = pplan(a.g, a.M, a.N);
     const int nblk = w.tiles * w.nsplit;

@@ -19,7 +19,7 @@ import torch.nn as nn
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
 from ..ops.convgemm import (deferred_bn_counters, flush_deferred, fused_block_ok, fused_bottleneck,
-                             prepare_backward_weights)
+                             prepare_backward_weights, resp_consumer_ok)
 from ..ops.pool import MaxPool2d, global_avg_pool
 
 
@@ -112,8 +112,10 @@ class ResNet(nn.Module):
                 blks = self._blocks()
                 prepare_backward_weights(blks)  # all data-grad weight layouts, one kernel
                 # a block followed by a fused block leaves its output to that block's conv1 prologue
+                # where that pays (ops/convgemm.py resp_consumer_ok)
+                on = os.environ.get("PS_AMD_RESP", "1") != "0"
                 for a, b in zip(blks, blks[1:] + [None]):
-                    a._defer_out = b is not None and b.fuse_block and os.environ.get("PS_AMD_RESP", "1") != "0"
+                    a._defer_out = on and b is not None and b.fuse_block and resp_consumer_ok(b)
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.fused_bn:
             x = global_avg_pool(x)  # NHWC gradient straight into the last block's backward

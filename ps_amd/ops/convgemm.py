@@ -212,10 +212,25 @@ class _Deferred:
 
 def _resp_enabled(c: int) -> bool:
     """Block outputs of up to PS_AMD_RESP_MAX_C channels (0: never) are applied in the consumer's
-    conv1 prologue.  The prologue stages A through registers from two row sources, so it pays
-    where conv1's K is short (256 = the layer-1 outputs, 4 K-stages); deeper K keeps the apply
-    pass + the LDS-DMA GEMM."""
-    return c <= int(os.environ.get("PS_AMD_RESP_MAX_C", "256"))
+    conv1 prologue (which consumers take it: models/resnet.py ResNet.forward, resp_consumer_ok)."""
+    return c <= int(os.environ.get("PS_AMD_RESP_MAX_C", "4096"))
+
+
+def twosrc_glds_min_nk() -> int:
+    """Mirror of csrc convgemm.hip twosrc_glds_min_nk: two-source prologues with K >= 64 x this run
+    on the LDS-DMA variant."""
+    return int(os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4"))
+
+
+def resp_consumer_ok(blk: nn.Module) -> bool:
+    """Whether the block-output prologue pays on ``blk``'s conv1: with one channel tile (N <= 128,
+    _twosrc_max_n) -- the layer-1 and layer-2 blocks and the layer-1 -> 2 boundary (LDS-DMA
+    variant: 1.01 vs 1.21 ms at 256 -> 64 channels, 0.53 vs 0.62 ms at 512 -> 128); with two or
+    more tiles each re-reads both sources and the apply pass + plain GEMM is faster
+    (profiles/r4_twosrc_probe.txt)."""
+    c1 = blk.conv1
+    return c1.out_channels <= _twosrc_max_n() and (
+        c1.in_channels >= 64 * twosrc_glds_min_nk() or c1.out_channels <= 64)
 
 
 def flush_deferred() -> None:
@@ -226,14 +241,22 @@ def flush_deferred() -> None:
         pend.flush()
 
 
-def _bwd_prologue_enabled(c3: int) -> bool:
+def _twosrc_max_n() -> int:
+    """Two-source prologues pay while the GEMM has ONE channel tile (N <= 128): every further tile
+    re-reads both row sources (scripts/probe_twosrc.py, profiles/r4_twosrc_probe.txt: conv3 data
+    grad 0.51 vs 0.64 ms at N = 128, 0.36 vs 0.25 ms at N = 512)."""
+    return int(os.environ.get("PS_AMD_TWOSRC_MAX_N", "128"))
+
+
+def _bwd_prologue_enabled(c3: int, n: int = 0) -> bool:
     """bn3 backward applied in the conv3 data-gradient prologue, up to PS_AMD_BN_BWD_PROLOGUE_MAX_C
-    bn3 channels (0: never, the separate apply pass).  The prologue stages A through registers
-    from TWO row sources: at 256 channels (4 K-stages, persistent grid) it replaces the apply pass
-    + the LDS-DMA GEMM (1.29 -> 1.05-1.08 ms per layer-1 block); at 512-2048 channels the
-    register-staged deep-K GEMM is 2-6x slower than apply + LDS-DMA GEMM
-    (profiles/r3_bn_bwd_prologue_ab.txt)."""
-    return c3 <= int(os.environ.get("PS_AMD_BN_BWD_PROLOGUE_MAX_C", "256"))
+    bn3 channels (0: never, the separate apply pass).  At 256 channels (4 K-stages, persistent
+    grid) the prologue stages A through registers from TWO row sources and replaces the apply
+    pass + the LDS-DMA GEMM (1.29 -> 1.05-1.08 ms per layer-1 block); deeper K (512-2048
+    channels, where the register-staged GEMM was 2-6x slower: profiles/r3_bn_bwd_prologue_ab.txt)
+    runs the LDS-DMA two-source variant: both row sources land in LDS by DMA and one in-place pass
+    per stage applies the BN backward (csrc convgemm.hip TWO_GLDS, scripts/probe_twosrc.py)."""
+    return c3 <= int(os.environ.get("PS_AMD_BN_BWD_PROLOGUE_MAX_C", "4096")) and n <= _twosrc_max_n()
 
 
 def _fold_enabled() -> bool:
@@ -328,7 +351,7 @@ class _BottleneckFn(torch.autograd.Function):
                 ds_part = torch.stack([lk.part[0], lk.part[2]])
                 lk.part = lk.part[:2]
                 FOLD_STATS["ds"] += 1
-            if _bwd_prologue_enabled(z3.shape[1]):
+            if _bwd_prologue_enabled(z3.shape[1], w3.shape[1]):
                 # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
                 # the weight gradient: no separate apply pass over the widest tensors
                 dg3, db3, cb3 = nat.bn_bwd_coef(lk.part, g3, m3, i3, d2.shape[0])

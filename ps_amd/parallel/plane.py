@@ -128,6 +128,9 @@ class XgmiPlane:
         self._arena = None
         self._seg = None
         self._ctl = None
+        # what the bench JSON reports at N > 1: mapping mode, self-test result, round-end mechanism
+        self.info: Dict[str, str] = {"mode": "threads" if self.threads else "shm (cpu)", "self_test": "skipped",
+                                     "round_end": "host flags"}
         self._tmp_engine = None
         self._opened: List[_ShmSeg] = []
         if self.gpu:
@@ -152,6 +155,9 @@ class XgmiPlane:
             self._agree(err is None, f"mapping the peer arenas failed: {err!r}")
             self.bases = bases
             self.peers = None
+            devs = sorted({d for _, d in hs})
+            self.info["mode"] = "threads (shared device pointers)" if self.threads else (
+                "ipc, one device" if len(devs) == 1 else f"ipc, peer access across {len(devs)} devices")
         else:
             if self.threads:
                 self.arena = torch.zeros(self.nbytes, dtype=torch.uint8)
@@ -192,6 +198,7 @@ class XgmiPlane:
             except Exception as e:  # noqa: BLE001
                 err = e
             self._agree(err is None, f"self-test failed: {err!r}")
+            self.info["self_test"] = "ok (2 probe round trips through every peer arena)"
 
     def _agree(self, ok: bool, what: str) -> None:
         oks = self.t.all_gather_object(bool(ok))
@@ -268,6 +275,7 @@ class XgmiPlane:
         if self.ipc_events:
             hs = eng.ipc_event_handles(self.nslots + 1)
             eng.enable_ipc_events(self.t.all_gather_object(list(hs)))
+            self.info["round_end"] = "ipc events (serve published at enqueue)"
         self.engine = eng
         self._tmp_engine = None
         eng.start()

@@ -1,0 +1,92 @@
+"""Two-source prologues on the ResNet-50 bs1024 shapes: the BN-backward prologue of the conv3
+data gradient (epi 3) and the block-output prologue of conv1 (epi 1), each against the separate
+apply pass + plain GEMM it replaces.  Which two-source variant runs (register-staged or
+LDS-DMA) is fixed per process by PS_AMD_TWOSRC_GLDS_MIN_NK, so run this once per setting:
+
+    PS_AMD_TWOSRC_GLDS_MIN_NK=99 python scripts/probe_twosrc.py   # register-staged everywhere
+    PS_AMD_TWOSRC_GLDS_MIN_NK=4  python scripts/probe_twosrc.py   # LDS-DMA from K = 256
+
+One JSON line per shape: ms of the fused launch and of apply + GEMM (median of 3 x 10 runs)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ps_amd.ops._ext import native  # noqa: E402
+
+nat = native()
+dev = torch.device("cuda")
+MIN_NK = os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "5")
+
+
+def timed(fn, reps=10):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) / reps)
+    return sorted(ts)[1]
+
+
+def rnd(*s, scale=1.0):
+    return (torch.randn(*s, device=dev) * scale).bfloat16()
+
+
+def coef(k):
+    return torch.cat([torch.rand(k, device=dev) + 0.5, torch.randn(k, device=dev) * 0.5])
+
+
+def bwd_case(M, K, N):
+    g, z, z2 = rnd(M, K), rnd(M, K), rnd(M, N)
+    w = rnd(N, K, scale=K ** -0.5)
+    gamma, mean, invstd = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1, torch.rand(K, device=dev) + 0.5
+    part = torch.randn(2, 1, K, device=dev)
+    mc, m2, i2 = coef(N), torch.randn(N, device=dev) * 0.1, torch.rand(N, device=dev) + 0.5
+    geo = [M, 1, M, 1, 1, 1, 0]
+    _, _, cf = nat.bn_bwd_coef(part, gamma, mean, invstd, M)
+
+    def fused():
+        nat.conv_gemm(g, w, geo, None, 3, z2, None, mc, m2, i2, a2=z, bwd=cf)
+
+    def split():
+        dz = nat.bn_bwd_partials(g, z, part, gamma, mean, invstd)[0]
+        nat.conv_gemm(dz, w, geo, None, 3, z2, None, mc, m2, i2)
+
+    return timed(fused), timed(split)
+
+
+def resp_case(M, K, N):
+    z3, r = rnd(M, K), rnd(M, K)
+    cf, ks = coef(K), torch.randn(N, device=dev) * 0.1
+    w = rnd(N, K, scale=K ** -0.5)
+    y = torch.empty_like(z3)
+    bits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev)
+    geo = [M, 1, M, 1, 1, 1, 0]
+
+    def fused():
+        nat.conv_gemm(z3, w, geo, cf, 1, None, ks, a2=r, aout=y, abits=bits)
+
+    def split():
+        yy = nat.bn_apply_coef(z3, cf, r, None, 1, True)[0]
+        nat.conv_gemm(yy, w, geo, None, 1, None, ks)
+
+    return timed(fused), timed(split)
+
+
+BWD = [(3211264, 256, 64), (802816, 512, 128), (200704, 1024, 256), (50176, 2048, 512)]
+RESP = [(3211264, 256, 64), (3211264, 256, 128), (802816, 512, 128), (802816, 512, 256), (200704, 1024, 256),
+        (200704, 1024, 512), (50176, 2048, 512)]
+for kind, shapes, fn in (("bn_bwd_prologue", BWD, bwd_case), ("block_output_prologue", RESP, resp_case)):
+    for M, K, N in shapes:
+        f, s = fn(M, K, N)
+        print(json.dumps({"kind": kind, "M": M, "K": K, "N": N, "min_nk": MIN_NK, "fused_ms": round(f, 4),
+                          "apply_plus_gemm_ms": round(s, 4)}), flush=True)
+        torch.cuda.empty_cache()

@@ -103,7 +103,8 @@ def test_conv1x1_bn_backward_epilogue(M, K, N):
     torch.testing.assert_close(part[1].sum(0).cpu(), (cg * ((z - mean) * invstd)).sum(0), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("M,K,N", [(300, 256, 64), (1000, 512, 128), (4099, 256, 64), (517, 1024, 256)])
+@pytest.mark.parametrize("M,K,N", [(300, 256, 64), (1000, 512, 128), (4099, 256, 64), (517, 1024, 256),
+                                   (333, 2048, 512)])
 def test_bn_backward_prologue_matches_apply_then_gemm(M, K, N):
     """conv_gemm(a=d, a2=z, bwd=coef) == bn_bwd_partials(d, z) then conv_gemm on its output: the
     data gradient of the previous BN computed while staging A (and stored as a third output),
@@ -423,8 +424,8 @@ def test_fold_epilogues_previous_block_bn3_reduce(epi, K):
     torch.testing.assert_close(part[1].sum(0).cpu(), (gc * (z3 - mean) * invstd).sum(0), rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("extra_consumer", [False, True])
-def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
+@pytest.mark.parametrize("extra_consumer,wide", [(False, False), (True, False), (False, True)])
+def test_chained_blocks_fold_bn3_backward(extra_consumer, wide, monkeypatch):
     """Three fused bottlenecks (downsample first) inside the ResNet forward context: block i's
     conv1 data-grad epilogue reduces block i-1's bn3 backward.  Checked against the same fused
     chain with the fold disabled (PS_AMD_FOLD_BN3=0: every block runs its own reduce pass).
@@ -437,16 +438,18 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, monkeypatch):
     from ps_amd.ops.bn import BatchNormAct2d
 
     torch.manual_seed(1)
-    ds = nn.Sequential(nn.Conv2d(128, 256, 1, stride=2, bias=False), BatchNormAct2d(256, act="none"))
-    a = nn.Sequential(Bottleneck(128, 64, 2, ds), Bottleneck(256, 64), Bottleneck(256, 64))
+    # wide: 1024-channel block outputs -- the deep-K (LDS-DMA) two-source prologues
+    cin, pl = (512, 256) if wide else (128, 64)
+    ds = nn.Sequential(nn.Conv2d(cin, 4 * pl, 1, stride=2, bias=False), BatchNormAct2d(4 * pl, act="none"))
+    a = nn.Sequential(Bottleneck(cin, pl, 2, ds), Bottleneck(4 * pl, pl), Bottleneck(4 * pl, pl))
     for m in a.modules():
         if isinstance(m, nn.BatchNorm2d):
             nn.init.uniform_(m.weight, 0.5, 1.5)
             nn.init.uniform_(m.bias, -0.2, 0.2)
     a = prepare_for_mi355x(a.cuda())
-    x = torch.randn(4, 128, 17, 17, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
-    gw = torch.randn(4, 256, 9, 9, device=DEV)
-    gw1 = torch.randn(4, 256, 9, 9, device=DEV)
+    x = torch.randn(4, cin, 17, 17, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gw = torch.randn(4, 4 * pl, 9, 9, device=DEV)
+    gw1 = torch.randn(4, 4 * pl, 9, 9, device=DEV)
     state = copy.deepcopy(a.state_dict())
 
     def run(defer=False):
@@ -649,12 +652,14 @@ def test_epilogue9_downsample_bn_sum(M, K, N):
 
 
 @pytest.mark.parametrize("M,C,N,dual", [(300, 256, 64, False), (4099, 256, 128, True), (1000, 64, 64, False),
-                                        (517, 512, 256, True)])
+                                        (517, 512, 256, True), (700, 1024, 128, False), (129, 2048, 512, False)])
 def test_block_output_prologue_matches_apply_then_gemm(M, C, N, dual):
     """conv_gemm(z3, pro=bn3 coef, a2=r[, pro2=downsample coef], aout, abits) == bn_apply_coef
     (the block output relu(bn3(z3) + r) and its ReLU bits) then conv_gemm on that output with
     the BN-statistics epilogue: the consumer block's conv1 applies the previous block's output
-    while staging A and stores it (rows + bits) for the residual and the backward."""
+    while staging A and stores it (rows + bits) for the residual and the backward.  K >= 320 runs
+    the LDS-DMA two-source variant (both row sources DMA'd, one in-place pass per stage), below
+    the register-staged one."""
     g = _gen(M + C + N)
     z3, r = _rnd(M, C, g=g), _rnd(M, C, g=g)
     cf3 = _coef(C, g).to(DEV)
