@@ -298,6 +298,18 @@ struct ConvGeo {
   int RH, RW, ra, rb;  // RH > 0: output pixel (i, oh, ow) lands at row (i, 2 oh + ra, 2 ow + rb) of an
                        // RH x RW map (one phase of a stride-2 data gradient); 0: rows in order
 };
+// n / d for 0 <= n < 2^31 as (umulhi(n, mul) + n) >> shift (d fixed per launch): the wide
+// weight-gradient kernel decodes pixel indices with it instead of two integer divisions per DMA
+// instruction per stage.
+struct FastDiv {
+  uint32_t mul, shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t sh = 0;
+  while (sh < 32 && (uint64_t(1) << sh) < d) ++sh;
+  const uint64_t one = 1;
+  return FastDiv{static_cast<uint32_t>(((one << 32) * ((one << sh) - d)) / d + 1), sh};
+}
 struct ConvGemmArgs {
   const uint16_t* a;    // [images, H, W, C] bf16
   const uint16_t* b;    // [N, K] bf16, K = ks * ks * C
@@ -335,6 +347,7 @@ struct ConvGemmArgs {
   // downsample BN's [sc2 | sh2]); the block output goes to aout, its ReLU bits to abits [M C / 8]
   const float* pro2;    // [2C]; nullable
   uint8_t* abits;
+  FastDiv fd_ohw, fd_ow;  // set by launch_conv_fwd (OH * OW, OW)
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
@@ -348,18 +361,6 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, hipStream_t s);
 
-// n / d for 0 <= n < 2^31 as (umulhi(n, mul) + n) >> shift (d fixed per launch): the wide
-// weight-gradient kernel decodes pixel indices with it instead of two integer divisions per DMA
-// instruction per stage.
-struct FastDiv {
-  uint32_t mul, shift;
-};
-inline FastDiv make_fastdiv(uint32_t d) {
-  uint32_t sh = 0;
-  while (sh < 32 && (uint64_t(1) << sh) < d) ++sh;
-  const uint64_t one = 1;
-  return FastDiv{static_cast<uint32_t>(((one << 32) * ((one << sh) - d)) / d + 1), sh};
-}
 struct ConvWgradArgs {
   const uint16_t* dz;   // [M, N] output gradient rows
   const uint16_t* x;    // [images, H, W, C] input map

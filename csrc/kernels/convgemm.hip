@@ -270,7 +270,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
   const ConvGeo& g = p.g;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave id through readfirstlane: provably uniform, so LDS-DMA destinations (M0) and other
+  // per-wave addresses stay in SGPRs instead of VALU + v_readfirstlane per instruction
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nN = p.N / BN, mtiles = (p.M + BM - 1) / BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int mg = L / nN, n0 = (L - mg * nN) * BN;
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     rok = 0;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const PixSrc ps = pix_src(mt * BM + srow + 32 * i, p.M, g);
+      const PixSrc ps = pix_src_fd(mt * BM + srow + 32 * i, p.M, g, p.fd_ohw, p.fd_ow);
       rok |= (ps.img >= 0 ? 1u : 0u) << i;
       rih[i] = ps.ih0;
       riw[i] = ps.iw0;
@@ -470,7 +472,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // destination row of output pixel m (a stride-2 data-gradient phase scatters to every other row)
   auto orow = [&](int m) -> int64_t {
     if (g.RH == 0) return m;
-    const int ohw = g.OH * g.OW, im = m / ohw, r = m - im * ohw, i = r / g.OW, j = r - i * g.OW;
+    const int ohw = g.OH * g.OW, im = static_cast<int>(fdiv(static_cast<uint32_t>(m), p.fd_ohw)), r = m - im * ohw,
+              i = static_cast<int>(fdiv(static_cast<uint32_t>(r), p.fd_ow)), j = r - i * g.OW;
     return (static_cast<int64_t>(im) * g.RH + 2 * i + g.ra) * g.RW + 2 * j + g.rb;
   };
   constexpr bool RD_AUX = BASE == 5 || BASE == 2 || BASE == 4 || EPI == 3;
@@ -486,7 +489,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       const int64_t o = orow(m) * p.N + nc;
       if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
         const int ohw = g.OH * g.OW;
-        const int im = m / ohw, r = m - im * ohw, h = r / g.OW, w = r - h * g.OW;
+        const int im = static_cast<int>(fdiv(static_cast<uint32_t>(m), p.fd_ohw)), r = m - im * ohw,
+                  h = static_cast<int>(fdiv(static_cast<uint32_t>(r), p.fd_ow)), w = r - h * g.OW;
         const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
         ra[i] = kZero8;
         rodd |= static_cast<unsigned>((h | w) & 1) << i;
@@ -664,7 +668,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         const int m = m0 + wm + 32 * j + fr;
         int sl = 0;
         if (m < p.M) {
-          const int im = m / ohw, r = m - im * ohw, oh = r / g.OW, ow = r - oh * g.OW;
+          const int im = static_cast<int>(fdiv(static_cast<uint32_t>(m), p.fd_ohw)), r = m - im * ohw,
+                    oh = static_cast<int>(fdiv(static_cast<uint32_t>(r), p.fd_ow)), ow = r - oh * g.OW;
           sl = (im == img0 ? oh - oh0 : nA + oh) * PW + ow;
         }
         abase[j] = static_cast<uint32_t>(fh * PLB + sl * 16);  // bytes from the LDS base
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int r = (wave * AI + i) * 8 + lrow;
-      const PixSrc ps = pix_src(mg * BM + r, p.M, g);
+      const PixSrc ps = pix_src_fd(mg * BM + r, p.M, g, p.fd_ohw, p.fd_ow);
       gok |= (ps.img >= 0 ? 1u : 0u) << i;
       gih[i] = ps.ih0;
       giw[i] = ps.iw0;
@@ -784,15 +789,19 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     auto issue = [&](int kt, int buf) {
       uint16_t* As = lds + buf * (BM * kBK);
       uint16_t* Bs = lds + B_BASE + buf * (BN * kBK);
-      const int64_t toff = KS1 ? qcc : static_cast<int64_t>(qkh * g.W + qkw) * g.C + qcc;
+      // the cursor is wave-uniform; readfirstlane lets the compiler keep it (and the tap offset) in
+      // SGPRs: one 64-bit VALU add per instruction below
+      const int ukh = __builtin_amdgcn_readfirstlane(qkh), ukw = __builtin_amdgcn_readfirstlane(qkw);
+      const int toff = __builtin_amdgcn_readfirstlane(KS1 ? qcc : (ukh * g.W + ukw) * g.C + qcc);
+      const uint16_t* abase = p.a + toff;
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         bool v = (gok >> i) & 1u;
         if constexpr (!KS1) {
-          v = v && static_cast<unsigned>(gih[i] + qkh) < static_cast<unsigned>(g.H) &&
-              static_cast<unsigned>(giw[i] + qkw) < static_cast<unsigned>(g.W);
+          v = v && static_cast<unsigned>(gih[i] + ukh) < static_cast<unsigned>(g.H) &&
+              static_cast<unsigned>(giw[i] + ukw) < static_cast<unsigned>(g.W);
         }
-        const uint16_t* src = v ? p.a + gbase[i] + toff : kZeroPage;
+        const uint16_t* src = v ? abase + gbase[i] : kZeroPage;
         __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(As + (wave * AI + i) * 8 * kBK), 16, 0, 0);
       }
 #pragma unroll
@@ -811,9 +820,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     if constexpr (TWO_GLDS) {
       // the second source (BN input z / block residual r) of stage kt into the single Z tile
       auto issue_z = [&](int kt) {
+        const uint16_t* zbase = p.a2 + kt * kBK;
 #pragma unroll
         for (int i = 0; i < AI; ++i) {
-          const uint16_t* src = ((gok >> i) & 1u) ? p.a2 + gbase[i] + kt * kBK : kZeroPage;
+          const uint16_t* src = ((gok >> i) & 1u) ? zbase + gbase[i] : kZeroPage;
           __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + Z_BASE + (wave * AI + i) * 8 * kBK), 16,
                                            0, 0);
         }
@@ -971,7 +981,9 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STAGE];
 
   const ConvGeo& g = p.g;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave id through readfirstlane: provably uniform, so LDS-DMA destinations (M0) and other
+  // per-wave addresses stay in SGPRs instead of VALU + v_readfirstlane per instruction
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int ntk = p.K / BKO, tiles = (p.N / BNO) * ntk;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L / tiles, tile = L - split * tiles;
@@ -999,7 +1011,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
 #pragma unroll
     for (int i = 0; i < XIT; ++i) {
       const int r = (t + 256 * i) / XCPR;
-      const PixSrc s = pix_src(mc + r < me ? mc + r : p.M, p.M, g);
+      const PixSrc s = pix_src_fd(mc + r < me ? mc + r : p.M, p.M, g, p.fd_ohw, p.fd_ow);
       const int64_t o = tap_off(s, kh, kw, cc0 + xc * 8, g);
       xok |= (o >= 0 ? 1u : 0u) << i;
       rx[i] = *reinterpret_cast<const u16x8*>(p.x + (o >= 0 ? o : 0));
@@ -1070,7 +1082,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
       for (int i = 0; i < XI; ++i) {
         const int L = (wave * XI + i) * 64 + lane, r = L / XCPR, pc = L % XCPR;
         const int lc = BKO == 128 ? (pc ^ ((r & 3) << 2)) : (pc ^ (((r >> 1) & 1) << 2));
-        const PixSrc ps = pix_src(mc + r < me ? mc + r : p.M, p.M, g);
+        const PixSrc ps = pix_src_fd(mc + r < me ? mc + r : p.M, p.M, g, p.fd_ohw, p.fd_ow);
         const int64_t o = tap_off(ps, kh, kw, cc0 + lc * 8, g);
         const uint16_t* src = o >= 0 ? p.x + o : kZeroPage;
         __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(Xs + (wave * XI + i) * 512), 16, 0, 0);
@@ -1168,9 +1180,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int TN, int TK, int WN, int WK, bool PRO, bool DB = false, bool LIN = false>
+// PROL (with PRO, 1x1, BKO 128 / 256): the prologue runs as one in-place pass over each staged X
+// tile (16 elements per thread per stage) instead of on the X fragments in registers, where each
+// of the WN waves sharing a k-column re-transformed it (17-20 VALU per MFMA:
+// profiles/r3_resnet50_pmc_ranked_final.txt).
+template <int TN, int TK, int WN, int WK, bool PRO, bool DB = false, bool LIN = false, bool PROL = false>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgradArgs p, int rows_per_split) {
   constexpr int BNO = WN * 32 * TN, BKO = WK * 32 * TK;
+  static_assert(!PROL || (PRO && (BKO == 128 || BKO == 256)), "LDS-pass prologue: 16-B chunks tile 512 threads");
   static_assert(WN * WK == 8, "8 waves");
   constexpr int STAGE = kWP * (BNO + BKO);
   constexpr int GCPR = BNO / 8, XCPR = BKO / 8;                // 16-B chunks per tile row
@@ -1180,7 +1197,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
   __shared__ __attribute__((aligned(16))) uint16_t lds[kWS * STAGE];
 
   const ConvGeo& g = p.g;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave id through readfirstlane: provably uniform, so LDS-DMA destinations (M0) and other
+  // per-wave addresses stay in SGPRs instead of VALU + v_readfirstlane per instruction
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int ntk = p.K / BKO, tiles = (p.N / BNO) * ntk;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L / tiles, tile = L - split * tiles;
@@ -1288,7 +1307,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
       for (int i = 0; i < TN; ++i) asm volatile("" : "+v"(ga[i]));
 #pragma unroll
       for (int j = 0; j < TK; ++j) asm volatile("" : "+v"(xb[j]));
-      if constexpr (PRO) {
+      if constexpr (PRO && !PROL) {
 #pragma unroll
         for (int j = 0; j < TK; ++j) {
           u16x8 v = __builtin_bit_cast(u16x8, xb[j]);
@@ -1315,6 +1334,32 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
   const bool dbt = DB && (tile % ntk) == 0;  // block-uniform
   constexpr int DBR = 512 / GCPR;            // threads per column chunk
   float dbacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // PROL: thread t owns logical X chunk t % XCPR (8 channels, coefficients held in registers) of
+  // rows t / XCPR + (512 / XCPR) i -- same swizzle (r & 3) for all of them
+  constexpr int XROWS = PROL ? 512 / XCPR : 1, XPT = PROL ? kWP / XROWS : 1;
+  float lsc[PROL ? 8 : 1], lsh[PROL ? 8 : 1];
+  const int xlc = t % XCPR, xr0 = t / XCPR;
+  if constexpr (PROL) {
+    load8(p.pro, k0 + xlc * 8, lsc);
+    load8(p.pro + g.C, k0 + xlc * 8, lsh);
+  }
+  auto xform = [&](int buf) {
+    if constexpr (PROL) {
+      uint16_t* Xs = lds + buf * STAGE + kWP * BNO;
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int r = xr0 + XROWS * i;
+        uint16_t* q = Xs + r * BKO + ((xlc ^ tr_swz<BKO>(r)) << 3);
+        u16x8 v = *reinterpret_cast<const u16x8*>(q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf16_to_f32(v[e]) * lsc[e] + lsh[e];
+          v[e] = f32_to_bf16(f > 0.f ? f : 0.f);
+        }
+        *reinterpret_cast<u16x8*>(q) = v;
+      }
+    }
+  };
   const int pre = nst < kWS - 1 ? nst : kWS - 1;
   for (int st = 0; st < pre; ++st) issue(st, st);
   for (int st = 0; st < nst; ++st) {
@@ -1325,6 +1370,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
     else wait_vmcnt<0>();
     lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
     if (st + kWS - 1 < nst) issue(st + kWS - 1, (st + kWS - 1) % kWS);
+    if constexpr (PROL) {
+      xform(st % kWS);
+      lds_barrier();  // the transformed X tile is visible to every wave
+    }
     if constexpr (DB) {
       if (dbt) {
         const uint16_t* Gs = lds + (st % kWS) * STAGE;
@@ -1415,7 +1464,9 @@ __global__ __launch_bounds__(768, 1) void conv_wgrad_patch_kernel(const ConvWgra
   __shared__ __attribute__((aligned(16))) uint16_t lds[KPS * STB / 2];
 
   const ConvGeo& g = p.g;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave id through readfirstlane: provably uniform, so LDS-DMA destinations (M0) and other
+  // per-wave addresses stay in SGPRs instead of VALU + v_readfirstlane per instruction
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nct = g.C / 64, tiles = (p.N / 64) * nct;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L / tiles, tile = L - split * tiles;
@@ -1707,8 +1758,11 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   return pl;
 }
 
-void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s) {
-  if (a.M <= 0) return;
+void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
+  if (a0.M <= 0) return;
+  ConvGemmArgs a = a0;
+  a.fd_ohw = make_fastdiv(static_cast<uint32_t>(a.g.OH * a.g.OW));
+  a.fd_ow = make_fastdiv(static_cast<uint32_t>(a.g.OW));
   const bool bwd = a.bwd != nullptr;
   const bool resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
   const int src2 = resp ? 1 : bwd ? 2 : 0;
@@ -1958,9 +2012,18 @@ void launch_conv_wgrad(const ConvWgradArgs& a0, hipStream_t s) {
   const int nblk = w.tiles * w.nsplit;
   // LIN: 1x1 stride-1 pad-0 geometry (X row m = pixel m), DMA sources without the pixel decode
   const bool lin = a.g.ks == 1 && a.g.stride == 1 && a.g.pad == 0;
+  static const bool prol_env = [] {
+    const char* e = std::getenv("PS_AMD_WGRAD_PRO_LDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  const bool prol = prol_env && a.g.ks == 1;  // the LDS pass maps k to the channel directly
 #define PSAMD_CWW3(TN, TK, WN, WK, L)                                                                             \
-  if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true, false, L>), dim3(nblk), dim3(512), \
-                                0, s, a, w.rows);                                                               \
+  if (a.pro && prol && (WK * 32 * TK == 128 || WK * 32 * TK == 256))                                            \
+    hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true, false, L, (WK * 32 * TK == 128 ||          \
+                                                                             WK * 32 * TK == 256)>),            \
+                       dim3(nblk), dim3(512), 0, s, a, w.rows);                                                  \
+  else if (a.pro) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true, false, L>), dim3(nblk),      \
+                                     dim3(512), 0, s, a, w.rows);                                               \
   else if (a.db) hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, true, L>), dim3(nblk),        \
                                     dim3(512), 0, s, a, w.rows);                                                \
   else hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, false, false, L>), dim3(nblk), dim3(512), 0, s, \
