@@ -1362,17 +1362,31 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
   };
   const int pre = nst < kWS - 1 ? nst : kWS - 1;
   for (int st = 0; st < pre; ++st) issue(st, st);
+  if constexpr (PROL) {
+    // the LDS pass runs one stage ahead (stage st + 1 while stage st computes), so the barrier
+    // that publishes it is the next iteration's: still one barrier per stage
+    if (pre == 3) wait_vmcnt<2 * PER>();
+    else if (pre == 2) wait_vmcnt<PER>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (nst > 0) xform(0);
+  }
   for (int st = 0; st < nst; ++st) {
     // this wave's DMAs of stage st landed (later stages may stay in flight), then everyone's
+    // (PROL: of stage st + 1, whose LDS pass runs in this iteration)
     const int ahead = min(kWS - 2, nst - 1 - st);
-    if (ahead >= 2) wait_vmcnt<2 * PER>();
-    else if (ahead == 1) wait_vmcnt<PER>();
-    else wait_vmcnt<0>();
+    if constexpr (PROL) {
+      if (ahead >= 2) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    } else {
+      if (ahead >= 2) wait_vmcnt<2 * PER>();
+      else if (ahead == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    }
     lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
     if (st + kWS - 1 < nst) issue(st + kWS - 1, (st + kWS - 1) % kWS);
     if constexpr (PROL) {
-      xform(st % kWS);
-      lds_barrier();  // the transformed X tile is visible to every wave
+      if (st + 1 < nst) xform((st + 1) % kWS);  // published by the next iteration's barrier
     }
     if constexpr (DB) {
       if (dbt) {
