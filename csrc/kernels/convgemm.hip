@@ -237,6 +237,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // over the stage tile applies the prologue in place (a single third buffer for the second
   // source: it is refilled once the pass has read it)
   constexpr bool TWO_GLDS = GLDS && (BWD || RESP);
+  // PRO 1 (BN + ReLU of A) on the LDS-DMA path: the same in-place pass, one source (1x1 only:
+  // the pass cannot tell a 3x3 halo slot's zero from a real 0)
+  constexpr bool ONE_GLDS = GLDS && PRO == 1;
+  static_assert(!ONE_GLDS || KS1, "the LDS-pass BN prologue is for 1x1 convolutions");
+  constexpr bool XF_GLDS = TWO_GLDS || ONE_GLDS;
   constexpr int AR2 = BWD || RESP ? BM / 32 : 1;
   // epilogues 6/7/8 = base epilogue 5/2/4 + the previous block's bn3 backward reduce; 9 = 6 + the
   // previous block's downsample-BN sum (third partial slab)
@@ -763,7 +768,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
     // 128 B lane-linearly, so the chunk swizzle moves to the SOURCE address (linear destination +
     // swizzled source + swizzled read).  Out-of-map taps / rows past M load the zero page.  Two
     // buffers: issue stage t+1, counted vmcnt for stage t, barrier, MFMAs, barrier.
-    static_assert(!PRO || TWO_GLDS, "the one-source BN prologue needs register staging");
+    static_assert(!PRO || XF_GLDS, "LDS-DMA prologues: the in-place LDS pass variants");
     constexpr int AI = BM / 32, BI = BN / 32;  // LDS-DMA instructions per wave per stage
     const int lrow = lane >> 3, lch = lane & 7;
     int64_t gbase[AI];
@@ -817,9 +822,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         }
       }
     };
-    if constexpr (TWO_GLDS) {
+    if constexpr (XF_GLDS) {
       // the second source (BN input z / block residual r) of stage kt into the single Z tile
       auto issue_z = [&](int kt) {
+        if constexpr (!TWO_GLDS) return;
         const uint16_t* zbase = p.a2 + kt * kBK;
 #pragma unroll
         for (int i = 0; i < AI; ++i) {
@@ -837,6 +843,19 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         const uint16_t* Zs = lds + Z_BASE;
         const int cc = kt * kBK + lc * 8;
         float c0[8], c1[8], c2[8], c3[8];
+        if constexpr (ONE_GLDS) {  // BN + ReLU of the previous layer's output
+          load8(p.pro, cc, c0);
+          load8(p.pro + g.C, cc, c1);
+#pragma unroll
+          for (int i = 0; i < BM / 32; ++i) {
+            const int r = tr0 + 32 * i, m = mg * BM + r;
+            const int off = r * kBK + swz(r, lc) * 8;
+            u16x8 v = bn_relu8(*reinterpret_cast<const u16x8*>(As + off), c0, c1);
+            if (m >= p.M) v = kZero8;
+            *reinterpret_cast<u16x8*>(As + off) = v;
+          }
+          return;
+        }
         if constexpr (BWD) {
           load8(p.bwd, cc, c0);
           load8(p.bwd + g.C, cc, c1);
@@ -1729,8 +1748,21 @@ int twosrc_glds_min_nk() {
 // src2: two-source prologue of the launch (0 none, 1 block output, 2 BN backward)
 bool twosrc_glds(int K, int src2) { return src2 != 0 && K / kBK >= twosrc_glds_min_nk(); }
 
+int pro_glds_min_nk() {
+  static const int v = [] {
+    const char* e = std::getenv("PS_AMD_PRO_GLDS_MIN_NK");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
+// the one-source BN + ReLU prologue (1x1) on the LDS-DMA path from this K depth
+bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
+  return pro && src2 == 0 && g.ks == 1 && g.ksw <= 1 && g.stride == 1 && g.pad == 0 && K / kBK >= pro_glds_min_nk();
+}
+
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2) {
-  if (twosrc_glds(K, src2)) {  // LDS-DMA two-source prologue: one 128-pixel tile per block
+  if (twosrc_glds(K, src2) || pro_glds(K, pro, src2, g)) {  // LDS-DMA prologue: one 128-pixel tile per block
     ConvFwdPlan pl;
     pl.bm = 128;
     pl.bn = N % 128 == 0 ? 128 : 64;
@@ -1783,6 +1815,22 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
+  if (pro_glds(a.K, a.pro != nullptr, src2, a.g)) {
+    if (pl.bn == 128) {
+      if (a.epi == 1) {
+        hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, 1, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
+      } else {
+        hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, 0, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
+      }
+    } else {
+      if (a.epi == 1) {
+        hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, 1, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
+      } else {
+        hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, 0, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
+      }
+    }
+    return;
+  }
   if (twosrc_glds(a.K, src2)) {  // (1x1: the binding checks)
 #define PSAMD_CF2S(BN, PRO, EPI) \
   hipLaunchKernelGGL((conv_fwd_kernel<128, BN, PRO, EPI, true, true>), dim3(nblk), dim3(256), 0, s, a, GM)

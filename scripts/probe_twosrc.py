@@ -18,7 +18,7 @@ from ps_amd.ops._ext import native  # noqa: E402
 
 nat = native()
 dev = torch.device("cuda")
-MIN_NK = os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "5")
+MIN_NK = os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4") + "/" + os.environ.get("PS_AMD_PRO_GLDS_MIN_NK", "2")
 
 
 def timed(fn, reps=10):
@@ -81,10 +81,33 @@ def resp_case(M, K, N):
     return timed(fused), timed(split)
 
 
+def pro_case(M, K, N):
+    """conv3 forward: bn2 + ReLU applied while staging (one source) vs apply pass + plain GEMM."""
+    z2 = rnd(M, K)
+    cf, ks = coef(K), torch.randn(N, device=dev) * 0.1
+    w = rnd(N, K, scale=K ** -0.5)
+    geo = [M, 1, M, 1, 1, 1, 0]
+
+    def fused():
+        nat.conv_gemm(z2, w, geo, cf, 1, None, ks)
+
+    def split():
+        yy = nat.bn_apply_coef(z2, cf, None, None, 1)[0]
+        nat.conv_gemm(yy, w, geo, None, 1, None, ks)
+
+    return timed(fused), timed(split)
+
+
+PRO = [(3211264, 64, 256), (802816, 128, 512), (200704, 256, 1024), (50176, 512, 2048)]
 BWD = [(3211264, 256, 64), (802816, 512, 128), (200704, 1024, 256), (50176, 2048, 512)]
 RESP = [(3211264, 256, 64), (3211264, 256, 128), (802816, 512, 128), (802816, 512, 256), (200704, 1024, 256),
         (200704, 1024, 512), (50176, 2048, 512)]
-for kind, shapes, fn in (("bn_bwd_prologue", BWD, bwd_case), ("block_output_prologue", RESP, resp_case)):
+CASES = [("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
+         ("block_output_prologue", RESP, resp_case)]
+only = os.environ.get("PROBE_ONLY")
+for kind, shapes, fn in CASES:
+    if only and kind != only:
+        continue
     for M, K, N in shapes:
         f, s = fn(M, K, N)
         print(json.dumps({"kind": kind, "M": M, "K": K, "N": N, "min_nk": MIN_NK, "fused_ms": round(f, 4),
