@@ -987,6 +987,245 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   }
 }
 
+// ------------------------------------------------------------------------------ conv3x3 64 -> 64
+// The 64-channel 3x3 stride-1 layers (ResNet-50 layer 1: forward and data gradient at 56 x 56):
+// a persistent block per CU keeps the WHOLE weight (9 taps x 64 x 64 = 72 KiB) resident in LDS
+// and walks row-aligned tiles of two image rows (112 of 128 MFMA rows used).  Each tile's input is
+// staged once as a zero-haloed patch of 4 x 58 slots (eight 16-B channel planes) by LDS-DMA, two
+// patch slots deep: the next tile's patch streams in while this one computes, and the nine taps
+// read their A fragments from the same patch at shifted slots -- no per-tap barrier, no im2col
+// re-read of the input.  The im2col tile (256 x 64, LDS-DMA per tap) moved nine copies of every
+// input pixel through L2 per layer and ran at 0.55-0.6 PF/s.
+// Epilogues: 0 (store), 1 (+ the next BN's statistics about kshift), 3 (ReLU mask from z * mc +
+// shift and the BN-backward sums) -- partials [2][gridDim.x][64] like the persistent conv_fwd grid.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int W, int EPI>
+__global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs p) {
+  constexpr int C = 64, N = 64, RT = 128 / W, TP = RT * W;  // image rows / pixels per tile
+  constexpr int PW = W + 2, PR = RT + 2, NSL = PR * PW;       // patch slots (rows x cols)
+  constexpr int PPP = (NSL + 63) / 64;                         // 1-KiB pieces per plane
+  constexpr int PLB = PPP * 1024;                              // bytes per 16-B channel plane
+  constexpr int SLOT = 8 * PLB;                                // bytes per patch
+  constexpr int NPIECE = 8 * PPP, PPW = NPIECE / 4;            // pieces, per wave
+  static_assert(NPIECE % 4 == 0 && RT >= 1, "patch pieces over 4 waves");
+  constexpr int BTAP = N * 64 * 2;                             // bytes per tap of the weight
+  constexpr int CS = N + 4;                                    // output tile row stride (bf16)
+  constexpr int B_OFF = 2 * SLOT, CS_OFF = B_OFF + 9 * BTAP, RED_OFF = CS_OFF + 128 * CS * 2;
+  constexpr int LDS_BYTES = RED_OFF + 8 * N * 4;
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  uint16_t* const Cs = reinterpret_cast<uint16_t*>(lds + CS_OFF);
+  float* const red = reinterpret_cast<float*>(lds + RED_OFF);
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int GM = gridDim.x, mg = blockIdx.x;
+  const int tpi = g.OH / RT, ntiles = (p.M / (g.OH * g.OW)) * tpi;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 32;  // 2 x 2 waves of 64 px x 32 ch
+
+  // the resident weight: tap k-slab [64 n][64 k] with chunk c of row n at swz(n, c)
+  {
+    const int lrow = lane >> 3, lch = lane & 7;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n = (wave * 2 + i) * 8 + lrow;
+        __builtin_amdgcn_global_load_lds((gptr_t*)(p.b + static_cast<int64_t>(n) * p.K + tap * C + swz(n, lch) * 8),
+                                         (lptr_t*)(lds + B_OFF + tap * BTAP + (wave * 2 + i) * 8 * 128), 16, 0, 0);
+      }
+  }
+  // patch of tile mt into slot sl: plane pl, piece k = 64 lane-linear slots of row-major (row, col)
+  auto issue_patch = [&](int mt, int sl) {
+    const int img = mt / tpi, oh0 = (mt - img * tpi) * RT;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave + 4 * i, pl = pc / PPP, sq = (pc - pl * PPP) * 64 + lane;
+      const int pr = sq / PW, pcol = sq - pr * PW, ih = oh0 - 1 + pr, iw = pcol - 1;
+      const bool ok = sq < NSL && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const uint16_t* src = ok ? p.a + ((static_cast<int64_t>(img) * g.H + ih) * W + iw) * C + pl * 8 : kZeroPage;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + sl * SLOT + pl * PLB + (pc - pl * PPP) * 1024), 16,
+                                       0, 0);
+    }
+  };
+  // A-fragment slot of this lane's pixel rows (tap (0, 0)); pixels past the tile read slot 0
+  uint32_t abase[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int px = wm + 32 * j + fr;
+    const int pr = px / W, pcol = px - pr * W;
+    abase[j] = static_cast<uint32_t>(fh * PLB + (px < TP ? pr * PW + pcol : 0) * 16);
+  }
+  const int brow = wn + fr;
+  f32x16 acc[2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  };
+  auto compute = [&](int sl) {
+    const uint8_t* P = lds + sl * SLOT;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw, toff = (kh * PW + kw) * 16;
+        const uint8_t* B = lds + B_OFF + tap * BTAP;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int ch = 2 * s2 + fh;
+          const bf16x8_t wb = *reinterpret_cast<const bf16x8_t*>(B + brow * 128 + swz(brow, ch) * 16);
+          bf16x8_t xa[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            xa[j] = *reinterpret_cast<const bf16x8_t*>(P + abase[j] + toff + 2 * s2 * PLB);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc[j], 0, 0, 0);
+        }
+      }
+  };
+  // epilogue: thread t owns channels [8 cg, 8 cg + 8) of tile rows r0 + 32 i
+  const int cg = t & 7, r0 = t >> 3, nc = cg * 8;
+  float s1[8], s2[8], e0[8], e1[8], e2[8], e3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = e0[j] = e1[j] = e2[j] = e3[j] = 0.f;
+  if constexpr (EPI == 1) {
+    if (p.kshift) load8(p.kshift, nc, e0);
+  } else if constexpr (EPI == 3) {
+    load8(p.mc, nc, e0);
+    load8(p.mc + N, nc, e1);
+    load8(p.mean, nc, e2);
+    load8(p.invstd, nc, e3);
+  }
+  u16x8 ra[4];
+  auto epi_load = [&](int m0) {
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = r0 + 32 * i;
+        ra[i] = *reinterpret_cast<const u16x8*>(p.aux + static_cast<int64_t>(m0 + (rr < TP ? rr : 0)) * N + nc);
+      }
+    }
+  };
+  auto acc_to_lds = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int nl = wn + 8 * q4 + 4 * fh, ml = wm + 32 * j + fr;
+        const u16x4 v = {f32_to_bf16(acc[j][4 * q4]), f32_to_bf16(acc[j][4 * q4 + 1]),
+                         f32_to_bf16(acc[j][4 * q4 + 2]), f32_to_bf16(acc[j][4 * q4 + 3])};
+        *reinterpret_cast<u16x4*>(Cs + ml * CS + nl) = v;
+      }
+  };
+  auto epilogue_rows = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = r0 + 32 * i;
+      if (rr >= TP) break;
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + nc);
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + nc + 4);
+      u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf16_to_f32(v[j]) - e0[j];
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      } else if constexpr (EPI == 3) {
+        const u16x8 z8 = ra[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = bf16_to_f32(z8[j]);
+          const bool on = z * e0[j] + e1[j] > 0.f;
+          const float gv = on ? bf16_to_f32(v[j]) : 0.f;
+          s1[j] += gv;
+          s2[j] += gv * ((z - e2[j]) * e3[j]);
+          if (!on) v[j] = 0;
+        }
+      }
+      *reinterpret_cast<u16x8*>(p.c + static_cast<int64_t>(m0 + rr) * N + nc) = v;
+    }
+  };
+
+  // prologue: weight + the first two patches in flight; wait for the weight and patch 0
+  zero_acc();
+  const bool has0 = mg < ntiles, has1 = mg + GM < ntiles;
+  if (has0) issue_patch(mg, 0);
+  if (has1) issue_patch(mg + GM, 1);
+  if (has1) wait_vm<PPW>();
+  else wait_vm<0>();
+  lds_barrier();
+  for (int ti = 0, mt = mg; mt < ntiles; ++ti, mt += GM) {
+    const int sl = ti & 1, m0 = mt * TP;
+    epi_load(m0);
+    compute(sl);
+    acc_to_lds();
+    lds_barrier();  // the output tile is complete; every wave is done with patch slot sl
+    const bool more2 = mt + 2 * GM < ntiles;
+    if (more2) issue_patch(mt + 2 * GM, sl);  // streams in during this epilogue and the next tile
+    epilogue_rows(m0);
+    zero_acc();
+    // the next tile's patch landed (this wave's pieces): the just-issued patch and the epilogue's
+    // row stores (3 or 4 per thread; vmcnt retires in issue order, so counting the smaller is
+    // safe) may stay in flight
+    if (more2) wait_vm<PPW + 3>();
+    else wait_vm<3>();
+    lds_barrier();  // every wave's pieces landed; the output tile was read out
+  }
+  if constexpr (EPI == 1 || EPI == 3) {
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], off, 64);
+        s2[j] += __shfl_xor(s2[j], off, 64);
+      }
+    if (lane < 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave * N + nc + j] = s1[j];
+        red[(4 + wave) * N + nc + j] = s2[j];
+      }
+    }
+    lds_barrier();
+    if (t < N) {
+      p.part[static_cast<int64_t>(mg) * N + t] = (red[t] + red[N + t]) + (red[2 * N + t] + red[3 * N + t]);
+      p.part[(static_cast<int64_t>(GM) + mg) * N + t] =
+          (red[4 * N + t] + red[5 * N + t]) + (red[6 * N + t] + red[7 * N + t]);
+    }
+  }
+}
+
+bool c64_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_C64");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// the layers conv3x3_c64_kernel takes: 3x3 / stride 1 / pad 1, 64 -> 64 channels, 56-wide maps
+// with an even row count, no prologue
+bool c64_ok(const ConvGeo& g, int N, bool pro) {
+  return c64_enabled() && !pro && g.ks == 3 && (g.ksw == 0 || g.ksw == 3) && g.stride == 1 && g.pad == 1 &&
+         g.RH == 0 && g.C == 64 && N == 64 && g.W == 56 && g.OW == 56 && g.OH == g.H && g.OH % 2 == 0;
+}
+
+int c64_blocks(int M, const ConvGeo& g) {
+  const int ntiles = (M / (g.OH * g.OW)) * (g.OH / 2);
+  return std::max(1, std::min(ntiles, 256));
+}
+
 // ------------------------------------------------------------------------------ conv_wgrad
 // dW tile [n0, n0 + 64 TNO) x [k0, k0 + 64 TKO) over pixels [mb, me): grid = tiles * nsplit
 // blocks; logical id -> tile = id % tiles, split = id / tiles, so blocks on one XCD share a
@@ -1751,7 +1990,9 @@ bool twosrc_glds(int K, int src2) { return src2 != 0 && K / kBK >= twosrc_glds_m
 int pro_glds_min_nk() {
   static const int v = [] {
     const char* e = std::getenv("PS_AMD_PRO_GLDS_MIN_NK");
-    return e ? std::atoi(e) : 2;
+    // off by default: slower than the persistent register-staged prologue at every ResNet-50
+    // depth (layer 2: 0.41 vs 0.33 ms, profiles/r4_twosrc_probe.txt)
+    return e ? std::atoi(e) : 1 << 20;
   }();
   return v;
 }
@@ -1762,6 +2003,13 @@ bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
 }
 
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2) {
+  if (src2 == 0 && c64_ok(g, N, pro)) {  // persistent row-tile patch kernel, one block per CU
+    ConvFwdPlan pl;
+    pl.bm = 128;
+    pl.bn = 64;
+    pl.gm = c64_blocks(M, g);
+    return pl;
+  }
   if (twosrc_glds(K, src2) || pro_glds(K, pro, src2, g)) {  // LDS-DMA prologue: one 128-pixel tile per block
     ConvFwdPlan pl;
     pl.bm = 128;
@@ -1815,6 +2063,12 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
+  if (src2 == 0 && c64_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
+    if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 1>), dim3(GM), dim3(256), 0, s, a);
+    else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 3>), dim3(GM), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_c64_kernel<56, 0>), dim3(GM), dim3(256), 0, s, a);
+    return;
+  }
   if (pro_glds(a.K, a.pro != nullptr, src2, a.g)) {
     if (pl.bn == 128) {
       if (a.epi == 1) {

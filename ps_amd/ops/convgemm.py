@@ -259,6 +259,13 @@ def _bwd_prologue_enabled(c3: int, n: int = 0) -> bool:
     return c3 <= int(os.environ.get("PS_AMD_BN_BWD_PROLOGUE_MAX_C", "4096")) and n <= _twosrc_max_n()
 
 
+def _pro_fuse_max_k() -> int:
+    """conv3's forward applies bn2 + ReLU while staging up to this many input channels; deeper
+    (layer 4, 512) the apply pass + plain GEMM is faster: 0.16 vs 0.21 ms (layer 3: 0.26 either
+    way; profiles/r4_twosrc_probe.txt, bn_relu_prologue rows)."""
+    return int(os.environ.get("PS_AMD_PRO_FUSE_MAX_K", "256"))
+
+
 def _fold_enabled() -> bool:
     return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
 
@@ -299,7 +306,10 @@ class _BottleneckFn(torch.autograd.Function):
             m2, i2, cf2 = nat.bn_stats(z2r, g2, b2, bn2.running_mean, bn2.running_var, True, _momentum(bn2),
                                        float(bn2.eps))
         k3 = bn3.running_mean
-        z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
+        if z2r.shape[1] <= _pro_fuse_max_k():
+            z3, p3 = nat.conv_gemm(z2r, _mat(w3), go, cf2, 1, None, k3)  # bn2 + ReLU in the prologue
+        else:  # the apply pass + plain LDS-DMA GEMM is faster at this depth
+            z3, p3 = nat.conv_gemm(nat.bn_apply_coef(z2r, cf2, None, None, 1)[0], _mat(w3), go, None, 1, None, k3)
         m3, i3, cf3 = _finalize(p3, k3, n * oh * ow, bn3)
         cfd = None
         if wd is not None:

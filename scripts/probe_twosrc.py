@@ -102,7 +102,27 @@ PRO = [(3211264, 64, 256), (802816, 128, 512), (200704, 256, 1024), (50176, 512,
 BWD = [(3211264, 256, 64), (802816, 512, 128), (200704, 1024, 256), (50176, 2048, 512)]
 RESP = [(3211264, 256, 64), (3211264, 256, 128), (802816, 512, 128), (802816, 512, 256), (200704, 1024, 256),
         (200704, 1024, 512), (50176, 2048, 512)]
-CASES = [("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
+def c64_case(M, K, N):
+    """3x3 64 -> 64 at 56 x 56: forward (epi 1) and data gradient (epi 3); 'fused' = the default
+    routing (conv3x3_c64_kernel unless PS_AMD_CONV_C64=0), 'split' = forward + data gradient sum."""
+    n = M // (56 * 56)
+    x, w = rnd(M, 64), rnd(64, 576, scale=576 ** -0.5)
+    z1, cf = rnd(M, 64), coef(64)
+    mean, invstd, ks = torch.randn(64, device=dev) * 0.1, torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev)
+    geo = [56, 56, 56, 56, 3, 1, 1]
+
+    def fwd():
+        nat.conv_gemm(x, w, geo, None, 1, None, ks)
+
+    def dgrad():
+        nat.conv_gemm(x, w, geo, None, 3, z1, None, cf, mean, invstd)
+
+    del n
+    return timed(fwd), timed(dgrad)
+
+
+C64 = [(1024 * 56 * 56, 576, 64), (256 * 56 * 56, 576, 64)]
+CASES = [("conv3x3_c64 (fwd_ms, dgrad_ms)", C64, c64_case), ("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
          ("block_output_prologue", RESP, resp_case)]
 only = os.environ.get("PROBE_ONLY")
 for kind, shapes, fn in CASES:
