@@ -1064,12 +1064,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs 
     abase[j] = static_cast<uint32_t>(fh * PLB + (px < TP ? pr * PW + pcol : 0) * 16);
   }
   const int brow = wn + fr;
-  f32x16 acc[2];
+  // two accumulator sets by k-step parity: four independent MFMA chains per wave (one wave per
+  // SIMD here, so the chains -- not a partner wave -- cover the MFMA dependency latency)
+  f32x16 acc[2], acc2[2];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+      for (int q = 0; q < 16; ++q) acc[j][q] = acc2[j][q] = 0.f;
   };
   auto compute = [&](int sl) {
     const uint8_t* P = lds + sl * SLOT;
@@ -1088,9 +1090,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs 
           for (int j = 0; j < 2; ++j)
             xa[j] = *reinterpret_cast<const bf16x8_t*>(P + abase[j] + toff + 2 * s2 * PLB);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc[j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) {
+            if (s2 & 1) acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc2[j], 0, 0, 0);
+            else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc[j], 0, 0, 0);
+          }
         }
       }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] += acc2[j];
   };
   // epilogue: thread t owns channels [8 cg, 8 cg + 8) of tile rows r0 + 32 i
   const int cg = t & 7, r0 = t >> 3, nc = cg * 8;
@@ -1209,7 +1216,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs 
 bool c64_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("PS_AMD_CONV_C64");
-    return e == nullptr || e[0] != '0';
+    // opt-in: 0.476 / 0.507 ms vs the tall im2col tile's 0.451 / 0.456 (fwd / data grad at bs1024,
+    // profiles/r4_conv3x3_c64_probe.txt)
+    return e != nullptr && e[0] == '1';
   }();
   return on;
 }
