@@ -227,7 +227,9 @@ struct StageRegs {
 template <int BN>
 constexpr int patch_bytes() { return BN == 64 ? 65536 : 40960; }  // 8 channel planes of 8 / 5 KiB
 
-template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, bool PATCH = false>
+// VAR: 0 the plain paths, 1 PATCH (3x3 patch-staged tiles), 2 the plain LDS-DMA path with a
+// 3-stage ring (two stages in flight behind the MFMAs; one block per CU by LDS)
+template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, int VAR = 0>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
   constexpr bool BWD = PRO == 2;
   constexpr bool RESP = PRO == 3;
@@ -268,10 +270,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // registers it pushed the register-staged variant from 20 to 76 B/lane of scratch
   constexpr int RED_ELEMS = 4 * NSUM * BN * 2 > (FOLD_DS ? 256 * 8 * 2 : 0) ? 4 * NSUM * BN * 2 : 256 * 8 * 2;
   constexpr int EPI_ELEMS = BM * CS + RED_ELEMS;
-  constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : (TWO_GLDS ? 3 : 2) * BM * kBK;
+  constexpr bool PATCH = VAR == 1;
+  constexpr int NST = VAR == 2 ? 3 : 2;  // plain LDS-DMA ring depth
+  static_assert(VAR != 2 || (GLDS && !PRO), "the deep ring is the plain LDS-DMA path");
+  constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : (TWO_GLDS ? 3 : NST) * BM * kBK;
   constexpr int Z_BASE = 2 * BM * kBK;  // TWO_GLDS: the second source's stage tile
   constexpr int B_BASE = ((A_ELEMS > EPI_ELEMS ? A_ELEMS : EPI_ELEMS) + 7) & ~7;
-  constexpr int LDS_ELEMS = B_BASE + 2 * BN * kBK;
+  constexpr int LDS_ELEMS = B_BASE + NST * BN * kBK;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
   const ConvGeo& g = p.g;
@@ -915,6 +920,31 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
         epi_load(mg);
         epilogue(mg);
       }
+    } else if (VAR == 2 && mg < mtiles) {  // 3-stage ring: issue kt + 2, wait for kt
+      issue(0, 0);
+      if (nk > 1) issue(1, 1);
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // refills compute(kt - 1)'s buffer
+        const int ahead = min(2, nk - 1 - kt);         // stages issued after kt, in flight
+        if (ahead == 2) {
+          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          else if constexpr (AI + BI == 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+          else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (ahead == 1) {
+          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else if constexpr (AI + BI == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();  // every wave's stage-kt DMAs landed
+        compute(kt % 3);
+        lds_barrier();  // stage kt read out before stage kt + 3 is issued into its buffer
+      }
+      epi_load(mg);
+      epilogue(mg);
     } else if (mg < mtiles) {  // block-uniform
       issue(0, 0);
       for (int kt = 0; kt < nk; ++kt) {
@@ -2121,13 +2151,28 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
     return;
   }
   const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
-  // deep K without the BN prologue: LDS-DMA staging (one tile per block)
+  // deep K without the BN prologue: LDS-DMA staging (one tile per block); PS_AMD_GLDS_STAGES=3:
+  // a 3-stage ring (one block per CU) for K >= 64 x PS_AMD_GLDS_DEEP_MIN_NK
   const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
+  static const int stages = [] {
+    const char* e = std::getenv("PS_AMD_GLDS_STAGES");
+    return e ? std::atoi(e) : 2;
+  }();
+  static const int deep_min_nk = [] {
+    const char* e = std::getenv("PS_AMD_GLDS_DEEP_MIN_NK");
+    return e ? std::atoi(e) : 8;
+  }();
+  const bool deep = stages == 3 && a.K / kBK >= deep_min_nk;
 #define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \
   if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, GL>), dim3(nblk), dim3(256), 0, s, a, GM); \
   else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, GL>), dim3(nblk), dim3(256), 0, s, a, GM)
+#define PSAMD_CF3V(BM, BN, PRO, EPI)                                                                          \
+  if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, true, 2>), dim3(nblk), dim3(256), 0, s, a, \
+                              GM);                                                                              \
+  else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, true, 2>), dim3(nblk), dim3(256), 0, s, a, GM)
 #define PSAMD_CF2(BM, BN, PRO, EPI)                        \
   if constexpr (PRO) { PSAMD_CF3(BM, BN, PRO, EPI, false); } \
+  else if (glds && deep) { PSAMD_CF3V(BM, BN, PRO, EPI); }   \
   else if (glds) { PSAMD_CF3(BM, BN, PRO, EPI, true); }       \
   else { PSAMD_CF3(BM, BN, PRO, EPI, false); }
 #define PSAMD_CF(BN, PRO, EPI) PSAMD_CF2(128, BN, PRO, EPI)
@@ -2145,7 +2190,8 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
     default: PSAMD_CF(BN, PRO, 0); break; \
   }
   if (pl.bm == 256) {  // LDS-DMA only (no prologue, deep K)
-#define PSAMD_CFT(EPI) PSAMD_CF3(256, 64, false, EPI, true)
+#define PSAMD_CFT(EPI) \
+  if (deep) { PSAMD_CF3V(256, 64, false, EPI); } else { PSAMD_CF3(256, 64, false, EPI, true); }
     switch (a.epi) {
       case 1: PSAMD_CFT(1); break;
       case 2: PSAMD_CFT(2); break;
@@ -2190,6 +2236,7 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
 #undef PSAMD_CF
 #undef PSAMD_CF2
 #undef PSAMD_CF3
+#undef PSAMD_CF3V
 }
 
 namespace {
