@@ -235,7 +235,9 @@ def main():
                     step()
                 torch.cuda.set_sync_debug_mode(0)
             sync()
-            hits = [str(w.message).split("\n")[0][:80] for w in ws if "synchroniz" in str(w.message)]
+            # (torch's one-time "Synchronization debug mode is a prototype feature" notice is not a sync)
+            hits = [str(w.message).split("\n")[0][:80] for w in ws
+                    if "synchroniz" in str(w.message) and "prototype feature" not in str(w.message)]
             audit = {"host_syncs_per_step": round(len(hits) / n_audit, 2), "sync_ops": sorted(set(hits))[:4]}
         except Exception as e:  # diagnostics only
             torch.cuda.set_sync_debug_mode(0)
