@@ -36,3 +36,5 @@ def test_bench_json_contract_cpu(world, tmp_path):
     assert rec["value"] == pytest.approx(2 * world * 1e3 / rec["ms_per_step"], rel=1e-2)
     if world > 1:
         assert set(rec["config"]["ps_phase_ms_per_step"]) >= {"push_ms", "serve_ms", "pull_ms"}
+        if rec["config"].get("data_plane") == "xgmi":  # mapping mode / self-test / round end reported
+            assert {"mode", "self_test", "round_end"} <= set(rec["config"]["plane_info"])
