@@ -172,7 +172,7 @@ def main():
     if use_graph:
         from ps_amd.train.graphs import GraphedStep
 
-        step = GraphedStep(step, warmup=max(1, args.warmup - 1))
+        step = GraphedStep(step, warmup=max(1, args.warmup - 1), feed=bench.feed)
     else:
         for _ in range(args.warmup):
             step()

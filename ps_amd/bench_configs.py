@@ -42,6 +42,9 @@ class Bench:
     engine: object = None
     stats: Optional[Callable[[], Dict]] = None  # extra counters for the JSON line (read after timing)
     dtype: str = "bf16"  # compute dtype reported in the JSON line
+    # HIP-graph mode: the step reads static input buffers and ``feed`` copies the next batch of the
+    # pool into them before every replay (the graph never sees a Python-side batch change)
+    feed: Optional[Callable[[], None]] = None
 
 
 def setup_resnet50(args, tp, dev) -> Bench:
@@ -59,18 +62,33 @@ def setup_resnet50(args, tp, dev) -> Bench:
         memory_format=torch.channels_last), torch.randint(0, 1000, (B,), device=dev, generator=g))
         for _ in range(POOL)]
     it = _cycle(pool)
+    feed = None
+    if str(getattr(args, "graph", "0")) != "0":
+        xs, ys = pool[0][0].clone(), pool[0][1].clone()
 
-    def step():
-        x, y = next(it)
-        loss = F.cross_entropy(model(x).float(), y)
-        loss.backward()
-        ps.finish_step()
-        return loss
+        def feed():
+            x, y = next(it)
+            xs.copy_(x)
+            ys.copy_(y)
+
+        def step():
+            loss = F.cross_entropy(model(xs).float(), ys)
+            loss.backward()
+            ps.finish_step()
+            return loss
+    else:
+        def step():
+            x, y = next(it)
+            loss = F.cross_entropy(model(x).float(), y)
+            loss.backward()
+            ps.finish_step()
+            return loss
 
     return Bench(step, B, "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X workers", "samples/s",
                  {"model": "ResNet-50", "global_batch": B * tp.world, "seq_len": None, "image_size": S,
                   "parallelism": f"ps-bsp-colocated-dp{tp.world}", "optimizer": upd.name,
-                  "bucket_mb": args.bucket_mb, "staleness": args.staleness, "fused_bn": bool(args.fused_bn)}, ps)
+                  "bucket_mb": args.bucket_mb, "staleness": args.staleness, "fused_bn": bool(args.fused_bn)}, ps,
+                 feed=feed)
 
 
 def setup_bert_ssp(args, tp, dev) -> Bench:

@@ -22,15 +22,20 @@ import torch
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[[], Optional[torch.Tensor]], warmup: int = 3,
-                 pool=None):
+                 pool=None, feed: Optional[Callable[[], None]] = None):
+        """``feed`` (optional) refreshes the step's static inputs; it runs eagerly before every
+        warm-up step and every replay, never inside the graph."""
         if not torch.cuda.is_available():
             raise RuntimeError("GraphedStep needs a GPU")
         self.step_fn = step_fn
+        self.feed = feed
         self.graph = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
+                if feed is not None:
+                    feed()
                 step_fn()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -39,5 +44,7 @@ class GraphedStep:
         torch.cuda.synchronize()
 
     def __call__(self):
+        if self.feed is not None:
+            self.feed()
         self.graph.replay()
         return self.out

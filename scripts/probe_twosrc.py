@@ -18,7 +18,8 @@ from ps_amd.ops._ext import native  # noqa: E402
 
 nat = native()
 dev = torch.device("cuda")
-MIN_NK = os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4") + "/" + os.environ.get("PS_AMD_PRO_GLDS_MIN_NK", "2")
+MIN_NK = (os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4") + "/" + os.environ.get("PS_AMD_PRO_GLDS_MIN_NK", "off") + "/st"
+          + os.environ.get("PS_AMD_GLDS_STAGES", "2") + ":" + os.environ.get("PS_AMD_GLDS_DEEP_MIN_NK", "8"))
 
 
 def timed(fn, reps=10):
@@ -121,8 +122,26 @@ def c64_case(M, K, N):
     return timed(fwd), timed(dgrad)
 
 
+def plain_case(M, K, N):
+    """plain LDS-DMA GEMM (1x1, epi 1; K = 576 / N = 64: the 3x3 tall tile at 56 x 56): ms of the
+    forward with statistics (both columns); compare runs with PS_AMD_GLDS_STAGES=2 / 3."""
+    if K == 576:
+        x, geo = rnd(M, 64), [56, 56, 56, 56, 3, 1, 1]
+    else:
+        x, geo = rnd(M, K), [M, 1, M, 1, 1, 1, 0]
+    w, ks = rnd(N, K, scale=K ** -0.5), torch.randn(N, device=dev) * 0.1
+
+    def fwd():
+        nat.conv_gemm(x, w, geo, None, 1, None, ks)
+
+    f = timed(fwd)
+    return f, f
+
+
+PLAIN = [(802816, 512, 128), (200704, 1024, 256), (50176, 2048, 512), (200704, 512, 1024), (3211264, 576, 64),
+         (200704, 256, 1024), (802816, 128, 512)]
 C64 = [(1024 * 56 * 56, 576, 64), (256 * 56 * 56, 576, 64)]
-CASES = [("conv3x3_c64 (fwd_ms, dgrad_ms)", C64, c64_case), ("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
+CASES = [("plain_gemm", PLAIN, plain_case), ("conv3x3_c64 (fwd_ms, dgrad_ms)", C64, c64_case), ("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
          ("block_output_prologue", RESP, resp_case)]
 only = os.environ.get("PROBE_ONLY")
 for kind, shapes, fn in CASES:
