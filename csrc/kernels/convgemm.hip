@@ -2253,6 +2253,14 @@ bool wide_enabled() {
   return on;
 }
 
+// Slab reduction levels: > 16 slabs reduce in two fixed-order levels (16 slabs per first-level
+// group) unless the weight has >= 256K elements -- then one thread per element over every slab
+// already fills the chip, and the second launch (plus its gap) is saved.
+int slab_groups(int nsplit, int64_t E) {
+  if (nsplit <= 16 || (E >= (int64_t(1) << 18) && nsplit <= 64)) return 0;
+  return (nsplit + 15) / 16;
+}
+
 // Split count that fills WHOLE rounds of `slots` resident blocks (one or two rounds), at most
 // `cap` splits: rounding the block count up past a round (e.g. 9 tiles x 57 splits = 513 of 512)
 // adds a round of one block and halves the kernel's throughput.
@@ -2294,7 +2302,7 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
     w.rows = ((chunks + ns - 1) / ns) * kWM;
   }
   w.nsplit = (M + w.rows - 1) / w.rows;
-  w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;
+  w.groups = slab_groups(w.nsplit, static_cast<int64_t>(N) * K);
   return w;
 }
 }  // namespace
@@ -2331,7 +2339,7 @@ PPlan pplan(const ConvGeo& g, int M, int N) {
   const int ns = fill_rounds(w.tiles, 256, std::max(1, stages / 4));  // one 12-wave block per CU
   w.spp = (stages + ns - 1) / ns;
   w.nsplit = (stages + w.spp - 1) / w.spp;
-  w.groups = w.nsplit > 16 ? (w.nsplit + 15) / 16 : 0;
+  w.groups = slab_groups(w.nsplit, static_cast<int64_t>(N) * 9 * g.C);
   return w;
 }
 
