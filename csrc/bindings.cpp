@@ -1509,13 +1509,16 @@ std::vector<Tensor> bn_apply_coef(Tensor x, Tensor coef, c10::optional<Tensor> r
 
 // Backward weight layouts (convgemm.hip weight_prep): jobs = int64 [J, 4] on the device, rows
 // {src ptr, dst ptr, kind | A << 32, B} (the WPrepJob layout) -- built once per weight set and reused
-void weight_prep(Tensor jobs) {
+// max_blocks: the largest (taps x 64-tiles) count over the jobs (one block per transposed tile)
+void weight_prep(Tensor jobs, int64_t max_blocks) {
   check_gpu(jobs, "jobs");
   TORCH_CHECK(jobs.scalar_type() == torch::kInt64 && jobs.dim() == 2 && jobs.size(1) == 4 && jobs.is_contiguous(),
               "jobs: int64 [J, 4]");
   static_assert(sizeof(void*) == 8, "64-bit pointers");
   const c10::DeviceGuard guard(jobs.device());
-  psamd::launch_weight_prep(jobs.data_ptr(), static_cast<int>(jobs.size(0)), cur_stream(jobs));
+  TORCH_CHECK(max_blocks > 0 && max_blocks < (1 << 20), "max_blocks");
+  psamd::launch_weight_prep(jobs.data_ptr(), static_cast<int>(jobs.size(0)), static_cast<int>(max_blocks),
+                            cur_stream(jobs));
 }
 
 // BN backward coefficients only (dx = ca * g + cb * x + cc for a GEMM prologue to apply) from
@@ -1579,7 +1582,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("abits") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("bn_bwd_coef", &bn_bwd_coef);
-  m.def("weight_prep", &weight_prep);
+  m.def("weight_prep", &weight_prep, py::arg("jobs"), py::arg("max_blocks") = 1024);
   m.def("conv_dgrad_s2", &conv_dgrad_s2, py::arg("dz"), py::arg("wph"), py::arg("H"), py::arg("W"),
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());

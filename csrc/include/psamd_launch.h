@@ -359,7 +359,7 @@ ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, i
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
-void launch_weight_prep(const void* jobs, int njobs, hipStream_t s);
+void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s);
 
 struct ConvWgradArgs {
   const uint16_t* dz;   // [M, N] output gradient rows

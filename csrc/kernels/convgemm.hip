@@ -178,13 +178,16 @@ __device__ __forceinline__ bf16x8_t tr_frag_imm(uint32_t addr) {
   return as_bf16x8(s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
 }
 
+// relu(bf16(x * scale + shift)): the ReLU runs on the packed bf16 result as signed 16-bit
+// integers (every negative bf16, -0 included, has the sign bit set, so max(., 0) as int16 is the
+// bf16 ReLU) -- one v_pk_max_i16 per pair instead of a float max per element; identical results
+// (rounding a negative value never makes it positive)
+typedef short s16x8i __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ u16x8 bn_relu8(u16x8 v, const float (&sc)[8], const float (&sh)[8]) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float f = bf16_to_f32(v[j]) * sc[j] + sh[j];
-    v[j] = f32_to_bf16(f > 0.f ? f : 0.f);
-  }
-  return v;
+  for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) * sc[j] + sh[j]);
+  const s16x8i z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return __builtin_bit_cast(u16x8, __builtin_elementwise_max(__builtin_bit_cast(s16x8i, v), z));
 }
 
 constexpr u16x8 kZero8 = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1935,40 +1938,57 @@ struct WPrepJob {
   int A, B;
 };
 
+// Every layout is a set of 2D transposes (a 1x1 weight: one; a 3x3: one per tap, nine in all for
+// the flipped layout and for the four stride-2 phases together): source rows r (A of them, the
+// weight's first index) with the channel c contiguous, destination rows c with r contiguous.
+// One block moves one 64 x 64 tile of one of them through LDS, so both the reads and the writes
+// are coalesced (the element-per-thread gather with 64-bit index divisions took 0.16-0.18 ms per
+// step for 51 MB; profiles/r4_resnet50_step_breakdown_baseline.txt).
 __global__ __launch_bounds__(256) void weight_prep_kernel(const WPrepJob* __restrict__ jobs) {
   const WPrepJob jb = jobs[blockIdx.y];
-  const int A = jb.A, B = jb.B;
-  const int64_t E = (jb.kind == 0 ? 1 : 9) * static_cast<int64_t>(A) * B;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < E; e += static_cast<int64_t>(gridDim.x) * 256) {
-    int64_t so;
-    if (jb.kind == 0) {  // dst[b][a] = src[a][b]
-      const int64_t b = e / A, a = e - b * A;
-      so = a * B + b;
-    } else if (jb.kind == 1) {  // dst[c][kh][kw][n] = src[n][2 - kh][2 - kw][c]
-      const int64_t c = e / (9 * A);
-      const int r = static_cast<int>(e - c * 9 * A), kh = r / (3 * A), kw = (r / A) % 3, n = r % A;
-      so = ((static_cast<int64_t>(n) * 3 + (2 - kh)) * 3 + (2 - kw)) * B + c;
-    } else {  // phases (a, b) = (0,0), (0,1), (1,0), (1,1): [B][nh][nw][A], taps 1 (even) or {2, 0} (odd)
-      const int64_t AB = static_cast<int64_t>(A) * B;
-      int ph;
-      int64_t q;
-      if (e < AB) { ph = 0; q = e; }
-      else if (e < 3 * AB) { ph = 1; q = e - AB; }
-      else if (e < 5 * AB) { ph = 2; q = e - 3 * AB; }
-      else { ph = 3; q = e - 5 * AB; }
-      const int pa = ph >> 1, pb = ph & 1, nh = pa ? 2 : 1, nw = pb ? 2 : 1;
-      const int64_t c1 = q / (nh * nw * A);
-      const int r = static_cast<int>(q - c1 * nh * nw * A), dh = r / (nw * A), dw = (r / A) % nw, c2 = r % A;
-      const int kh = pa ? (dh ? 0 : 2) : 1, kw = pb ? (dw ? 0 : 2) : 1;
-      so = ((static_cast<int64_t>(c2) * 3 + kh) * 3 + kw) * B + c1;
-    }
-    jb.dst[e] = jb.src[so];
+  const int A = jb.A, B = jb.B, ta = (A + 63) / 64, tb = (B + 63) / 64, tiles = ta * tb;
+  const int nsub = jb.kind == 0 ? 1 : 9;
+  const int idx = blockIdx.x;
+  if (idx >= nsub * tiles) return;  // block-uniform
+  const int sub = idx / tiles, ti = idx - sub * tiles, r0 = (ti / tb) * 64, c0 = (ti - (ti / tb) * tb) * 64;
+  int64_t soff = 0, ss = B, doff = 0, ds = A;
+  if (jb.kind == 1) {  // dst[c][kh][kw][r] = src[r][2 - kh][2 - kw][c]
+    const int kh = sub / 3, kw = sub - kh * 3;
+    soff = ((2 - kh) * 3 + (2 - kw)) * static_cast<int64_t>(B);
+    ss = 9 * static_cast<int64_t>(B);
+    doff = sub * static_cast<int64_t>(A);
+    ds = 9 * static_cast<int64_t>(A);
+  } else if (jb.kind == 2) {
+    // phases (0,0) (0,1) (1,0) (1,1) at 0, AB, 3AB, 5AB, each [B][nh][nw][A]; sub -> (phase, dh, dw)
+    const int ph = sub == 0 ? 0 : sub < 3 ? 1 : sub < 5 ? 2 : 3;
+    const int q = sub - (ph == 0 ? 0 : ph == 1 ? 1 : ph == 2 ? 3 : 5);
+    const int pa = ph >> 1, pb = ph & 1, nh = pa ? 2 : 1, nw = pb ? 2 : 1;
+    const int dh = q / nw, dw = q - dh * nw;
+    const int kh = pa ? (dh ? 0 : 2) : 1, kw = pb ? (dw ? 0 : 2) : 1;
+    const int64_t AB = static_cast<int64_t>(A) * B;
+    soff = (kh * 3 + kw) * static_cast<int64_t>(B);
+    ss = 9 * static_cast<int64_t>(B);
+    doff = (ph == 0 ? 0 : ph == 1 ? AB : ph == 2 ? 3 * AB : 5 * AB) + (dh * nw + dw) * static_cast<int64_t>(A);
+    ds = static_cast<int64_t>(nh) * nw * A;
+  }
+  __shared__ uint16_t tile[64][66];
+  const int t = threadIdx.x, tc = t & 63, tr = t >> 6;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + tr + 4 * i, c = c0 + tc;
+    if (r < A && c < B) tile[tr + 4 * i][tc] = jb.src[soff + r * ss + c];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + tr + 4 * i, r = r0 + tc;
+    if (r < A && c < B) jb.dst[doff + c * ds + r] = tile[tc][tr + 4 * i];
   }
 }
 
-void launch_weight_prep(const void* jobs, int njobs, hipStream_t s) {
+void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(weight_prep_kernel, dim3(64, njobs), dim3(256), 0, s, static_cast<const WPrepJob*>(jobs));
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(max_blocks, njobs), dim3(256), 0, s, static_cast<const WPrepJob*>(jobs));
 }
 
 // ------------------------------------------------------------------------------ launchers

@@ -508,13 +508,14 @@ def prepare_backward_weights(blocks) -> None:
                  b.downsample[0].weight.data_ptr() if b.downsample is not None else 0) for b in blks)
     ent = _PREP_CACHE.get(key)
     if ent is None:
-        rows, outs = [], {}
+        rows, outs, nblk = [], {}, [1]
         dev = blks[0].conv1.weight.device
 
         def job(src, kind, a, b):
             n = (1 if kind == 0 else 9) * a * b
             dst = torch.empty(n, dtype=torch.bfloat16, device=dev)
             rows.append([src.data_ptr(), dst.data_ptr(), kind | (a << 32), b])
+            nblk[0] = max(nblk[0], (1 if kind == 0 else 9) * ((a + 63) // 64) * ((b + 63) // 64))
             return dst
 
         for b in blks:
@@ -536,11 +537,11 @@ def prepare_backward_weights(blocks) -> None:
                 wd = b.downsample[0].weight
                 wdt = job(wd, 0, wd.shape[0], wd.shape[1]).view(wd.shape[1], wd.shape[0])
             outs[id(b)] = (w1t, w3t, w2d, wdt, (w1.data_ptr(), w2.data_ptr(), w3.data_ptr()))
-        ent = (torch.tensor(rows, dtype=torch.int64).to(dev), outs)
+        ent = (torch.tensor(rows, dtype=torch.int64).to(dev), outs, nblk[0])
         if len(_PREP_CACHE) >= 4:
             _PREP_CACHE.pop(next(iter(_PREP_CACHE)))
         _PREP_CACHE[key] = ent
-    native().weight_prep(ent[0])
+    native().weight_prep(ent[0], ent[2])
     _tls.prep = ent[1]
 
 
