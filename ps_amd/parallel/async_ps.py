@@ -197,6 +197,9 @@ class AsyncPS:
             raise ValueError("CPU AsyncPS shards are fp32")
         self.staleness = staleness
         self.timeout_s = timeout_s
+        # SSP audit: set to a list to record (clock, gate target, min ack seen) per gated pull --
+        # AsyncRowTable.gate_log records the same triple for the rows (one round window for both)
+        self.gate_log: Optional[list] = None
         self.gscale = (1.0 / W) if gscale is None else float(gscale)
         self.params = dict(params)
         self.overlap = overlap
@@ -468,7 +471,10 @@ class AsyncPS:
         waits on the copy, the host does not."""
         W, L, A = self.world, self.L, self.A
         if gate and self.staleness is not None:
-            A.wait_min_ack(self.ctl, self.clock - int(self.staleness), self.timeout_s)
+            target = self.clock - int(self.staleness)
+            A.wait_min_ack(self.ctl, target, self.timeout_s)
+            if self.gate_log is not None:
+                self.gate_log.append((self.clock, target, min(min(r) for r in A.snapshot(self.ctl)["ack"])))
         pins = [(r, A.pin(self.ctl, r)) for r in range(W)]
         back = 1 - self.cur
         dst = self.flats[back]

@@ -105,6 +105,9 @@ class AsyncRowTable(TcpSparseTable):
         super().__init__(name, dim, rows, _AsyncRowClient(self), updater, init=init, id_mode=id_mode, seed=seed,
                          fields=fields, device=device)
         self.staleness = staleness
+        # SSP audit (AsyncPS.gate_log's twin): a list records (clock, gate target, min applied
+        # row push seen) per gated pull
+        self.gate_log: Optional[list] = None
         self.C = int(capacity)
         self.timeout_s = timeout_s
         self.gpu = self.device.type == "cuda"
@@ -205,13 +208,24 @@ class AsyncRowTable(TcpSparseTable):
         if n > self.C:
             raise RuntimeError(f"async row table {self.name}: {n} keys for one owner exceed capacity {self.C}")
 
+    def _ssp_gate(self) -> None:
+        """SSP(s): every owner applied every worker's first (clock - s) row pushes -- this
+        worker's clock = rounds pushed, the same target AsyncPS's dense gate uses for its pull
+        (host words, no device sync)."""
+        if self.staleness is None or self.W == 1:
+            return
+        W, c = self.W, self.ctl
+        words = [c.pack(o, w) for o in range(W) for w in range(W)]
+        target = self.pushes - int(self.staleness)
+        if target > 0:
+            self.shm.wait_ge(words, target, c.stop, self.timeout_s)
+        if self.gate_log is not None:
+            self.gate_log.append((self.pushes, target, min(self.shm.ld(a) for a in words)))
+
     def _pull(self, ukeys: torch.Tensor) -> torch.Tensor:
         """Rows of the unique ``ukeys`` (CPU int64) -> [n, dim] fp32 on CPU."""
         W, me, c = self.W, self.me, self.ctl
-        if self.staleness is not None and self.W > 1:  # SSP gate over every (owner, worker)
-            target = self.pushes - int(self.staleness)  # this worker's clock = rounds pushed
-            if target > 0:
-                self.shm.wait_ge([c.pack(o, w) for o in range(W) for w in range(W)], target, c.stop, self.timeout_s)
+        self._ssp_gate()
         own = self._owner(ukeys)
         parts = []
         with self._io():
@@ -344,10 +358,7 @@ class AsyncRowTable(TcpSparseTable):
 
     def _pull_dev(self, plan: dict) -> torch.Tensor:
         W, me, c = self.W, self.me, self.ctl
-        if self.staleness is not None and W > 1:  # SSP gate (host words, no device sync)
-            target = self.pushes - int(self.staleness)
-            if target > 0:
-                self.shm.wait_ge([c.pack(o, w) for o in range(W) for w in range(W)], target, c.stop, self.timeout_s)
+        self._ssp_gate()
         self._check_cap(plan["n"])
         self._send(plan["ubuf"], plan["meta"], [self.peer_rq[o][me] for o in range(W)], True, 1)
         self._notify.after(self._io_stream.cuda_stream, self.device.index, [c.req(o, me) for o in range(W)])

@@ -138,6 +138,8 @@ def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0
     s = None if consistency == "asp" else staleness
     m = _build(True, async_table_factory(tp, DEV, seed=7, staleness=s)).to(DEV)
     eng = CollectiveEngine(m, tp, consistency=consistency, staleness=staleness or 0)
+    eng.ps.gate_log = []
+    m.tables()["emF"].gate_log = []
     tr = Trainer(m, eng, device=DEV)
     n = 64
     lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
@@ -159,10 +161,12 @@ def _wide_gpu_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0
     eng.ps.refresh()
     dense = {k: v.detach().float().cpu().clone() for k, v in m.named_parameters()}
     probe = m.tables()["emF"].pull(torch.arange(40).repeat(4, 1).t().contiguous()).cpu()
+    dgates, rgates = list(eng.ps.gate_log), list(m.tables()["emF"].gate_log)
     eng.ps.close()
     for t in m.tables().values():
         t.close()
-    return {"losses": losses, "dlead": dlead, "rlead": rlead, "skew": skew, "dense": dense, "probe": probe}
+    return {"losses": losses, "dlead": dlead, "rlead": rlead, "skew": skew, "dense": dense, "probe": probe,
+            "dgates": dgates, "rgates": rgates}
 
 
 @pytest.mark.parametrize("consistency,staleness", [("asp", None), ("ssp", 1)])
@@ -185,3 +189,12 @@ def test_ssp1_straggler_bound_dense_and_rows_gpu():
     # slowest worker's dense and row clocks seen together never drift more than the bound apart
     for r in res:
         assert max(abs(k) for k in r["skew"]) <= 2, r["skew"]  # staleness 1 + one push in flight
+        # one forward's dense pull and row pull: the same gate target c - 1 and both views inside
+        # [c - 1, c] (tests/test_async_rows_cpu.py, the CPU twin)
+        dense = {c: (t, seen) for c, t, seen in r["dgates"]}
+        rows = {c: (t, seen) for c, t, seen in r["rgates"]}
+        common = sorted(set(dense) & set(rows))
+        assert len(common) >= 8, (r["dgates"], r["rgates"])
+        for c in common:
+            assert dense[c][0] == rows[c][0] == c - 1
+            assert c - 1 <= dense[c][1] <= c and c - 1 <= rows[c][1] <= c, (c, dense[c], rows[c])

@@ -52,6 +52,8 @@ def _wide_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0):
     s = None if consistency == "asp" else staleness
     m = _build(True, async_table_factory(tp, None, seed=7, staleness=s))
     eng = CollectiveEngine(m, tp, consistency=consistency, staleness=staleness or 0)
+    eng.ps.gate_log = []
+    m.tables()["emF"].gate_log = []
     tr = Trainer(m, eng)
     n = 64
     lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
@@ -73,10 +75,12 @@ def _wide_body(tp, consistency, staleness, steps, delay_rank=-1, delay_s=0.0):
     dense = {k: v.detach().clone() for k, v in m.named_parameters()}
     probe = m.tables()["emF"].pull(torch.arange(40).repeat(4, 1).t().contiguous())
     segs = [u.name.split("@")[0] for u, _, _ in eng.ps.segs]
+    dgates, rgates = list(eng.ps.gate_log), list(m.tables()["emF"].gate_log)
     eng.ps.close()
     for t in m.tables().values():
         t.close()
-    return {"losses": losses, "dlead": dlead, "rlead": rlead, "dense": dense, "probe": probe, "segs": segs}
+    return {"losses": losses, "dlead": dlead, "rlead": rlead, "dense": dense, "probe": probe, "segs": segs,
+            "dgates": dgates, "rgates": rgates}
 
 
 @pytest.mark.parametrize("consistency,staleness", [("asp", None), ("ssp", 1)])
@@ -99,6 +103,28 @@ def test_ssp_straggler_bound_holds_on_dense_and_rows():
     fast = res[0]
     assert max(fast["dlead"]) <= s + 1, fast["dlead"]
     assert max(fast["rlead"]) <= s + 1, fast["rlead"]
+
+
+def test_ssp_dense_and_row_gates_share_one_round_window():
+    """The dense weights (AsyncPS pull at the end of step k) and the rows (AsyncRowTable pull in
+    step k + 1's forward) that one forward sees are gated on the SAME clock target c - s and
+    both include every worker's first c - s pushes and at most this worker's c (c = rounds this
+    worker pushed): one round window [c - s, c] for both views."""
+    s = 1
+    res = dist_util.run(_wide_body, 2, ("ssp", s, 10, 1, 0.15))
+    for r in res:
+        dense = {c: (t, seen) for c, t, seen in r["dgates"]}
+        rows = {c: (t, seen) for c, t, seen in r["rgates"]}
+        common = sorted(set(dense) & set(rows))
+        assert len(common) >= 8, (r["dgates"], r["rgates"])
+        for c in common:
+            (td, sd), (tr, sr) = dense[c], rows[c]
+            assert td == tr == c - s
+            assert c - s <= sd <= c and c - s <= sr <= c, (c, sd, sr)
+    # the straggler holds the fast worker at the window's lower edge: the gate was binding
+    fast = res[0]
+    assert any(seen == c - s for c, _, seen in fast["dgates"] if c > s)
+    assert any(seen == c - s for c, _, seen in fast["rgates"] if c > s)
 
 
 def test_asp_straggler_runs_ahead_on_dense_and_rows():
