@@ -912,12 +912,24 @@ std::vector<Tensor> stem_conv_fwd(Tensor x, Tensor wp, c10::optional<Tensor> ksh
 // BN statistics from producer partial sums: part [2, G, C] about kshift over R rows.
 // [2, G, C] partials -> a [2, S, C] first-level fold when G is tall (S = partials_fold_rows(G)),
 // else the input itself
+// part [2, G, C] with contiguous slabs (part.stride(0) >= G * C: e.g. slabs 0 and 2 of a [3, G, C]
+// epilogue-9 part, no stacking copy); the second slab starts part.stride(0) floats after the first
+static bool slabs_ok(const Tensor& part) {
+  return part.dim() == 3 && part.size(0) == 2 && part.stride(2) == 1 && part.stride(1) == part.size(2) &&
+         part.stride(0) >= part.size(1) * part.size(2);
+}
+
+static void check_part_slabs(const Tensor& part) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32, "part must be a float32 GPU tensor");
+  TORCH_CHECK(slabs_ok(part), "part [2, G, C] (contiguous slabs)");
+}
+
 static Tensor fold_partials(const Tensor& part, hipStream_t s) {
   const int G = static_cast<int>(part.size(1)), C = static_cast<int>(part.size(2));
   const int S = psamd::partials_fold_rows(G);
   if (S == 0) return part;
   auto f = torch::empty({2, S, C}, part.options());
-  psamd::launch_partials_fold(part.data_ptr<float>(), part.data_ptr<float>() + static_cast<int64_t>(G) * C, G, C,
+  psamd::launch_partials_fold(part.data_ptr<float>(), part.data_ptr<float>() + part.stride(0), G, C,
                               f.data_ptr<float>(), f.data_ptr<float>() + static_cast<int64_t>(S) * C, s);
   return f;
 }
@@ -1388,6 +1400,44 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dz, std::vector<Tensor> wph, int64_t H,
   }
   const c10::DeviceGuard guard(dz.device());
   auto dx = torch::empty({imgs * H * W, C1}, dz.options());
+  static const bool merged = [] {
+    const char* e = std::getenv("PS_AMD_DGRAD_S2_MERGED");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (merged) {  // the four phases in one grid (csrc convgemm.hip conv_dgrad_phases_kernel)
+    std::vector<Tensor> ws;  // (stream-ordered lifetime, as in the per-phase path)
+    ws.reserve(4);
+    psamd::ConvGemmArgs ps[4] = {};
+    const int gm = psamd::conv_dgrad_phase_gm(static_cast<int>(M));
+    Tensor part = epi == 3 ? torch::empty({2, 4 * gm, C1}, dz.options().dtype(torch::kFloat32)) : Tensor();
+    for (int ph = 0; ph < 4; ++ph) {
+      const int a = ph >> 1, b = ph & 1, nh = a ? 2 : 1, nw = b ? 2 : 1;
+      ws.push_back(wph[ph].contiguous());
+      const Tensor& w = ws.back();
+      check_rows(w, "phase weight");
+      TORCH_CHECK(w.dim() == 2 && w.size(0) == C1 && w.size(1) == nh * nw * C2, "phase weight [C1, nh*nw*C2]");
+      psamd::ConvGemmArgs& p = ps[ph];
+      p.a = u16(dz);
+      p.b = u16(w);
+      p.c = u16m(dx);
+      p.M = static_cast<int>(M);
+      p.N = static_cast<int>(C1);
+      p.K = static_cast<int>(nh * nw * C2);
+      p.g = psamd::ConvGeo{static_cast<int>(OH), static_cast<int>(OW), static_cast<int>(OH), static_cast<int>(OW),
+                           static_cast<int>(C2), nh, 1, 0, nw, static_cast<int>(H), static_cast<int>(W), a, b};
+      p.epi = static_cast<int>(epi);
+      if (epi == 3) {
+        p.aux = zp;
+        p.mc = f32_opt(mc, 2 * C1, "mc");
+        p.mean = f32_opt(mean, C1, "mean");
+        p.invstd = f32_opt(invstd, C1, "invstd");
+        p.part = part.data_ptr<float>() + static_cast<int64_t>(ph) * gm * C1;  // rows [ph gm, (ph + 1) gm)
+        p.pgm = 4 * gm;
+      }
+    }
+    psamd::launch_conv_dgrad_phases(ps, cur_stream(dz));
+    return {dx, part};
+  }
   std::vector<Tensor> parts;
   for (int ph = 0; ph < 4; ++ph) {
     const int a = ph >> 1, b = ph & 1, nh = a ? 2 : 1, nw = b ? 2 : 1;
@@ -1524,8 +1574,7 @@ void weight_prep(Tensor jobs, int64_t max_blocks) {
 // BN backward coefficients only (dx = ca * g + cb * x + cc for a GEMM prologue to apply) from
 // producer partial sums part [2, G, C] over R rows -> [dgamma, dbeta, coef = ca | cb | cc]
 std::vector<Tensor> bn_bwd_coef(Tensor part, c10::optional<Tensor> gamma, Tensor mean, Tensor invstd, int64_t R) {
-  check_f32(part, "part");
-  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.is_contiguous(), "part [2, G, C]");
+  check_part_slabs(part);
   const int64_t C = part.size(2);
   TORCH_CHECK(C % 8 == 0, "C % 8");
   const c10::DeviceGuard guard(part.device());
@@ -1533,7 +1582,7 @@ std::vector<Tensor> bn_bwd_coef(Tensor part, c10::optional<Tensor> gamma, Tensor
   auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt), coef = torch::empty({3 * C}, fopt);
   const Tensor fp = fold_partials(part, cur_stream(part));
   const int64_t Gf = fp.size(1);
-  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + Gf * C, static_cast<int>(Gf), nullptr,
+  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + fp.stride(0), static_cast<int>(Gf), nullptr,
                                 nullptr, f32_opt(gamma, C, "gamma"), f32_opt(mean, C, "mean"), f32_opt(invstd, C, "invstd"),
                                 dg.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), nullptr, R,
                                 static_cast<int>(C), cur_stream(part));
@@ -1547,15 +1596,15 @@ std::vector<Tensor> bn_bwd_partials(Tensor g, Tensor x, Tensor part, c10::option
   check_rows(x, "x");
   TORCH_CHECK(x.dim() == 2 && g.sizes() == x.sizes() && x.size(1) % 8 == 0, "g/x [R, C], C % 8");
   const int64_t R = x.size(0), C = x.size(1);
-  check_f32(part, "part");
-  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.size(2) == C && part.is_contiguous(), "part [2, G, C]");
+  check_part_slabs(part);
+  TORCH_CHECK(part.size(2) == C, "part [2, G, C]");
   const c10::DeviceGuard guard(x.device());
   auto fopt = x.options().dtype(torch::kFloat32);
   auto dx = torch::empty_like(x);
   auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt), coef = torch::empty({3 * C}, fopt);
   const Tensor fp = fold_partials(part, cur_stream(x));
   const int64_t Gf = fp.size(1);
-  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + Gf * C, static_cast<int>(Gf), u16(g), u16(x),
+  psamd::launch_bn_bwd_partials(fp.data_ptr<float>(), fp.data_ptr<float>() + fp.stride(0), static_cast<int>(Gf), u16(g), u16(x),
                                 f32_opt(gamma, C, "gamma"), f32_opt(mean, C, "mean"), f32_opt(invstd, C, "invstd"),
                                 dg.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), u16m(dx), R,
                                 static_cast<int>(C), cur_stream(x));

@@ -348,11 +348,16 @@ struct ConvGemmArgs {
   const float* pro2;    // [2C]; nullable
   uint8_t* abits;
   FastDiv fd_ohw, fd_ow;  // set by launch_conv_fwd (OH * OW, OW)
+  int pgm;                // rows per partial slab (0: the launch's gm); several GEMMs share one part
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
+// the four stride-2 data-gradient phase GEMMs (epi 3, no prologue, LDS-DMA staging, 128-pixel tiles)
+// in one launch; phase i's partials go to rows [sum gm(<i), ..) of a part with pgm = sum of gm
+void launch_conv_dgrad_phases(const ConvGemmArgs* ph, hipStream_t s);
+int conv_dgrad_phase_gm(int M);
 // the plan launch_conv_fwd uses for this geometry (the 3x3 patch-staged tiles where they apply)
 // src2: the launch's two-source prologue (0 none, 1 block output, 2 BN backward)
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2 = 0);

@@ -232,8 +232,10 @@ constexpr int patch_bytes() { return BN == 64 ? 65536 : 40960; }  // 8 channel p
 
 // VAR: 0 the plain paths, 1 PATCH (3x3 patch-staged tiles), 2 the plain LDS-DMA path with a
 // 3-stage ring (two stages in flight behind the MFMAs; one block per CU by LDS)
+// The kernel body takes its logical block id L (XCD-remapped) from the launching kernel: conv_fwd_kernel
+// (one GEMM per launch) or conv_dgrad_phases_kernel (the four stride-2 data-gradient phases in one grid).
 template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, int VAR = 0>
-__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
+__device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int L) {
   constexpr bool BWD = PRO == 2;
   constexpr bool RESP = PRO == 3;
   static_assert(!BWD || (KS1 && EPI == 3), "the BN-backward prologue is a 1x1 data-gradient prologue");
@@ -287,8 +289,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
   // per-wave addresses stay in SGPRs instead of VALU + v_readfirstlane per instruction
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nN = p.N / BN, mtiles = (p.M + BM - 1) / BM;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int mg = L / nN, n0 = (L - mg * nN) * BN;
+  if (mg >= GM) return;  // (block-uniform) padding blocks of a phase-merged grid
   const int nk = p.K / kBK;
   const int my_tiles = mg < mtiles ? (mtiles - mg + GM - 1) / GM : 0;
   const int nq = my_tiles * nk;  // block-uniform
@@ -1009,15 +1011,42 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, 
       }
     }
     lds_barrier();
+    const int64_t PG = p.pgm > 0 ? p.pgm : GM;  // rows per partial slab
     for (int c = t; c < BN; c += 256) {
       p.part[mg * static_cast<int64_t>(p.N) + n0 + c] = (red[c] + red[BN + c]) + (red[2 * BN + c] + red[3 * BN + c]);
-      p.part[(static_cast<int64_t>(GM) + mg) * p.N + n0 + c] =
-          (red[4 * BN + c] + red[5 * BN + c]) + (red[6 * BN + c] + red[7 * BN + c]);
+      p.part[(PG + mg) * p.N + n0 + c] = (red[4 * BN + c] + red[5 * BN + c]) + (red[6 * BN + c] + red[7 * BN + c]);
       if constexpr (FOLD_DS)
-        p.part[(2 * static_cast<int64_t>(GM) + mg) * p.N + n0 + c] =
+        p.part[(2 * PG + mg) * p.N + n0 + c] =
             (red[8 * BN + c] + red[9 * BN + c]) + (red[10 * BN + c] + red[11 * BN + c]);
     }
   }
+}
+
+template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, int VAR = 0>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const ConvGemmArgs p, int GM) {
+  conv_fwd_body<BM, BN, PRO, EPI, KS1, GLDS, VAR>(p, GM, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// The four phase GEMMs of a stride-2 3x3 data gradient (conv_dgrad_s2) in ONE grid: blocks
+// [start[i], start[i + 1]) run phase order[i], heaviest (2 x 2 taps) first so the 1-tap phase
+// fills the tail.  Every range starts at a multiple of 8, so the XCD remap stays local to it.
+// Sequential launches left the chip idle in each launch's tail and ran the 1-tap phase (two
+// 64-deep stages per tile) alone at its HBM-latency bound.
+struct ConvPhaseArgs {
+  ConvGemmArgs ph[4];
+  int start[5];  // block ranges in launch order
+  int order[4];  // phase of each range
+  int gm[4];     // pixel tiles of each phase (one tile per block)
+};
+
+template <int BN, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_phases_kernel(const ConvPhaseArgs P) {
+  static_assert(EPI == 0 || EPI == 3, "plain store or the ReLU-mask + BN-backward-sums epilogue");
+  const int b = blockIdx.x;
+  const int i = b >= P.start[3] ? 3 : b >= P.start[2] ? 2 : b >= P.start[1] ? 1 : 0;
+  const int ph = P.order[i];
+  conv_fwd_body<128, BN, 0, EPI, false, true, 0>(P.ph[ph], P.gm[ph],
+                                                 xcd_remap(b - P.start[i], P.start[i + 1] - P.start[i]));
 }
 
 // ------------------------------------------------------------------------------ conv3x3 64 -> 64
@@ -2257,6 +2286,36 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
 #undef PSAMD_CF2
 #undef PSAMD_CF3
 #undef PSAMD_CF3V
+}
+
+int conv_dgrad_phase_gm(int M) { return (M + 127) / 128; }
+
+void launch_conv_dgrad_phases(const ConvGemmArgs* ph, hipStream_t s) {
+  ConvPhaseArgs P{};
+  const int N = ph[0].N;
+  const int bn = N % 128 == 0 ? 128 : 64;
+  static constexpr int kOrder[4] = {3, 1, 2, 0};  // taps 4, 2, 2, 1
+  int at = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int q = kOrder[i];
+    P.ph[q] = ph[q];
+    P.ph[q].fd_ohw = make_fastdiv(static_cast<uint32_t>(ph[q].g.OH * ph[q].g.OW));
+    P.ph[q].fd_ow = make_fastdiv(static_cast<uint32_t>(ph[q].g.OW));
+    P.gm[q] = conv_dgrad_phase_gm(ph[q].M);
+    P.order[i] = q;
+    P.start[i] = at;
+    at += (P.gm[q] * (N / bn) + 7) / 8 * 8;  // ranges start at multiples of 8 (XCD-local remap)
+  }
+  P.start[4] = at;
+  if (at == 0) return;
+  const bool e3 = ph[0].epi == 3;  // (the binding allows 0 or 3 and sets the part / aux / mc of epi 3)
+  if (bn == 128) {
+    if (e3) hipLaunchKernelGGL((conv_dgrad_phases_kernel<128, 3>), dim3(at), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((conv_dgrad_phases_kernel<128, 0>), dim3(at), dim3(256), 0, s, P);
+  } else {
+    if (e3) hipLaunchKernelGGL((conv_dgrad_phases_kernel<64, 3>), dim3(at), dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((conv_dgrad_phases_kernel<64, 0>), dim3(at), dim3(256), 0, s, P);
+  }
 }
 
 namespace {

@@ -348,7 +348,7 @@ class _BottleneckFn(torch.autograd.Function):
         gi, go = geo(h, w), geo(oh, ow)
         d2 = rows(dout)
         # weight gradients run on the side stream, overlapped with this data-gradient chain
-        sd = _side.Fork(d2.device, (w1, w2, w3, wd))
+        sd = _side.Fork(d2.device, (w1, w2, w3, wd), images=n)
         pw = ctx.prep
         w3t = pw[1] if pw else _mat(w3).t()
         lk = ctx.link_out
@@ -358,7 +358,7 @@ class _BottleneckFn(torch.autograd.Function):
                 and d2._version == lk.dx_version):
             # the consumer block already masked dout and reduced bn3's backward sums
             if lk.part.shape[0] == 3:
-                ds_part = torch.stack([lk.part[0], lk.part[2]])
+                ds_part = lk.part[0::2]  # sum(g), sum(g * xhat_d): a strided view, no copy
                 lk.part = lk.part[:2]
                 FOLD_STATS["ds"] += 1
             if _bwd_prologue_enabled(z3.shape[1], w3.shape[1]):

@@ -20,11 +20,13 @@ Protocol (``Fork``):
   * consumers that read gradients DURING backward (the parameter-server bucket hooks,
     parallel/colocated.py ``_launch``) call ``join(stream)`` before reading.
 
-Opt-in (``PS_AMD_WGRAD_STREAM=1``): measured on ResNet-50 bs1024 the streams overlap for 29 ms
-of the 77 ms step, but the compute stream's HBM-bound kernels stretch by about as much as the
-weight gradients hide (profiles/r3_wgrad_side_stream_ab.txt: -1.5 %), so one stream is the
-default.  Also off on CPU, under graph capture, and when a parameter already holds a gradient
-(micro-batch accumulation would make AccumulateGrad add on the compute stream).
+Policy (``enabled``): on for per-GPU batches up to 512 images, where the layer-3/4 grids leave
+CUs idle (ResNet-50 bs256 +0.6 / +2.4 %); off above, where the compute stream's HBM-bound kernels
+stretch by about as much as the weight gradients hide (round 3 at bs1024: -1.5 %,
+profiles/r3_wgrad_side_stream_ab.txt; round 4: neutral, profiles/r4_wgrad_stream_policy.txt).
+``PS_AMD_WGRAD_STREAM=1`` / ``0`` forces it.  Also off on CPU, under graph capture, and when a
+parameter already holds a gradient (micro-batch accumulation would make AccumulateGrad add on the
+compute stream).
 """
 from __future__ import annotations
 
@@ -38,8 +40,15 @@ _STREAMS: Dict[int, torch.cuda.Stream] = {}
 _lock = threading.Lock()
 
 
-def enabled() -> bool:
-    return os.environ.get("PS_AMD_WGRAD_STREAM", "0") == "1"
+def enabled(images: Optional[int] = None) -> bool:
+    """PS_AMD_WGRAD_STREAM=1: always, 0: never; unset / auto: for batches of at most
+    PS_AMD_WGRAD_STREAM_MAX_IMAGES (512) images per GPU -- ResNet-50 bs256 +0.6 / +2.4 % on two
+    boxes, bs1024 neutral (profiles/r4_wgrad_stream_policy.txt); per-layer row thresholds
+    (layers 3-4 only, or 2-4) measured below all-layers at bs256 and below off at bs1024."""
+    mode = os.environ.get("PS_AMD_WGRAD_STREAM", "auto")
+    if mode in ("0", "1"):
+        return mode == "1"
+    return images is not None and images <= int(os.environ.get("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "512"))
 
 
 def side_stream(device: torch.device) -> torch.cuda.Stream:
@@ -83,8 +92,8 @@ def _match_layout(g: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
 class Fork:
     """Per-backward helper (see module docstring)."""
 
-    def __init__(self, device: torch.device, params=()):
-        self.on = (enabled() and device.type == "cuda" and not torch.cuda.is_current_stream_capturing()
+    def __init__(self, device: torch.device, params=(), images: Optional[int] = None):
+        self.on = (enabled(images) and device.type == "cuda" and not torch.cuda.is_current_stream_capturing()
                    and all(p is None or p.grad is None for p in params))
         self.queued = False
         if self.on:

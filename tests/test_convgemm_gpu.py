@@ -321,6 +321,15 @@ def test_bn_apply_coef_and_backward_from_partials():
     _close(dx, ref_dx)
     torch.testing.assert_close(db.cpu(), gr.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(dg.cpu(), (gr * xhat).sum(0), rtol=1e-4, atol=1e-3)
+    # strided slabs (slabs 0 and 2 of an epilogue-9 [3, G, C] part, as the downsample BN gets
+    # them) == the same slabs stacked contiguously -- bitwise, also through the tall-partials fold
+    for G in (1, 3000):
+        p3 = torch.randn(3, G, C, generator=g).to(DEV)
+        want = native().bn_bwd_partials(_bf(gr), _bf(x), p3[0::2].contiguous(), gamma.to(DEV), mean.to(DEV),
+                                        invstd.to(DEV))
+        got = native().bn_bwd_partials(_bf(gr), _bf(x), p3[0::2], gamma.to(DEV), mean.to(DEV), invstd.to(DEV))
+        for u, v in zip(want, got):
+            assert torch.equal(u, v)
 
 
 @pytest.mark.parametrize("conv3x3", ["1", "0"])
