@@ -142,37 +142,32 @@ __device__ __forceinline__ void stage_window(const uint16_t* __restrict__ x, uin
 // registers, publish the prefetched rows to LDS, THEN issue this row's output stores and pass
 // an LDS-only barrier -- CDNA4's vmcnt counts stores too, so waiting for the prefetch before
 // the stores are issued keeps the output stream from being drained every row.
-__global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
-                                                            const uint16_t* __restrict__ wp,
-                                                            uint16_t* __restrict__ z, int N, int H, int W, int OH,
-                                                            int OW, int splits, int rpb, int cin,
-                                                            const float* __restrict__ kshift,
-                                                            float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 1024];
-  uint16_t* lds_in = lds;
-  uint16_t* lds_red = lds + kSlots * kRS;  // 512 floats for the statistics combine
+// Wave w owns output channels [16w, 16w + 16) of every pixel tile of the row: its weight
+// fragments are 28 VGPRs (a 2 x 2 wave grid held 56) and the kernel fits 128 VGPRs, i.e. four
+// blocks per CU instead of two -- the row loop is latency-bound, so rows in flight per CU set
+// the rate (0.79 ms -> see profiles/r4_stem_fwd_occupancy_ab.txt at bs1024).
+__global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ wp,
+                                                               uint16_t* __restrict__ z, int N, int H, int W, int OH,
+                                                               int OW, int splits, int rpb, int cin,
+                                                               const float* __restrict__ kshift,
+                                                               float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds_in[kSlots * kRS];
   const int n = blockIdx.x / splits, chunk = blockIdx.x - n * splits;
   const int oh0 = chunk * rpb, oh1 = min(OH, oh0 + rpb);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  // 2 x 2 wave grid: wave (wm, wn) computes M-tiles wm, wm+2, wm+4, wm+6 and N-tiles 2wn, 2wn+1
-  const int wm = wave & 1, wn = wave >> 1;
-  // fused BN statistics from the accumulators: the lane keeps channels 32*wn + 16*j + 4*g + r of
-  // its pixels; combined across the 16 pixel lanes and the 2 M-waves at the end
-  float s1[2][4], s2[2][4], ks[2][4];
+  const int c0 = 16 * wave + 4 * g;  // this lane's 4 output channels c0 .. c0 + 3
+  // fused BN statistics from the accumulators (combined across the 16 pixel lanes at the end)
+  float s1[4], s2[4], ks[4];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int r = 0; r < 4; ++r) {
+    s1[r] = s2[r] = 0.f;
+    ks[r] = part ? kshift[c0 + r] : 0.f;
+  }
+  bf16x8_t bw[7];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      s1[j][r] = s2[j][r] = 0.f;
-      ks[j][r] = part ? kshift[32 * wn + 16 * j + 4 * g + r] : 0.f;
-    }
-  bf16x8_t bw[2][7];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int kh = 0; kh < 7; ++kh)
-      bw[j][kh] = *reinterpret_cast<const bf16x8_t*>(wp + (32 * wn + 16 * j + fr) * kKp + kh * 32 + 8 * g);
+  for (int kh = 0; kh < 7; ++kh) bw[kh] = *reinterpret_cast<const bf16x8_t*>(wp + (16 * wave + fr) * kKp + kh * 32 + 8 * g);
   if (oh0 < oh1) stage_window(x, lds_in, n, oh0, H, W, cin);  // block-uniform
   __syncthreads();
   const int mtiles = (OW + 15) / 16;  // <= 8
@@ -180,76 +175,58 @@ __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const uint16_t* __re
     RowPrefetch<256> pf;
     const bool more = oh + 1 < oh1;
     if (more) pf.load(x, threadIdx.x, n, 2 * oh + 4, H, W, cin);
-    f32x4v acc[4][2];
+    f32x4v acc[8];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      acc[t][0] = acc[t][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      const int mi = wm + 2 * t;
-      if (mi < mtiles) {  // wave-uniform
-        const int ow = 16 * mi + fr;  // pixels >= OW read finite staged data and are never stored
+    for (int t = 0; t < 8; ++t) {
+      acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (t < mtiles) {  // block-uniform
+        const int ow = 16 * t + fr;  // pixels >= OW read finite staged data and are never stored
 #pragma unroll
         for (int kh = 0; kh < 7; ++kh) {
           const int slot = (2 * oh - 3 + kh) & (kSlots - 1);
           const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(lds_in + slot * kRS + 8 * ow + 8 * g);
           // D[co][pixel] = W . patch^T: the lane ends up with 4 consecutive channels of one pixel
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], a, acc[t][j], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[kh], a, acc[t], 0, 0, 0);
         }
       }
     }
     if (more) pf.store(lds_in, threadIdx.x, 2 * oh + 4);  // ring slots not read by rows oh-1, oh
     uint16_t* zo = z + (static_cast<int64_t>(n) * OH + oh) * OW * 64;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ow = 16 * (wm + 2 * t) + fr;
-      if (ow < OW) {
+    for (int t = 0; t < 8; ++t) {
+      const int ow = 16 * t + fr;
+      if (t < mtiles && ow < OW) {
+        // C layout: row (channel) = 16 wave + 4 g + r, col (pixel) = fr -> one 8-B store per tile
+        uint16_t h[4];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          // C layout: row (channel) = 16*nt + 4*g + r, col (pixel) = fr -> one 8-B store per tile
-          uint16_t h[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            h[r] = f32_to_bf16(acc[t][j][r]);
-            if (part) {  // statistics of the bf16 values stored
-              const float d = bf16_to_f32(h[r]) - ks[j][r];
-              s1[j][r] += d;
-              s2[j][r] += d * d;
-            }
+        for (int r = 0; r < 4; ++r) {
+          h[r] = f32_to_bf16(acc[t][r]);
+          if (part) {  // statistics of the bf16 values stored
+            const float d = bf16_to_f32(h[r]) - ks[r];
+            s1[r] += d;
+            s2[r] += d * d;
           }
-          *reinterpret_cast<uint2*>(zo + ow * 64 + 32 * wn + 16 * j + 4 * g) =
-              make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
         }
+        *reinterpret_cast<uint2*>(zo + ow * 64 + c0) =
+            make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
       }
     }
     lds_barrier();
   }
-  if (part) {  // fixed-order combine: the 16 pixel lanes (xor shuffles), then the 2 M-waves
-    float* red = reinterpret_cast<float*>(lds_red);
+  if (part) {  // fixed-order combine over the 16 pixel lanes (xor shuffles); waves own disjoint channels
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          s1[j][r] += __shfl_xor(s1[j][r], off, 64);
-          s2[j][r] += __shfl_xor(s2[j][r], off, 64);
-        }
+      for (int off = 1; off < 16; off <<= 1) {
+        s1[r] += __shfl_xor(s1[r], off, 64);
+        s2[r] += __shfl_xor(s2[r], off, 64);
+      }
     if (fr == 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = 32 * wn + 16 * j + 4 * g + r;
-          red[wm * 64 + c] = s1[j][r];
-          red[128 + wm * 64 + c] = s2[j][r];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      const int c = threadIdx.x;
-      part[static_cast<int64_t>(blockIdx.x) * 64 + c] = red[c] + red[64 + c];
-      part[(static_cast<int64_t>(gridDim.x) + blockIdx.x) * 64 + c] = red[128 + c] + red[192 + c];
+      for (int r = 0; r < 4; ++r) {
+        part[static_cast<int64_t>(blockIdx.x) * 64 + c0 + r] = s1[r];
+        part[(static_cast<int64_t>(gridDim.x) + blockIdx.x) * 64 + c0 + r] = s2[r];
+      }
     }
   }
 }
