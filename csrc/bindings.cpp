@@ -1323,12 +1323,12 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   auto fopt = a.options().dtype(torch::kFloat32);
   const bool has_pro = pro.has_value() && pro->defined();
   const int G = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
-                                        has_pro || has_bwd, g, resp ? 1 : has_bwd ? 2 : 0).gm;
+                                        has_pro || has_bwd, g, resp ? 1 : has_bwd ? 2 : 0, static_cast<int>(epi)).gm;
   b = b.contiguous();  // b may be a strided view (e.g. a transposed weight)
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;
   TORCH_CHECK(epi != 9 || psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
-                                                   has_pro || has_bwd, g).bm == 128,
+                                                   has_pro || has_bwd, g, 0, static_cast<int>(epi)).bm == 128,
               "epi 9 runs on the 128-pixel tiles");
   Tensor part = sums ? torch::empty({epi == 9 ? 3 : 2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};

@@ -353,14 +353,15 @@ struct ConvGemmArgs {
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
-ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro);
+// epi: the fold epilogues (6-9) may run on one-tile-per-block LDS-DMA grids (PS_AMD_FOLD_GLDS)
+ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi = 0);
 // the four stride-2 data-gradient phase GEMMs (epi 3, no prologue, LDS-DMA staging, 128-pixel tiles)
 // in one launch; phase i's partials go to rows [sum gm(<i), ..) of a part with pgm = sum of gm
 void launch_conv_dgrad_phases(const ConvGemmArgs* ph, hipStream_t s);
 int conv_dgrad_phase_gm(int M);
 // the plan launch_conv_fwd uses for this geometry (the 3x3 patch-staged tiles where they apply)
 // src2: the launch's two-source prologue (0 none, 1 block output, 2 BN backward)
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2 = 0);
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2 = 0, int epi = 0);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)

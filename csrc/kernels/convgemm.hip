@@ -2090,7 +2090,7 @@ bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
   return pro && src2 == 0 && g.ks == 1 && g.ksw <= 1 && g.stride == 1 && g.pad == 0 && K / kBK >= pro_glds_min_nk();
 }
 
-ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2) {
+ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
   if (src2 == 0 && c64_ok(g, N, pro)) {  // persistent row-tile patch kernel, one block per CU
     ConvFwdPlan pl;
     pl.bm = 128;
@@ -2118,10 +2118,21 @@ ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, i
     pl.gm = (M + 127) / 128;
     return pl;
   }
-  return conv_fwd_plan(M, N, K, pro);
+  return conv_fwd_plan(M, N, K, pro, epi);
 }
 
-ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
+// The fold epilogues (6-9: residual + mask + the previous block's BN-backward sums) over shallow K
+// on one-tile-per-block LDS-DMA grids instead of the persistent register-staged grid, whose
+// epilogue-9 variant spills (PS_AMD_FOLD_GLDS=1)
+bool fold_glds(int epi, bool pro) {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_FOLD_GLDS");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on && epi >= 6 && !pro;
+}
+
+ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi) {
   ConvFwdPlan pl;
   if (!pro && N == 64 && K / kBK >= 8 && tall_enabled()) {  // 64-channel 3x3 (K = 576): 256 x 64 tiles
     pl.bm = 256;
@@ -2135,7 +2146,7 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro) {
   const int nk = K / kBK;
   // (a persistent grid for the read-heavy data-gradient epilogues measured no faster at 4-16
   // stages: scripts/probe_dgrad_epi.py)
-  const bool persist = nk <= 2 || (pro && nk <= persist_nk_pro());
+  const bool persist = !fold_glds(epi, pro) && (nk <= 2 || (pro && nk <= persist_nk_pro()));
   pl.gm = !persist ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
   return pl;
 }
@@ -2148,7 +2159,7 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const bool bwd = a.bwd != nullptr;
   const bool resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
   const int src2 = resp ? 1 : bwd ? 2 : 0;
-  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2);
+  const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2, a.epi);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   if (src2 == 0 && c64_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
@@ -2202,7 +2213,8 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
   // deep K without the BN prologue: LDS-DMA staging (one tile per block); PS_AMD_GLDS_STAGES=3:
   // a 3-stage ring (one block per CU) for K >= 64 x PS_AMD_GLDS_DEEP_MIN_NK
-  const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
+  const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm &&
+                    (a.K / kBK > 2 || fold_glds(a.epi, false));
   static const int stages = [] {
     const char* e = std::getenv("PS_AMD_GLDS_STAGES");
     return e ? std::atoi(e) : 2;
