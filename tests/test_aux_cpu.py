@@ -148,3 +148,21 @@ def test_fault_kill_at_step_exits_the_rank():
                        env={**os.environ, "PS_AMD_FAULT": "kill:rank=0:step=2"})
     assert r.returncode == 17, r.stderr[-2000:]
     assert r.stdout.split() == ["step", "0", "step", "1"]
+
+
+def test_wgrad_side_stream_policy(monkeypatch):
+    """ops/side_stream.enabled: on for per-GPU batches <= PS_AMD_WGRAD_STREAM_MAX_IMAGES (512) by
+    default (profiles/r4_wgrad_stream_policy.txt), PS_AMD_WGRAD_STREAM=0 / 1 forces it; a Fork on
+    the CPU never turns on."""
+    from ps_amd.ops import side_stream as side
+
+    monkeypatch.delenv("PS_AMD_WGRAD_STREAM", raising=False)
+    monkeypatch.delenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", raising=False)
+    assert side.enabled(256) and side.enabled(512) and not side.enabled(1024) and not side.enabled()
+    monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "2048")
+    assert side.enabled(1024)
+    monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "0")
+    assert not side.enabled(256)
+    monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "1")
+    assert side.enabled(4096) and side.enabled()
+    assert not side.Fork(torch.device("cpu"), (), images=8).on
