@@ -22,7 +22,10 @@ namespace psamd {
 // LCV >= 0 (C / 8 a power of two, 2^LCV): one output row (n, oh) per block iteration, its
 // (ow, channel-group) elements over the threads by shift / mask -- no per-element division (the
 // generic mapping's three runtime-divisor div/mods were most of these kernels' instructions).
-template <bool BN, typename IDX>
+// K3 (with BN, k = 3): the nine window taps are loaded together (clamped in bounds, flagged) before
+// any is used -- the runtime-k loop with its boundary `continue`s issued one tap load per
+// dependent step (the ResNet stem pool ran at ~4.2 TB/s)
+template <bool BN, typename IDX, bool K3 = false>
 __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const float* __restrict__ coef,
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
@@ -36,7 +39,41 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_kernel(const uint16_t* _
       load8(coef + C, c8 * 8, sh);
     }
     const int h0 = oh * s - p, w0 = ow * s - p;
-    if constexpr (BN) {
+    if constexpr (BN && K3) {
+      u16x8 a[9];
+      unsigned okm = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int h = h0 + q / 3, w = w0 + q % 3;
+        const bool ok = h >= 0 && h < H && w >= 0 && w < W;
+        okm |= (ok ? 1u : 0u) << q;
+        a[q] = *reinterpret_cast<const u16x8*>(
+            x + (ok ? ((static_cast<int64_t>(n) * H + h) * W + w) * C + c8 * 8 : 0));
+      }
+      unsigned key[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (the same keys as the generic path below)
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        if (!((okm >> q) & 1u)) continue;
+        const unsigned tag = 255u - static_cast<unsigned>(q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = bf16_to_f32(a[q][j]) * sc[j] + sh[j];
+          t = t > 0.f ? t : 0.f;
+          const unsigned kj = (static_cast<unsigned>(f32_to_bf16(t)) << 8) | tag;
+          key[j] = kj > key[j] ? kj : key[j];
+        }
+      }
+      u16x8 yv;
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        yv[j] = static_cast<uint16_t>(key[j] >> 8);
+        packed |= static_cast<uint64_t>(255u - (key[j] & 255u)) << (8 * j);
+      }
+      *reinterpret_cast<u16x8*>(y + static_cast<int64_t>(v) * 8) = yv;
+      *reinterpret_cast<uint64_t*>(idx + static_cast<int64_t>(v) * 8) = packed;
+      return;
+    } else if constexpr (BN) {
       // relu(bn(x)) rounded to bf16 is >= +0, so its bits order like the values: the window max
       // and its first argmax are one unsigned max over key = bits << 8 | (255 - tap) per element
       // (ties keep the lowest tap, as the unfused path's first-max-wins scan does)
@@ -420,7 +457,15 @@ void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, 
 #define PSAMD_MPF(BN, T) \
   hipLaunchKernelGGL((maxpool_nhwc_fwd_kernel<BN, T>), dim3(grid), dim3(256), 0, st, x, coef, y, idx, N, H, W, C, OH, \
                      OW, k, s, p, lcv)
-  if (coef) {
+  if (coef && k == 3) {
+    if (i32) {
+      hipLaunchKernelGGL((maxpool_nhwc_fwd_kernel<true, uint32_t, true>), dim3(grid), dim3(256), 0, st, x, coef, y, idx,
+                         N, H, W, C, OH, OW, k, s, p, lcv);
+    } else {
+      hipLaunchKernelGGL((maxpool_nhwc_fwd_kernel<true, int64_t, true>), dim3(grid), dim3(256), 0, st, x, coef, y, idx,
+                         N, H, W, C, OH, OW, k, s, p, lcv);
+    }
+  } else if (coef) {
     if (i32) { PSAMD_MPF(true, uint32_t); } else { PSAMD_MPF(true, int64_t); }
   } else {
     if (i32) { PSAMD_MPF(false, uint32_t); } else { PSAMD_MPF(false, int64_t); }
