@@ -20,11 +20,11 @@ Protocol (``Fork``):
   * consumers that read gradients DURING backward (the parameter-server bucket hooks,
     parallel/colocated.py ``_launch``) call ``join(stream)`` before reading.
 
-Policy (``enabled``): on for per-GPU batches up to 512 images, where the layer-3/4 grids leave
-CUs idle (ResNet-50 bs256 +0.6 / +2.4 %); off above, where the compute stream's HBM-bound kernels
-stretch by about as much as the weight gradients hide (round 3 at bs1024: -1.5 %,
-profiles/r3_wgrad_side_stream_ab.txt; round 4: neutral, profiles/r4_wgrad_stream_policy.txt).
-``PS_AMD_WGRAD_STREAM=1`` / ``0`` forces it.  Also off on CPU, under graph capture, and when a
+Policy (``enabled``): on wherever a fused block gives its batch size (ResNet-50 bs256 +0.6 / +2.4 %:
+the layer-3/4 grids leave CUs idle; bs1024 +0.35 %, where the compute stream's HBM-bound kernels
+stretch by nearly as much as the weight gradients hide -- round 3's kernels lost 1.5 % there,
+profiles/r3_wgrad_side_stream_ab.txt; round 4: profiles/r4_wgrad_stream_policy.txt).
+``PS_AMD_WGRAD_STREAM=1`` / ``0`` forces it, ``PS_AMD_WGRAD_STREAM_MAX_IMAGES`` caps the batch.  Also off on CPU, under graph capture, and when a
 parameter already holds a gradient (micro-batch accumulation would make AccumulateGrad add on the
 compute stream).
 """
@@ -42,13 +42,14 @@ _lock = threading.Lock()
 
 def enabled(images: Optional[int] = None) -> bool:
     """PS_AMD_WGRAD_STREAM=1: always, 0: never; unset / auto: for batches of at most
-    PS_AMD_WGRAD_STREAM_MAX_IMAGES (512) images per GPU -- ResNet-50 bs256 +0.6 / +2.4 % on two
-    boxes, bs1024 neutral (profiles/r4_wgrad_stream_policy.txt); per-layer row thresholds
-    (layers 3-4 only, or 2-4) measured below all-layers at bs256 and below off at bs1024."""
+    PS_AMD_WGRAD_STREAM_MAX_IMAGES images per GPU (default: any) -- ResNet-50 bs256 +0.6 / +2.4 %
+    on two boxes, bs1024 +0.35 % over three interleaved pairs on one box (every pair ahead;
+    profiles/r4_wgrad_stream_policy.txt); per-layer row thresholds (layers 3-4 only, or 2-4)
+    measured below all layers."""
     mode = os.environ.get("PS_AMD_WGRAD_STREAM", "auto")
     if mode in ("0", "1"):
         return mode == "1"
-    return images is not None and images <= int(os.environ.get("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "512"))
+    return images is not None and images <= int(os.environ.get("PS_AMD_WGRAD_STREAM_MAX_IMAGES", str(1 << 30)))
 
 
 def side_stream(device: torch.device) -> torch.cuda.Stream:

@@ -151,16 +151,16 @@ def test_fault_kill_at_step_exits_the_rank():
 
 
 def test_wgrad_side_stream_policy(monkeypatch):
-    """ops/side_stream.enabled: on for per-GPU batches <= PS_AMD_WGRAD_STREAM_MAX_IMAGES (512) by
-    default (profiles/r4_wgrad_stream_policy.txt), PS_AMD_WGRAD_STREAM=0 / 1 forces it; a Fork on
-    the CPU never turns on."""
+    """ops/side_stream.enabled: on wherever a batch size is given (capped by
+    PS_AMD_WGRAD_STREAM_MAX_IMAGES; profiles/r4_wgrad_stream_policy.txt), PS_AMD_WGRAD_STREAM=0 / 1
+    forces it; a Fork on the CPU never turns on."""
     from ps_amd.ops import side_stream as side
 
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM", raising=False)
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", raising=False)
-    assert side.enabled(256) and side.enabled(512) and not side.enabled(1024) and not side.enabled()
-    monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "2048")
-    assert side.enabled(1024)
+    assert side.enabled(256) and side.enabled(1024) and not side.enabled()
+    monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "512")
+    assert side.enabled(512) and not side.enabled(1024)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "0")
     assert not side.enabled(256)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "1")
