@@ -151,14 +151,20 @@ def test_fault_kill_at_step_exits_the_rank():
 
 
 def test_wgrad_side_stream_policy(monkeypatch):
-    """ops/side_stream.enabled: on wherever a batch size is given (capped by
-    PS_AMD_WGRAD_STREAM_MAX_IMAGES; profiles/r4_wgrad_stream_policy.txt), PS_AMD_WGRAD_STREAM=0 / 1
-    forces it; a Fork on the CPU never turns on."""
+    """ops/side_stream.enabled: batches <= 512 per GPU always, larger ones only for a single
+    process (profiles/r4_wgrad_stream_policy.txt); PS_AMD_WGRAD_STREAM_MAX_IMAGES sets the cap,
+    PS_AMD_WGRAD_STREAM=0 / 1 forces it; a Fork on the CPU never turns on."""
     from ps_amd.ops import side_stream as side
 
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM", raising=False)
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
     assert side.enabled(256) and side.enabled(1024) and not side.enabled()
+    monkeypatch.setenv("WORLD_SIZE", "8")  # (torch.distributed not initialised here: the env rules)
+    assert side.enabled(512) and not side.enabled(1024)
+    monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "2048")
+    assert side.enabled(1024)
+    monkeypatch.delenv("WORLD_SIZE")
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "512")
     assert side.enabled(512) and not side.enabled(1024)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "0")
