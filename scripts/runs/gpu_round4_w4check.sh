@@ -1,7 +1,7 @@
 #!/bin/bash
 # W = 4 ranks at bs1024 sharing ONE GPU: side stream on vs off (is the slow shared-GPU step the
 # side stream or the four-process time slicing?)
-O=gpurun_out/r4w4b
+O=gpurun_out/r4w4b  # (first run: r4w4 at the default bs1024)
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH PS_AMD_BENCH_ONE_GPU=1
 for m in 0 1; do for bpg in 512; do
