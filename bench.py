@@ -150,9 +150,15 @@ def main():
         local = 0
     if not cpu:
         torch.cuda.set_device(local)
-        if os.environ.get("PS_AMD_COMPUTE_PRIORITY", "normal") == "high":
-            # forward / backward on a high-priority stream: the PS's comm streams (normal priority)
-            # then only take the CUs the compute leaves idle (serve-overlap stretch A/B)
+        # forward / backward on a high-priority stream: the weight-gradient side stream and the
+        # PS's comm streams (normal priority) then take the CUs the compute chain leaves idle.
+        # Default: high for the single-process ResNet-50 line (bs1024 +0.15 %, three interleaved
+        # pairs, profiles/r4_wgrad_stream_policy.txt); normal with peers, whose serve / pull rounds
+        # must not queue behind the compute stream, and for the asynchronous configs, whose owner
+        # service threads launch on normal-priority streams (PS_AMD_COMPUTE_PRIORITY forces it)
+        solo = int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config == "resnet50"
+        prio = os.environ.get("PS_AMD_COMPUTE_PRIORITY", "high" if solo else "normal")
+        if prio == "high":
             torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     tp = init_distributed(backend="gloo" if (cpu or one_gpu) else None)
     rank, world = tp.rank, tp.world
