@@ -57,8 +57,6 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--dlrm-rows", type=int, default=1000000)
     ap.add_argument("--tiny", type=int, default=0, help="llama-onebit: tiny config (smoke only)")
-    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("PS_AMD_CONV_BENCHMARK", "1")),
-                    help="MIOpen find (exhaustive) for each conv shape during warm-up")
     ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
                     help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
                          "ResNet-50: 32.7 vs 31.6 ms, profiles/archive/r1_graph_vs_eager.txt)")
@@ -80,32 +78,19 @@ def parse():
     return ap.parse_args()
 
 
-def setup_miopen_db():
-    """Point MIOpen at a writable copy of the in-repo find/perf db (miopen_db/udb: conv
-    algorithm choices for the ResNet-50 shapes, recorded by our own warm-up runs) so a
-    fresh box skips most of the exhaustive search.  Naive reference solvers are excluded
-    from find (they are never chosen and cost minutes to benchmark)."""
-    import shutil
-    import tempfile
-
-    for k in ("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_BWD",
-              "MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_WRW"):
-        os.environ.setdefault(k, "0")
-    if "MIOPEN_USER_DB_PATH" in os.environ:
-        return
-    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
-    dst = os.path.join(tempfile.gettempdir(), f"ps_amd_miopen_{os.getuid()}_{os.environ.get('LOCAL_RANK', '0')}")
-    try:
-        for sub in ("udb", "cache"):
-            os.makedirs(os.path.join(dst, sub), exist_ok=True)
-            if os.path.isdir(os.path.join(src, sub)):
-                for f in os.listdir(os.path.join(src, sub)):
-                    if not os.path.exists(os.path.join(dst, sub, f)):
-                        shutil.copy2(os.path.join(src, sub, f), os.path.join(dst, sub, f))
-        os.environ["MIOPEN_USER_DB_PATH"] = os.path.join(dst, "udb")
-        os.environ["MIOPEN_CUSTOM_CACHE_DIR"] = os.path.join(dst, "cache")
-    except OSError:
-        pass
+def _stream_count(engine, prio: str, side: bool, cpu: bool) -> int:
+    """HIP streams this rank issues work on in the timed steps: compute (the default or a
+    high-priority one), the weight-gradient side stream, and the PS engine's comm streams."""
+    if cpu:
+        return 0
+    n = 1 + int(side)
+    if engine is None:
+        return n
+    if getattr(engine, "plane", None) is not None:
+        return n + 2  # the xGMI plane engine's native serve and pull streams (csrc/plane.cpp)
+    seen = {id(s) for s in (getattr(engine, a, None) for a in ("comm", "comm_pull", "pull_stream"))
+            if s is not None}
+    return n + len(seen)
 
 
 def main():
@@ -134,7 +119,6 @@ def main():
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
-    setup_miopen_db()
     cpu = args.device == "cpu"
     if not cpu and not torch.cuda.is_available():
         print(json.dumps({"metric": args.config, "value": None, "error": "no GPU visible"}))
@@ -150,25 +134,31 @@ def main():
         local = 0
     if not cpu:
         torch.cuda.set_device(local)
-        # forward / backward on a high-priority stream: the weight-gradient side stream and the
-        # PS's comm streams (normal priority) then take the CUs the compute chain leaves idle.
-        # Default: high for the single-process ResNet-50 line (bs1024 +0.15 %, three interleaved
-        # pairs, profiles/r4_wgrad_stream_policy.txt); normal with peers, whose serve / pull rounds
-        # must not queue behind the compute stream, and for the asynchronous configs, whose owner
-        # service threads launch on normal-priority streams (PS_AMD_COMPUTE_PRIORITY forces it)
-        solo = int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config == "resnet50"
-        prio = os.environ.get("PS_AMD_COMPUTE_PRIORITY", "high" if solo else "normal")
-        if prio == "high":
-            torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     tp = init_distributed(backend="gloo" if (cpu or one_gpu) else None)
     rank, world = tp.rank, tp.world
+    from ps_amd.ops import side_stream as _side
+    from ps_amd.parallel.transport import ranks_per_device
+
+    rpd = ranks_per_device()  # ranks computing on this rank's GPU (1 on a real node)
+    prio = "normal"
+    if not cpu:
+        # forward / backward on a high-priority stream: the weight-gradient side stream and the
+        # PS's comm streams (normal priority) then take the CUs the compute chain leaves idle.
+        # Default: high for ResNet-50 when this rank owns its GPU -- the single-process case it was
+        # measured on (bs1024 +0.15 %, three interleaved pairs, profiles/r4_wgrad_stream_policy.txt),
+        # which a one-process-per-GPU node reproduces whatever WORLD_SIZE is; normal when ranks
+        # share a GPU, and for the asynchronous configs, whose owner service threads launch on
+        # normal-priority streams (PS_AMD_COMPUTE_PRIORITY forces it)
+        prio = os.environ.get("PS_AMD_COMPUTE_PRIORITY",
+                              "high" if (rpd == 1 and args.config == "resnet50") else "normal")
+        if prio == "high":
+            torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)
 
     def sync():
         if not cpu:
             torch.cuda.synchronize()
 
-    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.manual_seed(1234)
     bench = BC.SETUPS[args.config](args, tp, dev)
     step = bench.step
@@ -185,7 +175,7 @@ def main():
     sync()
     if rank == 0:
         print(f"[bench] {args.config}: warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
-              f"(includes MIOpen find/compile for new conv shapes)", file=sys.stderr, flush=True)
+              f"(kernel warm-up, allocator growth, PS setup)", file=sys.stderr, flush=True)
     tp.barrier()
     sync()
     if bench.stats is not None:
@@ -278,6 +268,12 @@ def main():
     if rank == 0:
         cfg = dict(bench.config)
         cfg["hip_graph"] = bool(use_graph)
+        # the stream policy this run used (keyed on ranks sharing a GPU, not on WORLD_SIZE)
+        images = bench.samples_per_step if args.config == "resnet50" else None
+        cfg["ranks_per_device"] = rpd
+        cfg["compute_priority"] = prio
+        cfg["side_stream"] = bool(not cpu and images is not None and _side.enabled(images))
+        cfg["streams_per_rank"] = _stream_count(bench.engine, prio, cfg["side_stream"], cpu)
         if getattr(bench.engine, "plane_kind", None) is not None:
             cfg["data_plane"] = bench.engine.plane_kind
         if getattr(getattr(bench.engine, "plane", None), "info", None) is not None:

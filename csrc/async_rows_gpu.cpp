@@ -68,6 +68,7 @@ class GpuRowService {
   // row_base), overflow status, optimizer states
   void set_shard(Tensor table, Tensor flags, c10::optional<Tensor> hkeys, int64_t row_base, Tensor status,
                  c10::optional<Tensor> st0, c10::optional<Tensor> st1, int64_t seed, double lo, double hi) {
+    TORCH_CHECK(!running(), "row service: set_shard while the service thread runs (stop() first)");
     TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kFloat32 && table.dim() == 2 &&
                     table.size(1) == dim_ && table.is_contiguous(), "table [rows, dim] fp32");
     table_ = table;
@@ -86,6 +87,10 @@ class GpuRowService {
   // mode (0 none, 1 1 - beta^t per applied push, 2 constant), row-wise accumulator, FTRL skip
   void set_updater(int64_t kind, std::vector<double> h, int64_t bias_mode, bool rowwise, bool skip_zero,
                    double gscale) {
+    // The hyper-parameters are a snapshot: the thread copies a_ per push without a lock, so
+    // they may only change while it is stopped (AsyncRowTable.set_updater stops and restarts
+    // the service around a reconfiguration).
+    TORCH_CHECK(!running(), "row service: set_updater while the service thread runs (stop() first)");
     TORCH_CHECK(h.size() == 16, "16 hyper-parameters");
     a_ = psamd::SparseOptArgs{};
     a_.kind = static_cast<int>(kind);
@@ -99,7 +104,10 @@ class GpuRowService {
     has_updater_.store(true, std::memory_order_release);  // after a_: the service thread reads it first
   }
 
+  bool running() const { return th_.joinable(); }
+
   void start() {
+    TORCH_CHECK(!running(), "row service already running");
     TORCH_CHECK(rq_.defined() && table_.defined(), "row service: mailboxes and shard first");
     stop_ = false;
     th_ = std::thread([this] { run(); });
@@ -128,6 +136,19 @@ class GpuRowService {
     return n;
   }
 
+  // The owner's device hash map reports a full map (an insert that found no slot: its pull
+  // would return zero rows, its push would be dropped) in the shard's status word; the Python
+  // service checked it after every request (SparseShard.check), so this thread does too: the
+  // 4-byte read rides the synchronisation every request already ends with.
+  void check_status(hipStream_t s) {
+    if (!hkeys_.defined() || !status_.defined()) return;
+    hip_ok(hipMemcpyAsync(&status_host_, status_.data_ptr<int32_t>(), sizeof(int32_t), hipMemcpyDeviceToHost, s),
+           "status read");
+    hip_ok(hipStreamSynchronize(s), "status read");
+    TORCH_CHECK(status_host_ == 0, "sparse table shard full (device hash map of owner ", me_, ": ",
+                hkeys_.numel(), " slots)");
+  }
+
   void slots_of(const int64_t* keys, int64_t n, hipStream_t s) {
     int64_t* sl = slots_.data_ptr<int64_t>();
     if (hkeys_.defined())
@@ -148,7 +169,7 @@ class GpuRowService {
                                    lo_, hi_, s);
     psamd::launch_gather_rows(table_.data_ptr<float>(), 0, sl, n, dim_, rs_.data_ptr<float>() + k * cap_ * dim_, 0,
                               dim_, 0, 0, s);
-    hip_ok(hipStreamSynchronize(s), "row pull");
+    check_status(s);  // synchronises the stream
   }
 
   void serve_push(int64_t k, int m, hipStream_t s) {
@@ -176,7 +197,7 @@ class GpuRowService {
       a.nrows = n;
       a.dim = dim_;
       psamd::launch_sparse_opt(a, s);
-      hip_ok(hipStreamSynchronize(s), "row push");
+      check_status(s);  // synchronises the stream
     }
     applied_ += 1;
   }
@@ -231,6 +252,7 @@ class GpuRowService {
   int64_t row_base_ = 0;
   uint64_t seed_ = 0;
   float lo_ = 0.f, hi_ = 0.f;
+  int32_t status_host_ = 0;
   psamd::SparseOptArgs a_{};
   int bias_mode_ = 0;
   std::atomic<bool> has_updater_{false};
@@ -330,6 +352,7 @@ void register_async_rows(pybind11::module& m) {
       .def("set_shard", &GpuRowService::set_shard)
       .def("set_updater", &GpuRowService::set_updater)
       .def("start", &GpuRowService::start)
+      .def_property_readonly("running", &GpuRowService::running)
       .def("stop", &GpuRowService::stop, py::call_guard<py::gil_scoped_release>())
       .def("error", &GpuRowService::error)
       .def_property_readonly("applied", &GpuRowService::applied)

@@ -21,7 +21,7 @@ Protocol (``Fork``):
     parallel/colocated.py ``_launch``) call ``join(stream)`` before reading.
 
 Policy (``enabled``): on for batches up to 512 per GPU (ResNet-50 bs256 +0.6 / +2.4 %: the
-layer-3/4 grids leave CUs idle) and, for a single process, at any batch (bs1024 +0.35 %, where
+layer-3/4 grids leave CUs idle) and, for a rank that owns its GPU, at any batch (bs1024 +0.35 %, where
 the compute stream's HBM-bound kernels stretch by nearly as much as the weight gradients hide --
 round 3's kernels lost 1.5 % there, profiles/r3_wgrad_side_stream_ab.txt; round 4:
 profiles/r4_wgrad_stream_policy.txt).  ``PS_AMD_WGRAD_STREAM=1`` / ``0`` forces it,
@@ -41,22 +41,22 @@ _STREAMS: Dict[int, torch.cuda.Stream] = {}
 _lock = threading.Lock()
 
 
-def _world_size() -> int:
-    import torch.distributed as dist
+def _ranks_per_device() -> int:
+    from ..parallel.transport import ranks_per_device
 
-    if dist.is_available() and dist.is_initialized():
-        return dist.get_world_size()
-    return int(os.environ.get("WORLD_SIZE", "1"))
+    return ranks_per_device()
 
 
 def enabled(images: Optional[int] = None) -> bool:
     """PS_AMD_WGRAD_STREAM=1: always, 0: never; unset / auto: for batches of at most
-    PS_AMD_WGRAD_STREAM_MAX_IMAGES images per GPU -- by default any batch for a single process
-    and 512 with peers.  ResNet-50 bs256 +0.6 / +2.4 % on two boxes, bs1024 +0.35 % over three
+    PS_AMD_WGRAD_STREAM_MAX_IMAGES images per GPU -- by default any batch when this rank owns its
+    GPU (``ranks_per_device() == 1``: a single process, or one rank per GPU on a node) and 512
+    when several ranks share one GPU.  ResNet-50 bs256 +0.6 / +2.4 % on two boxes, bs1024 +0.35 % over three
     interleaved pairs on one box (profiles/r4_wgrad_stream_policy.txt); per-layer row thresholds
     (layers 3-4 only, or 2-4) measured below all layers.  With peers the large batches stay on
-    one stream: the multi-rank path was validated that way (W = 2 / 4 / 8 rehearsals), and four
-    bs1024 ranks sharing one GPU ran 4x slower with the side stream (profiles/r4_wgrad_stream_policy.txt)."""
+    one stream only where ranks SHARE a device: four bs1024 ranks on one GPU ran 4x slower with the
+    side stream (profiles/r4_wgrad_stream_policy.txt), while a rank that owns its GPU is exactly
+    the measured single-process case, whatever WORLD_SIZE is."""
     mode = os.environ.get("PS_AMD_WGRAD_STREAM", "auto")
     if mode in ("0", "1"):
         return mode == "1"
@@ -64,7 +64,7 @@ def enabled(images: Optional[int] = None) -> bool:
         return False
     cap = os.environ.get("PS_AMD_WGRAD_STREAM_MAX_IMAGES")
     if cap is None:
-        return images <= 512 or _world_size() == 1
+        return images <= 512 or _ranks_per_device() == 1
     return images <= int(cap)
 
 

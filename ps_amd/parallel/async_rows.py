@@ -163,9 +163,23 @@ class AsyncRowTable(TcpSparseTable):
         self.service.start()
 
     def _configure_native(self) -> None:
-        """Hand the shard (and the updater, once known) to the native GPU service."""
+        """Hand the shard (and the updater, once known) to the native GPU service.  The service
+        thread reads its configuration without a lock, so a reconfiguration after ``start()``
+        (``set_updater``, the ``init`` setter) stops the thread, reconfigures and restarts it;
+        requests that arrive meanwhile wait in the control words.  The hyper-parameters are a
+        snapshot taken here: changing ``updater.lr`` later needs another ``set_updater``."""
         if not self.gpu or getattr(self, "service", None) is None:
             return
+        was = self.service.running
+        if was:
+            self.service.stop()
+        try:
+            self._configure_native_body()
+        finally:
+            if was:
+                self.service.start()
+
+    def _configure_native_body(self) -> None:
         sh = self.shard
         st = list(sh.states) + [None] * (2 - len(sh.states))
         lo, hi = sh.init
@@ -204,9 +218,14 @@ class AsyncRowTable(TcpSparseTable):
     def _owner(self, keys: torch.Tensor) -> torch.Tensor:
         return torch.remainder(_mix64(keys), self.W) if self.W > 1 else torch.zeros_like(keys)
 
-    def _check_cap(self, n: int) -> None:
+    def _check_cap(self, n: int, what: str = "request") -> None:
+        """Mailbox bound.  CPU: ``n`` = one owner's unique keys.  GPU: the per-owner counts stay on
+        the device (no host sync), so the host checks the bound it knows -- the request's unique
+        ids over ALL owners -- i.e. on the GPU the capacity C is per request, not per owner: size
+        it to at least the (unique) ids of one step."""
         if n > self.C:
-            raise RuntimeError(f"async row table {self.name}: {n} keys for one owner exceed capacity {self.C}")
+            who = "for one owner" if not self.gpu else "in one GPU request (all owners; capacity is per request)"
+            raise RuntimeError(f"async row table {self.name}: {what} of {n} keys {who} exceeds capacity {self.C}")
 
     def _ssp_gate(self) -> None:
         """SSP(s): every owner applied every worker's first (clock - s) row pushes -- this
@@ -384,8 +403,14 @@ class AsyncRowTable(TcpSparseTable):
         if not self.gpu:
             return super().lookup(ids, out_dtype, grad_fn)
         plan = self._route_dev(self._keys_dev(ids))
-        rows = self._pull_dev(plan)
         want_grad = torch.is_grad_enabled()
+        if want_grad:
+            # the round's lookups leave as ONE merged push: check its bound now, before this pull,
+            # rather than in push_pending after the round's pulls already went out
+            merged = plan["n"] + sum(p["dev"]["n"] for p in self._pending) + sum(d["n"] for d, _ in
+                                                                               getattr(self, "_held", []))
+            self._check_cap(merged, "merged push")
+        rows = self._pull_dev(plan)
         leaf = rows.detach().requires_grad_(want_grad)
         out = _sp.gather_unique(leaf, plan["inv"], plan["perm"], plan["seg"], out_dtype)
         if want_grad:
@@ -473,7 +498,14 @@ class AsyncRowTable(TcpSparseTable):
         c = self.ctl
         if self.gpu:
             self._notify.drain()
-        self.shm.wait_ge([c.pack(o, self.me) for o in range(self.W)], self.pushes, c.stop, self.timeout_s)
+        try:
+            self.shm.wait_ge([c.pack(o, self.me) for o in range(self.W)], self.pushes, c.stop, self.timeout_s)
+        finally:
+            err = self.service.error() if (self.gpu and self.service is not None) else ""
+            if err:  # the owner service stopped the table (e.g. its hash map is full): say why
+                raise RuntimeError(f"async row table {self.name}: owner service failed: {err}")
+        if self.gpu:
+            self.shard.check()  # this rank's own shard: overflow of its device hash map
         if self.gpu and self._nbad is not None:
             nb = int(self._nbad.item())
             self._nbad = None

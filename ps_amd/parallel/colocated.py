@@ -374,15 +374,18 @@ class ColocatedPS:
             return a.elapsed_time(b) if self.gpu else (b - a) * 1e3
         if self.gpu:
             self._marks[-1][1].synchronize()
-        acc = {"push_ms": 0.0, "serve_ms": 0.0, "pull_ms": 0.0}
+        # only the phases that were marked: the xGMI plane path returns before any push / serve /
+        # pull mark (its phases are the plane's own device-timed statistics, ``plane_stats``), so
+        # its record carries no placeholder zeros for them
+        acc: Dict[str, float] = {}
         last = {}
         for name, t in self._marks:
             if name == "push1":
-                acc["push_ms"] += ms(last["push0"], t)
+                acc["push_ms"] = acc.get("push_ms", 0.0) + ms(last["push0"], t)
             elif name == "serve1":
-                acc["serve_ms"] += ms(last.get("push1", last.get("serve0")), t)
+                acc["serve_ms"] = acc.get("serve_ms", 0.0) + ms(last.get("push1", last.get("serve0")), t)
             elif name == "pull1":
-                acc["pull_ms"] += ms(last["serve1"], t)
+                acc["pull_ms"] = acc.get("pull_ms", 0.0) + ms(last["serve1"], t)
             last[name] = t
         if "bwd_end" in last and "round_end" in last:
             acc["exposed_comm_ms"] = max(0.0, ms(last["bwd_end"], last["round_end"]))

@@ -59,6 +59,7 @@ class KVStore:
         self._pf_queue: list = []
         self._pf_done = 0
         self._pf_sent = 0
+        self._gen = 0  # cache generation: clear() starts a new one; stale prefetches are dropped
         self._pf_err: Optional[BaseException] = None
         self._pf_thread: Optional[threading.Thread] = None
         self.prefetch_batches = 0
@@ -140,7 +141,7 @@ class KVStore:
             if self._pf_thread is None:
                 self._pf_thread = threading.Thread(target=self._prefetch_loop, name="kvstore-prefetch", daemon=True)
                 self._pf_thread.start()
-            self._pf_queue.append(dict(keys))
+            self._pf_queue.append((self._gen, dict(keys)))
             self._pf_sent += 1
             self._pf_cv.notify_all()
 
@@ -149,17 +150,21 @@ class KVStore:
             with self._pf_cv:
                 while not self._pf_queue:
                     self._pf_cv.wait()
-                batch = self._pf_queue.pop(0)
+                gen, batch = self._pf_queue.pop(0)
             try:
                 with self._lock:
-                    batch = {k: f for k, f in batch.items() if k not in self.store}
+                    batch = {k: f for k, f in batch.items() if k not in self.store} if gen == self._gen else {}
                 if batch:
                     got = self.client.get_list(list(batch))
                     missing = {k: batch[k]() for k, v in got.items() if v is None}
                     created = self.client.update_list(missing, replace=False) if missing else {}
                     with self._lock:
-                        for k, v in got.items():
-                            self.store[k] = v if v is not None else created[k]
+                        # a clear() since this batch was queued dropped the generation it belongs
+                        # to: its values may predate the round that clear() ended -- never cache
+                        # them (the next pull re-fetches post-barrier values)
+                        if gen == self._gen:
+                            for k, v in got.items():
+                                self.store[k] = v if v is not None else created[k]
                 self.prefetch_batches += 1
             except BaseException as e:  # noqa: BLE001 -- surfaced by async_wait
                 with self._pf_cv:
@@ -229,6 +234,7 @@ class KVStore:
             dropped = list(self.store) if self.distributed else []
             if self.distributed:
                 self.store.clear()  # per-step worker cache: next step re-pulls (Q16)
+                self._gen += 1  # in-flight prefetches of the previous generation are discarded
         if dropped and prefetch:
             self.prefetch({k: _no_init(k) for k in dropped})
 

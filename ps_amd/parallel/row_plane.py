@@ -113,7 +113,17 @@ class RowPlane:
         return off, o
 
     def _alloc(self, cap: int) -> None:
-        """(Re)allocate every rank's arena for ``cap`` keys and map the peers' (collective)."""
+        """(Re)allocate every rank's arena for ``cap`` keys and map the peers' (collective).
+
+        A grow frees this rank's arena and unmaps the peers': a peer's previous push
+        accumulate (or row send) may still be reading / writing our arena over IPC on its own
+        stream, and ``hipFree`` only waits for this process's work.  So every rank first drains
+        its device and then meets the others at a barrier: after it, no kernel of any rank
+        touches an old arena."""
+        if self.cap > 0:
+            if self.gpu:
+                torch.cuda.synchronize(self.device)
+            self.t.barrier()
         self._release_arena()
         self.cap = cap
         self.off, nbytes = self._layout(cap)

@@ -161,6 +161,49 @@ class Transport:
                 dist.barrier(group=self.group)
 
 
+_RANKS_PER_DEVICE: Optional[int] = None
+
+
+def device_key(device=None) -> str:
+    """Identity of the GPU (or host, for CPU ranks) this process computes on, unique across a
+    node whatever CUDA_VISIBLE_DEVICES says: hostname + the device UUID (index as fallback)."""
+    import socket
+
+    host = socket.gethostname()
+    if device is None or torch.device(device).type != "cuda":
+        return f"{host}/cpu/{os.getpid()}"
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    uid = getattr(torch.cuda.get_device_properties(idx), "uuid", None)
+    return f"{host}/gpu/{uid if uid is not None else idx}"
+
+
+def count_sharing(keys: List[str], rank: int) -> int:
+    """How many ranks share ``rank``'s device, given every rank's ``device_key``."""
+    return sum(1 for k in keys if k == keys[rank])
+
+
+def ranks_per_device(refresh: bool = False, device=None) -> int:
+    """Ranks of this job that compute on this rank's GPU: 1 on a real node (one process per
+    GPU), W in the one-GPU rehearsals.  The stream policies that were tuned on a single process
+    (ops/side_stream.py, bench.py's compute-stream priority) key on this, not on WORLD_SIZE.
+    Computed once by an all-gather of ``device_key`` -- a collective: the first call must be made
+    by every rank (``init_distributed`` does it); later calls return the cached count."""
+    global _RANKS_PER_DEVICE
+    if _RANKS_PER_DEVICE is not None and not refresh:
+        return _RANKS_PER_DEVICE
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        _RANKS_PER_DEVICE = 1
+        return 1
+    if device is None and torch.cuda.is_available() and (dist.get_backend() == "nccl" or torch.cuda.is_initialized()
+                                                         or os.environ.get("PS_AMD_BENCH_ONE_GPU", "0") == "1"):
+        device = torch.device("cuda", torch.cuda.current_device())
+    keys = [None] * dist.get_world_size()
+    dist.all_gather_object(keys, device_key(device))
+    _RANKS_PER_DEVICE = count_sharing(keys, dist.get_rank())
+    return _RANKS_PER_DEVICE
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> Transport:
     """Initialise torch.distributed from the torchrun env (RANK/WORLD_SIZE/MASTER_*).
 
@@ -182,6 +225,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(**kw)
+    ranks_per_device(refresh=True)  # collective, once per job: the stream policies key on it
     return Transport()
 
 

@@ -151,20 +151,25 @@ def test_fault_kill_at_step_exits_the_rank():
 
 
 def test_wgrad_side_stream_policy(monkeypatch):
-    """ops/side_stream.enabled: batches <= 512 per GPU always, larger ones only for a single
-    process (profiles/r4_wgrad_stream_policy.txt); PS_AMD_WGRAD_STREAM_MAX_IMAGES sets the cap,
-    PS_AMD_WGRAD_STREAM=0 / 1 forces it; a Fork on the CPU never turns on."""
+    """ops/side_stream.enabled: batches <= 512 per GPU always, larger ones only when the rank
+    owns its GPU (profiles/r4_wgrad_stream_policy.txt; tests/test_stream_policy_cpu.py);
+    PS_AMD_WGRAD_STREAM_MAX_IMAGES sets the cap, PS_AMD_WGRAD_STREAM=0 / 1 forces it; a Fork on
+    the CPU never turns on."""
     from ps_amd.ops import side_stream as side
+    from ps_amd.parallel import transport
 
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM", raising=False)
     monkeypatch.delenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", raising=False)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     assert side.enabled(256) and side.enabled(1024) and not side.enabled()
-    monkeypatch.setenv("WORLD_SIZE", "8")  # (torch.distributed not initialised here: the env rules)
+    monkeypatch.setenv("WORLD_SIZE", "8")  # one rank per GPU: still the single-process policy
+    assert side.enabled(512) and side.enabled(1024)
+    monkeypatch.setattr(transport, "_RANKS_PER_DEVICE", 8)  # eight ranks sharing one GPU
     assert side.enabled(512) and not side.enabled(1024)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "2048")
     assert side.enabled(1024)
     monkeypatch.delenv("WORLD_SIZE")
+    monkeypatch.setattr(transport, "_RANKS_PER_DEVICE", None)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM_MAX_IMAGES", "512")
     assert side.enabled(512) and not side.enabled(1024)
     monkeypatch.setenv("PS_AMD_WGRAD_STREAM", "0")

@@ -34,6 +34,10 @@ def test_bench_json_contract_cpu(world, tmp_path):
     assert rec["config"]["model"] == "ResNet-50" and rec["config"]["global_batch"] == 2 * world
     # value is the whole-job rate: global batch x steps / (max over ranks of the timed region)
     assert rec["value"] == pytest.approx(2 * world * 1e3 / rec["ms_per_step"], rel=1e-2)
+    # stream policy fields: keyed on ranks sharing a device (CPU ranks never share one)
+    assert rec["config"]["ranks_per_device"] == 1
+    assert rec["config"]["compute_priority"] == "normal" and rec["config"]["side_stream"] is False
+    assert rec["config"]["streams_per_rank"] == 0
     if world > 1:
         assert set(rec["config"]["ps_phase_ms_per_step"]) >= {"push_ms", "serve_ms", "pull_ms"}
         if rec["config"].get("data_plane") == "xgmi":  # mapping mode / self-test / round end reported

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _dlrm_body(tp, n, overlap, steps=4):
+def _dlrm_body(tp, n, overlap, steps=4, grow=()):
     from ps_amd.models.dlrm import DLRM, dlrm_batch
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import AdagradUpdater
@@ -29,9 +29,13 @@ def _dlrm_body(tp, n, overlap, steps=4):
     m = m.to(DEV)
     ps = ColocatedPS(m, AdagradUpdater(0.05, 1e-8), tp, bucket_mb=0.05, overlap=False,
                      plane="collective" if tp.world == 1 else "xgmi")
-    dense, sparse, y = dlrm_batch(n, rows, seed=11, device=DEV)
-    lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
-    for _ in range(steps):
+    # ``grow``: batch sizes of later steps -- a larger batch after the first pushes makes every
+    # rank's unique-key count outgrow the arena, i.e. a collective re-map while the peers' last
+    # accumulate may still be reading the old arenas (drain + barrier before release)
+    sizes = [n] * steps + list(grow)
+    for i, nb in enumerate(sizes):
+        dense, sparse, y = dlrm_batch(nb, rows, seed=11 + (i if grow else 0), device=DEV)
+        lo, hi = tp.rank * nb // tp.world, (tp.rank + 1) * nb // tp.world
         F.binary_cross_entropy_with_logits(m(dense[lo:hi], sparse[lo:hi]), y[lo:hi]).backward()
         m.push_sparse()
         ps.finish_step()
@@ -39,7 +43,7 @@ def _dlrm_body(tp, n, overlap, steps=4):
     m.emb.table.synchronize()
     table_rows = m.emb.table.pull_keys(torch.arange(2800, device=DEV)).cpu()
     torch.cuda.synchronize()
-    info = {"exchange": m.emb.table.exchange,
+    info = {"exchange": m.emb.table.exchange, "cap": m.emb.table.plane.cap if m.emb.table.plane is not None else 0,
             "plane": dict(m.emb.table.plane.stats) if m.emb.table.plane is not None else {}}
     out = ({k: v.detach().cpu() for k, v in m.named_parameters()}, table_rows, info)
     m.emb.table.close()
@@ -60,3 +64,16 @@ def test_dlrm_processes_row_plane_equals_single_rank(world, overlap):
         torch.testing.assert_close(wn[r][1], w1[1], rtol=1e-4, atol=1e-5)
         if r:
             torch.testing.assert_close(wn[r][1], wn[0][1], rtol=0, atol=0)
+
+
+def test_dlrm_processes_row_plane_arena_grows_after_pushes():
+    """Unique keys per rank: <= 256 for the first two steps (arena cap 1024), then up to 2800
+    (4 x 700 rows, batch 4096): the arenas grow after pushes went out -- same result as one rank."""
+    wn = dist_util.run(_dlrm_body, 2, (128, True, 2, (4096, 4096)))
+    w1 = dist_util.run(_dlrm_body, 1, (128, True, 2, (4096, 4096)))[0]
+    for r in range(2):
+        info = wn[r][2]
+        assert info["exchange"] == "plane" and info["plane"]["grows"] >= 2 and info["cap"] > 1024, info
+        for k, v in w1[0].items():
+            torch.testing.assert_close(wn[r][0][k], v, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(wn[r][1], w1[1], rtol=1e-4, atol=1e-5)
