@@ -1499,6 +1499,57 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   return dw;
 }
 
+// conv3's backward in one pass (csrc/kernels/conv_bwd_fused.hip): bn3's backward prologue
+// dz3 = bf16(ca g + cb z3 + cc) never leaves LDS; -> [gy [M, CI] (masked by bn2's ReLU), part
+// [2, G, CI] (bn2 backward sums, the conv_gemm epi-3 layout), dW3 [CO, CI] bf16]
+std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt, Tensor z2, Tensor cf2, Tensor mean2,
+                                     Tensor invstd2) {
+  check_rows(g, "g");
+  check_rows(z3, "z3");
+  check_rows(z2, "z2");
+  check_rows(wt, "wt");
+  TORCH_CHECK(g.dim() == 2 && z3.sizes() == g.sizes() && z2.dim() == 2 && z2.size(0) == g.size(0),
+              "g, z3 [M, CO]; z2 [M, CI]");
+  const int64_t M = g.size(0), CO = g.size(1), CI = z2.size(1);
+  TORCH_CHECK(psamd::conv11_bwd_fused_ok(static_cast<int>(CI), static_cast<int>(CO)),
+              "conv11_bwd_fused: unsupported channels CI=", CI, " CO=", CO);
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) / CO, "pixel count");
+  TORCH_CHECK(wt.dim() == 2 && wt.size(0) == CI && wt.size(1) == CO, "wt must be [CI, CO]");
+  check_f32(cbwd, "cbwd");
+  check_f32(cf2, "cf2");
+  check_f32(mean2, "mean2");
+  check_f32(invstd2, "invstd2");
+  TORCH_CHECK(cbwd.numel() == 3 * CO && cf2.numel() == 2 * CI && mean2.numel() == CI && invstd2.numel() == CI,
+              "cbwd [3 CO], cf2 [2 CI], mean2 / invstd2 [CI]");
+  const c10::DeviceGuard guard(g.device());
+  const int m = static_cast<int>(M), ci = static_cast<int>(CI), co = static_cast<int>(CO);
+  const int G = psamd::conv11_bwd_blocks(m, ci, co);
+  auto gy = torch::empty({M, CI}, g.options());
+  auto part = torch::empty({2, G, CI}, g.options().dtype(torch::kFloat32));
+  auto ws = torch::empty({psamd::conv11_bwd_ws(m, ci, co)}, g.options().dtype(torch::kFloat32));
+  auto dw = torch::empty({CO, CI}, g.options());
+  psamd::Conv11BwdArgs a{};
+  a.g = u16(g);
+  a.z3 = u16(z3);
+  a.cbwd = cbwd.data_ptr<float>();
+  a.wt = u16(wt);
+  a.z2 = u16(z2);
+  a.cf2 = cf2.data_ptr<float>();
+  a.mean2 = mean2.data_ptr<float>();
+  a.invstd2 = invstd2.data_ptr<float>();
+  a.gy = u16m(gy);
+  a.part = part.data_ptr<float>();
+  a.ws = ws.data_ptr<float>();
+  a.dw = u16m(dw);
+  a.M = m;
+  psamd::launch_conv11_bwd_fused(a, ci, co, cur_stream(g));
+  return {gy, part, dw};
+}
+
+bool conv11_bwd_fused_supported(int64_t ci, int64_t co) {
+  return psamd::conv11_bwd_fused_ok(static_cast<int>(ci), static_cast<int>(co));
+}
+
 // Linear weight + bias gradient in one pass over dz: [dW [N, K] bf16, db [N] fp32] with
 // dW = dz^T x (x [M, K] rows), db = column sums of dz (fused into the wide split-K kernel; a
 // torch reduction where the plan is not wide)
@@ -1636,6 +1687,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
+  m.def("conv11_bwd_fused", &conv11_bwd_fused);
+  m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported);
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);
   m.def("bn_bwd_partials", &bn_bwd_partials);

@@ -367,6 +367,32 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s);
 
+// Fused backward of a bottleneck's last 1x1 conv (conv3: CI -> CO channels) with bn3's backward
+// in its prologue (conv_bwd_fused.hip): per 128-pixel tile, dz3 = bf16(ca g + cb z3 + cc) is built
+// in LDS one 64-channel stage at a time and feeds BOTH GEMMs -- the data gradient
+// gy = dz3 W3 (bn2's ReLU mask + backward sums in the epilogue, the conv_gemm epi-3 contract) and
+// the weight gradient dW3 += dz3^T relu(bn2(z2)) (per-block fp32 slabs, fixed-order reduce) --
+// so dz3 never reaches HBM and z2 is read once for both.
+struct Conv11BwdArgs {
+  const uint16_t* g;      // [M, CO] gradient at bn3's output (already ReLU-masked)
+  const uint16_t* z3;     // [M, CO] bn3 input
+  const float* cbwd;      // [3 CO] ca | cb | cc (bn3 backward coefficients)
+  const uint16_t* wt;     // [CI, CO] conv3 weight transposed
+  const uint16_t* z2;     // [M, CI] bn2 input (conv3's input before bn2 + ReLU)
+  const float* cf2;       // [2 CI] bn2 scale | shift
+  const float* mean2;     // [CI]
+  const float* invstd2;   // [CI]
+  uint16_t* gy;           // [M, CI] masked data gradient (bn2's output gradient)
+  float* part;            // [2][gm][CI] bn2 backward partial sums
+  float* ws;              // conv11_bwd_ws(M, CI, CO) floats: dW slabs (+ reduce scratch)
+  uint16_t* dw;           // [CO, CI] bf16 conv3 weight gradient
+  int M;
+};
+bool conv11_bwd_fused_ok(int CI, int CO);
+int conv11_bwd_blocks(int M, int CI, int CO);
+int64_t conv11_bwd_ws(int M, int CI, int CO);
+void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t s);
+
 struct ConvWgradArgs {
   const uint16_t* dz;   // [M, N] output gradient rows
   const uint16_t* x;    // [images, H, W, C] input map

@@ -165,6 +165,8 @@ def setup_dlrm(args, tp, dev) -> Bench:
         st = tbl.stats
         d = {"sparse_host_syncs_per_pull": round((st["host_syncs"] - s0["host_syncs"]) / max(1, st["pulls"] - s0["pulls"]), 3)}
         s0.update(host_syncs=st["host_syncs"], pulls=st["pulls"])
+        if tbl.plane is not None and tbl.plane.timing:  # row-plane stage table (PS_AMD_ROWPLANE_TIMING=1)
+            d["row_plane_stages"] = tbl.plane.timing_summary()
         return d
 
     return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",

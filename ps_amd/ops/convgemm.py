@@ -266,6 +266,14 @@ def _pro_fuse_max_k() -> int:
     return int(os.environ.get("PS_AMD_PRO_FUSE_MAX_K", "256"))
 
 
+def _conv3_bwd_fused(ci: int, co: int) -> bool:
+    """conv3's data AND weight gradient in one pass with bn3's backward in the prologue
+    (csrc/kernels/conv_bwd_fused.hip): dz3 never reaches HBM and z2 is read once.
+    PS_AMD_CONV3_BWD_FUSED=0 keeps the two-kernel chain (prologue data gradient storing dz3 + the
+    weight-gradient GEMM re-reading it)."""
+    return os.environ.get("PS_AMD_CONV3_BWD_FUSED", "1") != "0" and bool(native().conv11_bwd_fused_supported(ci, co))
+
+
 def _fold_enabled() -> bool:
     return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
 
@@ -352,7 +360,7 @@ class _BottleneckFn(torch.autograd.Function):
         pw = ctx.prep
         w3t = pw[1] if pw else _mat(w3).t()
         lk = ctx.link_out
-        dz3 = None
+        dz3 = dw3f = None
         ds_part = None  # [2, G, C] downsample-BN sums from the consumer's epilogue 9
         if (lk is not None and lk.part is not None and d2.data_ptr() == lk.dx_ptr
                 and d2._version == lk.dx_version):
@@ -365,7 +373,12 @@ class _BottleneckFn(torch.autograd.Function):
                 # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
                 # the weight gradient: no separate apply pass over the widest tensors
                 dg3, db3, cb3 = nat.bn_bwd_coef(lk.part, g3, m3, i3, d2.shape[0])
-                gy2, p2, dz3 = nat.conv_gemm(d2, w3t, go, None, 3, z2r, None, cf2, m2, i2, a2=z3, bwd=cb3)
+                if _conv3_bwd_fused(w3.shape[1], w3.shape[0]):
+                    # data + weight gradient in ONE pass: dz3 stays in LDS, z2 is read once
+                    gy2, p2, dw3f = nat.conv11_bwd_fused(d2, z3, cb3, w3t.contiguous(), z2r, cf2, m2, i2)
+                    FOLD_STATS["conv3_fused"] = FOLD_STATS.get("conv3_fused", 0) + 1
+                else:
+                    gy2, p2, dz3 = nat.conv_gemm(d2, w3t, go, None, 3, z2r, None, cf2, m2, i2, a2=z3, bwd=cb3)
             else:
                 dz3, dg3, db3 = nat.bn_bwd_partials(d2, z3, lk.part, g3, m3, i3)
                 gy2 = None
@@ -379,8 +392,11 @@ class _BottleneckFn(torch.autograd.Function):
             lk.part = lk.dx_keep = None
         # conv3: data grad with bn2's ReLU mask + backward sums in the epilogue, weight grad with
         # relu(bn2(z2)) recomputed in the prologue
-        sd.fork()
-        dw3 = sd.run(lambda: nat.conv_wgrad(dz3, z2r, go, cf2), dz3, z2r, cf2, like=w3)
+        if dw3f is not None:
+            dw3 = _side._match_layout(dw3f, w3)
+        else:
+            sd.fork()
+            dw3 = sd.run(lambda: nat.conv_wgrad(dz3, z2r, go, cf2), dz3, z2r, cf2, like=w3)
         if gy2 is None:
             gy2, p2 = nat.conv_gemm(dz3, w3t, go, None, 3, z2r, None, cf2, m2, i2)
         dz2, dg2, db2 = nat.bn_bwd_partials(gy2, z2r, p2, g2, m2, i2)

@@ -40,6 +40,7 @@ through the control block and grow together (a collective re-map) when any rank 
 from __future__ import annotations
 
 import os
+import time
 import uuid
 from typing import List, Optional
 
@@ -86,6 +87,68 @@ class RowPlane:
         self._ev = None
         self._peer_ev = None
         self.stats = {"pulls": 0, "pushes": 0, "grows": 0, "host_syncs": 0}
+        # per-stage timing (bench --timing / PS_AMD_ROWPLANE_TIMING=1): device events around each
+        # stage's own work and host wall time in each cross-rank wait, plus the bytes every stage
+        # moves (``timing_summary``)
+        self.timing = os.environ.get("PS_AMD_ROWPLANE_TIMING", "0") == "1"
+        self._tev: List[tuple] = []  # (phase, start event, end event)
+        self._tsum: dict = {}
+        self._tn = {"pulls": 0, "pushes": 0, "applies": 0}
+
+    # ------------------------------------------------------------------ timing
+    def _t0(self):
+        """Start of a timed device phase on the current stream (None when timing is off)."""
+        if not self.timing:
+            return None
+        if not self.gpu:
+            return time.perf_counter()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _t1(self, phase: str, start) -> None:
+        if start is None:
+            return
+        if not self.gpu:
+            self._tadd(phase + "_ms", (time.perf_counter() - start) * 1e3)
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        self._tev.append((phase, start, ev))
+
+    def _tadd(self, k: str, v: float) -> None:
+        self._tsum[k] = self._tsum.get(k, 0.0) + float(v)
+
+    def timing_summary(self, reset: bool = True) -> dict:
+        """Per-pull / per-push means: device ms of each stage's own kernels (pub: key + segment
+        table copies; serve: the owner's recv + slot resolve + lazy init + row send; out: the
+        pulled rows copied out; grd: gradient rows into the arena; acc: the owner's rank-order
+        accumulate; apply: the one row-optimizer update), host ms waiting for the peers at each
+        cross-rank point (wait_*), and bytes moved per pull / push with the GB/s they imply."""
+        if self.gpu and self._tev:
+            torch.cuda.synchronize(self.device)  # the stages ran on the compute and side streams
+        for phase, a, b in self._tev:
+            self._tadd(phase + "_ms", a.elapsed_time(b))
+        self._tev = []
+        out = {}
+        n = self._tn
+        for k, v in self._tsum.items():
+            if k.endswith("_bytes"):
+                continue
+            per = n["pulls"] if k.split("_")[0] in ("pub", "serve", "out", "wait") and not k.startswith(
+                ("wait_grd", "wait_acc")) else (n["applies"] if k.startswith("apply") else n["pushes"])
+            out[k] = round(v / max(1, per), 4)
+        for k in ("pull_bytes", "serve_bytes", "push_bytes", "acc_bytes"):
+            if k in self._tsum:
+                per = n["pulls"] if k in ("pull_bytes", "serve_bytes") else n["pushes"]
+                out[k] = round(self._tsum[k] / max(1, per))
+        for b, t in (("serve_bytes", "serve_ms"), ("acc_bytes", "acc_ms")):
+            if out.get(t):
+                out[t.replace("_ms", "_GBps")] = round(out[b] / out[t] / 1e6, 2)
+        out.update({k: v for k, v in n.items()})
+        if reset:
+            self._tsum, self._tn = {}, {"pulls": 0, "pushes": 0, "applies": 0}
+        return out
 
     # ------------------------------------------------------------------ control words
     def _w(self, stage: str, r: int) -> int:
@@ -101,7 +164,10 @@ class RowPlane:
         return e
 
     def _wait_all(self, stage: str, e: int) -> None:
+        t = time.perf_counter() if self.timing else None
         self.shm.wait_ge([self._w(stage, r) for r in range(self.W)], e, self.ctl + 16, self.timeout_s)
+        if t is not None:
+            self._tadd(f"wait_{stage}_ms", (time.perf_counter() - t) * 1e3)
 
     # ------------------------------------------------------------------ arena
     def _layout(self, cap: int):
@@ -232,16 +298,28 @@ class RowPlane:
             self._alloc(_round_cap(need))
         cap, W = self.cap, self.W
         # publish this rank's keys + segment table (device ops, no host copy of a count)
+        t = self._t0()
         if n:
             self.skeys[:n].copy_(ubuf[:n])
         cnt = counts[:W].to(torch.int64)
         self.meta[W:].copy_(cnt)
         self.meta[:W].copy_(torch.cumsum(cnt, 0) - cnt)
+        self._t1("pub", t)
         self._stage("pub")
         # owner: every worker's segment for me -> slots -> rows into the workers' arenas
+        t = self._t0()
         st = self._serve(shard, fetch)
+        self._t1("serve", t)
         self._stage("rows")
+        t = self._t0()
         out = self.rows[:n].clone() if fetch else None
+        self._t1("out", t)
+        if self.timing:
+            # this rank's keys out + its rows back; the owner side moves the W workers' segments
+            # for it, about the same volume summed over the node
+            self._tadd("pull_bytes", n * 8 + (n * self.dim * 4 if fetch else 0))
+            self._tadd("serve_bytes", n * 8 + (n * self.dim * 4 if fetch else 0))
+            self._tn["pulls"] += 1
         self.stats["pulls"] += 1
         return out, st
 
@@ -289,11 +367,19 @@ class RowPlane:
         if self.ep["acc"] > 0:
             self._wait_all("acc", self.ep["acc"])
             self._stream_wait_peers("acc")
+        t = self._t0()
         if nu_bound:
             self.grads[:nu_bound].copy_(ug[:nu_bound])
+        self._t1("grd", t)
         self._stage("grd")
+        if self.timing:
+            self._tadd("push_bytes", nu_bound * self.dim * 4)
+            self._tadd("acc_bytes", nu_bound * self.dim * 4 * 3)  # read grads, read + write acc
+            self._tn["pushes"] += 1
         if self.gpu:
+            t = self._t0()
             acc.add_gpu(self, st)
+            self._t1("acc", t)
         else:
             parts = []
             for r, (off, c) in enumerate(st["segs"]):
@@ -362,10 +448,17 @@ class RowAccumulator:
         self._begin()
         self._cpu.append((slots, g))
 
-    def apply(self, gscale: float, step: int) -> None:
+    def apply(self, gscale: float, step: int, plane: Optional[RowPlane] = None) -> None:
         if not self.open:
             return
         self.open = False
+        t = plane._t0() if plane is not None else None
+        self._apply(gscale, step)
+        if t is not None:
+            plane._t1("apply", t)
+            plane._tn["applies"] += 1
+
+    def _apply(self, gscale: float, step: int) -> None:
         sh = self.shard
         if sh.gpu:
             u = sh.updater

@@ -587,7 +587,7 @@ class ShardedSparseTable:
         avg = self.average if average is None else average
         gs = gscale if gscale is not None else (1.0 / self.world if avg else 1.0)
         if self._rowacc is not None and self._rowacc.open:
-            self._rowacc.apply(gs, self.round + 1)
+            self._rowacc.apply(gs, self.round + 1, self.plane)
             self.round += 1
             return
         if not self._acc:

@@ -72,3 +72,29 @@ def test_plane_microbatch_accumulation_equals_big_batch():
     for r in range(2):
         assert all(rnd == steps for _, _, rnd in res[r][2].values())  # one owner step per round
         _assert_same(res[r][:2], single)
+
+
+def _timed(tp, steps, n):
+    import os
+
+    os.environ["PS_AMD_ROWPLANE_TIMING"] = "1"
+    ctx.init()
+    m = _build(True, sharded_table_factory(tp, None, seed=7))
+    tabs = m.tables()
+    tr = Trainer(m, CollectiveEngine(m, tp, bucket_mb=0.001))
+    lo, hi = tp.rank * n // tp.world, (tp.rank + 1) * n // tp.world
+    for b in _batches(steps, n, True):
+        tr.train([{k: v[lo:hi] for k, v in b.items()}])
+    return {k: t.plane.timing_summary() for k, t in tabs.items()}
+
+
+def test_plane_stage_timing_table():
+    """Per-stage table of the row plane (VERDICT r4 Next #3): every stage timed, host waits at
+    each cross-rank point, bytes per pull / push."""
+    res = dist_util.run(_timed, 2, (3, 40))
+    for r in range(2):
+        for name, tm in res[r].items():
+            assert tm["pulls"] >= 3 and tm["pushes"] >= 3 and tm["applies"] >= 3, (name, tm)
+            for k in ("pub_ms", "serve_ms", "out_ms", "grd_ms", "wait_pub_ms", "wait_rows_ms", "wait_grd_ms",
+                      "pull_bytes", "push_bytes"):
+                assert k in tm and tm[k] >= 0, (name, k, tm)
