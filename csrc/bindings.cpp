@@ -88,7 +88,8 @@ void fused_opt(int64_t kind, Tensor w, c10::optional<Tensor> st0, c10::optional<
 void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::optional<Tensor> st1, Tensor rows,
                 Tensor grad, bool rowwise, bool skip_zero, double lr, double beta1, double beta2, double eps,
                 double wd, double momentum, double dampening, bool nesterov, bool adamw, double bc1, double bc2,
-                double l1, double l2, double fbeta, int64_t ftrl_mode, double gscale, c10::optional<Tensor> perm) {
+                double l1, double l2, double fbeta, int64_t ftrl_mode, double gscale, c10::optional<Tensor> perm,
+                c10::optional<Tensor> ncount) {
   check_f32(table, "table");
   TORCH_CHECK(table.dim() == 2, "table must be [rows, dim]");
   check_i64(rows, "rows");
@@ -125,6 +126,11 @@ void sparse_opt(int64_t kind, Tensor table, c10::optional<Tensor> st0, c10::opti
   a.dampening = dampening; a.nesterov = nesterov; a.adamw = adamw;
   a.bc1 = bc1; a.bc2 = bc2; a.l1 = l1; a.l2 = l2; a.fbeta = fbeta; a.ftrl_mode = static_cast<int>(ftrl_mode);
   a.gscale = gscale;
+  if (ncount.has_value() && ncount->defined()) {  // device count of the live rows (a touched list)
+    check_gpu(*ncount, "ncount");
+    TORCH_CHECK(ncount->scalar_type() == torch::kInt32 && ncount->numel() == 1, "ncount: int32 [1]");
+    a.ncount = ncount->data_ptr<int32_t>();
+  }
   psamd::launch_sparse_opt(a, cur_stream(table));
 }
 
@@ -1697,7 +1703,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rows"), py::arg("grad"), py::arg("rowwise"), py::arg("skip_zero"), py::arg("lr"), py::arg("beta1"),
         py::arg("beta2"), py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"),
         py::arg("nesterov"), py::arg("adamw"), py::arg("bc1"), py::arg("bc2"), py::arg("l1"), py::arg("l2"),
-        py::arg("fbeta"), py::arg("ftrl_mode"), py::arg("gscale"), py::arg("perm") = py::none());
+        py::arg("fbeta"), py::arg("ftrl_mode"), py::arg("gscale"), py::arg("perm") = py::none(), py::arg("ncount") = py::none());
   m.def("sumsq", &sumsq);
   m.def("clip_factor", &clip_factor);
   m.def("cast_", &cast_);

@@ -106,6 +106,7 @@ struct SparseOptArgs {
   float bc1, bc2, l1, l2, fbeta;
   int ftrl_mode;
   float gscale;
+  const int32_t* ncount = nullptr;  // nullable device count: only rows [0, min(nrows, *ncount)) are live
 };
 void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s);
 

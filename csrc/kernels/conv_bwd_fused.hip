@@ -111,19 +111,18 @@ __device__ __forceinline__ bf16x8_t cat8(s16x4 lo, s16x4 hi) {
 // kh = wave >> 2) -- the two halves of a dW block are summed in fixed order at the end.
 template <int CI, int CO>
 __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11BwdArgs p) {
-  static_assert(CI == 64, "CI = 64: two 32-channel blocks");
-  static_assert(CO % kKS == 0 && CO >= 128 && CO <= 256, "CO: 2-4 stages of 64 and >= 16 chunks per weight row");
+  static_assert(CI == 64 && CO == 256, "the layer-1 conv3 shape (64 -> 256): 4 stages per tile");
   constexpr int NS = CO / kKS;        // stages per tile
+  constexpr int NR = 5, PD = NR - 1;  // ring slots; stage q + PD is issued during stage q
   constexpr int WROW = CO * 2;        // bytes per weight row
   constexpr int W_BYTES = CI * WROW;  // resident W3t
   constexpr int RING = W_BYTES;
-  constexpr int Z2 = RING + 3 * kSlot;
-  constexpr int A2B = Z2 + 2 * kSlot;      // per-wave a2 fragments of the tile: [8][4 ks][64 lanes] x 16 B
-  constexpr int PAR = A2B + kNW * 4 * 1024;
+  constexpr int Z2 = RING + NR * kSlot;
+  constexpr int PAR = Z2 + 2 * kSlot;
   constexpr int NPAR = 3 * CO + 4 * CI;  // ca | cb | cc | sc2 | sh2 | mean2 | invstd2
   constexpr int LDS_BYTES = PAR + NPAR * 4;
   static_assert(LDS_BYTES <= 163840, "LDS budget");
-  static_assert(4 * NS * 16 * 64 * 4 <= 5 * kSlot, "dW half-sum scratch fits the ring + z2 slots");
+  static_assert(4 * NS * 16 * 64 * 4 <= (NR + 2) * kSlot, "dW half-sum scratch fits the ring + z2 slots");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   float* const par = reinterpret_cast<float*>(lds + PAR);
   const uint32_t L0 = lds_addr(lds);
@@ -169,20 +168,22 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   };
   // z3 of a stage into registers: thread t owns logical chunk t & 7 of rows (t >> 3) + 64 i
   const int zr = t >> 3, zc = t & 7;
-  u16x8 z3r[2];
-  auto load_z3 = [&](int q) {
+  // two register sets by stage parity: z3 of stage q + 2 is loaded while stage q + 1's waits
+  u16x8 z3r[2][2];
+  auto load_z3 = [&](int q, u16x8 (&dst)[2]) {
     const int m0 = stage_m0(q), col = (q % NS) * kKS + zc * 8;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int m = m0 + zr + 64 * i;
-      z3r[i] = m < p.M ? *reinterpret_cast<const u16x8*>(p.z3 + static_cast<int64_t>(m) * CO + col)
+      dst[i] = m < p.M ? *reinterpret_cast<const u16x8*>(p.z3 + static_cast<int64_t>(m) * CO + col)
                        : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
   issue_tile(p.z2, CI, 0, stage_m0(0), Z2);
-  issue_tile(p.g, CO, 0, stage_m0(0), RING);
-  issue_tile(p.g, CO, (1 % NS) * kKS, stage_m0(1), RING + kSlot);
-  load_z3(0);
+#pragma unroll
+  for (int i = 0; i < PD; ++i) issue_tile(p.g, CO, (i % NS) * kKS, stage_m0(i), RING + i * kSlot);
+  load_z3(0, z3r[0]);
+  load_z3(1, z3r[1]);
   wait_vm<0>();
   lds_bar();
 
@@ -218,10 +219,8 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   float s1 = 0.f, s2 = 0.f;
 
   // a2 = relu(bf16(z2 sc + sh)) fragments of this tile (B operand of the weight gradient): lane's
-  // channel is fixed (32 cw + fr), its 8 values are 8 consecutive pixels.  Parked in this wave's
-  // own LDS slots (written and read back by the same wave: in order, no barrier) -- in registers
-  // they pushed the kernel past 256 VGPRs
-  const uint32_t a2s = L0 + A2B + wave * 4096 + lane * 16;
+  // channel is fixed (32 cw + fr), its 8 values are 8 consecutive pixels
+  bf16x8_t a2f[4];
   auto make_a2 = [&](int ti) {
     const uint32_t zs = L0 + Z2 + (ti & 1) * kSlot + khw * (4 * 2048);
     s16x4 lo[4], hi[4];
@@ -239,11 +238,11 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) * asc + ash);
       const s16x8i z = {0, 0, 0, 0, 0, 0, 0, 0};
-      st_b128(a2s + ks * 1024, __builtin_bit_cast(bf16x8_t, __builtin_elementwise_max(__builtin_bit_cast(s16x8i, v), z)));
+      a2f[ks] = __builtin_bit_cast(bf16x8_t, __builtin_elementwise_max(__builtin_bit_cast(s16x8i, v), z));
     }
   };
   // bn3 backward over stage slot `sl` in place: dz3 = bf16(ca g + cb z3 + cc); rows past M -> 0
-  auto transform = [&](int sl, int s, int m0) {
+  auto transform = [&](int sl, int s, int m0, const u16x8 (&z3v)[2]) {
     const uint32_t ds = L0 + RING + sl * kSlot;
     const uint32_t pa = L0 + PAR + (s * kKS + zc * 8) * 4;
     const f32x4 ca0 = ld_f4(pa), ca1 = ld_f4(pa + 16);
@@ -264,7 +263,7 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
     for (int i = 0; i < 2; ++i) {
       tie(gv[i]);
       const u16x8 g8 = __builtin_bit_cast(u16x8, gv[i]);
-      const u16x8 z8 = z3r[i];
+      const u16x8 z8 = z3v[i];
       u16x8 d;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -280,12 +279,11 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
     const uint32_t ds = L0 + RING + sl * kSlot;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x8_t wa[2], xb[2], af[2];
+      bf16x8_t wa[2], xb[2];
       s16x4 dlo[2], dhi[2];
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
         const int ks = 2 * h + k2;
-        af[k2] = ld_b128(a2s + ks * 1024);
         wa[k2] = ld_b128(wrow + ((((8 * s + 2 * ks + fh) ^ (fr & 15))) << 4));
         xb[k2] = ld_b128(ds + dpx * 128 + (((2 * ks + fh) ^ dsw) << 4));
         dlo[k2] = ld_tr(ds + (4 * khw + ks) * 2048 + tD0);
@@ -296,7 +294,6 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
       for (int k2 = 0; k2 < 2; ++k2) {
         tie(wa[k2]);
         tie(xb[k2]);
-        tie(af[k2]);
         tie(dlo[k2]);
         tie(dhi[k2]);
       }
@@ -305,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
         acc_dg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb[k2], wa[k2], acc_dg, 0, 0, 0);
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2)
-        aw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(dlo[k2], dhi[k2]), af[k2], aw, 0, 0, 0);
+        aw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(dlo[k2], dhi[k2]), a2f[2 * h + k2], aw, 0, 0, 0);
     }
   };
   // data-gradient epilogue of tile ti (the conv_gemm epi-3 arithmetic): bn2's ReLU mask from z2,
@@ -342,29 +339,30 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
     zero16(acc_dg);
   };
 
-  // ---- main loop: stage q of tile ti in ring slot q % 3; G(q + 2) and z3(q + 1) are issued during
-  // stage q (and z2 of tile ti + 1 during its stage 0), every issue unconditional (zero rows past
-  // the block's work) so the counted waits hold
+  // ---- main loop: stage q of tile ti in ring slot q % NR; G(q + PD) and z3(q + 2) are issued
+  // during stage q (and z2 of tile ti + 1 during its stage 0), every issue unconditional (zero
+  // rows past the block's work) so the counted waits hold
   int sl = 0, q = 0;
   for (int ti = 0; ti < my_tiles; ++ti) {
     const int m0 = (mg + ti * GM) * kTM;
 #pragma unroll
     for (int s = 0; s < NS; ++s, ++q) {
       if (s == 0) make_a2(ti);
-      transform(sl, s, m0);
+      transform(sl, s, m0, z3r[s & 1]);
       lds_bar();  // dz3 of stage q complete in slot sl; stage q - 1's slot is free
-      const int sl2 = sl == 0 ? 2 : sl - 1;  // (q + 2) % 3
-      issue_tile(p.g, CO, ((q + 2) % NS) * kKS, stage_m0(q + 2), RING + sl2 * kSlot);
-      load_z3(q + 1);
+      const int slp = sl == 0 ? NR - 1 : sl - 1;  // (q + PD) % NR = (q - 1) % NR
+      issue_tile(p.g, CO, ((q + PD) % NS) * kKS, stage_m0(q + PD), RING + slp * kSlot);
+      load_z3(q + 2, z3r[s & 1]);
       if (s == 0) issue_tile(p.z2, CI, 0, ti + 1 < my_tiles ? m0 + GM * kTM : p.M, Z2 + ((ti + 1) & 1) * kSlot);
       compute(sl, accW[s], s);
       if (s == NS - 1) epilogue(ti);
-      // G(q + 1) landed: every op younger than it -- G(q + 2) (2 DMAs) and, at s == 0, the z2 tile
-      // (2 DMAs) -- may stay in flight
-      if (s == 0) wait_vm<4>();
-      else wait_vm<2>();
+      // G(q + 1) (issued during stage q - 3) landed: younger than it are the G DMAs of stages
+      // q - 2 .. q (6) and the z2 tile issued in stage q - 3 .. q (2): vmcnt(8).  At a tile's last
+      // stage the z2 tile of the next one (issued at its stage 0) must have landed too: vmcnt(6)
+      if (s == NS - 1) wait_vm<6>();
+      else wait_vm<8>();
       lds_bar();
-      sl = sl == 2 ? 0 : sl + 1;
+      sl = sl == NR - 1 ? 0 : sl + 1;
     }
   }
   wait_vm<0>();  // no DMA may land in LDS after the block (or into the scratch below)
@@ -432,7 +430,7 @@ int slab_levels(int nslab) { return nslab > 16 ? (nslab + 15) / 16 : 0; }
 
 }  // namespace
 
-bool conv11_bwd_fused_ok(int CI, int CO) { return CI == 64 && (CO == 256 || CO == 128); }
+bool conv11_bwd_fused_ok(int CI, int CO) { return CI == 64 && CO == 256; }
 
 int conv11_bwd_blocks(int M, int CI, int CO) {
   (void)CI;
@@ -449,12 +447,8 @@ int64_t conv11_bwd_ws(int M, int CI, int CO) {
 void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t s) {
   if (a.M <= 0) return;
   const int gm = conv11_bwd_blocks(a.M, CI, CO);
-  if (CI == 64 && CO == 256)
-    hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256>), dim3(gm), dim3(512), 0, s, a);
-  else if (CI == 64 && CO == 128)
-    hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 128>), dim3(gm), dim3(512), 0, s, a);
-  else
-    return;
+  if (CI == 64 && CO == 256) hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256>), dim3(gm), dim3(512), 0, s, a);
+  else return;
   const int64_t E = static_cast<int64_t>(CI) * CO;
   const unsigned eb = static_cast<unsigned>((E + 255) / 256);
   const int groups = slab_levels(gm);

@@ -430,7 +430,8 @@ __global__ __launch_bounds__(256) void sparse_opt_kernel(float* __restrict__ tab
                                                           float* __restrict__ st1, const int64_t* __restrict__ rows,
                                                           const int64_t* __restrict__ perm,
                                                           const G* __restrict__ grad, int64_t nrows, int dim,
-                                                          OptParams p, int rowwise) {
+                                                          OptParams p, int rowwise, const int32_t* __restrict__ ncount) {
+  if (ncount) nrows = min(nrows, static_cast<int64_t>(*ncount));
   float scale = p.gscale;
   if (p.gscale_ptr) scale *= *p.gscale_ptr;
   const int lane = threadIdx.x & 63;
@@ -483,7 +484,9 @@ __global__ __launch_bounds__(256) void sparse_opt_vec_kernel(float* __restrict__
                                                               float* __restrict__ st1, const int64_t* __restrict__ rows,
                                                               const int64_t* __restrict__ perm,
                                                               const G* __restrict__ grad, int64_t nrows, int dim,
-                                                              int lg, OptParams p, int rowwise) {
+                                                              int lg, OptParams p, int rowwise,
+                                                              const int32_t* __restrict__ ncount) {
+  if (ncount) nrows = min(nrows, static_cast<int64_t>(*ncount));
   float scale = p.gscale;
   if (p.gscale_ptr) scale *= *p.gscale_ptr;
   const int lane = threadIdx.x & 63;
@@ -570,10 +573,11 @@ void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
   if (a.g_bf16)                                                                                                  \
     hipLaunchKernelGGL((sparse_opt_vec_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0,      \
                        a.st1, a.rows, a.perm, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, lg, p,     \
-                       a.rowwise);                                                                               \
+                       a.rowwise, a.ncount);                                                                     \
   else                                                                                                           \
     hipLaunchKernelGGL((sparse_opt_vec_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1, \
-                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, lg, p, a.rowwise);
+                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, lg, p, a.rowwise,    \
+                       a.ncount);
     switch (a.kind) {
       case kSGD: PSAMD_SPARSE_VEC(kSGD); break;
       case kAdam: PSAMD_SPARSE_VEC(kAdam); break;
@@ -588,10 +592,11 @@ void launch_sparse_opt(const SparseOptArgs& a, hipStream_t s) {
 #define PSAMD_SPARSE_LAUNCH(K)                                                                                  \
   if (a.g_bf16)                                                                                                 \
     hipLaunchKernelGGL((sparse_opt_kernel<K, uint16_t>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,  \
-                       a.rows, a.perm, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, p, a.rowwise);     \
+                       a.rows, a.perm, static_cast<const uint16_t*>(a.grad), a.nrows, a.dim, p, a.rowwise,      \
+                       a.ncount);                                                                               \
   else                                                                                                          \
     hipLaunchKernelGGL((sparse_opt_kernel<K, float>), dim3(grid), dim3(block), 0, s, a.table, a.st0, a.st1,     \
-                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, p, a.rowwise);
+                       a.rows, a.perm, static_cast<const float*>(a.grad), a.nrows, a.dim, p, a.rowwise, a.ncount);
   switch (a.kind) {
     case kSGD: PSAMD_SPARSE_LAUNCH(kSGD); break;
     case kAdam: PSAMD_SPARSE_LAUNCH(kAdam); break;

@@ -524,6 +524,12 @@ __global__ __launch_bounds__(256) void row_plane_send_kernel(const float* __rest
 // one worker's pushed rows into the owner's fp32 accumulator (pass w of W, launched in rank
 // order: deterministic sums, no atomics on the data).  A slot first seen this round (tflag !=
 // tag) is appended to the touched list and its accumulator row overwritten instead of added to.
+// Each block owns a contiguous chunk of kAccChunk entries and collects its first-touched slots in
+// LDS (LDS atomics), then reserves their range of the touched list with ONE global atomic: a
+// global atomic per first touch (one address, ~1M times per DLRM push) had serialised the kernel
+// at ~0.3 TB/s (profiles/r5_dlrm_w2_row_plane_stages_before.json).  The list order is arbitrary;
+// the apply updates each listed row once, so the result does not depend on it.
+constexpr int kAccChunk = 1024;
 template <int V>
 __global__ __launch_bounds__(256) void row_plane_accum_kernel(const RowPeers P, int w, const int64_t* __restrict__ rslots,
                                                               const int64_t* __restrict__ pmeta, float* __restrict__ acc,
@@ -531,19 +537,25 @@ __global__ __launch_bounds__(256) void row_plane_accum_kernel(const RowPeers P, 
                                                               int64_t* __restrict__ touched, int32_t* __restrict__ tcount,
                                                               int64_t cap, int dim, int lpe) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // worker w's pushed rows (system scope)
+  __shared__ int64_t lslots[kAccChunk];
+  __shared__ int lcount, lbase;
   const int epb = 256 / lpe;
   const int64_t cnt = pmeta[2 * w + 1], off = pmeta[2 * w];
-  const int64_t nb = (cnt + epb - 1) / epb;
+  const int64_t j0 = static_cast<int64_t>(blockIdx.x) * kAccChunk;
+  if (j0 >= cnt) return;  // block-uniform
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
+  const int64_t j1 = min(cnt, j0 + kAccChunk);
   const int sub = threadIdx.x / lpe, ql = threadIdx.x % lpe;
   const float* src = P.grads[w];
-  for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const int64_t j = b * epb + sub;
-    const int64_t slot = j < cnt ? rslots[static_cast<int64_t>(w) * cap + j] : -1;
+  for (int64_t jb = j0; jb < j1; jb += epb) {
+    const int64_t j = jb + sub;
+    const int64_t slot = j < j1 ? rslots[static_cast<int64_t>(w) * cap + j] : -1;
     // every lane of the entry reads the flag before its first lane writes it (one wave, in order)
     const bool first = slot >= 0 && tflag[slot] != tag;
     if (slot >= 0 && ql == 0 && first) {
       tflag[slot] = tag;
-      touched[atomicAdd(tcount, 1)] = slot;
+      lslots[atomicAdd(&lcount, 1)] = slot;
     }
     if (slot < 0) continue;
     const float* g = src + (off + j) * dim;
@@ -558,6 +570,10 @@ __global__ __launch_bounds__(256) void row_plane_accum_kernel(const RowPeers P, 
       }
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) lbase = lcount ? atomicAdd(tcount, lcount) : 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < lcount; i += blockDim.x) touched[lbase + i] = lslots[i];
 }
 
 static int row_lanes(int dim, int V) {  // lanes per entry: a power of two <= 64 covering dim / V
@@ -587,7 +603,7 @@ void launch_row_plane_accum(const RowPeers& P, const int64_t* rslots, const int6
                             int32_t tag, int64_t* touched, int32_t* tcount, int64_t cap, int dim, hipStream_t s) {
   const bool v4 = dim % 4 == 0;
   const int lpe = row_lanes(dim, v4 ? 4 : 1);
-  const int grid = static_cast<int>(std::min<int64_t>(std::max<int64_t>(1, cap / (256 / lpe)), 16384));
+  const int grid = static_cast<int>(std::max<int64_t>(1, (cap + kAccChunk - 1) / kAccChunk));
   for (int w = 0; w < P.W; ++w) {  // rank order
     if (v4)
       hipLaunchKernelGGL(row_plane_accum_kernel<4>, dim3(grid), dim3(256), 0, s, P, w, rslots, pmeta, acc, tflag, tag,

@@ -96,8 +96,12 @@ def fused_opt(kind: int, w: torch.Tensor, st0: Optional[torch.Tensor], st1: Opti
 
 def sparse_opt(kind: int, table: torch.Tensor, st0: Optional[torch.Tensor], st1: Optional[torch.Tensor],
                rows: torch.Tensor, grad: torch.Tensor, rowwise: bool = False, skip_zero: bool = False,
-               perm: Optional[torch.Tensor] = None, **hp) -> None:
+               perm: Optional[torch.Tensor] = None, ncount: Optional[torch.Tensor] = None, **hp) -> None:
     """Row-sparse optimizer step on ``table[rows]``.
+
+    ``ncount`` (int32 [1], device): only ``rows[:ncount]`` are live -- a touched list whose length
+    stays on the device (the row plane's accumulator), so the kernel stops there instead of
+    walking the list's full capacity.
 
     ``perm is None``: ``rows`` unique, ``grad`` [len(rows), dim] row-aligned.
     ``perm`` given: ``rows`` SORTED with repeats, ``grad[perm[j]]`` belongs to ``rows[j]``; the
@@ -109,8 +113,11 @@ def sparse_opt(kind: int, table: torch.Tensor, st0: Optional[torch.Tensor], st1:
         native().sparse_opt(kind, table, st0, st1, rows, grad, bool(rowwise), bool(skip_zero), h["lr"], h["beta1"],
                             h["beta2"], h["eps"], h["wd"], h["momentum"], h["dampening"], bool(h["nesterov"]),
                             bool(h["adamw"]), h["bc1"], h["bc2"], h["l1"], h["l2"], h["fbeta"], int(h["ftrl_mode"]),
-                            h["gscale"], perm)
+                            h["gscale"], perm, ncount)
         return
+    if ncount is not None:
+        rows = rows[:int(ncount.item())]
+        perm = perm[:rows.numel()] if perm is not None else None
     if rows.numel() == 0:
         return
     dim = table.shape[1]

@@ -463,8 +463,9 @@ class RowAccumulator:
         if sh.gpu:
             u = sh.updater
             skip = getattr(u, "mode", "") == "reference"
+            # the touched list is capacity-sized; its live length is the device count tcount
             u.step_rows(sh.table, sh.states, self.touched, self.acc, gscale=gscale, step=step,
-                        rowwise=getattr(u, "rowwise", False), skip_zero=skip, perm=self.touched)
+                        rowwise=getattr(u, "rowwise", False), skip_zero=skip, perm=self.touched, ncount=self.tcount)
             return
         slots = torch.cat([s for s, _ in self._cpu])
         g = torch.cat([x for _, x in self._cpu])

@@ -75,14 +75,16 @@ class Updater:
 
     def step_rows(self, table: torch.Tensor, states: List[torch.Tensor], rows: torch.Tensor, grad: torch.Tensor,
                   gscale: float = 1.0, step: Optional[int] = None, rowwise: bool = False,
-                  skip_zero: bool = False, perm: Optional[torch.Tensor] = None) -> None:
+                  skip_zero: bool = False, perm: Optional[torch.Tensor] = None,
+                  ncount: Optional[torch.Tensor] = None) -> None:
         """Row-sparse step; with ``perm`` the rows are sorted with repeats and each run's
-        gradient rows are summed into one update (ops/optim.py sparse_opt)."""
+        gradient rows are summed into one update (ops/optim.py sparse_opt); ``ncount`` bounds a
+        device-counted row list."""
         st = list(states) + [None] * (2 - len(states))
         h = self.hyper(self.t + 1 if step is None else step)
         h["gscale"] = h.get("gscale", 1.0) * gscale
         _o.sparse_opt(self.kind, table, st[0], st[1], rows, grad, rowwise=rowwise, skip_zero=skip_zero, perm=perm,
-                      **h)
+                      ncount=ncount, **h)
 
     # ---------------------------------------------------------------- reference API
     def update(self, key: str, w: torch.Tensor, dw: torch.Tensor) -> torch.Tensor:
