@@ -11,15 +11,20 @@ batch-prefetch many keys (:109-127, 279-298); rows of the sparse layers are keys
 Here the same API drives the GPU engines directly, with no ``nn.Module`` in between:
 
 * ``init(specs)``  declares keys (name -> initial tensor, or (shape, dtype) for zeros, or a
-  callable).  Declaration is collective and ends at the first data-plane call: the store then
-  SEALS -- every rank checks that all ranks declared the same keys, rank 0's initial values
-  are broadcast, and the engine lays the keys out in its flat buckets once:
+  callable).  Declaration is collective and ends at the next data-plane call: the store then
+  SEALS the pending keys as one KEY GROUP -- every rank checks that all ranks declared the same
+  keys, rank 0's initial values are broadcast, and an engine lays the group out in its flat
+  buckets (owner ranges, fp32 masters, optimizer state, plane arenas):
     consistency "bsp" (staleness s >= 0) -> ``ColocatedPS`` (xGMI plane on one node, RCCL
                                             collectives otherwise, gloo on CPU);
     consistency "ssp" / "asp"            -> ``AsyncPS`` (one-sided mailboxes + native owner
                                             threads).
   Keys are registered in declaration order and the engines lay them out in reverse (the
   order gradients become ready in a backward pass), so declare keys in forward order.
+  Keys may appear at ANY round (the reference creates a key on its first ``get(key, init)``,
+  store/KVStore.java:136-190): keys declared after a group was sealed form the next group, sealed
+  by the next data-plane call -- a new engine beside the first, on the same ranks, whose rounds
+  ``barrier`` advances together with the others (groups in creation order on every rank).
 * ``pull(keys)``   the replica views of the current weight slot (device tensors; valid until
   the next ``barrier``, clone to keep them).  After ``barrier`` the compute stream already
   waits for the round the next forward may see (BSP: the one just pushed; SSP: t - s), so a
@@ -84,7 +89,9 @@ class GpuKVStore:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
-        self.ps = None  # the engine, once sealed
+        self.ps = None  # the first group's engine, once sealed
+        self.engines: List[object] = []  # one engine per key group, in creation order
+        self._key_engine: Dict[str, object] = {}
         self.umap: Optional[Dict[str, Updater]] = None
         if updaters is not None:
             self.set_updaters(updaters)
@@ -118,16 +125,17 @@ class GpuKVStore:
         return self.ps is not None
 
     def keys(self) -> List[str]:
-        return list(self.params if self.sealed else self._decl)
+        return list(self.params) + [k for k in self._decl if k not in self.params]
 
     def __contains__(self, key: str) -> bool:
-        return key in (self.params if self.sealed else self._decl)
+        return key in self.params or key in self._decl
 
     # ------------------------------------------------------------------ declaration
     def init(self, specs: Mapping[str, Spec]) -> None:
         """Declare keys (collective: every rank declares the same keys, in the same order).
         A key declared again with the same shape and dtype keeps its first value (the
-        reference's upsert with replace=false: the first writer wins)."""
+        reference's upsert with replace=false: the first writer wins).  After the first seal,
+        new keys wait as the next key group until the next pull / push / barrier seals it."""
         for k, v in specs.items():
             t = self._materialize(v)
             if k in self._decl or k in self.params:
@@ -136,9 +144,6 @@ class GpuKVStore:
                     raise ValueError(f"key {k!r} re-declared as {tuple(t.shape)} {t.dtype}, "
                                      f"was {tuple(have.shape)} {have.dtype}")
                 continue
-            if self.sealed:
-                raise KeyError(f"key {k!r} declared after the store was sealed: declare every key with init() "
-                               "before the first pull / push / barrier (the engine lays out its buckets once)")
             self._decl[k] = t
 
     def _materialize(self, v: Spec) -> torch.Tensor:
@@ -152,7 +157,9 @@ class GpuKVStore:
         return v.detach().to(self.device).clone()
 
     def _seal(self) -> None:
-        if self.ps is not None:
+        """Seal the pending keys (collective): the first call builds the first key group's
+        engine; keys declared later become further groups, each with an engine of its own."""
+        if self.ps is not None and not self._decl:
             return
         if not self._decl:
             raise RuntimeError("GpuKVStore: no keys declared (call init() first)")
@@ -163,32 +170,39 @@ class GpuKVStore:
         if any(s != sigs[0] for s in sigs):
             bad = [r for r, s in enumerate(sigs) if s != sigs[0]]
             raise RuntimeError(f"GpuKVStore: ranks {bad} declared different keys than rank 0")
-        self.params = {k: torch.nn.Parameter(v, requires_grad=True) for k, v in self._decl.items()}
-        self._init_host = {k: v.detach().float().cpu() for k, v in self._decl.items()}
+        group = {k: torch.nn.Parameter(v, requires_grad=True) for k, v in self._decl.items()}
+        for k, v in self._decl.items():
+            self._init_host[k] = v.detach().float().cpu()
         self._decl = {}
-        bank = _KeyBank(self.params)
+        bank = _KeyBank(group)
         kw = self._kw
         if self.consistency == "bsp":
             from .colocated import ColocatedPS
 
-            self.ps = ColocatedPS(bank, self.umap, self.t, bucket_mb=kw["bucket_mb"],
-                                  last_bucket_mb=kw["last_bucket_mb"], staleness=self.staleness,
-                                  clip_norm=kw["clip_norm"], compress=kw["compress"],
-                                  compress_warmup=kw["compress_warmup"], average=kw["average"], overlap=True,
-                                  plane=kw["plane"], timeout_s=kw["timeout_s"])
+            eng = ColocatedPS(bank, self.umap, self.t, bucket_mb=kw["bucket_mb"],
+                              last_bucket_mb=kw["last_bucket_mb"], staleness=self.staleness,
+                              clip_norm=kw["clip_norm"], compress=kw["compress"],
+                              compress_warmup=kw["compress_warmup"], average=kw["average"], overlap=True,
+                              plane=kw["plane"], timeout_s=kw["timeout_s"])
         else:
             from .async_ps import AsyncPS
 
             if kw["clip_norm"] is not None or kw["compress"] is not None:
                 raise ValueError("clipping / compression are BSP-engine options")
-            self.ps = AsyncPS(bank, self.umap, self.t, staleness=None if self.consistency == "asp" else self.staleness,
-                              timeout_s=kw["timeout_s"], bucket_mb=kw["bucket_mb"],
-                              gscale=None if kw["average"] else 1.0)
+            eng = AsyncPS(bank, self.umap, self.t, staleness=None if self.consistency == "asp" else self.staleness,
+                          timeout_s=kw["timeout_s"], bucket_mb=kw["bucket_mb"],
+                          gscale=None if kw["average"] else 1.0)
+        self.engines.append(eng)
+        if self.ps is None:
+            self.ps = eng
+        self.params.update(group)
+        for k in group:
+            self._key_engine[k] = eng
         # the broadcast of rank 0's values happened inside the engine; the initial values the
         # loss surface interpolates from are the ones every rank now holds
         if self.world > 1:
-            for k in self.params:
-                self._init_host[k] = self.ps.weight(k).detach().float().cpu()
+            for k in group:
+                self._init_host[k] = eng.weight(k).detach().float().cpu()
 
     # ------------------------------------------------------------------ dense keys
     def pull(self, keys: Union[str, Sequence[str]]) -> Union[torch.Tensor, List[torch.Tensor]]:
@@ -201,7 +215,7 @@ class GpuKVStore:
     def weight(self, key: str) -> torch.Tensor:
         if key not in self.params:
             raise KeyError(f"unknown key {key!r}")
-        return self.ps.weight(key)
+        return self._key_engine[key].weight(key)
 
     def push(self, keys: Union[str, Sequence[str]], grads: Union[torch.Tensor, Sequence[torch.Tensor]]) -> None:
         """Hand gradients of ``keys`` to the engine; a bucket leaves once its last key arrived."""
@@ -213,29 +227,25 @@ class GpuKVStore:
         for k, g in zip(keys, grads):
             if k not in self.params:
                 raise KeyError(f"unknown key {k!r}")
-            self.ps.push_key(k, g)
+            self._key_engine[k].push_key(k, g)
 
     def barrier(self) -> None:
         """End of the round: every bucket leaves, the PS clock advances and the next pull sees
         the round the consistency mode allows (store/KVStore.java:265, net/PServer.java:238-283)."""
         self._seal()
-        self.ps.finish_step()
+        for eng in self.engines:  # creation order on every rank: the collectives line up
+            eng.finish_step()
         self.round += 1
 
     def get(self, key: str, init: Optional[Spec] = None) -> Optional[torch.Tensor]:
         """``get(key)``: the current weights or None for an unknown key; ``get(key, init)``
-        declares the key first if the store is still open (store/KVStore.java:136-159)."""
-        if not self.sealed and init is not None and key not in self._decl:
+        creates the key first (store/KVStore.java:136-159 -> create :168-190), at any round:
+        collective, like ``init`` -- every rank gets the same new key at the same point."""
+        if init is not None and key not in self.params and key not in self._decl:
             self.init({key: init})
-        if not self.sealed:
-            if key not in self._decl:
-                return None
-            self._seal()
-        if key not in self.params:
-            if init is not None:
-                raise KeyError(f"key {key!r} is unknown and the store is sealed (declare it before the first "
-                               "pull / push / barrier)")
+        if key not in self.params and key not in self._decl:
             return None
+        self._seal()
         w = self.weight(key)
         if ctx.status == Stat.LOSS_SURFACE_EVAL:
             s = ctx.weights_scale
@@ -338,20 +348,30 @@ class GpuKVStore:
 
     # ------------------------------------------------------------------ lifecycle
     def synchronize(self) -> None:
-        if self.ps is not None:
-            self.ps.synchronize()
+        for eng in self.engines:
+            eng.synchronize()
         for t in self.tables.values():
             t.synchronize()
 
     def shard_state(self) -> dict:
-        return self.ps.shard_state()
+        """This rank's server state: the engine's for one key group, ``{"groups": [...]}`` for more."""
+        if len(self.engines) == 1:
+            return self.ps.shard_state()
+        return {"groups": [e.shard_state() for e in self.engines]}
 
     def load_shard_state(self, st: dict) -> None:
         self._seal()
-        self.ps.load_shard_state(st)
+        if "groups" in st:
+            if len(st["groups"]) != len(self.engines):
+                raise ValueError(f"checkpoint has {len(st['groups'])} key groups, the store {len(self.engines)}")
+            for e, s in zip(self.engines, st["groups"]):
+                e.load_shard_state(s)
+        else:
+            self.ps.load_shard_state(st)
 
     def stats(self) -> dict:
-        d = {"round": self.round, "keys": len(self.keys()), "engine": type(self.ps).__name__ if self.ps else None}
+        d = {"round": self.round, "keys": len(self.keys()), "engine": type(self.ps).__name__ if self.ps else None,
+             "groups": len(self.engines)}
         if self.ps is not None and hasattr(self.ps, "plane_stats"):
             d["plane"] = self.ps.plane_stats()
             d["plane_kind"] = self.ps.plane_kind
@@ -362,6 +382,8 @@ class GpuKVStore:
             if hasattr(t, "close"):
                 t.close()
         self.tables = {}
-        if self.ps is not None:
-            self.ps.close()
-            self.ps = None
+        for eng in self.engines:
+            eng.close()
+        self.engines = []
+        self._key_engine = {}
+        self.ps = None

@@ -27,7 +27,7 @@ def timeit(fn, reps=10, rounds=3):
 
 def main():
     dev = "cuda"
-    for M, CI, CO in [(1024 * 56 * 56, 64, 256), (256 * 56 * 56, 64, 256)]:
+    for M, CI, CO in [(1024 * 56 * 56, 64, 256), (256 * 56 * 56, 64, 256), (1024 * 28 * 28, 128, 512)]:
         g = torch.Generator(device=dev).manual_seed(0)
         d = torch.randn(M, CO, device=dev, generator=g).bfloat16()
         z3 = torch.randn(M, CO, device=dev, generator=g).bfloat16()

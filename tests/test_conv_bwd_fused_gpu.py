@@ -39,9 +39,9 @@ def _problem(M, CI, CO, seed):
     return d, z3, coef, w3, z2, cf2, m2, i2
 
 
-@pytest.mark.parametrize("M,CO", [(300, 256), (4099, 256), (100003, 256), (38401, 256)])
-def test_conv3_fused_backward_matches_fp32_and_two_kernel_chain(M, CO):
-    CI = 64
+@pytest.mark.parametrize("M,CI,CO", [(300, 64, 256), (4099, 64, 256), (100003, 64, 256), (38401, 64, 256),
+                                     (300, 128, 512), (50001, 128, 512)])
+def test_conv3_fused_backward_matches_fp32_and_two_kernel_chain(M, CI, CO):
     d, z3, coef, w3, z2, cf2, m2, i2 = _problem(M, CI, CO, M + CO)
     assert native().conv11_bwd_fused_supported(CI, CO)
     w3t = _bf(w3.t())
@@ -69,8 +69,9 @@ def test_conv3_fused_backward_matches_fp32_and_two_kernel_chain(M, CO):
     torch.testing.assert_close(part.sum(1), p_ref.sum(1), rtol=2e-3, atol=3e-2)
 
 
-def test_conv3_fused_backward_deterministic():
-    M, CI, CO = 70001, 64, 256
+@pytest.mark.parametrize("CI,CO", [(64, 256), (128, 512)])
+def test_conv3_fused_backward_deterministic(CI, CO):
+    M = 70001
     d, z3, coef, w3, z2, cf2, m2, i2 = _problem(M, CI, CO, 5)
     args = (_bf(d), _bf(z3), coef, _bf(w3.t()), _bf(z2), cf2.to(DEV), m2.to(DEV), i2.to(DEV))
     a = native().conv11_bwd_fused(*args)

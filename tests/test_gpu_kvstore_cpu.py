@@ -125,10 +125,13 @@ def test_single_rank_api_semantics():
         kv.init({"w": torch.zeros(4)})
     torch.testing.assert_close(kv.get("w"), torch.ones(3))  # seals
     assert kv.get("nope") is None
-    with pytest.raises(KeyError):
-        kv.get("nope", lambda: torch.zeros(1))
-    with pytest.raises(KeyError):
-        kv.init({"late": torch.zeros(1)})
+    # keys may appear after the seal (reference: create on the first get(key, init)): a second
+    # key group with an engine of its own
+    torch.testing.assert_close(kv.get("nope", lambda: torch.zeros(1)), torch.zeros(1))
+    kv.init({"late": torch.full((1,), 3.0)})
+    assert "late" in kv and kv.stats()["groups"] == 2
+    torch.testing.assert_close(kv.pull("late"), torch.full((1,), 3.0))
+    assert kv.stats()["groups"] == 3
     # a key pushed twice in a round is summed while its bucket waits for its other key
     kv.push("w", torch.ones(3))
     kv.push("w", torch.ones(3))
@@ -226,3 +229,71 @@ def test_reference_model_trains_through_kvengine_on_gpu_kvstore():
     kv, coll = res[0]
     for k in coll:
         torch.testing.assert_close(kv[k], coll[k], rtol=1e-5, atol=1e-6)
+
+
+LATE = "late.w"
+
+
+def _late_oracle(world, steps, t_new, lr=0.1, mom=0.9):
+    """_oracle's model plus a key created at round t_new (rank 0's initial value 2.0) whose loss
+    term is 0.1 * sum((L - 1)^2) per rank -- momentum state starting at its creation."""
+    x, y = _data()
+    w = _init(0)
+    buf = {k: torch.zeros_like(v) for k, v in w.items()}
+    for t in range(steps):
+        if t == t_new:
+            w[LATE] = torch.full((5,), 2.0)
+            buf[LATE] = torch.zeros(5)
+        gs = [_grads({k: v for k, v in w.items() if k != LATE}, x[r::world], y[r::world]) for r in range(world)]
+        for k in list(w):
+            g = (0.2 * (w[k] - 1.0)) if k == LATE else sum(gr[k] for gr in gs) / world
+            buf[k] = mom * buf[k] + g
+            w[k] = w[k] - lr * buf[k]
+    return w
+
+
+def _late_body(tp, consistency, plane, steps, t_new, mom=0.9):
+    from ps_amd.parallel.gpu_kvstore import GpuKVStore
+    from ps_amd.parallel.updaters import MomentumUpdater, SimpleUpdater
+
+    dev = "cuda" if plane == "gpu" else "cpu"
+    if dev == "cuda":
+        torch.cuda.set_device(0)
+    kv = GpuKVStore(tp, MomentumUpdater(0.1, mom) if mom else SimpleUpdater(0.1), consistency=consistency,
+                    device=dev, bucket_mb=0.0005,
+                    last_bucket_mb=0.0002, plane="xgmi" if plane == "gpu" else plane, timeout_s=60)
+    kv.init({k: v.to(dev) for k, v in _init(tp.rank).items()})
+    x, y = _data()
+    xs, ys = x[tp.rank::tp.world].to(dev), y[tp.rank::tp.world].to(dev)
+    names = list(KEYS)
+    for t in range(steps):
+        if t == t_new:  # a key first appears in round t_new (collective; rank 0's value wins)
+            assert kv.get(LATE, lambda: torch.full((5,), 2.0 + tp.rank, device=dev)) is not None
+        ws = dict(zip(names, kv.pull(names)))
+        g = _grads(ws, xs, ys)
+        kv.push(names, [g[k] for k in names])
+        if t >= t_new:
+            lw = kv.pull(LATE)
+            kv.push(LATE, 0.2 * (lw - 1.0))
+        kv.barrier()
+    kv.synchronize()
+    out = {k: kv.get(k).detach().float().cpu().clone() for k in names + [LATE]}
+    st = kv.stats()
+    kv.close()
+    return out, st
+
+
+@pytest.mark.parametrize("consistency,plane", [("bsp", "collective"), ("bsp", "xgmi"), ("ssp", None)])
+def test_key_created_after_seal_matches_oracle(consistency, plane):
+    """VERDICT r4 Next #6: a dense key first appears in round 3, after the store sealed -- it
+    becomes a second key group (its own engine on the same ranks) and trains like the others."""
+    steps, t_new = 6, 3
+    # the async owners apply each worker's push on arrival (gradient / W): with plain SGD and the
+    # SSP(0) gate that is the BSP trajectory (test_ssp0_async_engine_is_bsp_exact)
+    mom = 0.9 if consistency == "bsp" else 0.0
+    res = dist_util.run(_late_body, 2, (consistency, plane, steps, t_new, mom))
+    want = _late_oracle(2, steps, t_new, mom=mom)
+    for k in want:
+        torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-6)
+        assert torch.equal(res[0][0][k], res[1][0][k])
+    assert res[0][1]["groups"] == 2
