@@ -1552,6 +1552,28 @@ std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt
   return {gy, part, dw};
 }
 
+// A stream whose kernels may only run on n_cus of the device's CUs (hipExtStreamCreateWithCUMask),
+// spread evenly over the CU index space (every (CUs / n)-th CU, so every XCD keeps a share) or the
+// first n.  The PS serve of a single-GPU Llama step runs on it beside backward
+// (parallel/colocated.py, PS_AMD_SERVE_CUS): the serve keeps a bounded slice of the chip instead
+// of contending for all of it.  Returned as the raw handle for torch.cuda.ExternalStream; it lives
+// for the process.
+int64_t cu_mask_stream(int64_t device, int64_t n_cus, bool spread) {
+  hipDeviceProp_t prop;
+  TORCH_CHECK(hipGetDeviceProperties(&prop, static_cast<int>(device)) == hipSuccess, "hipGetDeviceProperties");
+  const int ncu = prop.multiProcessorCount;
+  TORCH_CHECK(n_cus >= 1 && n_cus <= ncu, "n_cus must be in 1..", ncu);
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  const int step = spread ? std::max(1, ncu / static_cast<int>(n_cus)) : 1;
+  int set = 0;
+  for (int c = 0; c < ncu && set < n_cus; c += step, ++set) mask[c / 32] |= 1u << (c % 32);
+  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, static_cast<c10::DeviceIndex>(device)));
+  hipStream_t st = nullptr;
+  TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess,
+              "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<int64_t>(st);
+}
+
 bool conv11_bwd_fused_supported(int64_t ci, int64_t co) {
   return psamd::conv11_bwd_fused_ok(static_cast<int>(ci), static_cast<int>(co));
 }
@@ -1695,6 +1717,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
   m.def("conv11_bwd_fused", &conv11_bwd_fused);
   m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported);
+  m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("n_cus"), py::arg("spread") = true);
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);
   m.def("bn_bwd_partials", &bn_bwd_partials);

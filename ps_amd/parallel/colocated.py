@@ -204,6 +204,19 @@ class ColocatedPS:
         self._key_bucket = {n: R.keys[n].bucket for n in self.params}
         self._landing: List[Dict[str, torch.Tensor]] = [dict() for _ in R.buckets]  # parked grads
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
+        # PS_AMD_SERVE_CUS=N: the comm stream -- where a single-GPU step's optimizer serve runs
+        # beside backward -- only gets N of the CUs (spread over every XCD), so the serve takes a
+        # bounded slice of the chip instead of contending with the backward GEMMs for all of it
+        # (profiles/r5_llama_serve_overlap.txt)
+        import os as _os
+
+        self.serve_cus = int(_os.environ.get("PS_AMD_SERVE_CUS", "0")) if self.gpu else 0
+        if self.serve_cus > 0:
+            from ..ops._ext import native as _nat
+
+            h = _nat().cu_mask_stream(self.device.index if self.device.index is not None
+                                      else torch.cuda.current_device(), self.serve_cus, True)
+            self.comm = torch.cuda.ExternalStream(h, device=self.device)
         # separate push / pull communicators: the all-gather of bucket b runs on
         # its own communicator + stream, so the reduce-scatter of bucket b+1 need not wait behind
         # it; opt-in (PS_AMD_SPLIT_COMM=1) -- the default single communicator is what the
@@ -329,7 +342,9 @@ class ColocatedPS:
                 bk = self.reg.buckets[b]
                 gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
                 words, scales = self.plane.words(b, self.gslot)
-                _cmp.onebit_pack(gin, self.err[b], words, scales)
+                self._mark("pack0")
+                _cmp.onebit_pack(gin, self.err[b], words, scales)  # sign bits + scales + error feedback
+                self._mark("pack1")
             with _trace.range(f"ps.push.b{b}"):
                 self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
             return
@@ -386,6 +401,9 @@ class ColocatedPS:
                 acc["serve_ms"] = acc.get("serve_ms", 0.0) + ms(last.get("push1", last.get("serve0")), t)
             elif name == "pull1":
                 acc["pull_ms"] = acc.get("pull_ms", 0.0) + ms(last["serve1"], t)
+            elif name == "pack1":  # 1-bit pack + error feedback of one bucket (plane path)
+                acc["pack_ms"] = acc.get("pack_ms", 0.0) + ms(last["pack0"], t)
+                acc["packs"] = acc.get("packs", 0.0) + 1.0
             last[name] = t
         if "bwd_end" in last and "round_end" in last:
             acc["exposed_comm_ms"] = max(0.0, ms(last["bwd_end"], last["round_end"]))

@@ -37,7 +37,8 @@ from ps_amd.models.reference import CNN, FullConnectedNN  # noqa: E402
 from ps_amd.train.trainer import CollectiveEngine, Trainer  # noqa: E402
 
 
-def run(kind: str, seed: int, epochs: int, raw: bool = True, device: str = "cpu") -> dict:
+def run(kind: str, seed: int, epochs: int, raw: bool = True, device: str = "cpu", train_rows: int = 800,
+        temp: float = 10000.0) -> dict:
     d = load_reference_mnist()
     X = d["X"] * (255.0 if raw else 1.0)
     Y = d["Y"]
@@ -45,18 +46,20 @@ def run(kind: str, seed: int, epochs: int, raw: bool = True, device: str = "cpu"
     torch.manual_seed(seed)
     gen = torch.Generator().manual_seed(seed)
     if kind == "mlp":
-        model, k, bs = FullConnectedNN.build_model(784, [150, 50, 10], gen=gen), 4, 100
+        model, k, bs = FullConnectedNN.build_model(784, [150, 50, 10], gen=gen, softmax_temp=temp), 4, 100
     else:
-        model, k, bs = CNN.build_model(28, 28, 1, [150, 50, 10], gen=gen), 1, 100
+        model, k, bs = CNN.build_model(28, 28, 1, [150, 50, 10], gen=gen, softmax_temp=temp), 1, 100
     dev = torch.device(device)
     model.to(dev)
     tr = Trainer(model, CollectiveEngine(model), n_threads=k, device=dev if dev.type == "cuda" else None)
-    Xt, Yt = X[:800], Y[:800]
+    n = train_rows  # rows 0 .. n-1 train (a learning curve below 800); rows 800-999 are always held out
+    Xt, Yt = X[:n], Y[:n]
+    bs = min(bs, n // k)
     t0 = time.time()
     ep = 0
     for ep in range(epochs):
-        perm = torch.randperm(800, generator=gen)
-        for i in range(0, 800 - bs * k + 1, bs * k):
+        perm = torch.randperm(n, generator=gen)
+        for i in range(0, n - bs * k + 1, bs * k):
             idx = perm[i:i + bs * k]
             tr.train([{"X": Xt[idx[j * bs:(j + 1) * bs]], "Y": Yt[idx[j * bs:(j + 1) * bs]]} for j in range(k)])
             if ctx.finish:
@@ -65,8 +68,12 @@ def run(kind: str, seed: int, epochs: int, raw: bool = True, device: str = "cpu"
             break
     p = tr.predict([{"X": X[800:]}])[0]
     acc = SoftmaxPrecision(Y[800:], p.cpu()).calculate()
-    return {"model": kind, "seed": seed, "epochs_run": ep + 1, "heldout_acc": round(float(acc), 4),
-            "raw_pixels": raw, "device": device, "seconds": round(time.time() - t0, 1)}
+    from ps_amd.models.losses import CrossEntropy
+
+    return {"model": kind, "seed": seed, "train_rows": n, "softmax_temp": temp, "slim": CrossEntropy.slim,
+            "epochs_run": ep + 1,
+            "heldout_acc": round(float(acc), 4), "raw_pixels": raw, "device": device,
+            "seconds": round(time.time() - t0, 1)}
 
 
 def main():
@@ -75,12 +82,21 @@ def main():
     ap.add_argument("--epochs", type=int, default=100)
     ap.add_argument("--model", default="both", choices=["mlp", "cnn", "both"])
     ap.add_argument("--device", default="cpu", choices=["cpu", "cuda"])
+    ap.add_argument("--train-rows", type=int, nargs="+", default=[800])
+    ap.add_argument("--temp", type=float, default=10000.0, help="softmax temperature (reference: 10000)")
+    ap.add_argument("--slim", type=float, default=None,
+                    help="early-stop threshold on a batch's loss (reference CrossEntropy.slim = 0.01; 0 = off)")
     a = ap.parse_args()
+    if a.slim is not None:
+        from ps_amd.models.losses import CrossEntropy
+
+        CrossEntropy.slim = a.slim if a.slim > 0 else -1.0
     torch.set_num_threads(4)
     kinds = ["mlp", "cnn"] if a.model == "both" else [a.model]
-    for kind in kinds:
-        for s in a.seeds:
-            print(json.dumps(run(kind, s, a.epochs, device=a.device)), flush=True)
+    for n in a.train_rows:
+        for kind in kinds:
+            for s in a.seeds:
+                print(json.dumps(run(kind, s, a.epochs, device=a.device, train_rows=n, temp=a.temp)), flush=True)
 
 
 if __name__ == "__main__":

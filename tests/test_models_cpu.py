@@ -37,6 +37,27 @@ def test_mnist_reference_config_quality(kind, threshold):
     assert r["heldout_acc"] > threshold, r
 
 
+@pytest.mark.skipif(not os.path.exists(MNIST), reason="reference MNIST fixture not mounted")
+def test_mnist_cnn_vs_mlp_relative_quality():
+    """The CNN-over-MLP margin on identical rows (README.md:29-31 claims 0.96 vs 0.92 on the
+    reference's absent training file).  Named cause of the small margin at the reference config
+    (docs/PARITY.md, profiles/r5_cnn_vs_mlp_parity.txt): with softmax T = 1e4 on raw 0-255 pixels
+    the CNN's logits run ~11x hotter than the MLP's (std 53K vs 4.7K at init), its softmax
+    saturates and one batch reaches the per-batch early stop (loss <= 0.01) by epoch 8-12; at
+    T = 1e5 the CNN trains longer and the margin is the README's ~4 points.  Pinned over seeds
+    0-2: CNN >= MLP at the reference config, CNN - MLP >= 2.5 points at T = 1e5."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from mnist_parity import run
+
+    def mean(kind, temp):
+        return sum(run(kind, s, 100, temp=temp)["heldout_acc"] for s in (0, 1, 2)) / 3
+
+    assert mean("cnn", 1e4) >= mean("mlp", 1e4)
+    assert mean("cnn", 1e5) - mean("mlp", 1e5) >= 0.025
+
+
 def test_cnn_reference_shapes_and_grad():
     gen = torch.Generator().manual_seed(1)
     m = CNN.build_model(28, 28, 1, [150, 50, 10], gen=gen)
