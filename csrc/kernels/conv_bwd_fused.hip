@@ -405,16 +405,15 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   }
 }
 
-// The layer-2 shape (CI = 128 -> CO = 512): the per-block dW (512 x 128 fp32) needs 256 VGPRs
-// per lane even over 256 lanes, so this variant runs ONE wave per SIMD (4 waves, 512 VGPRs each)
-// on 64-pixel tiles, and the transposed weight (128 KiB) streams per stage from L2 through its
-// own 3-slot ring (two stages ahead) instead of staying resident.  Waves: data gradient 2 pixel
-// blocks x 2 channel-block pairs (pb = wave & 1, channel blocks 2 (wave >> 1) + j), weight gradient
-// c block = wave over both n blocks of the stage; lane-level layouts as in the CI = 64 kernel.
-// z2 tile [64 px][128 c]: 256-B rows, chunk c of row r at c ^ ((r & 3) << 2) (a transposed read's
-// four rows land in four different 64-B bank quarters).
+// The layer-2 shape (CI = 128 -> CO = 512): 64-pixel tiles, 8 waves (2 per SIMD), the per-block
+// dW (512 x 128 fp32) spread over all 512 lanes (128 VGPRs each), and the transposed weight
+// (128 KiB) streamed per stage from L2 through its own 3-slot ring (two stages ahead) instead of
+// staying resident.  Waves: data gradient pb = wave & 1 (32-pixel block) x cb = wave >> 1
+// (32-channel block) -- ONE output channel per lane; weight gradient nb = wave & 1 (32-row n block
+// of the stage) x cw = wave >> 1 (32-column c block).  z2 tile [64 px][128 c]: 256-B rows, chunk c
+// of row r at c ^ ((r & 3) << 2) (a transposed read's four rows land in four 64-B bank quarters).
 template <int CI, int CO>
-__global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Conv11BwdArgs p) {
+__global__ __launch_bounds__(512, 1) void conv11_bwd_fused_w128_kernel(const Conv11BwdArgs p) {
   static_assert(CI == 128 && CO == 512, "the layer-2 conv3 shape (128 -> 512)");
   constexpr int TM = 64;                    // pixels per tile
   constexpr int NS = CO / kKS;              // 8 stages per tile
@@ -423,9 +422,9 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
   constexpr int ZSL = TM * CI * 2;          // 16 KiB: z2 tile [64 px][128 c]
   constexpr int NRG = 5, PDG = NRG - 1;     // g ring: stage q + 4 issued during stage q
   constexpr int NRW = 3, PDW = NRW - 1;     // W ring: stage q + 2 issued during stage q
-  // A2: per-wave a2 fragments of the tile ([4 waves][4 ks][64 lanes] x 16 B; written and read back
-  // by the same wave, in order: no barrier) -- in registers they pushed the kernel into spills
-  constexpr int GR = 0, WR = GR + NRG * GSL, ZR = WR + NRW * WSL, A2 = ZR + 2 * ZSL, PAR = A2 + 4 * 4096;
+  // A2: per-wave a2 fragments of the tile ([8 waves][4 ks][64 lanes] x 16 B), written and read
+  // back by the same wave in order (no barrier); in registers they pushed the kernel into spills
+  constexpr int GR = 0, WR = GR + NRG * GSL, ZR = WR + NRW * WSL, A2 = ZR + 2 * ZSL, PAR = A2 + 8 * 4096;
   constexpr int NPAR = 3 * CO + 4 * CI;
   constexpr int LDS_BYTES = PAR + NPAR * 4;
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -441,7 +440,7 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
   const int nq = my_tiles * NS;
   auto stage_m0 = [&](int q) { return q < nq ? (mg + (q / NS) * GM) * TM : p.M; };
 
-  for (int i = t; i < NPAR; i += 256) {
+  for (int i = t; i < NPAR; i += 512) {
     float v;
     if (i < 3 * CO) v = p.cbwd[i];
     else if (i < 3 * CO + 2 * CI) v = p.cf2[i - 3 * CO];
@@ -449,46 +448,39 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
     else v = p.invstd2[i - 3 * CO - 3 * CI];
     par[i] = v;
   }
-  // g stage [64][64] (8 pieces of 8 rows: 2 per wave); rows past M read the zero row
+  // g stage [64][64]: 8 pieces of 8 rows, one per wave; rows past M read the zero row
   auto issue_g = [&](int q, int sl) {
     const int m0 = stage_m0(q), col0 = (q % NS) * kKS;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = wave * 2 + i, r = 8 * k + (lane >> 3), m = m0 + r;
-      const uint16_t* src = m < p.M ? p.g + static_cast<int64_t>(m) * CO + col0 + ((lane & 7) ^ swf(r)) * 8 : kZeroRow;
-      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + GR + sl * GSL + k * 1024), 16, 0, 0);
-    }
+    const int r = 8 * wave + (lane >> 3), m = m0 + r;
+    const uint16_t* src = m < p.M ? p.g + static_cast<int64_t>(m) * CO + col0 + ((lane & 7) ^ swf(r)) * 8 : kZeroRow;
+    __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + GR + sl * GSL + wave * 1024), 16, 0, 0);
   };
-  // W3t slice of stage q (columns 64 (q % NS) ..): [128 c][64 n], 16 pieces, 4 per wave
+  // W3t slice of stage q (columns 64 (q % NS) ..): [128 c][64 n], 16 pieces, 2 per wave
   auto issue_w = [&](int q, int sl) {
     const int col0 = (q % NS) * kKS;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = wave * 4 + i, r = 8 * k + (lane >> 3);
+    for (int i = 0; i < 2; ++i) {
+      const int k = wave * 2 + i, r = 8 * k + (lane >> 3);
       __builtin_amdgcn_global_load_lds((gptr_t*)(p.wt + static_cast<int64_t>(r) * CO + col0 + ((lane & 7) ^ swf(r)) * 8),
                                        (lptr_t*)(lds + WR + sl * WSL + k * 1024), 16, 0, 0);
     }
   };
-  // z2 tile [64][128]: 16 pieces of 4 rows, 4 per wave
+  // z2 tile [64][128]: 16 pieces of 4 rows, 2 per wave
   auto issue_z2 = [&](int m0, int sl) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = wave * 4 + i, r = 4 * k + (lane >> 4), m = m0 + r;
+    for (int i = 0; i < 2; ++i) {
+      const int k = wave * 2 + i, r = 4 * k + (lane >> 4), m = m0 + r;
       const uint16_t* src =
           m < p.M ? p.z2 + static_cast<int64_t>(m) * CI + ((lane & 15) ^ ((r & 3) << 2)) * 8 : kZeroRow;
       __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + ZR + sl * ZSL + k * 1024), 16, 0, 0);
     }
   };
-  const int zr = t >> 3, zc = t & 7;  // z3: logical chunk zc of rows zr, zr + 32
-  u16x8 z3r[2][2];
-  auto load_z3 = [&](int q, u16x8 (&dst)[2]) {
-    const int m0 = stage_m0(q), col = (q % NS) * kKS + zc * 8;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + zr + 32 * i;
-      dst[i] = m < p.M ? *reinterpret_cast<const u16x8*>(p.z3 + static_cast<int64_t>(m) * CO + col)
-                       : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+  const int zr = t >> 3, zc = t & 7;  // z3: logical chunk zc of row zr (one chunk per thread)
+  u16x8 z3r[2];
+  auto load_z3 = [&](int q, u16x8& dst) {
+    const int m = stage_m0(q) + zr, col = (q % NS) * kKS + zc * 8;
+    dst = m < p.M ? *reinterpret_cast<const u16x8*>(p.z3 + static_cast<int64_t>(m) * CO + col)
+                  : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   };
   issue_z2(stage_m0(0), 0);
 #pragma unroll
@@ -500,53 +492,44 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
   wait_vm<0>();
   lds_bar();
 
-  const int pb = wave & 1, cbp = wave >> 1;  // data gradient: pixel block, channel-block pair
+  const int pb = wave & 1, cb = wave >> 1;  // data gradient block; weight gradient: nb = pb, cw = cb
   const int dpx = 32 * pb + fr, dsw = swf(dpx);
+  const int ec = 32 * cb + fr;              // this lane's output channel (data gradient) / dW column
   const int gi = lane >> 4, i16 = lane & 15;
   const int trow = 8 * (gi >> 1) + (i16 >> 2), tcol = 16 * (gi & 1) + 4 * (i16 & 3);
-  // dz3 stage tile, transposed read for the n block nb (A operand of the weight gradient)
-  auto trD = [&](int nb, int h) {
+  // dz3 stage tile, transposed read of the n block pb (A operand of the weight gradient)
+  auto trD = [&](int h) {
     const int r = trow + 4 * h;
-    return static_cast<uint32_t>(r * 128 + ((((32 * nb + tcol) >> 3) ^ swf(r)) << 4) + (tcol & 7) * 2);
+    return static_cast<uint32_t>(r * 128 + ((((32 * pb + tcol) >> 3) ^ swf(r)) << 4) + (tcol & 7) * 2);
   };
-  const uint32_t tD00 = trD(0, 0), tD01 = trD(0, 1), tD10 = trD(1, 0), tD11 = trD(1, 1);
-  // z2 tile, transposed read at column block cb, rows 16 s + trow (+ 4): 256-B rows
-  auto trZ = [&](int cb, int r) {
-    const int col = 32 * cb + tcol;
+  const uint32_t tD0 = trD(0), tD1 = trD(1);
+  // z2 tile, transposed read at column block cbk, row r (256-B rows)
+  auto trZ = [&](int cbk, int r) {
+    const int col = 32 * cbk + tcol;
     return static_cast<uint32_t>(r * 256 + (((col >> 3) ^ ((r & 3) << 2)) << 4) + (col & 7) * 2);
   };
-  const float asc = par[3 * CO + 32 * wave + fr], ash = par[3 * CO + CI + 32 * wave + fr];
-  float emc[2], esh[2], emu[2], eis[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int c = 32 * (2 * cbp + j) + fr;
-    emc[j] = par[3 * CO + c];
-    esh[j] = par[3 * CO + CI + c];
-    emu[j] = par[3 * CO + 2 * CI + c];
-    eis[j] = par[3 * CO + 3 * CI + c];
-  }
+  const float asc = par[3 * CO + ec], ash = par[3 * CO + CI + ec];
+  const float emc = asc, esh = ash, emu = par[3 * CO + 2 * CI + ec], eis = par[3 * CO + 3 * CI + ec];
+  const uint32_t wrow_off = static_cast<uint32_t>(ec * 128);  // W slice row of this lane's channel
+  const int wsw = swf(ec);
 
-  f32x16 acc_dg[2], accW[NS][2];
+  f32x16 acc_dg, accW[NS];
   auto zero16 = [](f32x16& a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) a[i] = 0.f;
   };
-  zero16(acc_dg[0]);
-  zero16(acc_dg[1]);
+  zero16(acc_dg);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    zero16(accW[s][0]);
-    zero16(accW[s][1]);
-  }
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  for (int s = 0; s < NS; ++s) zero16(accW[s]);
+  float s1 = 0.f, s2 = 0.f;
   const uint32_t a2s = L0 + A2 + wave * 4096 + lane * 16;
   auto make_a2 = [&](int ti) {
     const uint32_t zs = L0 + ZR + (ti & 1) * ZSL;
     s16x4 lo[4], hi[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      lo[ks] = ld_tr(zs + trZ(wave, 16 * ks + trow));
-      hi[ks] = ld_tr(zs + trZ(wave, 16 * ks + trow + 4));
+      lo[ks] = ld_tr(zs + trZ(cb, 16 * ks + trow));
+      hi[ks] = ld_tr(zs + trZ(cb, 16 * ks + trow + 4));
     }
     lgkm0();
 #pragma unroll
@@ -560,92 +543,84 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
       st_b128(a2s + ks * 1024, __builtin_bit_cast(bf16x8_t, __builtin_elementwise_max(__builtin_bit_cast(s16x8i, v), z)));
     }
   };
-  auto transform = [&](int sl, int s, int m0, const u16x8 (&z3v)[2]) {
+  auto transform = [&](int sl, int s, int m0, const u16x8& z8) {
     const uint32_t ds = L0 + GR + sl * GSL;
     const uint32_t pa = L0 + PAR + (s * kKS + zc * 8) * 4;
     const f32x4 ca0 = ld_f4(pa), ca1 = ld_f4(pa + 16);
     const f32x4 cb0 = ld_f4(pa + CO * 4), cb1 = ld_f4(pa + CO * 4 + 16);
     const f32x4 cc0 = ld_f4(pa + 2 * CO * 4), cc1 = ld_f4(pa + 2 * CO * 4 + 16);
-    bf16x8_t gv[2];
-    uint32_t ga[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = zr + 32 * i;
-      ga[i] = ds + r * 128 + ((zc ^ swf(r)) << 4);
-      gv[i] = ld_b128(ga[i]);
-    }
+    const uint32_t ga = ds + zr * 128 + ((zc ^ swf(zr)) << 4);
+    bf16x8_t gv = ld_b128(ga);
     lgkm0();
     f32x4 c0a = ca0, c0b = ca1, c1a = cb0, c1b = cb1, c2a = cc0, c2b = cc1;
     tie(c0a); tie(c0b); tie(c1a); tie(c1b); tie(c2a); tie(c2b);
+    tie(gv);
+    const u16x8 g8 = __builtin_bit_cast(u16x8, gv);
+    u16x8 d;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      tie(gv[i]);
-      const u16x8 g8 = __builtin_bit_cast(u16x8, gv[i]);
-      const u16x8 z8 = z3v[i];
-      u16x8 d;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = j < 4 ? c0a[j] : c0b[j - 4], b = j < 4 ? c1a[j] : c1b[j - 4], c = j < 4 ? c2a[j] : c2b[j - 4];
-        d[j] = f32_to_bf16(a * bf16_to_f32(g8[j]) + b * bf16_to_f32(z8[j]) + c);
-      }
-      if (m0 + zr + 32 * i >= p.M) d = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      st_b128(ga[i], __builtin_bit_cast(bf16x8_t, d));
+    for (int j = 0; j < 8; ++j) {
+      const float a = j < 4 ? c0a[j] : c0b[j - 4], b = j < 4 ? c1a[j] : c1b[j - 4], c = j < 4 ? c2a[j] : c2b[j - 4];
+      d[j] = f32_to_bf16(a * bf16_to_f32(g8[j]) + b * bf16_to_f32(z8[j]) + c);
     }
+    if (m0 + zr >= p.M) d = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    st_b128(ga, __builtin_bit_cast(bf16x8_t, d));
   };
-  auto compute = [&](int gsl, int wsl, f32x16 (&aw)[2]) {
+  auto compute = [&](int gsl, int wsl, f32x16& aw) {
     const uint32_t ds = L0 + GR + gsl * GSL, ws = L0 + WR + wsl * WSL;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8_t xa = ld_b128(ds + dpx * 128 + (((2 * ks + fh) ^ dsw) << 4));
-      bf16x8_t wb[2];
+    for (int h = 0; h < 2; ++h) {  // two k-steps at a time (register budget)
+      bf16x8_t xa[2], wb[2], af[2];
+      s16x4 dl[2], dh[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = 32 * (2 * cbp + j) + fr;
-        wb[j] = ld_b128(ws + c * 128 + (((2 * ks + fh) ^ swf(c)) << 4));
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int ks = 2 * h + k2;
+        af[k2] = ld_b128(a2s + ks * 1024);
+        xa[k2] = ld_b128(ds + dpx * 128 + (((2 * ks + fh) ^ dsw) << 4));
+        wb[k2] = ld_b128(ws + wrow_off + (((2 * ks + fh) ^ wsw) << 4));
+        dl[k2] = ld_tr(ds + ks * 2048 + tD0);
+        dh[k2] = ld_tr(ds + ks * 2048 + tD1);
       }
-      const s16x4 d0l = ld_tr(ds + ks * 2048 + tD00), d0h = ld_tr(ds + ks * 2048 + tD01);
-      const s16x4 d1l = ld_tr(ds + ks * 2048 + tD10), d1h = ld_tr(ds + ks * 2048 + tD11);
-      const bf16x8_t af0 = ld_b128(a2s + ks * 1024);
       lgkm0();
-      bf16x8_t af = af0;
-      tie(af);
-      bf16x8_t x = xa, w0 = wb[0], w1 = wb[1];
-      s16x4 e0l = d0l, e0h = d0h, e1l = d1l, e1h = d1h;
-      tie(x); tie(w0); tie(w1); tie(e0l); tie(e0h); tie(e1l); tie(e1h);
-      acc_dg[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w0, acc_dg[0], 0, 0, 0);
-      acc_dg[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w1, acc_dg[1], 0, 0, 0);
-      aw[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(e0l, e0h), af, aw[0], 0, 0, 0);
-      aw[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(e1l, e1h), af, aw[1], 0, 0, 0);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        tie(xa[k2]);
+        tie(wb[k2]);
+        tie(af[k2]);
+        tie(dl[k2]);
+        tie(dh[k2]);
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+        acc_dg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[k2], wb[k2], acc_dg, 0, 0, 0);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+        aw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(dl[k2], dh[k2]), af[k2], aw, 0, 0, 0);
     }
   };
   auto epilogue = [&](int ti) {
     const int m0 = (mg + ti * GM) * TM;
     const uint32_t zs = L0 + ZR + (ti & 1) * ZSL;
+    s16x4 zv[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      s16x4 zv[4];
+    for (int q4 = 0; q4 < 4; ++q4) zv[q4] = ld_tr(zs + trZ(cb, 32 * pb + 8 * q4 + 4 * (gi >> 1) + (i16 >> 2)));
+    lgkm0();
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) zv[q4] = ld_tr(zs + trZ(2 * cbp + j, 32 * pb + 8 * q4 + 4 * (gi >> 1) + (i16 >> 2)));
-      lgkm0();
-      const int c = 32 * (2 * cbp + j) + fr;
+    for (int q4 = 0; q4 < 4; ++q4) {
+      tie(zv[q4]);
+      const u16x4 z4 = __builtin_bit_cast(u16x4, zv[q4]);
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        tie(zv[q4]);
-        const u16x4 z4 = __builtin_bit_cast(u16x4, zv[q4]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint16_t val = f32_to_bf16(acc_dg[j][4 * q4 + e]);
-          const float z = bf16_to_f32(z4[e]);
-          const bool on = z * emc[j] + esh[j] > 0.f;
-          const float gv = on ? bf16_to_f32(val) : 0.f;
-          s1[j] += gv;
-          s2[j] += gv * ((z - emu[j]) * eis[j]);
-          const int m = m0 + 32 * pb + 8 * q4 + 4 * fh + e;
-          if (m < p.M) p.gy[static_cast<int64_t>(m) * CI + c] = on ? val : static_cast<uint16_t>(0);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t val = f32_to_bf16(acc_dg[4 * q4 + e]);
+        const float z = bf16_to_f32(z4[e]);
+        const bool on = z * emc + esh > 0.f;
+        const float gv = on ? bf16_to_f32(val) : 0.f;
+        s1 += gv;
+        s2 += gv * ((z - emu) * eis);
+        const int m = m0 + 32 * pb + 8 * q4 + 4 * fh + e;
+        if (m < p.M) p.gy[static_cast<int64_t>(m) * CI + ec] = on ? val : static_cast<uint16_t>(0);
       }
-      zero16(acc_dg[j]);
     }
+    zero16(acc_dg);
   };
 
   int slg = 0, slw = 0, q = 0;
@@ -653,8 +628,8 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
     const int m0 = (mg + ti * GM) * TM;
 #pragma unroll
     for (int s = 0; s < NS; ++s, ++q) {
-      // the stage counter through an opaque copy: the per-stage DMA / load addresses are computed
-      // here instead of being hoisted for all 8 unrolled stages (that had pinned ~150 VGPRs)
+      // the stage counter through an opaque copy: per-stage DMA / load addresses are computed here
+      // instead of being hoisted for all 8 unrolled stages
       int qo = q;
       asm volatile("" : "+s"(qo));
       if (s == 0) make_a2(ti);
@@ -666,11 +641,10 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
       if (s == 0) issue_z2(ti + 1 < my_tiles ? m0 + GM * TM : p.M, (ti + 1) & 1);
       compute(slg, slw, accW[s]);
       if (s == NS - 1) epilogue(ti);
-      // W(q + 1) (issued during stage q - 1) and G(q + 1) (stage q - 3) landed: younger than W(q + 1)
-      // are at least this stage's G + W DMAs (6) and the z2 tile when it was issued in stage q - 1
-      // or q (4); at a tile's last stage the next tile's z2 (stage 0) is older than 6 ops
-      if (s <= 1) wait_vm<10>();
-      else wait_vm<6>();
+      // W(q + 1) (issued in stage q - 1) and G(q + 1) (stage q - 3) landed: younger than W(q + 1)
+      // are at least this stage's G + W DMAs (3) and the z2 tile if issued in stage q - 1 or q (2)
+      if (s <= 1) wait_vm<5>();
+      else wait_vm<3>();
       lds_bar();
       slg = slg == NRG - 1 ? 0 : slg + 1;
       slw = slw == NRW - 1 ? 0 : slw + 1;
@@ -679,37 +653,29 @@ __global__ __launch_bounds__(256, 1) void conv11_bwd_fused_w128_kernel(const Con
   wait_vm<0>();
   lds_bar();
 
-  // bn2 partial sums: lanes l / l + 32, then the two pixel-block waves of each channel-block pair
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    s1[j] += __shfl_xor(s1[j], 32, 64);
-    s2[j] += __shfl_xor(s2[j], 32, 64);
-  }
+  // bn2 partial sums: lanes l / l + 32 (pixel halves), then the two pixel-block waves of a channel
+  // block in fixed order
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
   float* red = reinterpret_cast<float*>(lds);  // [2][2 pb][CI]
   if (fh == 0) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = 32 * (2 * cbp + j) + fr;
-      red[pb * CI + c] = s1[j];
-      red[(2 + pb) * CI + c] = s2[j];
-    }
+    red[pb * CI + ec] = s1;
+    red[(2 + pb) * CI + ec] = s2;
   }
   __syncthreads();
   if (t < CI) {
     p.part[static_cast<int64_t>(mg) * CI + t] = red[t] + red[CI + t];
     p.part[static_cast<int64_t>(GM + mg) * CI + t] = red[2 * CI + t] + red[3 * CI + t];
   }
-  // dW slab: wave owns column block c = 32 wave + fr of every row n
+  // dW slab: rows n of every stage's n block pb, column ec
   float* slab = p.ws + static_cast<int64_t>(mg) * CO * CI;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int n = s * kKS + 32 * nb + 8 * (i >> 2) + 4 * fh + (i & 3);
-        slab[n * CI + 32 * wave + fr] = accW[s][nb][i];
-      }
+    for (int i = 0; i < 16; ++i) {
+      const int n = s * kKS + 32 * pb + 8 * (i >> 2) + 4 * fh + (i & 3);
+      slab[n * CI + ec] = accW[s][i];
+    }
 }
 
 // out[y][e] = sum_{b in [y*per, y*per + per)} in[b][e], fixed order (bf16 or fp32 out)
@@ -756,7 +722,7 @@ void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t
   const int gm = conv11_bwd_blocks(a.M, CI, CO);
   if (CI == 64 && CO == 256) hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256>), dim3(gm), dim3(512), 0, s, a);
   else if (CI == 128 && CO == 512)
-    hipLaunchKernelGGL((conv11_bwd_fused_w128_kernel<128, 512>), dim3(gm), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv11_bwd_fused_w128_kernel<128, 512>), dim3(gm), dim3(512), 0, s, a);
   else return;
   const int64_t E = static_cast<int64_t>(CI) * CO;
   const unsigned eb = static_cast<unsigned>((E + 255) / 256);
