@@ -28,6 +28,7 @@
 // (ds_read_b64_tr_b16: 4 rows x 4 chunks per half-wave) are both conflict-free.  The resident
 // transposed weight [CI][CO] keeps 2*CO-byte rows with chunk c at c ^ (row & 15).
 #include <algorithm>
+#include <cstdlib>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -703,7 +704,16 @@ int slab_levels(int nslab) { return nslab > 16 ? (nslab + 15) / 16 : 0; }
 
 }  // namespace
 
-bool conv11_bwd_fused_ok(int CI, int CO) { return (CI == 64 && CO == 256) || (CI == 128 && CO == 512); }
+// The layer-2 variant (CI = 128) is built but opt-in (PS_AMD_CONV3_FUSED_W128=1): with the weight
+// streamed per stage it ran 0.78 ms (4 waves) / 0.96 ms (8 waves) against the two-kernel chain's
+// 0.76 ms at batch 1024 (profiles/r5_conv3_bwd_fused_probe_w128.jsonl)
+bool conv11_bwd_fused_ok(int CI, int CO) {
+  static const bool w128 = [] {
+    const char* e = std::getenv("PS_AMD_CONV3_FUSED_W128");
+    return e != nullptr && e[0] == '1';
+  }();
+  return (CI == 64 && CO == 256) || (w128 && CI == 128 && CO == 512);
+}
 
 int conv11_bwd_blocks(int M, int CI, int CO) {
   (void)CO;

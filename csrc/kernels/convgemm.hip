@@ -1275,15 +1275,18 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs 
   }
 }
 
-bool c64_enabled() {
-  static const bool on = [] {
+// PS_AMD_CONV_C64: "1" the round-4 resident-weight kernel above (0.476 / 0.507 ms vs the tall
+// im2col tile's 0.451 / 0.456, profiles/r4_conv3x3_c64_probe.txt), "2" the planar-LDS kernel of
+// conv3x3_c64.hip (asm fragment reads, no compiler vmcnt at the loop edge), "0" / unset the tall
+// im2col tile
+int c64_mode() {
+  static const int m = [] {
     const char* e = std::getenv("PS_AMD_CONV_C64");
-    // opt-in: 0.476 / 0.507 ms vs the tall im2col tile's 0.451 / 0.456 (fwd / data grad at bs1024,
-    // profiles/r4_conv3x3_c64_probe.txt)
-    return e != nullptr && e[0] == '1';
+    return e == nullptr ? 0 : std::atoi(e);
   }();
-  return on;
+  return m;
 }
+bool c64_enabled() { return c64_mode() != 0; }
 
 // the layers conv3x3_c64_kernel takes: 3x3 / stride 1 / pad 1, 64 -> 64 channels, 56-wide maps
 // with an even row count, no prologue
@@ -2163,6 +2166,10 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
   if (src2 == 0 && c64_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
+    if (c64_mode() == 2 && (a.epi == 1 || a.epi == 3)) {
+      launch_conv3x3_c64s(a, GM, s);
+      return;
+    }
     if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 1>), dim3(GM), dim3(256), 0, s, a);
     else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 3>), dim3(GM), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv3x3_c64_kernel<56, 0>), dim3(GM), dim3(256), 0, s, a);
