@@ -1508,8 +1508,8 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
 // conv3's backward in one pass (csrc/kernels/conv_bwd_fused.hip): bn3's backward prologue
 // dz3 = bf16(ca g + cb z3 + cc) never leaves LDS; -> [gy [M, CI] (masked by bn2's ReLU), part
 // [2, G, CI] (bn2 backward sums, the conv_gemm epi-3 layout), dW3 [CO, CI] bf16]
-std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt, Tensor z2, Tensor cf2, Tensor mean2,
-                                     Tensor invstd2) {
+std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt, Tensor z2, c10::optional<Tensor> cf2,
+                                     c10::optional<Tensor> mean2, c10::optional<Tensor> invstd2) {
   check_rows(g, "g");
   check_rows(z3, "z3");
   check_rows(z2, "z2");
@@ -1517,21 +1517,29 @@ std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt
   TORCH_CHECK(g.dim() == 2 && z3.sizes() == g.sizes() && z2.dim() == 2 && z2.size(0) == g.size(0),
               "g, z3 [M, CO]; z2 [M, CI]");
   const int64_t M = g.size(0), CO = g.size(1), CI = z2.size(1);
-  TORCH_CHECK(psamd::conv11_bwd_fused_ok(static_cast<int>(CI), static_cast<int>(CO)),
-              "conv11_bwd_fused: unsupported channels CI=", CI, " CO=", CO);
+  // no bn2 parameters: the PLAIN (downsample) pass -- z2 is the weight gradient's operand as is and
+  // the data gradient leaves unmasked, with no partial sums
+  const bool plain = !cf2.has_value();
+  TORCH_CHECK(plain == !mean2.has_value() && plain == !invstd2.has_value(), "cf2, mean2, invstd2: all or none");
+  TORCH_CHECK(plain ? psamd::conv11_bwd_plain_ok(static_cast<int>(CI), static_cast<int>(CO))
+                    : psamd::conv11_bwd_built(static_cast<int>(CI), static_cast<int>(CO)),
+              "conv11_bwd_fused: unsupported channels CI=", CI, " CO=", CO, plain ? " (plain)" : "");
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) / CO, "pixel count");
   TORCH_CHECK(wt.dim() == 2 && wt.size(0) == CI && wt.size(1) == CO, "wt must be [CI, CO]");
   check_f32(cbwd, "cbwd");
-  check_f32(cf2, "cf2");
-  check_f32(mean2, "mean2");
-  check_f32(invstd2, "invstd2");
-  TORCH_CHECK(cbwd.numel() == 3 * CO && cf2.numel() == 2 * CI && mean2.numel() == CI && invstd2.numel() == CI,
-              "cbwd [3 CO], cf2 [2 CI], mean2 / invstd2 [CI]");
+  TORCH_CHECK(cbwd.numel() == 3 * CO, "cbwd [3 CO]");
+  if (!plain) {
+    check_f32(*cf2, "cf2");
+    check_f32(*mean2, "mean2");
+    check_f32(*invstd2, "invstd2");
+    TORCH_CHECK(cf2->numel() == 2 * CI && mean2->numel() == CI && invstd2->numel() == CI,
+                "cf2 [2 CI], mean2 / invstd2 [CI]");
+  }
   const c10::DeviceGuard guard(g.device());
   const int m = static_cast<int>(M), ci = static_cast<int>(CI), co = static_cast<int>(CO);
   const int G = psamd::conv11_bwd_blocks(m, ci, co);
   auto gy = torch::empty({M, CI}, g.options());
-  auto part = torch::empty({2, G, CI}, g.options().dtype(torch::kFloat32));
+  auto part = torch::empty({plain ? 0 : 2, G, CI}, g.options().dtype(torch::kFloat32));
   auto ws = torch::empty({psamd::conv11_bwd_ws(m, ci, co)}, g.options().dtype(torch::kFloat32));
   auto dw = torch::empty({CO, CI}, g.options());
   psamd::Conv11BwdArgs a{};
@@ -1540,11 +1548,11 @@ std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt
   a.cbwd = cbwd.data_ptr<float>();
   a.wt = u16(wt);
   a.z2 = u16(z2);
-  a.cf2 = cf2.data_ptr<float>();
-  a.mean2 = mean2.data_ptr<float>();
-  a.invstd2 = invstd2.data_ptr<float>();
+  a.cf2 = plain ? nullptr : cf2->data_ptr<float>();
+  a.mean2 = plain ? nullptr : mean2->data_ptr<float>();
+  a.invstd2 = plain ? nullptr : invstd2->data_ptr<float>();
   a.gy = u16m(gy);
-  a.part = part.data_ptr<float>();
+  a.part = plain ? nullptr : part.data_ptr<float>();
   a.ws = ws.data_ptr<float>();
   a.dw = u16m(dw);
   a.M = m;
@@ -1574,8 +1582,9 @@ int64_t cu_mask_stream(int64_t device, int64_t n_cus, bool spread) {
   return reinterpret_cast<int64_t>(st);
 }
 
-bool conv11_bwd_fused_supported(int64_t ci, int64_t co) {
-  return psamd::conv11_bwd_fused_ok(static_cast<int>(ci), static_cast<int>(co));
+bool conv11_bwd_fused_supported(int64_t ci, int64_t co, bool plain) {
+  return plain ? psamd::conv11_bwd_plain_ok(static_cast<int>(ci), static_cast<int>(co))
+               : psamd::conv11_bwd_fused_ok(static_cast<int>(ci), static_cast<int>(co));
 }
 
 // Linear weight + bias gradient in one pass over dz: [dW [N, K] bf16, db [N] fp32] with
@@ -1715,8 +1724,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
-  m.def("conv11_bwd_fused", &conv11_bwd_fused);
-  m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported);
+  m.def("conv11_bwd_fused", &conv11_bwd_fused, py::arg("g"), py::arg("z3"), py::arg("cbwd"), py::arg("wt"), py::arg("z2"),
+        py::arg("cf2") = py::none(), py::arg("mean2") = py::none(), py::arg("invstd2") = py::none());
+  m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported, py::arg("ci"), py::arg("co"),
+        py::arg("plain") = false);
   m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("n_cus"), py::arg("spread") = true);
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);

@@ -382,7 +382,8 @@ struct Conv11BwdArgs {
   const float* cbwd;      // [3 CO] ca | cb | cc (bn3 backward coefficients)
   const uint16_t* wt;     // [CI, CO] conv3 weight transposed
   const uint16_t* z2;     // [M, CI] bn2 input (conv3's input before bn2 + ReLU)
-  const float* cf2;       // [2 CI] bn2 scale | shift
+  const float* cf2;       // [2 CI] bn2 scale | shift; nullptr: PLAIN (downsample: z2 used as is,
+                          // gy unmasked, no part) -- the 64 -> 256 kernel only
   const float* mean2;     // [CI]
   const float* invstd2;   // [CI]
   uint16_t* gy;           // [M, CI] masked data gradient (bn2's output gradient)
@@ -392,6 +393,8 @@ struct Conv11BwdArgs {
   int M;
 };
 bool conv11_bwd_fused_ok(int CI, int CO);
+bool conv11_bwd_plain_ok(int CI, int CO);
+bool conv11_bwd_built(int CI, int CO);  // launchable (conv11_bwd_fused_ok: also chosen by default)
 int conv11_bwd_blocks(int M, int CI, int CO);
 int64_t conv11_bwd_ws(int M, int CI, int CO);
 void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t s);

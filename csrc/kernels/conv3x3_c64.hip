@@ -20,6 +20,7 @@
 // reads per MFMA).  The epilogue leaves straight from the accumulators (4 channels = 8 B per
 // store); its statistics accumulate per lane over the block's tiles and fold once at the end.
 #include <algorithm>
+#include <cstdlib>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -66,7 +67,7 @@ __device__ __forceinline__ void lds_bar() {
   asm volatile("" ::: "memory");
 }
 
-template <int W, int EPI>
+template <int W, int EPI, int LA>
 __global__ __launch_bounds__(256, 1) void conv3x3_c64s_kernel(const ConvGemmArgs p) {
   static_assert(EPI == 1 || EPI == 3, "forward statistics or data-gradient mask + sums");
   constexpr int C = 64, N = 64, RT = 2, TP = RT * W;       // rows / pixels per tile
@@ -177,7 +178,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64s_kernel(const ConvGemmArgs
       for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
     // ---- 36 k-steps (9 taps x 4 of 16 channels): the reads of step i + 1 before the MFMAs of i
     const uint32_t pb0 = L0 + static_cast<uint32_t>(sl * SLOT) + bbase[0], pb1 = L0 + static_cast<uint32_t>(sl * SLOT) + bbase[1];
-    bf16x8_t wa[2], xa[2][2];
+    // LA + 1 register sets: the reads of step st + LA are in flight while step st's MFMAs issue
+    // (LDS latency exceeds the 64 cycles of one step's two MFMAs at one wave per SIMD)
+    constexpr int NB = LA + 1;
+    bf16x8_t wa[NB], xa[NB][2];
     auto fetch = [&](int st, int buf) {
       const int tap = st >> 2, ks = st & 3, kh = tap / 3, kw = tap - kh * 3;
       const uint32_t ao = static_cast<uint32_t>(2 * ks * WPL + tap * 1024);
@@ -186,13 +190,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64s_kernel(const ConvGemmArgs
       xa[buf][0] = ld_b128(pb0 + bo);
       xa[buf][1] = ld_b128(pb1 + bo);
     };
-    fetch(0, 0);
+#pragma unroll
+    for (int st = 0; st < LA; ++st) fetch(st, st);
 #pragma unroll
     for (int st = 0; st < 36; ++st) {
-      const int cur = st & 1;
-      if (st + 1 < 36) {
-        fetch(st + 1, cur ^ 1);
-        wait_lgkm<3>();  // step st's three reads landed; step st + 1's stay in flight
+      const int cur = st % NB;
+      if (st + LA < 36) {
+        fetch(st + LA, (st + LA) % NB);
+        wait_lgkm<3 * LA>();  // step st's three reads landed; the next LA steps' stay in flight
+      } else if (st + 2 == 36 && LA >= 2) {
+        wait_lgkm<3>();
       } else {
         wait_lgkm<0>();
       }
@@ -274,8 +281,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64s_kernel(const ConvGemmArgs
 }  // namespace
 
 void launch_conv3x3_c64s(const ConvGemmArgs& a, int gm, hipStream_t s) {
-  if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 1>), dim3(gm), dim3(256), 0, s, a);
-  else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 3>), dim3(gm), dim3(256), 0, s, a);
+  static const int la = [] {
+    const char* e = std::getenv("PS_AMD_C64_LOOKAHEAD");
+    return e != nullptr && e[0] == '1' ? 1 : 2;
+  }();
+  if (la == 1) {
+    if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 1, 1>), dim3(gm), dim3(256), 0, s, a);
+    else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 3, 1>), dim3(gm), dim3(256), 0, s, a);
+  } else {
+    if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 1, 2>), dim3(gm), dim3(256), 0, s, a);
+    else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64s_kernel<56, 3, 2>), dim3(gm), dim3(256), 0, s, a);
+  }
 }
 
 }  // namespace psamd

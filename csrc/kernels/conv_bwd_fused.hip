@@ -106,11 +106,16 @@ __device__ __forceinline__ bf16x8_t cat8(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8_t, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
 }
 
+// PLAIN: the same pass for the block's DOWNSAMPLE branch (1x1, stride 1, CI -> CO): g / z3 are the
+// block-output gradient and the downsample BN's input, z2 is the block input itself (the weight
+// gradient's operand as is: no BN / ReLU), and the data gradient leaves unmasked with no sums --
+// it is the residual-branch term the consumer's conv1 data-gradient epilogue adds.
+//
 // Persistent grid of one 8-wave block per CU (LDS: resident weight + 3 stage slots + 2 z2 slots).
 // Waves: data gradient 4 pixel blocks x 2 channel blocks of 32 x 32 (pb = wave & 3, cb = wave >> 2);
 // weight gradient 2 n blocks x 2 c blocks x 2 pixel halves (nb = wave & 1, cw = (wave >> 1) & 1,
 // kh = wave >> 2) -- the two halves of a dW block are summed in fixed order at the end.
-template <int CI, int CO>
+template <int CI, int CO, bool PLAIN>
 __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11BwdArgs p) {
   static_assert(CI == 64 && CO == 256, "the layer-1 conv3 shape (64 -> 256): 4 stages per tile");
   constexpr int NS = CO / kKS;        // stages per tile
@@ -140,6 +145,7 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   for (int i = t; i < NPAR; i += kNW * 64) {
     float v;
     if (i < 3 * CO) v = p.cbwd[i];
+    else if (PLAIN) v = 0.f;
     else if (i < 3 * CO + 2 * CI) v = p.cf2[i - 3 * CO];
     else if (i < 3 * CO + 3 * CI) v = p.mean2[i - 3 * CO - 2 * CI];
     else v = p.invstd2[i - 3 * CO - 3 * CI];
@@ -235,6 +241,10 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
     for (int ks = 0; ks < 4; ++ks) {
       tie(lo[ks]);
       tie(hi[ks]);
+      if constexpr (PLAIN) {
+        a2f[ks] = cat8(lo[ks], hi[ks]);
+        continue;
+      }
       u16x8 v = __builtin_bit_cast(u16x8, cat8(lo[ks], hi[ks]));
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) * asc + ash);
@@ -312,6 +322,15 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   // ONE transposed read (each 16-lane group reads the 4 x 16 block of its rows / channels)
   auto epilogue = [&](int ti) {
     const int m0 = (mg + ti * GM) * kTM;
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 32 * pb + 8 * (q >> 2) + 4 * fh + (q & 3);
+        if (m < p.M) p.gy[static_cast<int64_t>(m) * CI + ec] = f32_to_bf16(acc_dg[q]);
+      }
+      zero16(acc_dg);
+      return;
+    }
     const uint32_t zs = L0 + Z2 + (ti & 1) * kSlot;
     s16x4 zv[4];
 #pragma unroll
@@ -374,12 +393,12 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   s1 += __shfl_xor(s1, 32, 64);
   s2 += __shfl_xor(s2, 32, 64);
   float* red = reinterpret_cast<float*>(lds + RING);  // [2][4 pb][CI]
-  if (fh == 0) {
+  if (!PLAIN && fh == 0) {
     red[pb * CI + ec] = s1;
     red[(4 + pb) * CI + ec] = s2;
   }
   __syncthreads();
-  if (t < CI) {
+  if (!PLAIN && t < CI) {
     p.part[static_cast<int64_t>(mg) * CI + t] = (red[t] + red[CI + t]) + (red[2 * CI + t] + red[3 * CI + t]);
     p.part[static_cast<int64_t>(GM + mg) * CI + t] =
         (red[4 * CI + t] + red[5 * CI + t]) + (red[6 * CI + t] + red[7 * CI + t]);
@@ -715,6 +734,10 @@ bool conv11_bwd_fused_ok(int CI, int CO) {
   return (CI == 64 && CO == 256) || (w128 && CI == 128 && CO == 512);
 }
 
+bool conv11_bwd_plain_ok(int CI, int CO) { return CI == 64 && CO == 256; }
+
+bool conv11_bwd_built(int CI, int CO) { return (CI == 64 && CO == 256) || (CI == 128 && CO == 512); }
+
 int conv11_bwd_blocks(int M, int CI, int CO) {
   (void)CO;
   const int tm = CI == 128 ? 64 : kTM;
@@ -730,7 +753,10 @@ int64_t conv11_bwd_ws(int M, int CI, int CO) {
 void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t s) {
   if (a.M <= 0) return;
   const int gm = conv11_bwd_blocks(a.M, CI, CO);
-  if (CI == 64 && CO == 256) hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256>), dim3(gm), dim3(512), 0, s, a);
+  if (CI == 64 && CO == 256 && a.cf2 == nullptr)
+    hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256, true>), dim3(gm), dim3(512), 0, s, a);
+  else if (CI == 64 && CO == 256) hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256, false>), dim3(gm), dim3(512), 0, s, a);
+  else if (a.cf2 == nullptr) return;  // PLAIN: the 64 -> 256 kernel only
   else if (CI == 128 && CO == 512)
     hipLaunchKernelGGL((conv11_bwd_fused_w128_kernel<128, 512>), dim3(gm), dim3(512), 0, s, a);
   else return;

@@ -274,6 +274,15 @@ def _conv3_bwd_fused(ci: int, co: int) -> bool:
     return os.environ.get("PS_AMD_CONV3_BWD_FUSED", "1") != "0" and bool(native().conv11_bwd_fused_supported(ci, co))
 
 
+def _ds_bwd_fused(ci: int, co: int, s: int) -> bool:
+    """The downsample branch's data AND weight gradient in one pass with its BN backward in the
+    prologue (the PLAIN mode of conv_bwd_fused.hip; stride 1, layer 1's 64 -> 256): dzd never
+    reaches HBM and the block input is read once.  PS_AMD_DS_BWD_FUSED=0 keeps the apply pass +
+    weight-gradient GEMM + data-gradient GEMM."""
+    return (s == 1 and os.environ.get("PS_AMD_DS_BWD_FUSED", "1") != "0"
+            and bool(native().conv11_bwd_fused_supported(ci, co, True)))
+
+
 def _fold_enabled() -> bool:
     return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
 
@@ -439,13 +448,22 @@ class _BottleneckFn(torch.autograd.Function):
         fold = li is not None and _fold_enabled()
         fkw = dict(mean=li.mean, invstd=li.invstd, aux2=li.z3, bits2=li.bits) if fold else {}
         if wd is not None:
-            if ds_part is not None:  # d2 is masked already; sum(g), sum(g * xhat_d) came with it
-                dzd, dgd, dbd = nat.bn_bwd_partials(d2, zd, ds_part, gd, md, idd)
+            wdt = pw[3] if pw else _mat(wd).t()
+            if ds_part is not None and _ds_bwd_fused(wd.shape[1], wd.shape[0], s):
+                # d2 is masked already and the downsample BN's sums came with it: its backward
+                # coefficients, then ONE pass = data gradient t + weight gradient (dzd stays in LDS)
+                dgd, dbd, cbd = nat.bn_bwd_coef(ds_part, gd, md, idd, d2.shape[0])
+                t, _, dwdf = nat.conv11_bwd_fused(d2, zd, cbd, wdt.contiguous(), x2)
+                dwd = _side._match_layout(dwdf, wd)
+                FOLD_STATS["ds_fused"] = FOLD_STATS.get("ds_fused", 0) + 1
             else:
-                dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
-            sd.fork()
-            dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
-            t = nat.conv_gemm(dzd, pw[3] if pw else _mat(wd).t(), go)[0]
+                if ds_part is not None:  # d2 is masked already; sum(g), sum(g * xhat_d) came with it
+                    dzd, dgd, dbd = nat.bn_bwd_partials(d2, zd, ds_part, gd, md, idd)
+                else:
+                    dzd, _, dgd, dbd = nat.bn_act_bwd(d2, None, zd, gd, md, idd, 3, False, True, None, obits)
+                sd.fork()
+                dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
+                t = nat.conv_gemm(dzd, wdt, go)[0]
             epi = 4 if s == 2 else 2
             dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
         elif fold and li.zd is not None:  # the producer has a downsample BN: its sum rides along

@@ -41,7 +41,7 @@ def main():
         tf = timeit(lambda: native().conv_gemm(x, w, gg, None, 1, None, ks))
         td = timeit(lambda: native().conv_gemm(x, w, gg, None, 3, z1, None, coef, mean, inv))
         fl = 2 * n * 56 * 56 * 64 * 576 / 1e9
-        print(json.dumps({"mode": os.environ.get("PS_AMD_CONV_C64", "0"), "batch": n, "fwd_ms": round(tf, 4),
+        print(json.dumps({"mode": os.environ.get("PS_AMD_CONV_C64", "0"), "lookahead": os.environ.get("PS_AMD_C64_LOOKAHEAD", "2"), "batch": n, "fwd_ms": round(tf, 4),
                           "dgrad_ms": round(td, 4), "fwd_TFs": round(fl / tf, 1), "dgrad_TFs": round(fl / td, 1)}),
               flush=True)
 

@@ -38,3 +38,37 @@ with open(sys.argv[1] + ".timeline.txt", "w") as f:
         st = (int(r["Start_Timestamp"]) - t0) / 1e3
         grid = r.get("Grid_Size_X", r.get("Grid_Size", ""))
         f.write(f"{st:10.1f} {d:9.1f}us grid={grid:>8s} {r['Kernel_Name'][:110]}\n")
+
+# per-queue occupancy of the same step: busy = union of that queue's kernel intervals; overlap =
+# time with kernels of two or more queues in flight (the side-stream weight gradients hiding
+# under the data-gradient chain)
+ev = []
+byq = collections.defaultdict(list)
+for r in seg:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    byq[r.get("Queue_Id", "0")].append((s, e, r["Kernel_Name"]))
+    ev += [(s, 1), (e, -1)]
+print("queue occupancy:")
+for q, ks in sorted(byq.items(), key=lambda x: -len(x[1])):
+    ks.sort()
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in ks:
+        if cur_e is None or s > cur_e:
+            busy += (cur_e - cur_s) if cur_e is not None else 0
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    ksum = sum(e - s for s, e, _ in ks)
+    print(f"  queue {q}: {len(ks)} kernels, busy {busy / 1e6:.3f} ms, kernel sum {ksum / 1e6:.3f} ms")
+ev.sort()
+depth, last, multi, any_ = 0, None, 0, 0
+for t_, d in ev:
+    if last is not None:
+        if depth >= 1:
+            any_ += t_ - last
+        if depth >= 2:
+            multi += t_ - last
+    depth += d
+    last = t_
+print(f"  GPU busy (any queue) {any_ / 1e6:.3f} ms, 2+ kernels in flight {multi / 1e6:.3f} ms, idle {wall - any_ / 1e6:.3f} ms")

@@ -692,3 +692,46 @@ def test_block_output_prologue_matches_apply_then_gemm(M, C, N, dual):
     _close(c, c_ref, tol=1e-2, amax=0.05)
     assert p.shape[0] == 2 and p.shape[2] == N
     torch.testing.assert_close(p.sum(1), p_ref.sum(1), rtol=2e-3, atol=2e-2)
+
+
+def test_layer1_chain_single_pass_backwards_match_unfused(monkeypatch):
+    """Layer-1 shapes (64 -> 256, stride 1): conv3's backward and the downsample branch's backward
+    each run as ONE pass with the BN backward in the prologue (conv_bwd_fused.hip, normal and PLAIN
+    modes).  Against the same chain with both passes split back into apply + two GEMMs."""
+    import torch.nn as nn
+
+    from ps_amd.models.resnet import Bottleneck, prepare_for_mi355x
+    from ps_amd.ops import convgemm as cg
+    from ps_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(2)
+    ds = nn.Sequential(nn.Conv2d(64, 256, 1, bias=False), BatchNormAct2d(256, act="none"))
+    a = nn.Sequential(Bottleneck(64, 64, 1, ds), Bottleneck(256, 64), Bottleneck(256, 64))
+    for m in a.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    a = prepare_for_mi355x(a.cuda())
+    x = torch.randn(4, 64, 19, 19, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gw = torch.randn(4, 256, 19, 19, device=DEV)
+    state = copy.deepcopy(a.state_dict())
+
+    def run():
+        a.load_state_dict(state)
+        a.zero_grad()
+        xi = x.clone().requires_grad_()
+        with cg.deferred_bn_counters():
+            y = a(xi)
+        (y.float() * gw).sum().backward()
+        return xi.grad.clone(), {n: p.grad.clone() for n, p in a.named_parameters()}
+
+    c3, dsf = cg.FOLD_STATS.get("conv3_fused", 0), cg.FOLD_STATS.get("ds_fused", 0)
+    ga, pa = run()
+    assert cg.FOLD_STATS.get("conv3_fused", 0) - c3 == 2  # blocks 0 and 1 (block 2 has no consumer)
+    assert cg.FOLD_STATS.get("ds_fused", 0) - dsf == 1
+    monkeypatch.setenv("PS_AMD_DS_BWD_FUSED", "0")
+    monkeypatch.setenv("PS_AMD_CONV3_BWD_FUSED", "0")
+    gb, pb = run()
+    _close(ga, gb, tol=1e-2, amax=0.05)
+    for n in pb:
+        _close(pa[n], pb[n], tol=1e-2, amax=0.05)
