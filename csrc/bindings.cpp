@@ -982,6 +982,48 @@ Tensor stem_conv_wrw(Tensor x, Tensor dz) {
   return dwp;
 }
 
+// Stem backward with the BN-backward apply inside the weight gradient: the statistics pass of
+// pool_bn_bwd (dgamma, dbeta, coefficients), then stem_conv_wrw computing each dz row from the
+// pooled gradient + argmax + z -- the full-resolution dz never reaches HBM.  -> [dwp, dg, db]
+std::vector<Tensor> stem_bwd_fused(Tensor x, Tensor dy, Tensor idx, Tensor z, Tensor mask_coef, Tensor gamma,
+                                   Tensor mean, Tensor invstd) {
+  check_stem(x);
+  check_gpu(dy, "dy");
+  check_gpu(z, "z");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(z.dim() == 4 && z.size(0) == N && z.size(1) == OH && z.size(2) == OW && z.size(3) == 64 &&
+                  z.scalar_type() == torch::kBFloat16 && z.is_contiguous(), "z: [N, OH, OW, 64] bf16 contiguous");
+  TORCH_CHECK(OW <= 128 && OH % 2 == 0 && OW % 2 == 0, "stem: OW <= 128, even OH / OW");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == N && dy.size(1) == OH / 2 && dy.size(2) == OW / 2 && dy.size(3) == 64 &&
+                  dy.scalar_type() == torch::kBFloat16 && dy.is_contiguous(), "dy: [N, OH/2, OW/2, 64] bf16");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == torch::kUInt8 && idx.is_contiguous(), "idx like dy");
+  for (const Tensor* t : {&mask_coef, &gamma, &mean, &invstd}) check_f32(*t, "bn vector");
+  TORCH_CHECK(mask_coef.numel() == 128 && gamma.numel() == 64 && mean.numel() == 64 && invstd.numel() == 64, "bn sizes");
+  const c10::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(torch::kFloat32);
+  const int C = 64;
+  const int G = psamd::pool_bn_bwd_blocks(N, static_cast<int>(OH), static_cast<int>(OW), C);
+  auto pws = torch::empty({2 * G * C + 3 * C}, fopt);
+  auto dg = torch::empty({C}, fopt), db = torch::empty({C}, fopt);
+  const auto st = cur_stream(x);
+  psamd::launch_pool_bn_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                            reinterpret_cast<const uint16_t*>(z.data_ptr()), mask_coef.data_ptr<float>(),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                            pws.data_ptr<float>(), G, dg.data_ptr<float>(), db.data_ptr<float>(), nullptr,
+                            static_cast<int>(N), static_cast<int>(OH), static_cast<int>(OW), C,
+                            static_cast<int>(OH / 2), static_cast<int>(OW / 2), st);
+  const int nblk = psamd::stem_wrw_blocks(N, OH);
+  auto ws = torch::empty({(nblk + 32) * 64 * 224}, fopt);
+  auto dwp = torch::empty({64, 224}, fopt);
+  psamd::launch_stem_conv_wrw(reinterpret_cast<const uint16_t*>(x.data_ptr()), static_cast<int>(x.size(3)),
+                              reinterpret_cast<const uint16_t*>(z.data_ptr()), ws.data_ptr<float>(),
+                              dwp.data_ptr<float>(), N, H, W, OH, OW, st,
+                              reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                              mask_coef.data_ptr<float>(), pws.data_ptr<float>() + 2 * G * C);
+  return {dwp, dg, db};
+}
+
 // ------------------------------------------------------------------------------ NHWC max pool
 // x: [N, H, W, C] bf16 contiguous; coef: optional [scale | shift] (fused BN-apply + ReLU prologue)
 std::vector<Tensor> maxpool_nhwc_fwd(Tensor x, c10::optional<Tensor> coef, int64_t k, int64_t s, int64_t p) {
@@ -1234,6 +1276,18 @@ static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::v
   psamd::ConvGeo g{static_cast<int>(H), static_cast<int>(W), static_cast<int>(OH), static_cast<int>(OW),
                    static_cast<int>(C), static_cast<int>(ks), static_cast<int>(st), static_cast<int>(pd)};
   return {g, a.size(0) / (H * W)};
+}
+
+// The tile plan conv_gemm picks for a plain (no second row source) GEMM: [bm, bn, gm] -- tests
+// use it to check which kernel family a shape runs on (bm = bn = 256: conv_big.hip)
+std::vector<int64_t> conv_gemm_plan(int64_t M, int64_t N, int64_t C, std::vector<int64_t> geo, bool pro, int64_t epi) {
+  TORCH_CHECK(geo.size() == 7, "geo = [H, W, OH, OW, ks, stride, pad]");
+  const psamd::ConvGeo g{static_cast<int>(geo[0]), static_cast<int>(geo[1]), static_cast<int>(geo[2]),
+                         static_cast<int>(geo[3]), static_cast<int>(C), static_cast<int>(geo[4]),
+                         static_cast<int>(geo[5]), static_cast<int>(geo[6])};
+  const int K = static_cast<int>(geo[4] * geo[4] * C);
+  const auto pl = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), K, pro, g, 0, static_cast<int>(epi));
+  return {pl.bm, pl.bn, pl.gm};
 }
 
 // c [M, N] = epilogue(sum_k f(a[src(m, k)]) b[n, k]) -> [c, BN partials [2, G, N] (epi 1/3)]
@@ -1724,6 +1778,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
+  m.def("conv_gemm_plan", &conv_gemm_plan);
   m.def("conv11_bwd_fused", &conv11_bwd_fused, py::arg("g"), py::arg("z3"), py::arg("cbwd"), py::arg("wt"), py::arg("z2"),
         py::arg("cf2") = py::none(), py::arg("mean2") = py::none(), py::arg("invstd2") = py::none());
   m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported, py::arg("ci"), py::arg("co"),
@@ -1776,6 +1831,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_fwd", &stem_conv_fwd, py::arg("x"), py::arg("wp"), py::arg("kshift") = py::none());
   m.def("bn_finalize_sums", &bn_finalize_sums);
   m.def("stem_conv_wrw", &stem_conv_wrw);
+  m.def("stem_bwd_fused", &stem_bwd_fused);
   m.def("dlrm_interact_fwd", &dlrm_interact_fwd);
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

@@ -209,7 +209,8 @@ void launch_maxpool_nhwc_fwd(const uint16_t* x, const float* coef, uint16_t* y, 
 void launch_maxpool_nhwc_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                              int OW, int k, int s, int p, hipStream_t st);
 // stem backward: maxpool 3x3/2/1 scatter fused into the BN(+ReLU) backward of its input z
-// (mc = the forward's [scale | shift]); ws: [2 G C + 3 C] fp32, G = pool_bn_bwd_blocks(...)
+// (mc = the forward's [scale | shift]); ws: [2 G C + 3 C] fp32, G = pool_bn_bwd_blocks(...);
+// dz == nullptr: the statistics pass only (dgamma, dbeta and the coefficients at ws + 2 G C)
 int pool_bn_bwd_blocks(int64_t N, int H, int W, int C);
 void launch_pool_bn_bwd(const uint16_t* dy, const uint8_t* idx, const uint16_t* z, const float* mc, const float* mean,
                         const float* invstd, const float* gamma, float* ws, int G, float* dgamma, float* dbeta,
@@ -232,8 +233,12 @@ void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshi
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,
                              float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
 // ws: (stem_wrw_blocks + 32) * 64 * 224 floats; dwp: [64][224] fp32 packed weight gradient
+// pool_dy != nullptr: FUSED -- dz is z (the stem BN's input) and each dz row is computed in the
+// kernel from the pooled gradient pool_dy / pool_idx ([N, OH/2, OW/2, 64]), mc ([2 * 64] scale |
+// shift) and coef ([3 * 64] bn backward ca | cb | cc; pool.hip launch_pool_bn_bwd with dz null)
 void launch_stem_conv_wrw(const uint16_t* x, int cin, const uint16_t* dz, float* ws, float* dwp, int N, int H, int W,
-                          int OH, int OW, hipStream_t s);
+                          int OH, int OW, hipStream_t s, const uint16_t* pool_dy = nullptr,
+                          const uint8_t* pool_idx = nullptr, const float* mc = nullptr, const float* coef = nullptr);
 
 // ---------------------------------------------------------------- transformer.hip (row / elementwise)
 void launch_rmsnorm_fwd(const uint16_t* x, const uint16_t* r, const void* w, bool w_bf16, uint16_t* s, uint16_t* y,
@@ -356,6 +361,11 @@ struct ConvFwdPlan {
 };
 // epi: the fold epilogues (6-9) may run on one-tile-per-block LDS-DMA grids (PS_AMD_FOLD_GLDS)
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi = 0);
+// conv_big.hip: 256 x 256 tiles, one 512-thread block per CU, for plain deep-K 1x1 GEMMs (epi 0/1/3);
+// conv_fwd_plan_geo / launch_conv_fwd route there when conv_big_ok holds (gm = conv_big_gm(M))
+bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi);
+int conv_big_gm(int M);
+void launch_conv_big(const ConvGemmArgs& a, hipStream_t s);
 // the four stride-2 data-gradient phase GEMMs (epi 3, no prologue, LDS-DMA staging, 128-pixel tiles)
 // in one launch; phase i's partials go to rows [sum gm(<i), ..) of a part with pgm = sum of gm
 void launch_conv_dgrad_phases(const ConvGemmArgs* ph, hipStream_t s);

@@ -1,0 +1,370 @@
+// 256 x 256 output tiles for the deep-K 1x1 convolution GEMMs (ResNet-50 layers 3-4: K = 256-2048
+// input channels, N = 256-2048 output channels; stride 1 or a stride-2 downsample).
+//
+// Reference hot op: layer/Conv2DLayer.java:146-240 (the conv forward GEMM) and its data-gradient
+// twin.  The general conv_fwd_kernel (convgemm.hip) runs 128 x 128 tiles, two blocks per CU and a
+// barrier pair per 64-deep stage: 450-800 TF/s on these shapes, which are MFMA-bound at N >= 512 and
+// HBM-bound at N = 256.  Here one 512-thread block per CU owns a 256 x 256 tile:
+//   * 8 waves as 2 (pixels) x 4 (channels), each 128 pixels x 64 channels = 4 x 2 blocks of
+//     v_mfma_f32_32x32x16_bf16 (6 fragment reads per 8 MFMAs, half the LDS traffic per FLOP of a
+//     64 x 64 wave tile);
+//   * both operands global -> LDS by LDS-DMA into an NST-deep ring of BK-deep stages (128 KiB in
+//     total: BK = 64 x 2 stages or BK = 32 x 4), the DMA of stage kt + NST - 1 issued right after
+//     the ONE barrier of stage kt and waited for by a counted vmcnt, so NST - 1 stages stay in
+//     flight across the barrier (raw s_barrier: __syncthreads() would drain them);
+//   * fragment reads as inline asm, the next k-step's issued before this one's MFMAs;
+//   * the epilogue (plain store, BN statistics, or the data-gradient ReLU mask + BN-backward sums
+//     -- conv_gemm's epilogues 0 / 1 / 3) from a bf16 output tile in LDS, one 16-B column group
+//     per thread, rows coalesced.
+// Blocks are XCD-remapped so the channel tiles of one pixel tile share its A rows in one L2.
+#include <algorithm>
+#include <cstdlib>
+
+#include "psamd_device.h"
+#include "psamd_launch.h"
+
+namespace psamd {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(1))) const void gptr_t;
+typedef __attribute__((address_space(3))) void lptr_t;
+typedef __attribute__((address_space(3))) const char lds_char;
+
+__device__ __attribute__((aligned(16))) uint16_t kBigZero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+constexpr int kTM = 256, kTN = 256;
+constexpr int kRing = 131072;   // LDS bytes of the stage ring
+constexpr int kCS = kTN + 4;    // output tile row stride (elements): 130 dwords, conflict-free b64 writes
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));
+}
+__device__ __forceinline__ bf16x8_t ld_b128(uint32_t a) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8_t ld_b128o(uint32_t a) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void tie(T& v) {
+  asm volatile("" : "+v"(v));
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int xcd_remap_big(int b, int nblk) {
+  const int q = nblk >> 3, r = nblk & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+__device__ __forceinline__ uint32_t fdiv_big(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
+
+// Stage tile rows of BK bf16 (2 BK bytes).  BK = 64: 128-B rows, chunk c of row r at c ^ ((r >> 1)
+// & 7); BK = 32: 64-B rows, chunk c at c ^ ((r >> 2) & 3).  Either way the 16 rows of a
+// ds_read_b128 lane group land on 16 distinct 16-B bank slots, and the swizzle of a 32-row
+// fragment block depends on fr = r & 31 only.
+template <int BK>
+__device__ __forceinline__ int bswz(int r, int c) {
+  return BK == 64 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3);
+}
+
+template <int EPI, int BK>
+__global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) {
+  static_assert(EPI == 0 || EPI == 1 || EPI == 3, "plain / BN statistics / data-gradient mask + sums");
+  static_assert(BK == 64 || BK == 32, "stage depth");
+  constexpr int RB = 2 * BK;                    // bytes per stage row
+  constexpr int A_BYTES = kTM * RB, STAGE = (kTM + kTN) * RB;
+  constexpr int NST = kRing / STAGE;            // 2 (BK 64) or 4 (BK 32)
+  constexpr int CPR = RB / 16;                  // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;                 // rows per DMA wave-instruction
+  constexpr int PA = kTM / RPI / 8;             // A DMA instructions per wave per stage
+  constexpr int PB = kTN / RPI / 8;
+  constexpr int GPS = PA + PB;                  // DMA instructions per wave per stage
+  constexpr int KSTEPS = BK / 16;
+  constexpr int OUT_BYTES = kTM * kCS * 2;
+  constexpr int RED_OFF = OUT_BYTES > kRing ? OUT_BYTES : kRing;
+  constexpr int LDS_BYTES = RED_OFF + 2 * 8 * kTN * 4;
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const uint32_t L0 = lds_addr(lds);
+
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int nN = p.N / kTN, mtiles = (p.M + kTM - 1) / kTM;
+  const int L = xcd_remap_big(blockIdx.x, gridDim.x);
+  const int mt = L / nN, n0 = (L - mt * nN) * kTN;
+  const int m0 = mt * kTM;
+  const ConvGeo& g = p.g;
+  const int nk = p.K / BK;
+
+  // ---- DMA sources: lane-linear LDS rows, swizzled source chunk; A rows past M read zeros
+  const int lrow = lane / CPR, lch = lane % CPR;
+  int64_t abase[PA];
+  unsigned aok = 0;
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int r = (wave * PA + i) * RPI + lrow, m = m0 + r;
+    int64_t off = 0;
+    if (m < p.M) {
+      if (g.stride == 1) {
+        off = static_cast<int64_t>(m) * g.C;
+      } else {  // stride-2 downsample: output pixel (img, oh, ow) reads input (img, 2 oh, 2 ow)
+        const int img = static_cast<int>(fdiv_big(static_cast<uint32_t>(m), p.fd_ohw));
+        const int rr = m - img * (g.OH * g.OW);
+        const int oh = static_cast<int>(fdiv_big(static_cast<uint32_t>(rr), p.fd_ow)), ow = rr - oh * g.OW;
+        off = ((static_cast<int64_t>(img) * g.H + oh * g.stride) * g.W + ow * g.stride) * g.C;
+      }
+      aok |= 1u << i;
+    }
+    abase[i] = off + bswz<BK>(r, lch) * 8;
+  }
+  const uint16_t* bsrc[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int r = (wave * PB + i) * RPI + lrow;
+    bsrc[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + bswz<BK>(r, lch) * 8;
+  }
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint16_t* src = ((aok >> i) & 1u) ? p.a + abase[i] + k0 : kBigZero;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(As + (wave * PA + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t*)(bsrc[i] + k0), (lptr_t*)(Bs + (wave * PB + i) * 1024), 16, 0, 0);
+  };
+
+  // ---- fragment addresses: wave (wm, wn) = pixels 128 wm.., channels 64 wn..; the chunk swizzle
+  // of rows 32 j + fr is the same for every block j, so one address per k-step and operand, and
+  // the blocks are immediate offsets (32 rows = 32 RB bytes apart)
+  const int wm = wave >> 2, wn = wave & 3;
+  uint32_t fa[KSTEPS], fb[KSTEPS];
+#pragma unroll
+  for (int s = 0; s < KSTEPS; ++s) {
+    const int ch = bswz<BK>(fr, 2 * s + fh) * 16;
+    fa[s] = static_cast<uint32_t>((128 * wm + fr) * RB + ch);
+    fb[s] = static_cast<uint32_t>(A_BYTES + (64 * wn + fr) * RB + ch);
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  constexpr int OJ = 32 * RB;  // bytes between 32-row fragment blocks
+  bf16x8_t xa[2][4], wb[2][2];
+  auto fetch = [&](uint32_t sb, int s, int set) {
+    const uint32_t a = sb + fa[s], b = sb + fb[s];
+    xa[set][0] = ld_b128o<0>(a);
+    xa[set][1] = ld_b128o<OJ>(a);
+    xa[set][2] = ld_b128o<2 * OJ>(a);
+    xa[set][3] = ld_b128o<3 * OJ>(a);
+    wb[set][0] = ld_b128o<0>(b);
+    wb[set][1] = ld_b128o<OJ>(b);
+  };
+  auto mfma_set = [&](int set) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tie(xa[set][j]);
+    tie(wb[set][0]);
+    tie(wb[set][1]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[set][i], xa[set][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: stages 0 .. NST - 2 in flight
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) {
+    if (s < nk) issue(s, s);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed (this wave's DMAs): younger are the min(NST - 2, nk - 1 - kt) stages after it
+    const int younger = min(NST - 2, nk - 1 - kt);
+    if (younger >= 2) wait_vm<2 * GPS>();
+    else if (younger == 1) wait_vm<GPS>();
+    else wait_vm<0>();
+    lds_bar();  // every wave's stage kt landed; every wave is done with stage kt - 1's buffer
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    const uint32_t sb = L0 + static_cast<uint32_t>((kt % NST) * STAGE);
+    fetch(sb, 0, 0);
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      if (s + 1 < KSTEPS) {
+        fetch(sb, s + 1, (s + 1) & 1);
+        wait_lgkm<6>();
+      } else {
+        wait_lgkm<0>();
+      }
+      mfma_set(s & 1);
+    }
+  }
+  wait_vm<0>();
+  lds_bar();  // the output tile overlays the stage ring
+
+  // ---- accumulators -> bf16 output tile [256 px][kCS]: register q of acc[i][j] is channel
+  // 64 wn + 32 i + 8 (q >> 2) + 4 fh + (q & 3) of pixel 128 wm + 32 j + fr
+  uint16_t* Cs = reinterpret_cast<uint16_t*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int nl = 64 * wn + 32 * i + 8 * q4 + 4 * fh, ml = 128 * wm + 32 * j + fr;
+        const u16x4 v = {f32_to_bf16(acc[i][j][4 * q4]), f32_to_bf16(acc[i][j][4 * q4 + 1]),
+                         f32_to_bf16(acc[i][j][4 * q4 + 2]), f32_to_bf16(acc[i][j][4 * q4 + 3])};
+        *reinterpret_cast<u16x4*>(Cs + ml * kCS + nl) = v;
+      }
+  lds_bar();
+
+  // ---- row pass: thread t owns channels [8 cg, 8 cg + 8) of rows r0 + 16 i
+  const int cg = t & 31, r0 = t >> 5, nc = n0 + cg * 8;
+  float e0[8], e1[8], e2[8], e3[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) e0[e] = e1[e] = e2[e] = e3[e] = s1[e] = s2[e] = 0.f;
+  if constexpr (EPI == 1) {
+    if (p.kshift) load8(p.kshift, nc, e0);
+  } else if constexpr (EPI == 3) {
+    load8(p.mc, nc, e0);
+    load8(p.mc + p.N, nc, e1);
+    load8(p.mean, nc, e2);
+    load8(p.invstd, nc, e3);
+  }
+  constexpr int NPASS = kTM / 16;
+  constexpr int HALF = NPASS / 2;  // rows in flight per half (EPI 3's BN-input reads)
+#pragma unroll
+  for (int h = 0; h < NPASS; h += HALF) {
+    u16x8 zr[EPI == 3 ? HALF : 1];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) {
+        const int m = min(m0 + r0 + 16 * (h + i), p.M - 1);
+        zr[i] = *reinterpret_cast<const u16x8*>(p.aux + static_cast<int64_t>(m) * p.N + nc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const int rr = r0 + 16 * (h + i), m = m0 + rr;
+      if (m >= p.M) break;
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * kCS + cg * 8);
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * kCS + cg * 8 + 4);
+      u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = bf16_to_f32(v[e]) - e0[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+      } else if constexpr (EPI == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float z = bf16_to_f32(zr[i][e]);
+          const bool on = z * e0[e] + e1[e] > 0.f;
+          const float gv = on ? bf16_to_f32(v[e]) : 0.f;
+          s1[e] += gv;
+          s2[e] += gv * ((z - e2[e]) * e3[e]);
+          if (!on) v[e] = 0;
+        }
+      }
+      *reinterpret_cast<u16x8*>(p.c + static_cast<int64_t>(m) * p.N + nc) = v;
+    }
+  }
+  if constexpr (EPI == 1 || EPI == 3) {
+    // threads of one column group: lanes l, l + 32 of each wave, then the 8 waves in fixed order
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += __shfl_xor(s1[e], 32, 64);
+      s2[e] += __shfl_xor(s2[e], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(lds + RED_OFF);  // [2][8 waves][256]
+    if (fh == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wave * kTN + cg * 8 + e] = s1[e];
+        red[(8 + wave) * kTN + cg * 8 + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    if (t < kTN) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        a += red[w * kTN + t];
+        b += red[(8 + w) * kTN + t];
+      }
+      const int64_t PG = p.pgm > 0 ? p.pgm : mtiles;
+      p.part[static_cast<int64_t>(mt) * p.N + n0 + t] = a;
+      p.part[(PG + mt) * p.N + n0 + t] = b;
+    }
+  }
+}
+
+int big_bk() {
+  static const int bk = [] {
+    const char* e = std::getenv("PS_AMD_CONV_BIG_BK");
+    return e != nullptr && std::atoi(e) == 32 ? 32 : 64;
+  }();
+  return bk;
+}
+
+}  // namespace
+
+// Eligible: a plain 1x1 GEMM (no prologue, no second row source, rows in order), N a multiple of
+// 256, K >= 256, epilogue 0 / 1 / 3, and at least one block per CU.  PS_AMD_CONV_BIG=0 disables.
+bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
+  static const bool on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_BIG");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (!on || src2 != 0 || pro || g.RH != 0) return false;
+  if (g.ks != 1 || g.ksw > 1 || g.pad != 0) return false;
+  if (N % kTN != 0 || K % 64 != 0 || K < 256 || g.C != K) return false;
+  if (!(epi == 0 || epi == 1 || epi == 3)) return false;
+  const int64_t nblk = static_cast<int64_t>((M + kTM - 1) / kTM) * (N / kTN);
+  return nblk >= 256;
+}
+
+int conv_big_gm(int M) { return (M + kTM - 1) / kTM; }
+
+void launch_conv_big(const ConvGemmArgs& a, hipStream_t s) {
+  const int nblk = conv_big_gm(a.M) * (a.N / kTN);
+#define PSAMD_BIG(E, BK) hipLaunchKernelGGL((conv_big_kernel<E, BK>), dim3(nblk), dim3(512), 0, s, a)
+  if (big_bk() == 32) {
+    if (a.epi == 1) PSAMD_BIG(1, 32);
+    else if (a.epi == 3) PSAMD_BIG(3, 32);
+    else PSAMD_BIG(0, 32);
+  } else {
+    if (a.epi == 1) PSAMD_BIG(1, 64);
+    else if (a.epi == 3) PSAMD_BIG(3, 64);
+    else PSAMD_BIG(0, 64);
+  }
+#undef PSAMD_BIG
+}
+
+}  // namespace psamd

@@ -2094,6 +2094,13 @@ bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
 }
 
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
+  if (conv_big_ok(M, N, K, pro, g, src2, epi)) {  // 256 x 256 tiles (conv_big.hip)
+    ConvFwdPlan pl;
+    pl.bm = 256;
+    pl.bn = 256;
+    pl.gm = conv_big_gm(M);
+    return pl;
+  }
   if (src2 == 0 && c64_ok(g, N, pro)) {  // persistent row-tile patch kernel, one block per CU
     ConvFwdPlan pl;
     pl.bm = 128;
@@ -2165,6 +2172,10 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const ConvFwdPlan pl = conv_fwd_plan_geo(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2, a.epi);
   const int GM = pl.gm;
   const int nblk = GM * (a.N / pl.bn);
+  if (conv_big_ok(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2, a.epi)) {
+    launch_conv_big(a, s);
+    return;
+  }
   if (src2 == 0 && c64_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
     if (c64_mode() == 2 && (a.epi == 1 || a.epi == 3)) {
       launch_conv3x3_c64s(a, GM, s);

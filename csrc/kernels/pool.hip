@@ -431,6 +431,7 @@ void launch_pool_bn_bwd(const uint16_t* dy, const uint8_t* idx, const uint16_t* 
                      px, nullptr, N, H, W, C, OH, OW);
   launch_bn_bwd_partials(pd, px, G, nullptr, nullptr, gamma, mean, invstd, dgamma, dbeta, coef, nullptr,
                          static_cast<int64_t>(N) * H * W, C, st);
+  if (dz == nullptr) return;  // the apply runs inside the stem weight gradient (stem.hip FUSED)
   hipLaunchKernelGGL((pool_bn_bwd_kernel<true>), dim3(G), dim3(256), 0, st, dy, idx, z, mc, nullptr, nullptr, coef,
                      nullptr, nullptr, dz, N, H, W, C, OH, OW);
 }

@@ -254,14 +254,115 @@ struct DzPrefetch {
   }
 };
 
+// FUSED: the stem's BN-backward APPLY pass (pool.hip pool_bn_bwd_kernel<true>) computed per dz
+// row inside the weight-gradient kernel, so the full-resolution dz is never written nor re-read:
+//   dz = ca g' + cb z + cc,   g' = bf16(g) * relu'(z sc + sh),   g = the max-pool scatter of dy
+// Thread t owns 16-B channel group ch = t & 7 of the pixel PAIRS pp = (t >> 3) + 32 k (k = 0, 1):
+// pixels 2 pp, 2 pp + 1 of z row 2 a + dh take their gradient from the pooled windows (a + i,
+// pp + j), i <= dh, j <= dw (argmax code (dh + 1 - 2 i) 3 + (dw + 1 - 2 j)).  Row 2 a + 1 needs
+// pooled rows a and a + 1, row 2 a + 2 only a + 1: the windows of one pooled row are loaded per
+// TWO z rows and carried in registers.
+struct PoolWin {
+  u16x8 g[2][2];      // [pair k][j] pooled gradient, 8 channels
+  uint64_t c[2][2];   // [pair k][j] argmax codes (8 x 1 B); all-ones = no window
+};
+
+__device__ __forceinline__ void load_win(PoolWin& w, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                         int n, int pa, int OHp, int OWp) {
+  const int ch = threadIdx.x & 7;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int pp = (threadIdx.x >> 3) + 32 * k;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = pa < OHp && pp + j < OWp;
+      const int64_t o = ok ? ((static_cast<int64_t>(n) * OHp + pa) * OWp + pp + j) * 64 + ch * 8 : 0;
+      const u16x8 g = *reinterpret_cast<const u16x8*>(dy + o);
+      const uint64_t c = *reinterpret_cast<const uint64_t*>(idx + o);
+      w.g[k][j] = ok ? g : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      w.c[k][j] = ok ? c : ~uint64_t(0);
+    }
+  }
+}
+
+struct ZPair {
+  u16x8 v[2][2];  // [pair k][pixel d]
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ zr, int OW) {
+    const int ch = threadIdx.x & 7;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int px = 2 * ((threadIdx.x >> 3) + 32 * k) + d;
+        v[k][d] = *reinterpret_cast<const u16x8*>(zr + (px < OW ? px : 0) * 64 + ch * 8);
+      }
+  }
+};
+
+// dz of z row r (dh = r & 1) into the LDS dz tile: i = 0 windows from `lo` (pooled row r >> 1),
+// i = 1 windows (dh = 1 only) from `hi` (pooled row (r >> 1) + 1)
+// cf: LDS [5][64] floats sc | sh | ca | cb | cc (read per row: in registers they cost the kernel
+// its second wave per SIMD)
+__device__ __forceinline__ void dz_row_to_lds(uint16_t* lds_dz, const ZPair& z, const PoolWin& lo, const PoolWin& hi,
+                                              int dh, int OW, const float* cf) {
+  const int ch = threadIdx.x & 7;
+  float sc[8], sh[8], A[8], B[8], Cc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = cf[ch * 8 + e];
+    sh[e] = cf[64 + ch * 8 + e];
+    A[e] = cf[128 + ch * 8 + e];
+    B[e] = cf[192 + ch * 8 + e];
+    Cc[e] = cf[256 + ch * 8 + e];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int px = 2 * ((threadIdx.x >> 3) + 32 * k) + d;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (j > d) continue;  // compile-time
+          if (i == 1 && dh == 0) continue;
+          const PoolWin& w = i ? hi : lo;
+          const uint8_t code = static_cast<uint8_t>((dh + 1 - 2 * i) * 3 + (d + 1 - 2 * j));
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (static_cast<uint8_t>(w.c[k][j] >> (8 * e)) == code) acc[e] += bf16_to_f32(w.g[k][j][e]);
+        }
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float zf = bf16_to_f32(z.v[k][d][e]);
+        const float g = zf * sc[e] + sh[e] > 0.f ? bf16_to_f32(f32_to_bf16(acc[e])) : 0.f;
+        o[e] = px < OW ? f32_to_bf16(A[e] * g + B[e] * zf + Cc[e]) : static_cast<uint16_t>(0);
+      }
+      uint16_t* dst = lds_dz + px * kDzLd + ch * 8;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16));
+      *reinterpret_cast<uint2*>(dst + 4) = make_uint2(o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16));
+    }
+}
+
+struct StemBwdFuse {
+  const uint16_t* dy;  // [N, OH/2, OW/2, 64] pooled gradient
+  const uint8_t* idx;  // its argmax codes
+  const float* mc;     // [2 * 64] bn scale | shift (the ReLU mask)
+  const float* coef;   // [3 * 64] ca | cb | cc
+};
+
 // grid = N * splits blocks (as the forward); each accumulates its output rows into
-// part[b][64][224] (fp32).
-__global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __restrict__ x,
+// part[b][64][224] (fp32).  dz: the stem BN's input gradient, or (FUSED) z, the BN input.
+template <bool FUSED>
+__global__ __launch_bounds__(256, 2) void stem_conv_wrw_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ dz,
                                                             float* __restrict__ part, int N, int H, int W, int OH,
-                                                            int OW, int splits, int rpb, int cin) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 2 * 128 * kDzLd];
+                                                            int OW, int splits, int rpb, int cin, StemBwdFuse fz) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kSlots * kRS + 2 * 128 * kDzLd + (FUSED ? 5 * 64 * 2 : 0)];
   uint16_t* lds_in = lds;
+  float* cf = reinterpret_cast<float*>(lds + kSlots * kRS + 2 * 128 * kDzLd);  // FUSED: [5][64]
   const int n = blockIdx.x / splits, chunk = blockIdx.x - n * splits;
   const int oh0 = chunk * rpb, oh1 = min(OH, oh0 + rpb);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -273,9 +374,23 @@ __global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __re
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[mt][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  // FUSED: the BN coefficients into LDS, the carried pooled windows
+  PoolWin wlo, whi;
+  const int OHp = OH / 2, OWp = OW / 2;
+  if constexpr (FUSED) {
+    for (int i = threadIdx.x; i < 5 * 64; i += 256) cf[i] = i < 128 ? fz.mc[i] : fz.coef[i - 128];
+    __syncthreads();
+  }
   if (oh0 < oh1) {  // block-uniform
     stage_window(x, lds_in, n, oh0, H, W, cin);
-    {
+    if constexpr (FUSED) {
+      ZPair z0;
+      z0.load(dz + (static_cast<int64_t>(n) * OH + oh0) * OW * 64, OW);
+      load_win(wlo, fz.dy, fz.idx, n, oh0 >> 1, OHp, OWp);
+      if (oh0 & 1) load_win(whi, fz.dy, fz.idx, n, (oh0 >> 1) + 1, OHp, OWp);
+      dz_row_to_lds(lds + kSlots * kRS, z0, wlo, whi, oh0 & 1, OW, cf);
+      if (oh0 & 1) wlo = whi;
+    } else {
       DzPrefetch d0;
       d0.load(dz + (static_cast<int64_t>(n) * OH + oh0) * OW * 64, OW);
       d0.store(lds + kSlots * kRS);
@@ -285,9 +400,16 @@ __global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __re
       const bool more = oh + 1 < oh1;
       RowPrefetch<256> pf;
       DzPrefetch pd;
+      ZPair pz;
+      const bool odd = (oh + 1) & 1;
       if (more) {
         pf.load(x, threadIdx.x, n, 2 * oh + 4, H, W, cin);
-        pd.load(dz + (static_cast<int64_t>(n) * OH + oh + 1) * OW * 64, OW);
+        if constexpr (FUSED) {
+          pz.load(dz + (static_cast<int64_t>(n) * OH + oh + 1) * OW * 64, OW);
+          if (odd) load_win(whi, fz.dy, fz.idx, n, ((oh + 1) >> 1) + 1, OHp, OWp);
+        } else {
+          pd.load(dz + (static_cast<int64_t>(n) * OH + oh + 1) * OW * 64, OW);
+        }
       }
       const uint16_t* lds_dz = lds + kSlots * kRS + ((oh - oh0) & 1) * 128 * kDzLd;
 #pragma unroll
@@ -319,7 +441,13 @@ __global__ __launch_bounds__(256) void stem_conv_wrw_kernel(const uint16_t* __re
       }
       if (more) {
         pf.store(lds_in, threadIdx.x, 2 * oh + 4);
-        pd.store(lds + kSlots * kRS + ((oh + 1 - oh0) & 1) * 128 * kDzLd);
+        uint16_t* nxt = lds + kSlots * kRS + ((oh + 1 - oh0) & 1) * 128 * kDzLd;
+        if constexpr (FUSED) {
+          dz_row_to_lds(nxt, pz, wlo, whi, odd ? 1 : 0, OW, cf);
+          if (odd) wlo = whi;  // pooled row (oh + 1) / 2 + 1 serves the next (even) row as i = 0
+        } else {
+          pd.store(nxt);
+        }
       }
       __syncthreads();
     }
@@ -376,11 +504,18 @@ int stem_wrw_blocks(int N, int OH) { return N * kWrwSplits; }
 
 // ws: [nblk * 64 * 224 + 32 * 64 * 224] floats; dwp: [64 * 224] floats
 void launch_stem_conv_wrw(const uint16_t* x, int cin, const uint16_t* dz, float* ws, float* dwp, int N, int H, int W,
-                          int OH, int OW, hipStream_t s) {
+                          int OH, int OW, hipStream_t s, const uint16_t* pool_dy, const uint8_t* pool_idx,
+                          const float* mc, const float* coef) {
   if (N <= 0 || OH <= 0) return;
   const int nblk = stem_wrw_blocks(N, OH);
   const int rpb = (OH + kWrwSplits - 1) / kWrwSplits;
-  hipLaunchKernelGGL(stem_conv_wrw_kernel, dim3(nblk), dim3(256), 0, s, x, dz, ws, N, H, W, OH, OW, kWrwSplits, rpb, cin);
+  const StemBwdFuse fz{pool_dy, pool_idx, mc, coef};
+  if (pool_dy != nullptr)
+    hipLaunchKernelGGL(stem_conv_wrw_kernel<true>, dim3(nblk), dim3(256), 0, s, x, dz, ws, N, H, W, OH, OW, kWrwSplits,
+                       rpb, cin, fz);
+  else
+    hipLaunchKernelGGL(stem_conv_wrw_kernel<false>, dim3(nblk), dim3(256), 0, s, x, dz, ws, N, H, W, OH, OW, kWrwSplits,
+                       rpb, cin, fz);
   constexpr int E = 64 * kKp;
   const int groups = 32;
   const int per = (nblk + groups - 1) / groups;

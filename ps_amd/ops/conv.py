@@ -168,7 +168,13 @@ class _StemBnReluMaxPool(torch.autograd.Function):
         n, oh, ow, c = z.shape
         dyn = dy.permute(0, 2, 3, 1)
         dyn = dyn if dyn.is_contiguous() else dyn.contiguous()
-        if oh % 2 == 0 and ow % 2 == 0 and 256 % (c // 8) == 0 and os.environ.get("PS_AMD_POOL_BN_BWD", "1") != "0":
+        fusable = oh % 2 == 0 and ow % 2 == 0 and 256 % (c // 8) == 0 and os.environ.get("PS_AMD_POOL_BN_BWD", "1") != "0"
+        if fusable and c == 64 and os.environ.get("PS_AMD_STEM_BWD_FUSED", "1") != "0":
+            # statistics pass, then the weight gradient computing each dz row itself from the
+            # pooled gradient (csrc/kernels/stem.hip FUSED): dz is never written
+            dwp, dg, db = native().stem_bwd_fused(xin, dyn, idx, z, coef, gamma, mean, invstd)
+            return None, unpack_stem_grad(dwp, w.shape[1]).to(w.dtype), dg, db, None, None, None, None
+        if fusable:
             # pool scatter fused into both BN-backward passes: the full-resolution pool gradient
             # is never written (csrc/kernels/pool.hip pool_bn_bwd_kernel)
             dz, dg, db = native().pool_bn_bwd(dyn, idx, z, coef, gamma, mean, invstd)

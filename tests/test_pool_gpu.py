@@ -181,3 +181,32 @@ def test_pool_bn_bwd_fused_matches_unfused(N, H, C):
     d = (dz.float() - dz_ref.view_as(dz).float()).abs()
     ulp = dz_ref.view_as(dz).float().abs() * 2.0 ** -7 + 1e-6
     assert bool((d <= ulp).all()), d.max().item()
+
+
+@pytest.mark.parametrize("N,H,cin", [(2, 224, 3), (3, 64, 4), (2, 40, 3)])
+def test_stem_bwd_fused_matches_apply_then_wgrad(N, H, cin):
+    """Stem backward with the BN apply inside the weight gradient (stem.hip FUSED: each dz row is
+    rebuilt from the pooled gradient, argmax and z) vs the apply pass writing dz + the plain weight
+    gradient: dz is computed with the same arithmetic and accumulated in the same order, so the
+    packed weight gradient matches to fp32 rounding and dgamma / dbeta exactly."""
+    from ps_amd.ops import native
+    from ps_amd.ops.conv import nhwc_in
+
+    torch.manual_seed(5)
+    x = torch.randn(N, cin, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xin = nhwc_in(x)
+    OH = (H - 1) // 2 + 1
+    z = torch.randn(N, OH, OH, 64, device="cuda").bfloat16()
+    coef = torch.cat([torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.3]).float().contiguous()
+    zf = z.float()
+    mean = zf.mean(dim=(0, 1, 2))
+    invstd = 1.0 / (zf.var(dim=(0, 1, 2), unbiased=False) + 1e-5).sqrt()
+    gamma = torch.rand(64, device="cuda") + 0.5
+    y, idx = native().maxpool_nhwc_fwd(z, coef, 3, 2, 1)
+    dy = torch.randn_like(y.float()).bfloat16()
+    dz, dg_ref, db_ref = native().pool_bn_bwd(dy, idx, z, coef, gamma, mean, invstd)
+    dw_ref = native().stem_conv_wrw(xin, dz)
+    dw, dg, db = native().stem_bwd_fused(xin, dy, idx, z, coef, gamma, mean, invstd)
+    torch.cuda.synchronize()
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
+    torch.testing.assert_close(dw, dw_ref, rtol=1e-5, atol=1e-5 * dw_ref.abs().max().item())
