@@ -336,7 +336,8 @@ int big_bk() {
 }  // namespace
 
 // Eligible: a plain 1x1 GEMM (no prologue, no second row source, rows in order), N a multiple of
-// 256, K >= 256, epilogue 0 / 1 / 3, and at least one block per CU.  PS_AMD_CONV_BIG=0 disables.
+// 256, K >= 256, epilogue 0 / 1 / 3, and >= 1024 blocks or K >= 1024 (with >= 256 blocks).
+// PS_AMD_CONV_BIG=0 disables; PS_AMD_CONV_BIG_BK=32 selects the 4-stage ring of 32-deep stages.
 bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
   static const bool on = [] {
     const char* e = std::getenv("PS_AMD_CONV_BIG");
@@ -346,8 +347,11 @@ bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int 
   if (g.ks != 1 || g.ksw > 1 || g.pad != 0) return false;
   if (N % kTN != 0 || K % 64 != 0 || K < 256 || g.C != K) return false;
   if (!(epi == 0 || epi == 1 || epi == 3)) return false;
+  // one block per CU: below ~4 rounds of blocks the last round's idle CUs and the per-tile
+  // prologue / epilogue outweigh the faster K loop unless K is deep (profiles/r5_conv_big_probe.txt:
+  // at batch 256 the K = 256 / 512 shapes with 784 blocks ran 2-15 % slower, K >= 1024 faster)
   const int64_t nblk = static_cast<int64_t>((M + kTM - 1) / kTM) * (N / kTN);
-  return nblk >= 256;
+  return nblk >= 256 && (nblk >= 1024 || K >= 1024);
 }
 
 int conv_big_gm(int M) { return (M + kTM - 1) / kTM; }
