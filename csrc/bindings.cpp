@@ -1278,15 +1278,18 @@ static std::pair<psamd::ConvGeo, int64_t> conv_geo(const Tensor& a, const std::v
   return {g, a.size(0) / (H * W)};
 }
 
-// The tile plan conv_gemm picks for a plain (no second row source) GEMM: [bm, bn, gm] -- tests
-// use it to check which kernel family a shape runs on (bm = bn = 256: conv_big.hip)
-std::vector<int64_t> conv_gemm_plan(int64_t M, int64_t N, int64_t C, std::vector<int64_t> geo, bool pro, int64_t epi) {
+// The tile plan conv_gemm picks: [bm, bn, gm] (src2: 0 one row source, 1 the block-output
+// prologue, 2 the BN-backward prologue) -- tests and the fused ResNet path use it to see which
+// kernel family a shape runs on (bm = bn = 256: conv_big.hip)
+std::vector<int64_t> conv_gemm_plan(int64_t M, int64_t N, int64_t C, std::vector<int64_t> geo, bool pro, int64_t epi,
+                                    int64_t src2) {
   TORCH_CHECK(geo.size() == 7, "geo = [H, W, OH, OW, ks, stride, pad]");
   const psamd::ConvGeo g{static_cast<int>(geo[0]), static_cast<int>(geo[1]), static_cast<int>(geo[2]),
                          static_cast<int>(geo[3]), static_cast<int>(C), static_cast<int>(geo[4]),
                          static_cast<int>(geo[5]), static_cast<int>(geo[6])};
   const int K = static_cast<int>(geo[4] * geo[4] * C);
-  const auto pl = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), K, pro, g, 0, static_cast<int>(epi));
+  const auto pl = psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), K, pro, g, static_cast<int>(src2),
+                                           static_cast<int>(epi));
   return {pl.bm, pl.bn, pl.gm};
 }
 
@@ -1778,7 +1781,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi") = 0, py::arg("z") = py::none(), py::arg("mc") = py::none(), py::arg("mean") = py::none(),
         py::arg("invstd") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("geo"), py::arg("pro") = py::none());
-  m.def("conv_gemm_plan", &conv_gemm_plan);
+  m.def("conv_gemm_plan", &conv_gemm_plan, py::arg("M"), py::arg("N"), py::arg("C"), py::arg("geo"),
+        py::arg("pro") = false, py::arg("epi") = 0, py::arg("src2") = 0);
   m.def("conv11_bwd_fused", &conv11_bwd_fused, py::arg("g"), py::arg("z3"), py::arg("cbwd"), py::arg("wt"), py::arg("z2"),
         py::arg("cf2") = py::none(), py::arg("mean2") = py::none(), py::arg("invstd2") = py::none());
   m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported, py::arg("ci"), py::arg("co"),

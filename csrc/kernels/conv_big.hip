@@ -59,6 +59,13 @@ template <int N>
 __device__ __forceinline__ void wait_lgkm() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 }
+// a global 16-B load the compiler does not track: mixed with LDS-DMA in flight, a plain load's use
+// makes hipcc wait vmcnt(0) (draining the DMA); callers count vmcnt themselves and tie() the result
+__device__ __forceinline__ f32x4 gld_f4(const float* ptr) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -83,10 +90,22 @@ __device__ __forceinline__ int bswz(int r, int c) {
   return BK == 64 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3);
 }
 
-template <int EPI, int BK>
+// PRO (conv_gemm's A prologues, applied by ONE in-place pass over each landed A stage):
+//   0 none; 1 relu(bf16(a sc + sh)) (the previous BN + ReLU); 2 the BN backward
+//   bf16(ca a + cb a2 + cc) from two row sources, the result also stored to aout (the weight
+//   gradient's operand) by the channel-tile-0 blocks; 3 the previous block's output
+//   relu(a sc + sh + r), r = a2 or a2 sc2 + sh2, stored to aout with its ReLU bits (abits).
+// The second row source a2 lands by LDS-DMA into one extra 32 KiB tile, refilled for stage kt + 1
+// once the pass over stage kt has read it.  With a 256-wide channel tile the A rows are staged
+// (and transformed) once per channel tile -- once in all for N = 256, and for wider N the other
+// channel tiles of the pixel tile run on the same XCD (L2 re-reads, not HBM).
+template <int EPI, int BK, int PRO>
 __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) {
   static_assert(EPI == 0 || EPI == 1 || EPI == 3, "plain / BN statistics / data-gradient mask + sums");
   static_assert(BK == 64 || BK == 32, "stage depth");
+  static_assert(PRO == 0 || BK == 64, "the prologue variants run the 2 x 64-deep ring");
+  static_assert(PRO != 2 || EPI == 3, "the BN-backward prologue is the data-gradient GEMM");
+  constexpr bool TWO = PRO == 2 || PRO == 3;
   constexpr int RB = 2 * BK;                    // bytes per stage row
   constexpr int A_BYTES = kTM * RB, STAGE = (kTM + kTN) * RB;
   constexpr int NST = kRing / STAGE;            // 2 (BK 64) or 4 (BK 32)
@@ -98,7 +117,9 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
   constexpr int KSTEPS = BK / 16;
   constexpr int OUT_BYTES = kTM * kCS * 2;
   constexpr int RED_OFF = OUT_BYTES > kRing ? OUT_BYTES : kRing;
-  constexpr int LDS_BYTES = RED_OFF + 2 * 8 * kTN * 4;
+  constexpr int Z_OFF = kRing;                                    // TWO: the a2 stage tile
+  constexpr int LDS_A = RED_OFF + 2 * 8 * kTN * 4, LDS_Z = TWO ? Z_OFF + A_BYTES : 0;
+  constexpr int LDS_BYTES = LDS_A > LDS_Z ? LDS_A : LDS_Z;
   static_assert(LDS_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const uint32_t L0 = lds_addr(lds);
@@ -139,6 +160,118 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     const int r = (wave * PB + i) * RPI + lrow;
     bsrc[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + bswz<BK>(r, lch) * 8;
   }
+  auto issue_z = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint16_t* src = ((aok >> i) & 1u) ? p.a2 + abase[i] + k0 : kBigZero;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + Z_OFF + (wave * PA + i) * 1024), 16, 0, 0);
+    }
+  };
+  // the prologue pass over stage kt's A tile (in place): thread t owns logical chunk t & 7 (fixed
+  // channels: one coefficient load per stage) of rows (t >> 3) + 64 i
+  // coefficients of the pass over stage kt (thread t: logical chunk t & 7): NCO untracked 16-B loads
+  // issued before the stage's DMA, waited for by vmcnt(GPS) behind it
+  constexpr int NCO = PRO == 1 ? 4 : PRO == 2 ? 6 : 8;
+  f32x4 co[NCO];
+  auto load_coef = [&](int kt) {
+    const int cc = kt * BK + (t & 7) * 8;
+    const float* src[4] = {p.pro, p.pro, p.pro, p.pro};
+    if constexpr (PRO == 2) {
+      src[0] = p.bwd;
+      src[1] = p.bwd + g.C;
+      src[2] = p.bwd + 2 * g.C;
+    } else {
+      src[0] = p.pro;
+      src[1] = p.pro + g.C;
+      if constexpr (PRO == 3) {
+        const bool dual = p.pro2 != nullptr;  // block-uniform; without it two dummy loads keep the count
+        src[2] = dual ? p.pro2 : p.pro;
+        src[3] = dual ? p.pro2 + g.C : p.pro;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NCO / 2; ++i) {
+      co[2 * i] = gld_f4(src[i] + cc);
+      co[2 * i + 1] = gld_f4(src[i] + cc + 4);
+    }
+  };
+  // the prologue pass over stage kt's A tile (in place): thread t owns logical chunk t & 7 (fixed
+  // channels) of rows (t >> 3) + 64 i
+  auto transform = [&](int kt, int buf) {
+    uint8_t* As = lds + buf * STAGE;
+    const uint8_t* Zs = lds + Z_OFF;
+    const int lc = t & 7, tr0 = t >> 3, cc = kt * BK + lc * 8;
+#pragma unroll
+    for (int i = 0; i < NCO; ++i) tie(co[i]);
+    float c0[8], c1[8], c2[8], c3[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c0[j] = co[0][j];
+      c0[j + 4] = co[1][j];
+      c1[j] = co[2][j];
+      c1[j + 4] = co[3][j];
+      if constexpr (NCO >= 6) {
+        c2[j] = co[4][j];
+        c2[j + 4] = co[5][j];
+      }
+      if constexpr (NCO >= 8) {
+        c3[j] = co[6][j];
+        c3[j + 4] = co[7][j];
+      }
+    }
+    const bool dual = PRO == 3 && p.pro2 != nullptr;
+    const bool store_a = (PRO == 2 || PRO == 3) && p.aout != nullptr && n0 == 0;
+    constexpr int NR = kTM / 64, HB = TWO ? 2 : NR;  // rows read together (register budget)
+#pragma unroll
+    for (int h = 0; h < NR; h += HB) {
+    u16x8 va[HB], za[HB];
+#pragma unroll
+    for (int i = 0; i < HB; ++i) {  // the rows' reads before any use (one LDS latency per group)
+      const int r = tr0 + 64 * (h + i), off = r * RB + bswz<BK>(r, lc) * 16;
+      va[i] = *reinterpret_cast<const u16x8*>(As + off);
+      if constexpr (TWO) za[i] = *reinterpret_cast<const u16x8*>(Zs + off);
+    }
+#pragma unroll
+    for (int i = 0; i < HB; ++i) {
+      const int r = tr0 + 64 * (h + i), m = m0 + r;
+      const int off = r * RB + bswz<BK>(r, lc) * 16;
+      u16x8 v = va[i];
+      unsigned ob = 0;
+      if constexpr (PRO == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = bf16_to_f32(v[j]) * c0[j] + c1[j];
+          v[j] = f32_to_bf16(o > 0.f ? o : 0.f);
+        }
+      } else if constexpr (PRO == 2) {
+        const u16x8 z8 = za[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = f32_to_bf16(c0[j] * bf16_to_f32(v[j]) + c1[j] * bf16_to_f32(z8[j]) + c2[j]);
+      } else if constexpr (PRO == 3) {  // the arithmetic of bn_apply_kernel / bn_apply_dual_kernel
+        const u16x8 z8 = za[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float o = bf16_to_f32(v[j]) * c0[j] + c1[j];
+          if (dual) o = o + (bf16_to_f32(z8[j]) * c2[j] + c3[j]);
+          else o += bf16_to_f32(z8[j]);
+          o = o > 0.f ? o : 0.f;
+          ob |= (o > 0.f ? 1u : 0u) << j;
+          v[j] = f32_to_bf16(o);
+        }
+      }
+      const bool ok = m < p.M;
+      if (!ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<u16x8*>(As + off) = v;
+      if (store_a && ok) {
+        const int64_t e = static_cast<int64_t>(m) * g.C + cc;
+        *reinterpret_cast<u16x8*>(p.aout + e) = v;
+        if constexpr (PRO == 3) p.abits[e >> 3] = static_cast<uint8_t>(ob);
+      }
+    }
+    }
+  };
   auto issue = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
@@ -197,12 +330,46 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     __builtin_amdgcn_s_setprio(0);
   };
 
+  if constexpr (PRO != 0) {
+    // stage kt + 1 (and a2 of kt + 1 once the pass over kt has read the a2 tile) in flight behind
+    // stage kt's pass and MFMAs; the pass's aout stores drain with them
+    issue(0, 0);
+    if constexpr (TWO) issue_z(0);
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_vm<0>();
+      lds_bar();  // stage kt (and its a2 tile) landed; every wave is done with stage kt - 1
+      load_coef(kt);
+      if (kt + 1 < nk) {
+        issue(kt + 1, (kt + 1) & 1);
+        wait_vm<GPS>();  // the coefficients (older than the stage's GPS DMAs)
+      } else {
+        wait_vm<0>();
+      }
+      transform(kt, kt & 1);
+      lds_bar();  // the A tile is transformed and the a2 tile is free
+      if constexpr (TWO) {
+        if (kt + 1 < nk) issue_z(kt + 1);
+      }
+      const uint32_t sb = L0 + static_cast<uint32_t>((kt & 1) * STAGE);
+      fetch(sb, 0, 0);
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        if (s + 1 < KSTEPS) {
+          fetch(sb, s + 1, (s + 1) & 1);
+          wait_lgkm<6>();
+        } else {
+          wait_lgkm<0>();
+        }
+        mfma_set(s & 1);
+      }
+    }
+  }
   // ---- prologue: stages 0 .. NST - 2 in flight
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) {
-    if (s < nk) issue(s, s);
+    if (PRO == 0 && s < nk) issue(s, s);
   }
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < (PRO == 0 ? nk : 0); ++kt) {
     // stage kt landed (this wave's DMAs): younger are the min(NST - 2, nk - 1 - kt) stages after it
     const int younger = min(NST - 2, nk - 1 - kt);
     if (younger >= 2) wait_vm<2 * GPS>();
@@ -343,10 +510,20 @@ bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int 
     const char* e = std::getenv("PS_AMD_CONV_BIG");
     return e == nullptr || e[0] != '0';
   }();
-  if (!on || src2 != 0 || pro || g.RH != 0) return false;
+  static const bool pro_on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_BIG_PRO");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (!on || g.RH != 0) return false;
   if (g.ks != 1 || g.ksw > 1 || g.pad != 0) return false;
   if (N % kTN != 0 || K % 64 != 0 || K < 256 || g.C != K) return false;
   if (!(epi == 0 || epi == 1 || epi == 3)) return false;
+  // prologues (PRO 1: pro, src2 0; PRO 3: src2 1; PRO 2: src2 2 + epi 3): stride 1 only
+  if (pro || src2 != 0) {
+    if (!pro_on || g.stride != 1) return false;
+    if (src2 == 2 && epi != 3) return false;
+    if (src2 == 1 && epi == 3) return false;
+  }
   // one block per CU: below ~4 rounds of blocks the last round's idle CUs and the per-tile
   // prologue / epilogue outweigh the faster K loop unless K is deep (profiles/r5_conv_big_probe.txt:
   // at batch 256 the K = 256 / 512 shapes with 784 blocks ran 2-15 % slower, K >= 1024 faster)
@@ -358,15 +535,24 @@ int conv_big_gm(int M) { return (M + kTM - 1) / kTM; }
 
 void launch_conv_big(const ConvGemmArgs& a, hipStream_t s) {
   const int nblk = conv_big_gm(a.M) * (a.N / kTN);
-#define PSAMD_BIG(E, BK) hipLaunchKernelGGL((conv_big_kernel<E, BK>), dim3(nblk), dim3(512), 0, s, a)
-  if (big_bk() == 32) {
-    if (a.epi == 1) PSAMD_BIG(1, 32);
-    else if (a.epi == 3) PSAMD_BIG(3, 32);
-    else PSAMD_BIG(0, 32);
+  const bool bwd = a.bwd != nullptr, resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
+#define PSAMD_BIG(E, BK, P) hipLaunchKernelGGL((conv_big_kernel<E, BK, P>), dim3(nblk), dim3(512), 0, s, a)
+  if (bwd) {
+    PSAMD_BIG(3, 64, 2);
+  } else if (resp) {
+    if (a.epi == 1) PSAMD_BIG(1, 64, 3);
+    else PSAMD_BIG(0, 64, 3);
+  } else if (a.pro != nullptr) {
+    if (a.epi == 1) PSAMD_BIG(1, 64, 1);
+    else PSAMD_BIG(0, 64, 1);
+  } else if (big_bk() == 32) {
+    if (a.epi == 1) PSAMD_BIG(1, 32, 0);
+    else if (a.epi == 3) PSAMD_BIG(3, 32, 0);
+    else PSAMD_BIG(0, 32, 0);
   } else {
-    if (a.epi == 1) PSAMD_BIG(1, 64);
-    else if (a.epi == 3) PSAMD_BIG(3, 64);
-    else PSAMD_BIG(0, 64);
+    if (a.epi == 1) PSAMD_BIG(1, 64, 0);
+    else if (a.epi == 3) PSAMD_BIG(3, 64, 0);
+    else PSAMD_BIG(0, 64, 0);
   }
 #undef PSAMD_BIG
 }

@@ -114,8 +114,12 @@ class ResNet(nn.Module):
                 # a block followed by a fused block leaves its output to that block's conv1 prologue
                 # where that pays (ops/convgemm.py resp_consumer_ok)
                 on = os.environ.get("PS_AMD_RESP", "1") != "0"
+                h, w = x.shape[2], x.shape[3]
                 for a, b in zip(blks, blks[1:] + [None]):
-                    a._defer_out = on and b is not None and b.fuse_block and resp_consumer_ok(b)
+                    s = a.conv2.stride[0]
+                    h, w = (h - 1) // s + 1, (w - 1) // s + 1  # a's output map = b's input map
+                    a._defer_out = (on and b is not None and b.fuse_block
+                                    and resp_consumer_ok(b, x.shape[0] * h * w))
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.fused_bn:
             x = global_avg_pool(x)  # NHWC gradient straight into the last block's backward

@@ -222,13 +222,23 @@ def twosrc_glds_min_nk() -> int:
     return int(os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4"))
 
 
-def resp_consumer_ok(blk: nn.Module) -> bool:
+def big_tile(m: int, n: int, k: int, src2: int = 0, epi: int = 1, pro: bool = False) -> bool:
+    """Whether conv_gemm runs this 1x1 stride-1 GEMM ([m, k] x [k, n]) on the 256 x 256 tiles of
+    csrc/kernels/conv_big.hip (src2: 1 the block-output prologue, 2 the BN-backward prologue):
+    there a prologue stages and transforms the A rows once per 256-channel tile, and the tiles of
+    one pixel tile share an XCD, so the re-read that limits the 128-wide tiles to N <= 128 is gone."""
+    return tuple(native().conv_gemm_plan(m, n, k, [m, 1, m, 1, 1, 1, 0], pro, epi, src2)[:2]) == (256, 256)
+
+
+def resp_consumer_ok(blk: nn.Module, m: int = 0) -> bool:
     """Whether the block-output prologue pays on ``blk``'s conv1: with one channel tile (N <= 128,
     _twosrc_max_n) -- the layer-1 and layer-2 blocks and the layer-1 -> 2 boundary (LDS-DMA
     variant: 1.01 vs 1.21 ms at 256 -> 64 channels, 0.53 vs 0.62 ms at 512 -> 128); with two or
     more tiles each re-reads both sources and the apply pass + plain GEMM is faster
     (profiles/r4_twosrc_probe.txt)."""
     c1 = blk.conv1
+    if m > 0 and big_tile(m, c1.out_channels, c1.in_channels, src2=1):  # m: the consumer's input pixels
+        return True
     return c1.out_channels <= _twosrc_max_n() and (
         c1.in_channels >= 64 * twosrc_glds_min_nk() or c1.out_channels <= 64)
 
@@ -378,7 +388,8 @@ class _BottleneckFn(torch.autograd.Function):
                 ds_part = lk.part[0::2]  # sum(g), sum(g * xhat_d): a strided view, no copy
                 lk.part = lk.part[:2]
                 FOLD_STATS["ds"] += 1
-            if _bwd_prologue_enabled(z3.shape[1], w3.shape[1]):
+            if (_bwd_prologue_enabled(z3.shape[1], w3.shape[1])
+                    or big_tile(d2.shape[0], w3.shape[1], z3.shape[1], src2=2, epi=3)):
                 # bn3's backward runs in the conv3 data-grad prologue, which also stores dz3 for
                 # the weight gradient: no separate apply pass over the widest tensors
                 dg3, db3, cb3 = nat.bn_bwd_coef(lk.part, g3, m3, i3, d2.shape[0])
