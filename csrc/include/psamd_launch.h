@@ -376,6 +376,8 @@ ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, i
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 // the planar resident-weight 3x3 64 -> 64 kernel (conv3x3_c64.hip): epi 1 / 3, gm = the plan's blocks
 void launch_conv3x3_c64s(const ConvGemmArgs& a, int gm, hipStream_t s);
+// mode 3: the 64 x 576 weight held in registers by every wave (PS_AMD_CONV_C64=3)
+void launch_conv3x3_c64r(const ConvGemmArgs& a, int gm, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s);

@@ -29,6 +29,7 @@ namespace psamd {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8_c64 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(1))) const void gptr_t;
 typedef __attribute__((address_space(3))) void lptr_t;
 typedef __attribute__((address_space(3))) const char lds_char;
@@ -278,7 +279,219 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64s_kernel(const ConvGemmArgs
   }
 }
 
+
+// Mode 3: the weight in REGISTERS.  Every wave holds the whole 64 x 576 weight as MFMA A fragments
+// (36 k-steps x 2 output-channel blocks x 16 B = 288 VGPRs, one wave per SIMD) and owns 32 pixels x
+// all 64 channels of the tile, so a k-step is ONE ds_read_b128 of the patch for two MFMAs (0.5
+// LDS reads per MFMA, against 1.5 with the weight in LDS: there the LDS array was ~75 % busy
+// beside the MFMAs).  The LDS holds only the two patch slots and the epilogue parameters.
+template <int W, int EPI, int LA, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void conv3x3_c64r_kernel(const ConvGemmArgs p) {
+  // DBG (timing probes only): 1 = no MFMAs (data movement + epilogue), 2 = no patch DMA (compute
+  // on whatever the slots hold), 3 = no epilogue stores
+  static_assert(EPI == 1 || EPI == 3, "forward statistics or data-gradient mask + sums");
+  constexpr int C = 64, N = 64, RT = 2, TP = RT * W;
+  constexpr int PW = W + 2, PR = RT + 2, NSL = PR * PW;
+  constexpr int PLS = (NSL + 63) / 64 * 64;
+  constexpr int PLB = PLS * 16;
+  constexpr int SLOT = 8 * PLB;
+  constexpr int PPW = (8 * PLS / 64) / 4;
+  constexpr int PAR_OFF = 2 * SLOT;                    // [64 ch][4] floats: e0..e3 per channel
+  constexpr int RED_OFF = PAR_OFF + N * 4 * 4;
+  constexpr int LDS_BYTES = RED_OFF + 2 * 4 * N * 4;
+  static_assert((8 * PLS / 64) % 4 == 0, "pieces over 4 waves");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static_assert(TP <= 128, "four 32-pixel waves per tile");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const uint32_t L0 = lds_addr(lds);
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int GM = gridDim.x, mg = blockIdx.x;
+  const int tpi = g.OH / RT, ntiles = (p.M / (g.OH * W)) * tpi;
+  const int my_tiles = mg < ntiles ? (ntiles - mg + GM - 1) / GM : 0;
+
+  auto issue_patch = [&](int mt, bool real, int sl) {
+    const int img = mt / tpi, oh0 = (mt - img * tpi) * RT;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i, pl = pc / (PLS / 64), sq = (pc - pl * (PLS / 64)) * 64 + lane;
+      const int pr = sq / PW, pcol = sq - pr * PW, ih = oh0 - 1 + pr, iw = pcol - 1;
+      const bool ok = real && sq < NSL && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const uint16_t* src =
+          ok ? p.a + ((static_cast<int64_t>(img) * g.H + ih) * W + iw) * C + pl * 8 : kZeroPatch;
+      if constexpr (DBG == 2) src = kZeroPatch;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + sl * SLOT + pc * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- epilogue parameters -> LDS [c][4]
+  for (int c = t; c < N; c += 256) {
+    float* pr = reinterpret_cast<float*>(lds + PAR_OFF) + c * 4;
+    if constexpr (EPI == 1) {
+      pr[0] = p.kshift ? p.kshift[c] : 0.f;
+      pr[1] = pr[2] = pr[3] = 0.f;
+    } else {
+      pr[0] = p.mc[c];
+      pr[1] = p.mc[N + c];
+      pr[2] = p.mean[c];
+      pr[3] = p.invstd[c];
+    }
+  }
+  // ---- the weight as A fragments: k-step st = tap (st >> 2), channels 16 (st & 3) + 8 fh + j
+  bf16x8_t wr[36][2];
+#pragma unroll
+  for (int st = 0; st < 36; ++st)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wr[st][i] = *reinterpret_cast<const bf16x8_t*>(p.b + static_cast<int64_t>(32 * i + fr) * p.K + (st >> 2) * C +
+                                                      16 * (st & 3) + 8 * fh);
+  // ---- this lane's pixel: 32 wave + fr of the tile
+  const int px = 32 * wave + fr;
+  const bool pvalid = px < TP;
+  const uint32_t bbase = static_cast<uint32_t>(fh * PLB + (pvalid ? (px / W) * PW + (px % W) : 0) * 16);
+  float s1[32], s2[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) s1[i] = s2[i] = 0.f;
+
+  if (my_tiles > 0) issue_patch(mg, true, 0);
+  issue_patch(my_tiles > 1 ? mg + GM : mg, my_tiles > 1, 1);
+  wait_vm<PPW>();
+  __syncthreads();  // (the weight loads are plain loads: drained here with everything else once)
+
+  f32x16 acc[2];
+  for (int ti = 0, mt = mg; ti < my_tiles; ++ti, mt += GM) {
+    const int sl = ti & 1;
+    const int m0 = mt * TP;
+    u16x4 zr[2][4];  // EPI 3: the BN input at this lane's pixel, 4 channels per (block, q4)
+    if constexpr (EPI == 3) {
+      const int m = min(m0 + (pvalid ? px : 0), p.M - 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4)
+          zr[i][q4] = *reinterpret_cast<const u16x4*>(p.aux + static_cast<int64_t>(m) * N + 32 * i + 8 * q4 + 4 * fh);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+    const uint32_t pb = L0 + static_cast<uint32_t>(sl * SLOT) + bbase;
+    constexpr int NB = LA + 1;
+    bf16x8_t xb[NB];
+    auto fetch = [&](int st, int buf) {
+      const int tap = st >> 2, ks = st & 3, kh = tap / 3, kw = tap - kh * 3;
+      xb[buf] = ld_b128(pb + static_cast<uint32_t>(2 * ks * PLB + (kh * PW + kw) * 16));
+    };
+#pragma unroll
+    for (int st = 0; st < LA; ++st) fetch(st, st);
+#pragma unroll
+    for (int st = 0; st < 36; ++st) {
+      const int cur = st % NB;
+      if (st + LA < 36) {
+        fetch(st + LA, (st + LA) % NB);
+        wait_lgkm<LA>();
+      } else if (st + 2 == 36 && LA >= 2) {
+        wait_lgkm<1>();
+      } else {
+        wait_lgkm<0>();
+      }
+      tie(xb[cur]);
+      if constexpr (DBG != 1) {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[st][0], xb[cur], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[st][1], xb[cur], acc[1], 0, 0, 0);
+      } else {
+        acc[0][0] += static_cast<float>(__builtin_bit_cast(s16x8_c64, xb[cur])[0]);
+      }
+    }
+    lds_bar();  // every wave is done with patch slot sl
+    const bool more2 = ti + 2 < my_tiles;
+    issue_patch(more2 ? mt + 2 * GM : mg, more2, sl);
+    // ---- epilogue from the accumulators: register q of block i = channel 32 i + 8 (q >> 2) + 4 fh +
+    // (q & 3) of this lane's pixel; 8 stores of 4 channels, always issued (sink past the tile)
+    const int m = m0 + px;
+    const bool ok = pvalid && m < p.M;
+    const float* par = reinterpret_cast<const float*>(lds + PAR_OFF);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int c0 = 32 * i + 8 * q4 + 4 * fh;
+        u16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f32_to_bf16(acc[i][4 * q4 + e]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x4 pe = *reinterpret_cast<const f32x4*>(par + (c0 + e) * 4);
+          const int si = 16 * i + 4 * q4 + e;
+          if constexpr (EPI == 1) {
+            const float d = ok ? bf16_to_f32(v[e]) - pe[0] : 0.f;
+            s1[si] += d;
+            s2[si] += d * d;
+          } else {
+            const float z = bf16_to_f32(zr[i][q4][e]);
+            const bool on = ok && z * pe[0] + pe[1] > 0.f;
+            const float gv = on ? bf16_to_f32(v[e]) : 0.f;
+            s1[si] += gv;
+            s2[si] += gv * ((z - pe[2]) * pe[3]);
+            if (!on) v[e] = 0;
+          }
+        }
+        uint16_t* dst = ok && DBG != 3 ? p.c + static_cast<int64_t>(m) * N + c0 : kStoreSink + (lane & 63) * 4;
+        *reinterpret_cast<u16x4*>(dst) = v;
+      }
+    wait_vm<PPW + 8>();  // patch ti + 1 landed; younger: patch ti + 2 (PPW) + the 8 stores
+    lds_bar();
+  }
+  wait_vm<0>();
+  lds_bar();
+  // ---- statistics: over the 32 pixel lanes of each half, then the 4 pixel waves (fixed order)
+#pragma unroll
+  for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      s1[i] += __shfl_xor(s1[i], off, 64);
+      s2[i] += __shfl_xor(s2[i], off, 64);
+    }
+  float* red = reinterpret_cast<float*>(lds + RED_OFF);  // [2 stats][4 waves][N]
+  if (fr == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 32 * i + 8 * q4 + 4 * fh + e, si = 16 * i + 4 * q4 + e;
+          red[wave * N + c] = s1[si];
+          red[(4 + wave) * N + c] = s2[si];
+        }
+  }
+  __syncthreads();
+  if (t < N) {
+    p.part[static_cast<int64_t>(mg) * N + t] = (red[t] + red[N + t]) + (red[2 * N + t] + red[3 * N + t]);
+    p.part[(static_cast<int64_t>(GM) + mg) * N + t] =
+        (red[4 * N + t] + red[5 * N + t]) + (red[6 * N + t] + red[7 * N + t]);
+  }
+}
+
 }  // namespace
+
+void launch_conv3x3_c64r(const ConvGemmArgs& a, int gm, hipStream_t s) {
+  static const int dbg = [] {
+    const char* e = std::getenv("PS_AMD_C64R_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (a.epi == 1) {
+    if (dbg == 1) hipLaunchKernelGGL((conv3x3_c64r_kernel<56, 1, 3, 1>), dim3(gm), dim3(256), 0, s, a);
+    else if (dbg == 2) hipLaunchKernelGGL((conv3x3_c64r_kernel<56, 1, 3, 2>), dim3(gm), dim3(256), 0, s, a);
+    else if (dbg == 3) hipLaunchKernelGGL((conv3x3_c64r_kernel<56, 1, 3, 3>), dim3(gm), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_c64r_kernel<56, 1, 3>), dim3(gm), dim3(256), 0, s, a);
+  } else if (a.epi == 3) {
+    hipLaunchKernelGGL((conv3x3_c64r_kernel<56, 3, 3>), dim3(gm), dim3(256), 0, s, a);
+  }
+}
 
 void launch_conv3x3_c64s(const ConvGemmArgs& a, int gm, hipStream_t s) {
   static const int la = [] {

@@ -2181,6 +2181,10 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
       launch_conv3x3_c64s(a, GM, s);
       return;
     }
+    if (c64_mode() == 3 && (a.epi == 1 || a.epi == 3)) {
+      launch_conv3x3_c64r(a, GM, s);
+      return;
+    }
     if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 1>), dim3(GM), dim3(256), 0, s, a);
     else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 3>), dim3(GM), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv3x3_c64_kernel<56, 0>), dim3(GM), dim3(256), 0, s, a);

@@ -229,6 +229,13 @@ class ColocatedPS:
         self.tpull = self.t.split() if self.split_comm else self.t
         self.comm_pull = torch.cuda.Stream(device=self.device) if (self.gpu and self.split_comm) else self.comm
         self.round_events: deque = deque()
+        # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT: finish_step waits on the host until the
+        # step max_inflight - 1 steps back is done (0 = unbounded, the default).  A host that issues
+        # a ResNet-50 step in ~9.5 ms runs ahead of an 18 ms GPU step (bs256) until a queue blocks
+        # it for 20+ ms (scripts/probe_host_block.py); bounding it at 2 measured the same
+        # (profiles/r5_run_ahead_ab.txt), so it stays a knob.
+        self.max_inflight = int(_os.environ.get("PS_AMD_MAX_INFLIGHT", "0"))
+        self._host_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
         # fault injection (PS_AMD_FAULT / HIPPS_FAULT): kill at a step, delay pushes
         from ..utils.fault import FaultInjector
@@ -538,8 +545,18 @@ class ColocatedPS:
         self.pending = [len(b.keys) for b in self.reg.buckets]
         self.launched = [False] * len(self.reg.buckets)
         self._bind(self.wslot, self.gslot)
+        self._bound_run_ahead()
         if self.timing:
             self._close_timing_deferred()
+
+    def _bound_run_ahead(self) -> None:
+        if not self.gpu or self.max_inflight <= 0 or torch.cuda.is_current_stream_capturing():
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._host_events.append(ev)
+        while len(self._host_events) >= self.max_inflight:
+            self._host_events.popleft().synchronize()
 
     def _finish_plane_round(self) -> None:
         """Round bookkeeping of the xGMI plane: the engine runs serve / pull on its own streams;
@@ -557,6 +574,7 @@ class ColocatedPS:
         self.pending = [len(b.keys) for b in self.reg.buckets]
         self.launched = [False] * len(self.reg.buckets)
         self._bind(self.wslot, self.gslot)
+        self._bound_run_ahead()
         if self.timing:
             self._close_timing_deferred()
 
