@@ -378,6 +378,8 @@ void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
 void launch_conv3x3_c64s(const ConvGemmArgs& a, int gm, hipStream_t s);
 // mode 3: the 64 x 576 weight held in registers by every wave (PS_AMD_CONV_C64=3)
 void launch_conv3x3_c64r(const ConvGemmArgs& a, int gm, hipStream_t s);
+// mode 4: the weight in registers + a rolling 8-row window over contiguous 2-row tiles (PS_AMD_CONV_C64=4)
+void launch_conv3x3_c64v(const ConvGemmArgs& a, int gm, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s);

@@ -47,6 +47,11 @@ __device__ __forceinline__ bf16x8_t ld_b128(uint32_t a) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
+__device__ __forceinline__ f32x4 ld_f4c(uint32_t a) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
 __device__ __forceinline__ void st_b128(uint32_t a, bf16x8_t v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
@@ -476,7 +481,279 @@ __global__ __launch_bounds__(256, 1) void conv3x3_c64r_kernel(const ConvGemmArgs
   }
 }
 
+
+// Mode 4: the weight in registers (as mode 3) and a ROLLING row window: a block owns a contiguous
+// run of 2-row tiles (whole images top to bottom at ResNet batch sizes), so tile t + 1 shares
+// two of its four input rows with tile t and only two new rows are loaded -- the input is read
+// once instead of twice (the 2-row tiles of modes 0-3 re-read two halo rows per two output rows),
+// and the DMA per tile halves.  LDS: 8 ring row slots + 1 scratch slot per 16-B channel plane,
+// each a 64-slot (1 KiB) row: [plane][slot][64 columns] x 16 B.  A new image loads four rows (the
+// zero row above it included); a continuing one loads two and sends two dummy loads to the
+// scratch slot, so every wave issues the same number of DMAs per tile (counted vmcnt).
+template <int W, int EPI, int LA>
+__global__ __launch_bounds__(256, 1) void conv3x3_c64v_kernel(const ConvGemmArgs p) {
+  static_assert(EPI == 1 || EPI == 3, "forward statistics or data-gradient mask + sums");
+  constexpr int C = 64, N = 64, RT = 2, TP = RT * W;
+  static_assert(W + 2 <= 64 && TP <= 128, "one 64-column slot row; four 32-pixel waves per tile");
+  constexpr int NSLOT = 9, SCRATCH = 8;                // 8 ring slots + scratch
+  constexpr int PLANE = NSLOT * 1024;                  // bytes per channel plane
+  constexpr int PATCH = 8 * PLANE;
+  constexpr int PPW = 8;                               // DMA instructions per wave per tile
+  constexpr int PAR_OFF = PATCH;                       // [4][64] floats
+  constexpr int PAR4_OFF = PAR_OFF + N * 4 * 4;        // [64][4] floats (EPI 3)
+  constexpr int RED_OFF = PAR4_OFF + N * 4 * 4;
+  constexpr int LDS_BYTES = RED_OFF + 2 * 4 * N * 4;
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const uint32_t L0 = lds_addr(lds);
+
+  const ConvGeo& g = p.g;
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int GM = gridDim.x, mg = blockIdx.x;
+  const int tpi = g.OH / RT, ntiles = (p.M / (g.OH * W)) * tpi;
+  const int per = (ntiles + GM - 1) / GM;
+  const int t0 = mg * per, t1 = min(ntiles, t0 + per);
+  const int my_tiles = t1 > t0 ? t1 - t0 : 0;  // block-uniform
+
+  // rows of the tile loaded for tile index q (block-relative): returns the 4 slots of its rows
+  // through the running virtual row counter vrow (slot = vrow % 8)
+  int vrow = 0;
+  // load rows [ih0, ih0 + nrow) of image img into the next ring slots; pieces: plane x row, one
+  // 64-lane DMA each (columns -1 .. 62 of the row; zero outside the map); always PPW per wave
+  auto issue_rows = [&](int img, int ih0, int nrow, int vbase) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave * PPW + i;          // 0 .. 31: (row j, plane pl)
+      const int j = pc >> 3, pl = pc & 7;
+      const bool real = j < nrow;
+      const int ih = ih0 + j, iw = lane - 1;
+      const bool ok = real && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const uint16_t* src = ok ? p.a + ((static_cast<int64_t>(img) * g.H + ih) * W + iw) * C + pl * 8 : kZeroPatch;
+      const int slot = real ? ((vbase + j) & 7) : SCRATCH;
+      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + pl * PLANE + slot * 1024), 16, 0, 0);
+    }
+  };
+  // tile q's (image, first output row)
+  auto tile_pos = [&](int q, int& img, int& oh0) {
+    const int mt = t0 + q;
+    img = mt / tpi;
+    oh0 = (mt - img * tpi) * RT;
+  };
+
+  // epilogue parameters as [4][64] floats (4 consecutive channels of one parameter = one b128 read)
+  for (int c = t; c < N; c += 256) {
+    float* pr = reinterpret_cast<float*>(lds + PAR_OFF);
+    if constexpr (EPI == 1) {
+      pr[c] = p.kshift ? p.kshift[c] : 0.f;
+      pr[N + c] = pr[2 * N + c] = pr[3 * N + c] = 0.f;
+    } else {
+      pr[c] = p.mc[c];
+      pr[N + c] = p.mc[N + c];
+      pr[2 * N + c] = p.mean[c];
+      pr[3 * N + c] = p.invstd[c];
+      float* p4 = reinterpret_cast<float*>(lds + PAR4_OFF) + c * 4;
+      p4[0] = p.mc[c];
+      p4[1] = p.mc[N + c];
+      p4[2] = p.mean[c];
+      p4[3] = p.invstd[c];
+    }
+  }
+  bf16x8_t wr[36][2];
+#pragma unroll
+  for (int st = 0; st < 36; ++st)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wr[st][i] = *reinterpret_cast<const bf16x8_t*>(p.b + static_cast<int64_t>(32 * i + fr) * p.K + (st >> 2) * C +
+                                                      16 * (st & 3) + 8 * fh);
+  const int px = 32 * wave + fr;
+  const bool pvalid = px < TP;
+  const int prow = pvalid ? px / W : 0, pcol = pvalid ? px % W : 0;
+  float s1[32], s2[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) s1[i] = s2[i] = 0.f;
+
+  // ---- the rows of tile 0 (a new image: four rows), then those of tile 1 in flight
+  int slots[4] = {0, 1, 2, 3};   // this tile's four input rows -> ring slots (block-uniform)
+  int nslots[4] = {0, 0, 0, 0};  // the next tile's
+  int img = 0, oh0 = 0;
+  if (my_tiles > 0) {
+    tile_pos(0, img, oh0);
+    issue_rows(img, oh0 - 1, 4, vrow);
+    vrow += 4;
+  } else {
+    issue_rows(0, 0, 0, 0);
+  }
+  auto plan_next = [&](int q) {  // issue tile q's new rows (q < my_tiles) and fill nslots
+    if (q < my_tiles) {
+      int nimg, noh0;
+      tile_pos(q, nimg, noh0);
+      if (nimg == img && noh0 == oh0 + RT) {  // continuing: rows noh0 + 1, noh0 + 2 are new
+        issue_rows(nimg, noh0 + 1, 2, vrow);
+        nslots[0] = slots[2];
+        nslots[1] = slots[3];
+        nslots[2] = vrow & 7;
+        nslots[3] = (vrow + 1) & 7;
+        vrow += 2;
+      } else {  // a new image (or a jump): four rows
+        issue_rows(nimg, noh0 - 1, 4, vrow);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nslots[j] = (vrow + j) & 7;
+        vrow += 4;
+      }
+    } else {
+      issue_rows(0, 0, 0, 0);  // the count stays uniform
+    }
+  };
+  plan_next(1);
+  wait_vm<PPW>();
+  __syncthreads();
+
+  f32x16 acc[2];
+  for (int ti = 0; ti < my_tiles; ++ti) {
+    const int m0 = (t0 + ti) * TP;
+    u16x4 zr[2][4];
+    if constexpr (EPI == 3) {
+      const int m = min(m0 + (pvalid ? px : 0), p.M - 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4)
+          zr[i][q4] = *reinterpret_cast<const u16x4*>(p.aux + static_cast<int64_t>(m) * N + 32 * i + 8 * q4 + 4 * fh);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+    // per-lane bases of the three kernel rows: slot of input row prow + kh, column pcol (tap kw
+    // and the plane are immediate offsets)
+    uint32_t kb[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int sl = prow ? slots[kh + 1] : slots[kh];
+      kb[kh] = L0 + static_cast<uint32_t>(fh * PLANE + sl * 1024 + pcol * 16);
+    }
+    constexpr int NB = LA + 1;
+    bf16x8_t xb[NB];
+    auto fetch = [&](int st, int buf) {
+      const int tap = st >> 2, ks = st & 3, kh = tap / 3, kw = tap - kh * 3;
+      xb[buf] = ld_b128(kb[kh] + static_cast<uint32_t>(2 * ks * PLANE + kw * 16));
+    };
+#pragma unroll
+    for (int st = 0; st < LA; ++st) fetch(st, st);
+#pragma unroll
+    for (int st = 0; st < 36; ++st) {
+      const int cur = st % NB;
+      if (st + LA < 36) {
+        fetch(st + LA, (st + LA) % NB);
+        wait_lgkm<LA>();
+      } else if (st + 2 == 36 && LA >= 2) {
+        wait_lgkm<1>();
+      } else {
+        wait_lgkm<0>();
+      }
+      tie(xb[cur]);
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[st][0], xb[cur], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wr[st][1], xb[cur], acc[1], 0, 0, 0);
+    }
+    lds_bar();  // every wave is done with this tile's rows
+    // the tile after next: its new rows go to slots no tile in flight uses
+    {
+      int cimg, coh0;
+      tile_pos(ti + 1, cimg, coh0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slots[j] = nslots[j];
+      img = cimg;
+      oh0 = coh0;
+      plan_next(ti + 2);
+    }
+    const int m = m0 + px;
+    const bool ok = pvalid && m < p.M;
+    const uint32_t parl = L0 + PAR_OFF + static_cast<uint32_t>(4 * fh * 4);  // + (32 i + 8 q4) * 4
+    const float* par4 = reinterpret_cast<const float*>(lds + PAR4_OFF);        // EPI 3: [c][4]
+    // EPI 1: the 8 groups' shifts in one batch of LDS reads (one wait, not one per value)
+    f32x4 sh1[2][4];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) sh1[i][q4] = ld_f4c(parl + static_cast<uint32_t>((32 * i + 8 * q4) * 4));
+      wait_lgkm<0>();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int c0 = 32 * i + 8 * q4 + 4 * fh;
+        u16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f32_to_bf16(acc[i][4 * q4 + e]);
+        if constexpr (EPI == 1) {
+          const f32x4 pa = sh1[i][q4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int si = 16 * i + 4 * q4 + e;
+            const float d = ok ? bf16_to_f32(v[e]) - pa[e] : 0.f;
+            s1[si] += d;
+            s2[si] += d * d;
+          }
+        } else {  // per channel: [c][4] = mc scale, mc shift, mean, invstd (register budget: one
+                  // channel's four at a time)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x4 pe = *reinterpret_cast<const f32x4*>(par4 + (c0 + e) * 4);
+            const int si = 16 * i + 4 * q4 + e;
+            const float z = bf16_to_f32(zr[i][q4][e]);
+            const bool on = ok && z * pe[0] + pe[1] > 0.f;
+            const float gv = on ? bf16_to_f32(v[e]) : 0.f;
+            s1[si] += gv;
+            s2[si] += gv * ((z - pe[2]) * pe[3]);
+            if (!on) v[e] = 0;
+          }
+        }
+        uint16_t* dst = ok ? p.c + static_cast<int64_t>(m) * N + c0 : kStoreSink + (lane & 63) * 4;
+        *reinterpret_cast<u16x4*>(dst) = v;
+      }
+    wait_vm<PPW + 8>();  // tile ti + 1's rows landed; younger: tile ti + 2's (PPW) + the 8 stores
+    lds_bar();
+  }
+  wait_vm<0>();
+  lds_bar();
+#pragma unroll
+  for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      s1[i] += __shfl_xor(s1[i], off, 64);
+      s2[i] += __shfl_xor(s2[i], off, 64);
+    }
+  float* red = reinterpret_cast<float*>(lds + RED_OFF);
+  if (fr == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 32 * i + 8 * q4 + 4 * fh + e, si = 16 * i + 4 * q4 + e;
+          red[wave * N + c] = s1[si];
+          red[(4 + wave) * N + c] = s2[si];
+        }
+  }
+  __syncthreads();
+  if (t < N) {
+    p.part[static_cast<int64_t>(mg) * N + t] = (red[t] + red[N + t]) + (red[2 * N + t] + red[3 * N + t]);
+    p.part[(static_cast<int64_t>(GM) + mg) * N + t] =
+        (red[4 * N + t] + red[5 * N + t]) + (red[6 * N + t] + red[7 * N + t]);
+  }
+}
+
 }  // namespace
+
+void launch_conv3x3_c64v(const ConvGemmArgs& a, int gm, hipStream_t s) {
+  if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64v_kernel<56, 1, 3>), dim3(gm), dim3(256), 0, s, a);
+  else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64v_kernel<56, 3, 3>), dim3(gm), dim3(256), 0, s, a);
+}
 
 void launch_conv3x3_c64r(const ConvGemmArgs& a, int gm, hipStream_t s) {
   static const int dbg = [] {

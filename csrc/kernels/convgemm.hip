@@ -2185,6 +2185,10 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
       launch_conv3x3_c64r(a, GM, s);
       return;
     }
+    if (c64_mode() == 4 && (a.epi == 1 || a.epi == 3)) {
+      launch_conv3x3_c64v(a, GM, s);
+      return;
+    }
     if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 1>), dim3(GM), dim3(256), 0, s, a);
     else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 3>), dim3(GM), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv3x3_c64_kernel<56, 0>), dim3(GM), dim3(256), 0, s, a);

@@ -598,14 +598,16 @@ def test_weight_prep_matches_reference_layouts(monkeypatch):
         assert torch.equal(grads["1"][n], gr), n
 
 
-@pytest.mark.parametrize("n,hw,cin,cout", [(2, 56, 64, 64), (10, 56, 64, 64), (3, 28, 128, 128), (2, 14, 256, 256),
-                                           (2, 28, 64, 128)])
+@pytest.mark.parametrize("n,hw,cin,cout", [(2, 56, 64, 64), (10, 56, 64, 64), (20, 56, 64, 64), (3, 28, 128, 128),
+                                           (2, 14, 256, 256), (2, 28, 64, 128)])
 def test_conv3x3_patch_forward_statistics_and_data_grad(n, hw, cin, cout):
     """3x3 stride-1 forward on the patch-staged tiles (PS_AMD_CONV_PATCH, default on: the tile's
     input rows staged once per 64-channel chunk, tiles straddling two images) with the BN
     statistics epilogue, and the data gradient (flipped weight) with epilogue 3 -- vs fp32 torch.
     56 x 56 at 64 -> 64 channels runs conv3x3_c64_kernel (persistent row tiles, resident weight;
-    n = 10: 280 tiles over 256 blocks, so blocks walk several tiles through both patch slots)."""
+    n = 10: 280 tiles over 256 blocks, so blocks walk several tiles through both patch slots; n = 20:
+    three tiles per block, some crossing an image boundary -- the rolling row window of mode 4
+    restarts there)."""
     from ps_amd.ops.convgemm import _mat3_dgrad
 
     g = _gen(n * hw + cin + cout)
