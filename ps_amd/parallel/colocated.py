@@ -229,12 +229,13 @@ class ColocatedPS:
         self.tpull = self.t.split() if self.split_comm else self.t
         self.comm_pull = torch.cuda.Stream(device=self.device) if (self.gpu and self.split_comm) else self.comm
         self.round_events: deque = deque()
-        # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT: finish_step waits on the host until the
-        # step max_inflight - 1 steps back is done (0 = unbounded, the default).  A host that issues
-        # a ResNet-50 step in ~9.5 ms runs ahead of an 18 ms GPU step (bs256) until a queue blocks
-        # it for 20+ ms (scripts/probe_host_block.py); bounding it at 2 measured the same
-        # (profiles/r5_run_ahead_ab.txt), so it stays a knob.
-        self.max_inflight = int(_os.environ.get("PS_AMD_MAX_INFLIGHT", "0"))
+        # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT (0 = unbounded): finish_step waits on the
+        # host until the step max_inflight - 1 steps back is done.  The host issues a ResNet-50
+        # step in ~10 ms against a 62 ms GPU step (bs1024), so unbounded it runs many steps ahead;
+        # then, once per process at a random point in the first ~30 steps, the runtime stalls for
+        # 2-4 s (2 of 3 runs with --warmup 5 timed 6.2-6.9K img/s instead of 16.5K; with the
+        # bound at 2: 3 of 3 normal, and no steady-state cost -- profiles/r5_run_ahead_ab.txt).
+        self.max_inflight = int(_os.environ.get("PS_AMD_MAX_INFLIGHT", "2"))
         self._host_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
         # fault injection (PS_AMD_FAULT / HIPPS_FAULT): kill at a step, delay pushes

@@ -70,5 +70,58 @@ def main():
         torch.cuda.empty_cache()
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--pro" not in sys.argv:
     main()
+
+
+PRO_SHAPES = [  # name, M (batch 1024), K, N, kind
+    ("l3 BWD conv3 dgrad (g,z -> dz) 1024->256", 200704, 1024, 256, "bwd"),
+    ("l4 BWD conv3 dgrad 2048->512", 50176, 2048, 512, "bwd"),
+    ("l3 RESP conv1 1024->256", 200704, 1024, 256, "resp"),
+    ("l3b0 RESP conv1 512->256 (28x28)", 802816, 512, 256, "resp"),
+    ("l4 RESP conv1 2048->512", 50176, 2048, 512, "resp"),
+    ("l4b0 RESP conv1 1024->512 (14x14)", 200704, 1024, 512, "resp"),
+    ("l3 PRO1 conv3 256->1024", 200704, 256, 1024, "pro1"),
+]
+
+
+def main_pro():
+    """The prologue variants at their ResNet-50 bs1024 shapes: ms, TF/s and the HBM rate over every
+    tensor they move (A and a2 read, aout (+ bits) written, C written, epilogue rows read)."""
+    nat = native()
+    for name, M, K, N, kind in PRO_SHAPES:
+        a = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+        b = (torch.randn(N, K, device="cuda") * K ** -0.5).bfloat16()
+        gg = [M, 1, M, 1, 1, 1, 0]
+        ks = torch.zeros(N, device="cuda")
+        coef = torch.cat([torch.ones(K, device="cuda"), torch.zeros(K, device="cuda")])
+        if kind == "bwd":
+            z = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+            cb = torch.cat([torch.ones(K, device="cuda"), torch.zeros(2 * K, device="cuda")])
+            z2 = torch.randn(M, N, device="cuda").bfloat16()
+            mc = torch.cat([torch.ones(N, device="cuda"), torch.zeros(N, device="cuda")])
+            mean, inv = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+            fn = lambda: nat.conv_gemm(a, b, gg, None, 3, z2, None, mc, mean, inv, a2=z, bwd=cb)  # noqa: E731
+            byts = 2.0 * (3 * M * K + 2 * M * N)
+            src2 = 2
+        elif kind == "resp":
+            r = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
+            out = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+            bits = torch.empty(M * K // 8, device="cuda", dtype=torch.uint8)
+            fn = lambda: nat.conv_gemm(a, b, gg, coef, 1, None, ks, a2=r, aout=out, abits=bits)  # noqa: E731
+            byts = 2.0 * (3 * M * K + M * N) + M * K / 8
+            src2 = 1
+        else:
+            fn = lambda: nat.conv_gemm(a, b, gg, coef, 1, None, ks)  # noqa: E731
+            byts = 2.0 * (M * K + M * N)
+            src2 = 0
+        t = timeit(fn)
+        plan = nat.conv_gemm_plan(M, N, K, gg, True, 3 if kind == "bwd" else 1, src2)
+        print(json.dumps({"big": os.environ.get("PS_AMD_CONV_BIG", "1"), "pro_big": os.environ.get("PS_AMD_CONV_BIG_PRO", "1"),
+                          "shape": name, "tile": plan[:2], "ms": round(t, 4),
+                          "TFs": round(2.0 * M * K * N / t / 1e9, 1), "TBs": round(byts / t / 1e9, 2)}), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and "--pro" in sys.argv:
+    main_pro()
