@@ -45,8 +45,14 @@ class GpuRowService {
       : b_(reinterpret_cast<int64_t*>(ctl)), me_(static_cast<int>(me)), cap_(cap), dim_(static_cast<int>(dim)) {
     W_ = b_[1];
     TORCH_CHECK(W_ >= 1 && me >= 0 && me < W_, "row service rank");
+    // pinned landing words for the request count and the status word: a D2H copy into pageable
+    // memory is staged and synchronous (~2x the cost of the whole small request)
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&pinned_), 2 * sizeof(int64_t), hipHostMallocDefault), "pinned words");
   }
-  ~GpuRowService() { stop(); }
+  ~GpuRowService() {
+    stop();
+    if (pinned_ != nullptr) (void)hipHostFree(pinned_);
+  }
 
   // this owner's mailboxes: rq [W, cap + 1] int64, rs [W, cap, dim] f32, pk [W, MB, cap + 1]
   // int64, pg [W, MB, cap, dim] f32 (the word after cap entries = the count)
@@ -129,9 +135,9 @@ class GpuRowService {
 
   int64_t count_at(const int64_t* word, hipStream_t s) {
     psamd::launch_system_acquire(s);  // the mailbox was written by a peer's kernel
-    int64_t n = 0;
-    hip_ok(hipMemcpyAsync(&n, word, sizeof(n), hipMemcpyDeviceToHost, s), "count read");
+    hip_ok(hipMemcpyAsync(pinned_, word, sizeof(int64_t), hipMemcpyDeviceToHost, s), "count read");
     hip_ok(hipStreamSynchronize(s), "count read");
+    const int64_t n = *reinterpret_cast<volatile int64_t*>(pinned_);
     TORCH_CHECK(n >= 0 && n <= cap_, "row service: bad request count ", n);
     return n;
   }
@@ -142,11 +148,11 @@ class GpuRowService {
   // 4-byte read rides the synchronisation every request already ends with.
   void check_status(hipStream_t s) {
     if (!hkeys_.defined() || !status_.defined()) return;
-    hip_ok(hipMemcpyAsync(&status_host_, status_.data_ptr<int32_t>(), sizeof(int32_t), hipMemcpyDeviceToHost, s),
-           "status read");
+    int32_t* word = reinterpret_cast<int32_t*>(pinned_ + 1);
+    hip_ok(hipMemcpyAsync(word, status_.data_ptr<int32_t>(), sizeof(int32_t), hipMemcpyDeviceToHost, s), "status read");
     hip_ok(hipStreamSynchronize(s), "status read");
-    TORCH_CHECK(status_host_ == 0, "sparse table shard full (device hash map of owner ", me_, ": ",
-                hkeys_.numel(), " slots)");
+    TORCH_CHECK(*reinterpret_cast<volatile int32_t*>(word) == 0, "sparse table shard full (device hash map of owner ",
+                me_, ": ", hkeys_.numel(), " slots)");
   }
 
   void slots_of(const int64_t* keys, int64_t n, hipStream_t s) {
@@ -252,7 +258,7 @@ class GpuRowService {
   int64_t row_base_ = 0;
   uint64_t seed_ = 0;
   float lo_ = 0.f, hi_ = 0.f;
-  int32_t status_host_ = 0;
+  int64_t* pinned_ = nullptr;  // [0] request count, [1] status word (pinned host)
   psamd::SparseOptArgs a_{};
   int bias_mode_ = 0;
   std::atomic<bool> has_updater_{false};
