@@ -1300,7 +1300,7 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
                               c10::optional<Tensor> aux2, c10::optional<Tensor> bits2, c10::optional<Tensor> a2,
                               c10::optional<Tensor> bwd, c10::optional<Tensor> aux3, c10::optional<Tensor> mean2,
                               c10::optional<Tensor> invstd2, c10::optional<Tensor> pro2, c10::optional<Tensor> aout,
-                              c10::optional<Tensor> abits) {
+                              c10::optional<Tensor> abits, c10::optional<Tensor> tbuf) {
   check_rows(a, "a");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "a [rows, C], b [N, K]");
   const auto gi = conv_geo(a, geo);
@@ -1332,7 +1332,11 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   TORCH_CHECK(!(pro.has_value() && pro->defined()) || epi <= 1, "the BN prologue combines with epilogue 0 or 1 only");
   const bool has_bwd = bwd.has_value() && bwd->defined();
   if (has_bwd) {  // BN-backward prologue: A := ca * a + cb * a2 + cc, stored to a third output
-    TORCH_CHECK(epi == 3 && !(pro.has_value() && pro->defined()), "the BN-backward prologue combines with epi 3 only");
+    TORCH_CHECK(!(pro.has_value() && pro->defined()), "the BN-backward prologue excludes pro");
+    TORCH_CHECK(epi == 3 || ((epi == 2 || epi >= 4) &&
+                             psamd::conv_big_ok(static_cast<int>(gi.second * g.OH * g.OW), static_cast<int>(N),
+                                                static_cast<int>(K), true, g, 2, static_cast<int>(epi))),
+                "the BN-backward prologue combines with epi 3, or with 2 / 4-9 on the 256 x 256 tiles");
     TORCH_CHECK(g.ks == 1 && g.stride == 1 && g.pad == 0, "the BN-backward prologue is for 1x1 stride-1 convs");
     TORCH_CHECK(a2.has_value() && a2->defined(), "the BN-backward prologue needs a2");
     check_rows(*a2, "a2");
@@ -1391,8 +1395,8 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
   check_rows(b, "b");
   const bool sums = epi == 1 || epi == 3 || fold;
   TORCH_CHECK(epi != 9 || psamd::conv_fwd_plan_geo(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K),
-                                                   has_pro || has_bwd, g, 0, static_cast<int>(epi)).bm == 128,
-              "epi 9 runs on the 128-pixel tiles");
+                                                   has_pro || has_bwd, g, 0, static_cast<int>(epi)).bm >= 128,
+              "epi 9 runs on the 128- or 256-pixel tiles");
   Tensor part = sums ? torch::empty({epi == 9 ? 3 : 2, G, N}, fopt) : Tensor();
   psamd::ConvGemmArgs p{};
   p.a = u16(a);
@@ -1428,6 +1432,13 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     p.pro2 = f32_opt(pro2, 2 * g.C, "pro2");
     p.aout = u16m(*aout);
     p.abits = abits->data_ptr<uint8_t>();
+  }
+  if (tbuf.has_value() && tbuf->defined()) {  // phase stamps of the 256 x 256-tile kernel (probes)
+    check_gpu(*tbuf, "tbuf");
+    TORCH_CHECK(tbuf->scalar_type() == torch::kInt64 && tbuf->is_contiguous(), "tbuf: int64");
+    const auto pl = psamd::conv_fwd_plan_geo(p.M, p.N, p.K, has_pro || has_bwd, g, resp ? 1 : has_bwd ? 2 : 0, p.epi);
+    TORCH_CHECK(pl.bm == 256 && tbuf->numel() >= int64_t(8) * pl.gm * (N / pl.bn), "tbuf: [8 x blocks] on the big tiles");
+    p.tbuf = reinterpret_cast<uint64_t*>(tbuf->data_ptr<int64_t>());
   }
   psamd::launch_conv_fwd(p, cur_stream(a));
   if (has_bwd) return {c, part, bwd_out};
@@ -1773,7 +1784,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux2") = py::none(), py::arg("bits2") = py::none(), py::arg("a2") = py::none(),
         py::arg("bwd") = py::none(), py::arg("aux3") = py::none(), py::arg("mean2") = py::none(),
         py::arg("invstd2") = py::none(), py::arg("pro2") = py::none(), py::arg("aout") = py::none(),
-        py::arg("abits") = py::none());
+        py::arg("abits") = py::none(), py::arg("tbuf") = py::none());
   m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("weight_prep", &weight_prep, py::arg("jobs"), py::arg("max_blocks") = 1024);

@@ -355,15 +355,18 @@ struct ConvGemmArgs {
   uint8_t* abits;
   FastDiv fd_ohw, fd_ow;  // set by launch_conv_fwd (OH * OW, OW)
   int pgm;                // rows per partial slab (0: the launch's gm); several GEMMs share one part
+  uint64_t* tbuf = nullptr;  // conv_big only, diagnostics: 8 wall-clock stamps per block (nullable)
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
 // epi: the fold epilogues (6-9) may run on one-tile-per-block LDS-DMA grids (PS_AMD_FOLD_GLDS)
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi = 0);
-// conv_big.hip: 256 x 256 tiles, one 512-thread block per CU, for plain deep-K 1x1 GEMMs (epi 0/1/3);
+// conv_big.hip: 256 x 256 tiles, one 512-thread block per CU, for deep-K 1x1 GEMMs (every epilogue);
 // conv_fwd_plan_geo / launch_conv_fwd route there when conv_big_ok holds (gm = conv_big_gm(M))
 bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi);
+// the channel tile conv_big runs for this GEMM: 256, 128 (two blocks per CU), 0 = not eligible
+int conv_big_tn(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi);
 int conv_big_gm(int M);
 void launch_conv_big(const ConvGemmArgs& a, hipStream_t s);
 // the four stride-2 data-gradient phase GEMMs (epi 3, no prologue, LDS-DMA staging, 128-pixel tiles)

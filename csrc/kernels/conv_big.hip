@@ -33,9 +33,16 @@ typedef __attribute__((address_space(3))) const char lds_char;
 
 __device__ __attribute__((aligned(16))) uint16_t kBigZero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-constexpr int kTM = 256, kTN = 256;
-constexpr int kRing = 131072;   // LDS bytes of the stage ring
-constexpr int kCS = kTN + 4;    // output tile row stride (elements): 130 dwords, conflict-free b64 writes
+constexpr int kTM = 256;
+// block shapes (CFG):
+//   0  256 x 256 tile, 8 waves of 128 px x 64 ch, one 512-thread block per CU, 128 KiB ring;
+//   1  256 x 128 tile, 4 waves of 128 x 64, 256-thread blocks two per CU, a 72 KiB ring of three
+//      32-deep stages (one block's epilogue can overlap the other's K loop);
+//   2  256 x 256 tile, 4 waves of 128 px x 128 ch (256 accumulators each, one wave per SIMD):
+//      8 fragment reads per 16 MFMAs instead of 6 per 8 -- a third less LDS read traffic per FLOP.
+constexpr int cfg_tn(int cfg) { return cfg == 1 ? 128 : 256; }
+constexpr int cfg_waves(int cfg) { return cfg == 0 ? 8 : 4; }
+constexpr int cfg_ring(int cfg) { return cfg == 1 ? 73728 : 131072; }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));
@@ -99,26 +106,33 @@ __device__ __forceinline__ int bswz(int r, int c) {
 // once the pass over stage kt has read it.  With a 256-wide channel tile the A rows are staged
 // (and transformed) once per channel tile -- once in all for N = 256, and for wider N the other
 // channel tiles of the pixel tile run on the same XCD (L2 re-reads, not HBM).
-template <int EPI, int BK, int PRO>
-__global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) {
-  static_assert(EPI == 0 || EPI == 1 || EPI == 3, "plain / BN statistics / data-gradient mask + sums");
+template <int EPI, int BK, int PRO, int CFG>
+__global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_big_kernel(const ConvGemmArgs p) {
+  static_assert(EPI >= 0 && EPI <= 9, "conv_gemm's epilogues");
   static_assert(BK == 64 || BK == 32, "stage depth");
   static_assert(PRO == 0 || BK == 64, "the prologue variants run the 2 x 64-deep ring");
-  static_assert(PRO != 2 || EPI == 3, "the BN-backward prologue is the data-gradient GEMM");
+  static_assert(PRO != 2 || (EPI != 0 && EPI != 1), "the BN-backward prologue feeds a data-gradient GEMM");
+  static_assert(CFG != 1 || (BK == 32 && PRO == 0), "128-channel tiles: plain 32-deep ring");
+  constexpr int TN = cfg_tn(CFG), NW = cfg_waves(CFG), NT = 64 * NW;
+  constexpr int WCH = CFG == 2 ? 128 : 64;        // channels per wave (2 waves along the pixels)
+  constexpr int WN = TN / WCH, TI = WCH / 32;     // waves along the channels; 32-ch blocks per wave
+  constexpr int kRing = cfg_ring(CFG);
+  constexpr int kTN = TN, kCS = TN + 4;          // output tile row stride (elements)
   constexpr bool TWO = PRO == 2 || PRO == 3;
   constexpr int RB = 2 * BK;                    // bytes per stage row
   constexpr int A_BYTES = kTM * RB, STAGE = (kTM + kTN) * RB;
-  constexpr int NST = kRing / STAGE;            // 2 (BK 64) or 4 (BK 32)
+  constexpr int NST = kRing / STAGE;            // TN 256: 2 (BK 64) or 4 (BK 32); TN 128: 3
+  static_assert(NST >= 2, "ring depth");
   constexpr int CPR = RB / 16;                  // 16-B chunks per row
   constexpr int RPI = 64 / CPR;                 // rows per DMA wave-instruction
-  constexpr int PA = kTM / RPI / 8;             // A DMA instructions per wave per stage
-  constexpr int PB = kTN / RPI / 8;
+  constexpr int PA = kTM / RPI / NW;            // A DMA instructions per wave per stage
+  constexpr int PB = kTN / RPI / NW;
   constexpr int GPS = PA + PB;                  // DMA instructions per wave per stage
   constexpr int KSTEPS = BK / 16;
   constexpr int OUT_BYTES = kTM * kCS * 2;
   constexpr int RED_OFF = OUT_BYTES > kRing ? OUT_BYTES : kRing;
   constexpr int Z_OFF = kRing;                                    // TWO: the a2 stage tile
-  constexpr int LDS_A = RED_OFF + 2 * 8 * kTN * 4, LDS_Z = TWO ? Z_OFF + A_BYTES : 0;
+  constexpr int LDS_A = RED_OFF + 3 * NW * kTN * 4, LDS_Z = TWO ? Z_OFF + A_BYTES : 0;
   constexpr int LDS_BYTES = LDS_A > LDS_Z ? LDS_A : LDS_Z;
   static_assert(LDS_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
@@ -132,6 +146,11 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
   const int m0 = mt * kTM;
   const ConvGeo& g = p.g;
   const int nk = p.K / BK;
+  // diagnostics (p.tbuf set by probes only): wall-clock stamps of this block's phases
+  auto stamp = [&](int i) {
+    if (p.tbuf != nullptr && t == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + i] = wall_clock64();
+  };
+  stamp(0);
 
   // ---- DMA sources: lane-linear LDS rows, swizzled source chunk; A rows past M read zeros
   const int lrow = lane / CPR, lch = lane % CPR;
@@ -169,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     }
   };
   // the prologue pass over stage kt's A tile (in place): thread t owns logical chunk t & 7 (fixed
-  // channels: one coefficient load per stage) of rows (t >> 3) + 64 i
+  // channels: one coefficient load per stage) of rows (t >> 3) + (NT / 8) i
   // coefficients of the pass over stage kt (thread t: logical chunk t & 7): NCO untracked 16-B loads
   // issued before the stage's DMA, waited for by vmcnt(GPS) behind it
   constexpr int NCO = PRO == 1 ? 4 : PRO == 2 ? 6 : 8;
@@ -197,7 +216,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     }
   };
   // the prologue pass over stage kt's A tile (in place): thread t owns logical chunk t & 7 (fixed
-  // channels) of rows (t >> 3) + 64 i
+  // channels) of rows (t >> 3) + TRP i
   auto transform = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     const uint8_t* Zs = lds + Z_OFF;
@@ -222,19 +241,19 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     }
     const bool dual = PRO == 3 && p.pro2 != nullptr;
     const bool store_a = (PRO == 2 || PRO == 3) && p.aout != nullptr && n0 == 0;
-    constexpr int NR = kTM / 64, HB = TWO ? 2 : NR;  // rows read together (register budget)
+    constexpr int TRP = NT / 8, NR = kTM / TRP, HB = TWO ? 2 : NR;  // rows read together (register budget)
 #pragma unroll
     for (int h = 0; h < NR; h += HB) {
     u16x8 va[HB], za[HB];
 #pragma unroll
     for (int i = 0; i < HB; ++i) {  // the rows' reads before any use (one LDS latency per group)
-      const int r = tr0 + 64 * (h + i), off = r * RB + bswz<BK>(r, lc) * 16;
+      const int r = tr0 + TRP * (h + i), off = r * RB + bswz<BK>(r, lc) * 16;
       va[i] = *reinterpret_cast<const u16x8*>(As + off);
       if constexpr (TWO) za[i] = *reinterpret_cast<const u16x8*>(Zs + off);
     }
 #pragma unroll
     for (int i = 0; i < HB; ++i) {
-      const int r = tr0 + 64 * (h + i), m = m0 + r;
+      const int r = tr0 + TRP * (h + i), m = m0 + r;
       const int off = r * RB + bswz<BK>(r, lc) * 16;
       u16x8 v = va[i];
       unsigned ob = 0;
@@ -289,24 +308,24 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
   // ---- fragment addresses: wave (wm, wn) = pixels 128 wm.., channels 64 wn..; the chunk swizzle
   // of rows 32 j + fr is the same for every block j, so one address per k-step and operand, and
   // the blocks are immediate offsets (32 rows = 32 RB bytes apart)
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
   uint32_t fa[KSTEPS], fb[KSTEPS];
 #pragma unroll
   for (int s = 0; s < KSTEPS; ++s) {
     const int ch = bswz<BK>(fr, 2 * s + fh) * 16;
     fa[s] = static_cast<uint32_t>((128 * wm + fr) * RB + ch);
-    fb[s] = static_cast<uint32_t>(A_BYTES + (64 * wn + fr) * RB + ch);
+    fb[s] = static_cast<uint32_t>(A_BYTES + (WCH * wn + fr) * RB + ch);
   }
-  f32x16 acc[2][4];
+  f32x16 acc[TI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
   constexpr int OJ = 32 * RB;  // bytes between 32-row fragment blocks
-  bf16x8_t xa[2][4], wb[2][2];
+  bf16x8_t xa[2][4], wb[2][TI];
   auto fetch = [&](uint32_t sb, int s, int set) {
     const uint32_t a = sb + fa[s], b = sb + fb[s];
     xa[set][0] = ld_b128o<0>(a);
@@ -315,15 +334,20 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     xa[set][3] = ld_b128o<3 * OJ>(a);
     wb[set][0] = ld_b128o<0>(b);
     wb[set][1] = ld_b128o<OJ>(b);
+    if constexpr (TI == 4) {
+      wb[set][2] = ld_b128o<2 * OJ>(b);
+      wb[set][3] = ld_b128o<3 * OJ>(b);
+    }
   };
+  constexpr int FR = 4 + TI;  // fragment reads per k-step
   auto mfma_set = [&](int set) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) tie(xa[set][j]);
-    tie(wb[set][0]);
-    tie(wb[set][1]);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) tie(wb[set][i]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[set][i], xa[set][j], acc[i][j], 0, 0, 0);
@@ -356,7 +380,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
       for (int s = 0; s < KSTEPS; ++s) {
         if (s + 1 < KSTEPS) {
           fetch(sb, s + 1, (s + 1) & 1);
-          wait_lgkm<6>();
+          wait_lgkm<FR>();
         } else {
           wait_lgkm<0>();
         }
@@ -376,6 +400,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     else if (younger == 1) wait_vm<GPS>();
     else wait_vm<0>();
     lds_bar();  // every wave's stage kt landed; every wave is done with stage kt - 1's buffer
+    if (kt == 0) stamp(1);
     if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
     const uint32_t sb = L0 + static_cast<uint32_t>((kt % NST) * STAGE);
     fetch(sb, 0, 0);
@@ -383,13 +408,14 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     for (int s = 0; s < KSTEPS; ++s) {
       if (s + 1 < KSTEPS) {
         fetch(sb, s + 1, (s + 1) & 1);
-        wait_lgkm<6>();
+        wait_lgkm<FR>();
       } else {
         wait_lgkm<0>();
       }
       mfma_set(s & 1);
     }
   }
+  stamp(2);
   wait_vm<0>();
   lds_bar();  // the output tile overlays the stage ring
 
@@ -397,23 +423,40 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
   // 64 wn + 32 i + 8 (q >> 2) + 4 fh + (q & 3) of pixel 128 wm + 32 j + fr
   uint16_t* Cs = reinterpret_cast<uint16_t*>(lds);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
-        const int nl = 64 * wn + 32 * i + 8 * q4 + 4 * fh, ml = 128 * wm + 32 * j + fr;
+        const int nl = WCH * wn + 32 * i + 8 * q4 + 4 * fh, ml = 128 * wm + 32 * j + fr;
         const u16x4 v = {f32_to_bf16(acc[i][j][4 * q4]), f32_to_bf16(acc[i][j][4 * q4 + 1]),
                          f32_to_bf16(acc[i][j][4 * q4 + 2]), f32_to_bf16(acc[i][j][4 * q4 + 3])};
         *reinterpret_cast<u16x4*>(Cs + ml * kCS + nl) = v;
       }
   lds_bar();
+  stamp(3);
 
   // ---- row pass: thread t owns channels [8 cg, 8 cg + 8) of rows r0 + 16 i
-  const int cg = t & 31, r0 = t >> 5, nc = n0 + cg * 8;
-  float e0[8], e1[8], e2[8], e3[8], s1[8], s2[8];
+  // EPI 5/6/9: + the residual rows masked by the block output's ReLU bits (aux, bits); EPI 2/7:
+  // + the residual rows; EPI 4/8: + the stride-2 residual map at even (h, w); 6-9 also mask by the
+  // previous block's output bits (bits2) and reduce its bn3 backward sums over aux2 (and, 9, the
+  // downsample BN's sum over aux3) -- conv_gemm's epilogues, see convgemm.hip conv_fwd_body
+  constexpr bool FOLD = EPI >= 6;
+  constexpr bool FOLD_DS = EPI == 9;
+  constexpr int BASE = EPI == 6 || EPI == 9 ? 5 : EPI == 7 ? 2 : EPI == 8 ? 4 : EPI;
+  constexpr bool SUMS = EPI == 1 || EPI == 3 || FOLD;
+  constexpr bool RD_AUX = BASE == 2 || BASE == 4 || BASE == 5 || EPI == 3;
+  constexpr int CG = kTN / 8, RPP = NT / CG;  // 16-B column groups per row; rows per pass
+  const int cg = t % CG, r0 = t / CG, nc = n0 + cg * 8;
+  float e0[8], e1[8], e2[8], e3[8], s1[8], s2[8], s3[FOLD_DS ? 8 : 1], e4[FOLD_DS ? 8 : 1], e5[FOLD_DS ? 8 : 1];
 #pragma unroll
   for (int e = 0; e < 8; ++e) e0[e] = e1[e] = e2[e] = e3[e] = s1[e] = s2[e] = 0.f;
+  if constexpr (FOLD_DS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s3[e] = 0.f;
+    load8(p.mean2, nc, e4);
+    load8(p.invstd2, nc, e5);
+  }
   if constexpr (EPI == 1) {
     if (p.kshift) load8(p.kshift, nc, e0);
   } else if constexpr (EPI == 3) {
@@ -421,27 +464,58 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
     load8(p.mc + p.N, nc, e1);
     load8(p.mean, nc, e2);
     load8(p.invstd, nc, e3);
+  } else if constexpr (FOLD) {
+    load8(p.mean, nc, e2);
+    load8(p.invstd, nc, e3);
   }
-  constexpr int NPASS = kTM / 16;
-  constexpr int HALF = NPASS / 2;  // rows in flight per half (EPI 3's BN-input reads)
+  constexpr int NPASS = kTM / RPP;
+  // rows in flight per group: all of a group's row reads are issued before any is consumed (8: no
+  // spill with every epilogue at the K loop's 204-VGPR high-water mark)
+  constexpr int RIF = 4;
 #pragma unroll
-  for (int h = 0; h < NPASS; h += HALF) {
-    u16x8 zr[EPI == 3 ? HALF : 1];
-    if constexpr (EPI == 3) {
+  for (int h = 0; h < NPASS; h += RIF) {
+    u16x8 ra[RD_AUX ? RIF : 1], rz[FOLD ? RIF : 1], rd[FOLD_DS ? RIF : 1];
+    uint32_t rb[BASE == 5 ? RIF : 1], rp[FOLD ? RIF : 1];
+    unsigned rodd = 0;
 #pragma unroll
-      for (int i = 0; i < HALF; ++i) {
-        const int m = min(m0 + r0 + 16 * (h + i), p.M - 1);
-        zr[i] = *reinterpret_cast<const u16x8*>(p.aux + static_cast<int64_t>(m) * p.N + nc);
+    for (int i = 0; i < RIF; ++i) {
+      const int m = min(m0 + r0 + RPP * (h + i), p.M - 1);
+      const int64_t o = static_cast<int64_t>(m) * p.N + nc;
+      if constexpr (BASE == 4) {  // residual map (OH+1)/2 x (OW+1)/2, present at even (h, w)
+        const int ohw = g.OH * g.OW;
+        const int im = static_cast<int>(fdiv_big(static_cast<uint32_t>(m), p.fd_ohw)), r = m - im * ohw,
+                  hh = static_cast<int>(fdiv_big(static_cast<uint32_t>(r), p.fd_ow)), ww = r - hh * g.OW;
+        const int RH = (g.OH + 1) >> 1, RW = (g.OW + 1) >> 1;
+        rodd |= static_cast<unsigned>((hh | ww) & 1) << i;
+        const int64_t ro = ((static_cast<int64_t>(im) * RH + (hh >> 1)) * RW + (ww >> 1)) * p.N + nc;
+        ra[i] = *reinterpret_cast<const u16x8*>(p.aux + ((hh | ww) & 1 ? int64_t(0) : ro));
+      } else if constexpr (RD_AUX) {
+        ra[i] = *reinterpret_cast<const u16x8*>(p.aux + o);
       }
+      if constexpr (BASE == 5) rb[i] = p.bits[o >> 3];
+      if constexpr (FOLD) {
+        rz[i] = *reinterpret_cast<const u16x8*>(p.aux2 + o);
+        rp[i] = p.bits2[o >> 3];
+      }
+      if constexpr (FOLD_DS) rd[i] = *reinterpret_cast<const u16x8*>(p.aux3 + o);
     }
 #pragma unroll
-    for (int i = 0; i < HALF; ++i) {
-      const int rr = r0 + 16 * (h + i), m = m0 + rr;
+    for (int i = 0; i < RIF; ++i) {
+      const int rr = r0 + RPP * (h + i), m = m0 + rr;
       if (m >= p.M) break;
       const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * kCS + cg * 8);
       const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * kCS + cg * 8 + 4);
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if constexpr (EPI == 1) {
+      if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((rb[i] >> e) & 1u) v[e] = f32_to_bf16(bf16_to_f32(v[e]) + bf16_to_f32(ra[i][e]));
+      } else if constexpr (BASE == 2 || BASE == 4) {
+        if (BASE == 2 || !((rodd >> i) & 1u)) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = f32_to_bf16(bf16_to_f32(v[e]) + bf16_to_f32(ra[i][e]));
+        }
+      } else if constexpr (EPI == 1) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = bf16_to_f32(v[e]) - e0[e];
@@ -451,7 +525,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
       } else if constexpr (EPI == 3) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float z = bf16_to_f32(zr[i][e]);
+          const float z = bf16_to_f32(ra[i][e]);
           const bool on = z * e0[e] + e1[e] > 0.f;
           const float gv = on ? bf16_to_f32(v[e]) : 0.f;
           s1[e] += gv;
@@ -459,37 +533,75 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
           if (!on) v[e] = 0;
         }
       }
+      if constexpr (FOLD) {  // previous block's bn3: ReLU mask from its output bits + reduce sums
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (!((rp[i] >> e) & 1u)) v[e] = 0;
+          const float gv = bf16_to_f32(v[e]);
+          s1[e] += gv;
+          s2[e] += gv * ((bf16_to_f32(rz[i][e]) - e2[e]) * e3[e]);
+          if constexpr (FOLD_DS) s3[e] += gv * ((bf16_to_f32(rd[i][e]) - e4[e]) * e5[e]);
+        }
+      }
       *reinterpret_cast<u16x8*>(p.c + static_cast<int64_t>(m) * p.N + nc) = v;
     }
   }
-  if constexpr (EPI == 1 || EPI == 3) {
-    // threads of one column group: lanes l, l + 32 of each wave, then the 8 waves in fixed order
+  if constexpr (SUMS) {
+    // threads of one column group: lanes l, l + CG, .. of each wave, then the NW waves in fixed order
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += __shfl_xor(s1[e], 32, 64);
-      s2[e] += __shfl_xor(s2[e], 32, 64);
+    for (int off = CG; off < 64; off *= 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], off, 64);
+        s2[e] += __shfl_xor(s2[e], off, 64);
+        if constexpr (FOLD_DS) s3[e] += __shfl_xor(s3[e], off, 64);
+      }
     }
-    float* red = reinterpret_cast<float*>(lds + RED_OFF);  // [2][8 waves][256]
-    if (fh == 0) {
+    float* red = reinterpret_cast<float*>(lds + RED_OFF);  // [NSUM][NW waves][TN]
+    if (lane < CG) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         red[wave * kTN + cg * 8 + e] = s1[e];
-        red[(8 + wave) * kTN + cg * 8 + e] = s2[e];
+        red[(NW + wave) * kTN + cg * 8 + e] = s2[e];
+        if constexpr (FOLD_DS) red[(2 * NW + wave) * kTN + cg * 8 + e] = s3[e];
       }
     }
     __syncthreads();
     if (t < kTN) {
-      float a = 0.f, b = 0.f;
+      float a = 0.f, b = 0.f, c3 = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
+      for (int w = 0; w < NW; ++w) {
         a += red[w * kTN + t];
-        b += red[(8 + w) * kTN + t];
+        b += red[(NW + w) * kTN + t];
+        if constexpr (FOLD_DS) c3 += red[(2 * NW + w) * kTN + t];
       }
       const int64_t PG = p.pgm > 0 ? p.pgm : mtiles;
       p.part[static_cast<int64_t>(mt) * p.N + n0 + t] = a;
       p.part[(PG + mt) * p.N + n0 + t] = b;
+      if constexpr (FOLD_DS) p.part[(2 * PG + mt) * p.N + n0 + t] = c3;
     }
   }
+  if (p.tbuf != nullptr) {
+    stamp(4);  // stores issued
+    wait_vm<0>();
+    stamp(5);  // thread 0's stores acknowledged
+    if (t == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + 6] = __smid();
+  }
+}
+
+// auto choice of the 128-channel tiles (PS_AMD_CONV_BIG_TN unset): not yet (probe first)
+bool big_tn128(int M, int N, int K, const ConvGeo& g, int epi) {
+  (void)M, (void)N, (void)K, (void)g, (void)epi;
+  return false;
+}
+
+// PS_AMD_CONV_BIG_W4=1: the 256 x 256 tiles as 4 waves of 128 x 128 (CFG 2)
+bool big_w4() {
+  static const bool w4 = [] {
+    const char* e = std::getenv("PS_AMD_CONV_BIG_W4");
+    return e != nullptr && e[0] == '1';
+  }();
+  return w4;
 }
 
 int big_bk() {
@@ -502,10 +614,62 @@ int big_bk() {
 
 }  // namespace
 
-// Eligible: a plain 1x1 GEMM (no prologue, no second row source, rows in order), N a multiple of
-// 256, K >= 256, epilogue 0 / 1 / 3, and >= 1024 blocks or K >= 1024 (with >= 256 blocks).
-// PS_AMD_CONV_BIG=0 disables; PS_AMD_CONV_BIG_BK=32 selects the 4-stage ring of 32-deep stages.
-bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
+// the 256-channel-tile launches (CFG 0: 8 waves, CFG 2: 4 waves of 128 x 128)
+template <int C>
+static void launch_big256(const ConvGemmArgs& a, hipStream_t s, bool bwd, bool resp) {
+  const int nblk = conv_big_gm(a.M) * (a.N / 256);
+  const dim3 blk(64 * cfg_waves(C));
+#define PSAMD_BIG(E, BK, P) hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C>), dim3(nblk), blk, 0, s, a)
+  if (bwd) {
+    switch (a.epi) {
+      case 2: PSAMD_BIG(2, 64, 2); break;
+      case 4: PSAMD_BIG(4, 64, 2); break;
+      case 5: PSAMD_BIG(5, 64, 2); break;
+      case 6: PSAMD_BIG(6, 64, 2); break;
+      case 7: PSAMD_BIG(7, 64, 2); break;
+      case 8: PSAMD_BIG(8, 64, 2); break;
+      case 9: PSAMD_BIG(9, 64, 2); break;
+      default: PSAMD_BIG(3, 64, 2); break;
+    }
+  } else if (resp) {
+    if (a.epi == 1) PSAMD_BIG(1, 64, 3);
+    else PSAMD_BIG(0, 64, 3);
+  } else if (a.pro != nullptr) {
+    if (a.epi == 1) PSAMD_BIG(1, 64, 1);
+    else PSAMD_BIG(0, 64, 1);
+  } else if (a.epi == 2 || a.epi >= 4) {
+    switch (a.epi) {
+      case 2: PSAMD_BIG(2, 64, 0); break;
+      case 4: PSAMD_BIG(4, 64, 0); break;
+      case 5: PSAMD_BIG(5, 64, 0); break;
+      case 6: PSAMD_BIG(6, 64, 0); break;
+      case 7: PSAMD_BIG(7, 64, 0); break;
+      case 8: PSAMD_BIG(8, 64, 0); break;
+      default: PSAMD_BIG(9, 64, 0); break;
+    }
+  } else if (C == 0 && big_bk() == 32) {
+    if constexpr (C == 0) {
+      if (a.epi == 1) PSAMD_BIG(1, 32, 0);
+      else if (a.epi == 3) PSAMD_BIG(3, 32, 0);
+      else PSAMD_BIG(0, 32, 0);
+    }
+  } else {
+    if (a.epi == 1) PSAMD_BIG(1, 64, 0);
+    else if (a.epi == 3) PSAMD_BIG(3, 64, 0);
+    else PSAMD_BIG(0, 64, 0);
+  }
+#undef PSAMD_BIG
+}
+
+// Eligible: a 1x1 GEMM (rows in order) with K = C.  The 256-channel tiles: N a multiple of 256,
+// K >= 256, and >= 1024 blocks or K >= 1024 (with >= 256 blocks); epilogues 0 / 1 / 3 with or
+// without a stride-1 prologue, the residual / fold epilogues 2, 4-9 without one (or with the BN
+// backward one).  The 128-channel tiles (two blocks per CU): no prologue, N a multiple of 128,
+// K a multiple of 32, >= 512 blocks, where big_tn128 picks them.  PS_AMD_CONV_BIG=0 disables;
+// PS_AMD_CONV_BIG_FOLD=0 keeps 2, 4-9 on the 128-pixel tiles; PS_AMD_CONV_BIG_BK=32 selects the
+// 4-stage ring of 32-deep stages (256-channel tiles, epilogues 0 / 1 / 3); PS_AMD_CONV_BIG_TN=128 /
+// 256 forces one channel tile where it is eligible.
+int conv_big_tn(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
   static const bool on = [] {
     const char* e = std::getenv("PS_AMD_CONV_BIG");
     return e == nullptr || e[0] != '0';
@@ -514,47 +678,68 @@ bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int 
     const char* e = std::getenv("PS_AMD_CONV_BIG_PRO");
     return e == nullptr || e[0] != '0';
   }();
-  if (!on || g.RH != 0) return false;
-  if (g.ks != 1 || g.ksw > 1 || g.pad != 0) return false;
-  if (N % kTN != 0 || K % 64 != 0 || K < 256 || g.C != K) return false;
-  if (!(epi == 0 || epi == 1 || epi == 3)) return false;
-  // prologues (PRO 1: pro, src2 0; PRO 3: src2 1; PRO 2: src2 2 + epi 3): stride 1 only
+  static const bool fold_on = [] {
+    const char* e = std::getenv("PS_AMD_CONV_BIG_FOLD");
+    return e == nullptr || e[0] != '0';
+  }();
+  const char* tne = std::getenv("PS_AMD_CONV_BIG_TN");  // read per call: tests switch it in-process
+  const int tn_env = tne == nullptr ? 0 : std::atoi(tne);
+  if (!on || g.RH != 0) return 0;
+  if (g.ks != 1 || g.ksw > 1 || g.pad != 0 || g.C != K) return 0;
+  if (epi < 0 || epi > 9) return 0;
+  const bool plain_epi = epi == 0 || epi == 1 || epi == 3;
+  if (!plain_epi && !fold_on) return 0;
+  const int64_t mt = (M + kTM - 1) / kTM;
+  if (tn_env != 256 && !pro && src2 == 0 && N % 128 == 0 && K % 32 == 0 && K >= 64 && mt * (N / 128) >= 512) {
+    if (tn_env == 128 || big_tn128(M, N, K, g, epi)) return 128;
+  }
+  if (N % 256 != 0 || K % 64 != 0 || K < 256) return 0;
+  // the residual / fold epilogues (2, 4-9: the conv1 data gradients): no prologue, or the BN
+  // backward one (the conv1 data gradient with bn1's backward applied)
+  if (!plain_epi && ((pro && src2 != 2) || src2 == 1)) return 0;
+  // prologues (PRO 1: pro, src2 0; PRO 3: src2 1; PRO 2: src2 2 + a data-gradient epilogue): stride 1 only
   if (pro || src2 != 0) {
-    if (!pro_on || g.stride != 1) return false;
-    if (src2 == 2 && epi != 3) return false;
-    if (src2 == 1 && epi == 3) return false;
+    if (!pro_on || g.stride != 1) return 0;
+    if (src2 == 2 && (epi == 0 || epi == 1)) return 0;
+    if (src2 == 1 && epi == 3) return 0;
   }
   // one block per CU: below ~4 rounds of blocks the last round's idle CUs and the per-tile
   // prologue / epilogue outweigh the faster K loop unless K is deep (profiles/r5_conv_big_probe.txt:
   // at batch 256 the K = 256 / 512 shapes with 784 blocks ran 2-15 % slower, K >= 1024 faster)
-  const int64_t nblk = static_cast<int64_t>((M + kTM - 1) / kTM) * (N / kTN);
-  return nblk >= 256 && (nblk >= 1024 || K >= 1024);
+  const int64_t nblk = mt * (N / 256);
+  return nblk >= 256 && (nblk >= 1024 || K >= 1024) ? 256 : 0;
+}
+
+bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
+  return conv_big_tn(M, N, K, pro, g, src2, epi) != 0;
 }
 
 int conv_big_gm(int M) { return (M + kTM - 1) / kTM; }
 
 void launch_conv_big(const ConvGemmArgs& a, hipStream_t s) {
-  const int nblk = conv_big_gm(a.M) * (a.N / kTN);
   const bool bwd = a.bwd != nullptr, resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
-#define PSAMD_BIG(E, BK, P) hipLaunchKernelGGL((conv_big_kernel<E, BK, P>), dim3(nblk), dim3(512), 0, s, a)
-  if (bwd) {
-    PSAMD_BIG(3, 64, 2);
-  } else if (resp) {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 3);
-    else PSAMD_BIG(0, 64, 3);
-  } else if (a.pro != nullptr) {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 1);
-    else PSAMD_BIG(0, 64, 1);
-  } else if (big_bk() == 32) {
-    if (a.epi == 1) PSAMD_BIG(1, 32, 0);
-    else if (a.epi == 3) PSAMD_BIG(3, 32, 0);
-    else PSAMD_BIG(0, 32, 0);
-  } else {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 0);
-    else if (a.epi == 3) PSAMD_BIG(3, 64, 0);
-    else PSAMD_BIG(0, 64, 0);
+  const int tn = conv_big_tn(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, resp ? 1 : bwd ? 2 : 0, a.epi);
+  if (tn == 128) {
+    const int nb = conv_big_gm(a.M) * (a.N / 128);
+#define PSAMD_BIG128(E) hipLaunchKernelGGL((conv_big_kernel<E, 32, 0, 1>), dim3(nb), dim3(256), 0, s, a)
+    switch (a.epi) {
+      case 0: PSAMD_BIG128(0); break;
+      case 1: PSAMD_BIG128(1); break;
+      case 2: PSAMD_BIG128(2); break;
+      case 3: PSAMD_BIG128(3); break;
+      case 4: PSAMD_BIG128(4); break;
+      case 5: PSAMD_BIG128(5); break;
+      case 6: PSAMD_BIG128(6); break;
+      case 7: PSAMD_BIG128(7); break;
+      case 8: PSAMD_BIG128(8); break;
+      default: PSAMD_BIG128(9); break;
+    }
+#undef PSAMD_BIG128
+    return;
   }
-#undef PSAMD_BIG
+  if (big_w4()) launch_big256<2>(a, s, bwd, resp);
+  else launch_big256<0>(a, s, bwd, resp);
 }
+
 
 }  // namespace psamd

@@ -2094,10 +2094,10 @@ bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
 }
 
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
-  if (conv_big_ok(M, N, K, pro, g, src2, epi)) {  // 256 x 256 tiles (conv_big.hip)
+  if (const int tn = conv_big_tn(M, N, K, pro, g, src2, epi)) {  // 256 x TN tiles (conv_big.hip)
     ConvFwdPlan pl;
     pl.bm = 256;
-    pl.bn = 256;
+    pl.bn = tn;
     pl.gm = conv_big_gm(M);
     return pl;
   }

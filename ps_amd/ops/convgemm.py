@@ -293,6 +293,13 @@ def _ds_bwd_fused(ci: int, co: int, s: int) -> bool:
             and bool(native().conv11_bwd_fused_supported(ci, co, True)))
 
 
+def _conv1_bwd_prologue() -> bool:
+    """bn1's backward as the conv1 data-gradient GEMM's prologue where that GEMM runs on the 256 x 256
+    tiles: opt-in (PS_AMD_CONV1_BWD_PRO=1) -- at K = 256 / 512 the prologue (A and z1 re-read per channel
+    tile, transform pass per stage) costs more than the apply pass it removes (profiles/r5_conv1_dgrad_big.txt)."""
+    return os.environ.get("PS_AMD_CONV1_BWD_PRO", "0") != "0"
+
+
 def _fold_enabled() -> bool:
     return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
 
@@ -448,16 +455,32 @@ class _BottleneckFn(torch.autograd.Function):
                                          None, cf1, m1, i1)
             else:  # four stride-1 phase GEMMs, each writing every other dx row (no zero fill)
                 gy1, p1b = nat.conv_dgrad_s2(dz2, pw[2] if pw else _phase_weights(w2), h, w, 3, z1, cf1, m1, i1)
-            dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
-        else:
-            dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
-        sd.fork()
-        dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
-        w1t = pw[0] if pw else _mat(w1).t()
-        dwd = dgd = dbd = None
         li = ctx.link_in
         fold = li is not None and _fold_enabled()
         fkw = dict(mean=li.mean, invstd=li.invstd, aux2=li.z3, bits2=li.bits) if fold else {}
+        if wd is not None:
+            e1 = (8 if s == 2 else 7) if fold else (4 if s == 2 else 2)
+        else:
+            e1 = (9 if li.zd is not None else 6) if fold else 5
+        # bn1's backward in the conv1 data-gradient prologue (256 x 256 tiles, layers 3-4): the
+        # GEMM also stores dz1 for the weight gradient -- no apply pass over gy1 / z1
+        pro1 = ours_dgrad and _conv1_bwd_prologue() and big_tile(x2.shape[0], x2.shape[1], w1.shape[0], src2=2,
+                                                                 epi=e1)
+        dw1 = None
+        if pro1:
+            dg1, db1, cb1 = nat.bn_bwd_coef(p1b, g1, m1, i1, gy1.shape[0])
+            bkw = dict(a2=z1, bwd=cb1)
+        else:
+            if ours_dgrad:
+                dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
+            else:
+                dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
+            sd.fork()
+            dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
+            bkw = {}
+        a1 = gy1 if pro1 else dz1
+        w1t = pw[0] if pw else _mat(w1).t()
+        dwd = dgd = dbd = None
         if wd is not None:
             wdt = pw[3] if pw else _mat(wd).t()
             if ds_part is not None and _ds_bwd_fused(wd.shape[1], wd.shape[0], s):
@@ -475,13 +498,18 @@ class _BottleneckFn(torch.autograd.Function):
                 sd.fork()
                 dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
                 t = nat.conv_gemm(dzd, wdt, go)[0]
-            epi = 4 if s == 2 else 2
-            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, epi + 4 if fold else epi, t, **fkw)
-        elif fold and li.zd is not None:  # the producer has a downsample BN: its sum rides along
-            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, 9, d2, bits=obits, aux3=li.zd, mean2=li.md, invstd2=li.idd,
-                                      **fkw)
+            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, t, **fkw, **bkw)
+        elif e1 == 9:  # the producer has a downsample BN: its sum rides along
+            r1 = nat.conv_gemm(a1, w1t, gi, None, 9, d2, bits=obits, aux3=li.zd, mean2=li.md, invstd2=li.idd,
+                               **fkw, **bkw)
         else:
-            dx2, part = nat.conv_gemm(dz1, w1t, gi, None, 6 if fold else 5, d2, bits=obits, **fkw)
+            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, d2, bits=obits, **fkw, **bkw)
+        dx2, part = r1[0], r1[1]
+        if pro1:
+            dz1 = r1[2]
+            FOLD_STATS["conv1_pro"] = FOLD_STATS.get("conv1_pro", 0) + 1
+            sd.fork()
+            dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
         if fold:
             # dx_keep pins a second reference on dx2's storage, so autograd cannot sum another
             # consumer's gradient into it in place (it would not bump the version): a summed

@@ -210,3 +210,108 @@ def test_layer3_chain_on_big_tiles_matches_module_path():
     for nm, u, v, w in pairs:
         ef, eb = rel(u, w), rel(v, w)
         assert ef <= 1.25 * eb + 5e-3, (nm, ef, eb)
+
+
+def _unpack(bits, M, N):
+    return ((bits.view(-1, 1).int() >> torch.arange(8, device=DEV)) & 1).view(M, N).bool()
+
+
+@pytest.mark.parametrize("epi", [2, 4, 5, 6, 7, 8, 9])
+def test_big_tile_residual_and_fold_epilogues(epi):
+    """The conv1 data-gradient epilogues on the 256 x 256 tiles: + residual rows (2), + the stride-2
+    residual map at even (h, w) (4), + residual masked by the block output's bits (5); 6-8 = 5 / 2 / 4
+    then the previous block's ReLU mask (bits2) and its bn3 backward sums, 9 = 6 + the downsample
+    BN's sum (third partial slab)."""
+    n, h, K, N = 700, 14, 256, 512
+    M = n * h * h
+    g = _gen(40 + epi)
+    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    gg = geo(h, h)
+    _assert_big(M, N, K, gg, epi)
+    base = {6: 5, 9: 5, 7: 2, 8: 4}.get(epi, epi)
+    ref = (a.float() @ b.float().t()).bfloat16().float()
+    kw = {}
+    if base == 4:
+        r = (h + 1) // 2
+        aux = _rnd(n * r * r, N, g=g)
+        full = torch.zeros(n, h, h, N, device=DEV)
+        full[:, ::2, ::2] = aux.float().view(n, r, r, N)
+        want = ref + full.view(M, N)
+    else:
+        aux = _rnd(M, N, g=g)
+        want = ref + aux.float()
+    if base == 5:
+        bits = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
+        kw["bits"] = bits
+        want = torch.where(_unpack(bits, M, N), want, ref)
+    if epi >= 6:
+        z3 = _rnd(M, N, g=g)
+        bits2 = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
+        mean, invstd = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
+        kw.update(aux2=z3, bits2=bits2, mean=mean, invstd=invstd)
+        want = want * _unpack(bits2, M, N)
+    if epi == 9:
+        zd = _rnd(M, N, g=g)
+        m2, i2 = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
+        kw.update(aux3=zd, mean2=m2, invstd2=i2)
+    c, part = native().conv_gemm(a, b, gg, None, epi, aux, **kw)
+    _close(c, want)
+    if epi < 6:
+        assert part is None or part.numel() == 0
+        return
+    assert part.shape == (3 if epi == 9 else 2, (M + 255) // 256, N)
+    cg = c.float()
+    torch.testing.assert_close(part[0].sum(0), cg.sum(0), rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(part[1].sum(0), (cg * ((z3.float() - mean) * invstd)).sum(0), rtol=1e-3, atol=5e-2)
+    if epi == 9:
+        torch.testing.assert_close(part[2].sum(0), (cg * ((zd.float() - m2) * i2)).sum(0), rtol=1e-3, atol=5e-2)
+
+
+@pytest.mark.parametrize("M,K,N,epi", [(131101, 64, 256, 1), (131101, 128, 512, 0), (65613, 256, 1024, 3),
+                                       (65613, 256, 512, 6), (65613, 256, 512, 9), (70000, 512, 256, 1)])
+def test_big_tile_128_channel_tiles(monkeypatch, M, K, N, epi):
+    """256 x 128 tiles (256-thread blocks, two per CU, 3-deep ring of 32-deep stages) vs fp32: the
+    store, BN statistics, data-gradient and fold epilogues, K from 64 up."""
+    monkeypatch.setenv("PS_AMD_CONV_BIG_TN", "128")
+    g = _gen(M + K + N + epi)
+    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    gg = [M, 1, M, 1, 1, 1, 0]
+    bm, bn, gm = native().conv_gemm_plan(M, N, K, gg, False, epi)
+    assert (bm, bn, gm) == (256, 128, (M + 255) // 256)
+    ref = a.float() @ b.float().t()
+    if epi == 0:
+        _close(native().conv_gemm(a, b, gg)[0], ref)
+        return
+    if epi == 1:
+        kshift = torch.randn(N, generator=g, device=DEV) * 0.1
+        c, part = native().conv_gemm(a, b, gg, None, 1, None, kshift)
+        _close(c, ref)
+        cb = c.float() - kshift
+        torch.testing.assert_close(part[0].sum(0), cb.sum(0), rtol=1e-4, atol=5e-2)
+        torch.testing.assert_close(part[1].sum(0), (cb * cb).sum(0), rtol=1e-4, atol=5e-2)
+        return
+    mean, invstd = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
+    if epi == 3:
+        z = _rnd(M, N, g=g)
+        mc = _coef(N, g)
+        c, part = native().conv_gemm(a, b, gg, None, 3, z, None, mc, mean, invstd)
+        _close(c, ref * ((z.float() * mc[:N] + mc[N:]) > 0))
+    else:
+        aux, z = _rnd(M, N, g=g), _rnd(M, N, g=g)
+        bits = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
+        bits2 = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
+        kw = dict(bits=bits, aux2=z, bits2=bits2, mean=mean, invstd=invstd)
+        if epi == 9:
+            zd = _rnd(M, N, g=g)
+            m2, i2 = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
+            kw.update(aux3=zd, mean2=m2, invstd2=i2)
+        c, part = native().conv_gemm(a, b, gg, None, epi, aux, **kw)
+        r = ref.bfloat16().float()
+        want = torch.where(_unpack(bits, M, N), r + aux.float(), r) * _unpack(bits2, M, N)
+        _close(c, want)
+        if epi == 9:
+            torch.testing.assert_close(part[2].sum(0), (c.float() * ((zd.float() - m2) * i2)).sum(0),
+                                       rtol=1e-3, atol=5e-2)
+    cg = c.float()
+    torch.testing.assert_close(part[0].sum(0), cg.sum(0), rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(part[1].sum(0), (cg * ((z.float() - mean) * invstd)).sum(0), rtol=1e-3, atol=5e-2)
