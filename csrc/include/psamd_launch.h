@@ -356,6 +356,12 @@ struct ConvGemmArgs {
   FastDiv fd_ohw, fd_ow;  // set by launch_conv_fwd (OH * OW, OW)
   int pgm;                // rows per partial slab (0: the launch's gm); several GEMMs share one part
   uint64_t* tbuf = nullptr;  // conv_big only, diagnostics: 8 wall-clock stamps per block (nullable)
+  // conv_big stream-K (set by its launcher): block c owns (tile, stage) units [c sk_units, ..);
+  // a tile split across blocks is finished by the block holding its first stage, which adds the
+  // others' fp32 partials (sk_ws, one slot per block) once their flag reads sk_epoch
+  float* sk_ws = nullptr;
+  int* sk_flag = nullptr;
+  int sk_units = 0, sk_epoch = 0;
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)

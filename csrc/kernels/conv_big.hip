@@ -19,6 +19,9 @@
 // Blocks are XCD-remapped so the channel tiles of one pixel tile share its A rows in one L2.
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -38,8 +41,10 @@ constexpr int kTM = 256;
 //   0  256 x 256 tile, 8 waves of 128 px x 64 ch, one 512-thread block per CU, 128 KiB ring;
 //   1  256 x 128 tile, 4 waves of 128 x 64, 256-thread blocks two per CU, a 72 KiB ring of three
 //      32-deep stages (one block's epilogue can overlap the other's K loop);
-//   2  256 x 256 tile, 4 waves of 128 px x 128 ch (256 accumulators each, one wave per SIMD):
-//      8 fragment reads per 16 MFMAs instead of 6 per 8 -- a third less LDS read traffic per FLOP.
+//   2  256 x 256 tile, 4 waves of 128 px x 128 ch (256 accumulators each, one wave per SIMD): a
+//      third less LDS read traffic per FLOP, but 7-24 % slower (the K loop is bound by the stage
+//      DMAs, not LDS reads, and one wave per SIMD hides less latency: profiles/r5_conv_big_kloop.txt);
+//      kept compilable, not launched.
 constexpr int cfg_tn(int cfg) { return cfg == 1 ? 128 : 256; }
 constexpr int cfg_waves(int cfg) { return cfg == 0 ? 8 : 4; }
 constexpr int cfg_ring(int cfg) { return cfg == 1 ? 73728 : 131072; }
@@ -106,7 +111,7 @@ __device__ __forceinline__ int bswz(int r, int c) {
 // once the pass over stage kt has read it.  With a 256-wide channel tile the A rows are staged
 // (and transformed) once per channel tile -- once in all for N = 256, and for wider N the other
 // channel tiles of the pixel tile run on the same XCD (L2 re-reads, not HBM).
-template <int EPI, int BK, int PRO, int CFG>
+template <int EPI, int BK, int PRO, int CFG, bool SK = false>
 __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_big_kernel(const ConvGemmArgs p) {
   static_assert(EPI >= 0 && EPI <= 9, "conv_gemm's epilogues");
   static_assert(BK == 64 || BK == 32, "stage depth");
@@ -138,19 +143,45 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   const uint32_t L0 = lds_addr(lds);
 
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int fr = lane & 31, fh = lane >> 5;
   const int nN = p.N / kTN, mtiles = (p.M + kTM - 1) / kTM;
-  const int L = xcd_remap_big(blockIdx.x, gridDim.x);
-  const int mt = L / nN, n0 = (L - mt * nN) * kTN;
-  const int m0 = mt * kTM;
   const ConvGeo& g = p.g;
   const int nk = p.K / BK;
   // diagnostics (p.tbuf set by probes only): wall-clock stamps of this block's phases
   auto stamp = [&](int i) {
-    if (p.tbuf != nullptr && t == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + i] = wall_clock64();
+    if (p.tbuf != nullptr && threadIdx.x == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + i] = wall_clock64();
   };
   stamp(0);
+  // ---- work: one tile over all of K, or (SK) the contiguous (tile, stage) units of this block --
+  // the last round of a grid with few tiles per CU leaves most CUs idle; stream-K spreads the units
+  const int cself = xcd_remap_big(blockIdx.x, gridDim.x);
+  int u = 0, u_end = 1;
+  if constexpr (SK) {
+    const int tot = mtiles * nN * nk;
+    u = min(tot, cself * p.sk_units);
+    u_end = min(tot, (cself + 1) * p.sk_units);
+  }
+  while (u < u_end) {
+  int L, kb, ke;
+  if constexpr (SK) {
+    L = u / nk;
+    kb = u - L * nk;
+    ke = min(nk, kb + (u_end - u));
+    u += ke - kb;
+    lds_bar();  // the previous item's epilogue is done with the LDS
+  } else {
+    L = cself;
+    kb = 0;
+    ke = nk;
+    u = u_end;
+  }
+  const int mt = L / nN, n0 = (L - mt * nN) * kTN;
+  const int m0 = mt * kTM;
+  // per-thread indices from an opaque copy of threadIdx: nothing derived from them is hoisted out of
+  // the SK item loop (kept live across the epilogue, it spilled)
+  int tid = threadIdx.x;
+  if constexpr (SK) asm volatile("" : "+v"(tid));
+  const int t = tid, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
 
   // ---- DMA sources: lane-linear LDS rows, swizzled source chunk; A rows past M read zeros
   const int lrow = lane / CPR, lch = lane % CPR;
@@ -357,24 +388,24 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   if constexpr (PRO != 0) {
     // stage kt + 1 (and a2 of kt + 1 once the pass over kt has read the a2 tile) in flight behind
     // stage kt's pass and MFMAs; the pass's aout stores drain with them
-    issue(0, 0);
-    if constexpr (TWO) issue_z(0);
-    for (int kt = 0; kt < nk; ++kt) {
+    issue(kb, 0);
+    if constexpr (TWO) issue_z(kb);
+    for (int kt = kb; kt < ke; ++kt) {
       wait_vm<0>();
       lds_bar();  // stage kt (and its a2 tile) landed; every wave is done with stage kt - 1
       load_coef(kt);
-      if (kt + 1 < nk) {
-        issue(kt + 1, (kt + 1) & 1);
+      if (kt + 1 < ke) {
+        issue(kt + 1, (kt + 1 - kb) & 1);
         wait_vm<GPS>();  // the coefficients (older than the stage's GPS DMAs)
       } else {
         wait_vm<0>();
       }
-      transform(kt, kt & 1);
+      transform(kt, (kt - kb) & 1);
       lds_bar();  // the A tile is transformed and the a2 tile is free
       if constexpr (TWO) {
-        if (kt + 1 < nk) issue_z(kt + 1);
+        if (kt + 1 < ke) issue_z(kt + 1);
       }
-      const uint32_t sb = L0 + static_cast<uint32_t>((kt & 1) * STAGE);
+      const uint32_t sb = L0 + static_cast<uint32_t>(((kt - kb) & 1) * STAGE);
       fetch(sb, 0, 0);
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
@@ -391,18 +422,22 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   // ---- prologue: stages 0 .. NST - 2 in flight
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) {
-    if (PRO == 0 && s < nk) issue(s, s);
+    if (PRO == 0 && kb + s < ke) issue(kb + s, s);
   }
-  for (int kt = 0; kt < (PRO == 0 ? nk : 0); ++kt) {
-    // stage kt landed (this wave's DMAs): younger are the min(NST - 2, nk - 1 - kt) stages after it
-    const int younger = min(NST - 2, nk - 1 - kt);
-    if (younger >= 2) wait_vm<2 * GPS>();
-    else if (younger == 1) wait_vm<GPS>();
-    else wait_vm<0>();
+  for (int kt = kb; kt < (PRO == 0 ? ke : kb); ++kt) {
+    // stage kt landed (this wave's DMAs): younger are the min(NST - 2, ke - 1 - kt) stages after it
+    const int younger = min(NST - 2, ke - 1 - kt);
+    if (younger >= 2) {
+      wait_vm<2 * GPS>();
+    } else if (younger == 1) {
+      wait_vm<GPS>();
+    } else {
+      wait_vm<0>();
+    }
     lds_bar();  // every wave's stage kt landed; every wave is done with stage kt - 1's buffer
-    if (kt == 0) stamp(1);
-    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
-    const uint32_t sb = L0 + static_cast<uint32_t>((kt % NST) * STAGE);
+    if (kt == kb) stamp(1);
+    if (kt + NST - 1 < ke) issue(kt + NST - 1, (kt - kb + NST - 1) % NST);
+    const uint32_t sb = L0 + static_cast<uint32_t>(((kt - kb) % NST) * STAGE);
     fetch(sb, 0, 0);
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
@@ -418,6 +453,49 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   stamp(2);
   wait_vm<0>();
   lds_bar();  // the output tile overlays the stage ring
+
+  if constexpr (SK) {
+    // partial slots: [block][TI * 16 float4 groups][NT threads], coalesced per group
+    constexpr int NG = TI * 4 * 4;
+    if (kb > 0) {  // a continuation piece: fp32 partial to this block's slot, then its flag
+      f32x4* dst = reinterpret_cast<f32x4*>(p.sk_ws) + static_cast<int64_t>(cself) * NG * NT + t;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            dst[((i * 4 + j) * 4 + q4) * NT] = f32x4{acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2],
+                                                    acc[i][j][4 * q4 + 3]};
+      __threadfence();
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(p.sk_flag + cself, p.sk_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    // the first piece finishes the tile: the following blocks' pieces, added in block order
+    for (int c2 = cself + 1, done = ke; done < nk; ++c2) {
+      if (t == 0) {  // bounded: a piece that never lands (a bug) gives a wrong tile, not a hung GPU
+        const long long w0 = wall_clock64();
+        while (__hip_atomic_load(p.sk_flag + c2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+               wall_clock64() - w0 < 50000000)
+          __builtin_amdgcn_s_sleep(2);
+      }
+      __syncthreads();
+      __threadfence();
+      const f32x4* src = reinterpret_cast<const f32x4*>(p.sk_ws) + static_cast<int64_t>(c2) * NG * NT + t;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const f32x4 v = __builtin_nontemporal_load(src + ((i * 4 + j) * 4 + q4) * NT);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][4 * q4 + e] += v[e];
+          }
+      done += min(nk - done, p.sk_units);
+    }
+  }
 
   // ---- accumulators -> bf16 output tile [256 px][kCS]: register q of acc[i][j] is channel
   // 64 wn + 32 i + 8 (q >> 2) + 4 fh + (q & 3) of pixel 128 wm + 32 j + fr
@@ -581,11 +659,12 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
       if constexpr (FOLD_DS) p.part[(2 * PG + mt) * p.N + n0 + t] = c3;
     }
   }
+  }  // work items
   if (p.tbuf != nullptr) {
     stamp(4);  // stores issued
     wait_vm<0>();
     stamp(5);  // thread 0's stores acknowledged
-    if (t == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + 6] = __smid();
+    if (threadIdx.x == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + 6] = __smid();
   }
 }
 
@@ -593,15 +672,6 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
 bool big_tn128(int M, int N, int K, const ConvGeo& g, int epi) {
   (void)M, (void)N, (void)K, (void)g, (void)epi;
   return false;
-}
-
-// PS_AMD_CONV_BIG_W4=1: the 256 x 256 tiles as 4 waves of 128 x 128 (CFG 2)
-bool big_w4() {
-  static const bool w4 = [] {
-    const char* e = std::getenv("PS_AMD_CONV_BIG_W4");
-    return e != nullptr && e[0] == '1';
-  }();
-  return w4;
 }
 
 int big_bk() {
@@ -614,12 +684,86 @@ int big_bk() {
 
 }  // namespace
 
-// the 256-channel-tile launches (CFG 0: 8 waves, CFG 2: 4 waves of 128 x 128)
+// stream-K workspace of one (device, stream): a partial slot (256 KiB) and a flag per block
+struct SkWorkspace {
+  float* ws = nullptr;
+  int* flag = nullptr;
+  int nslots = 0, epoch = 0;
+};
+static SkWorkspace& sk_workspace(hipStream_t s, int nslots) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> all;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  SkWorkspace& w = all[{dev, s}];
+  if (w.nslots < nslots) {
+    if (w.ws != nullptr) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(w.ws);
+      (void)hipFree(w.flag);
+    }
+    (void)hipMalloc(reinterpret_cast<void**>(&w.ws), static_cast<size_t>(nslots) * 512 * 32 * 16);
+    (void)hipMalloc(reinterpret_cast<void**>(&w.flag), static_cast<size_t>(nslots) * sizeof(int));
+    (void)hipMemsetAsync(w.flag, 0, static_cast<size_t>(nslots) * sizeof(int), s);
+    w.nslots = nslots;
+    w.epoch = 0;
+  }
+  return w;
+}
+static int device_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (n[dev & 63] == 0) {
+    hipDeviceProp_t pr;
+    (void)hipGetDeviceProperties(&pr, dev);
+    n[dev & 63] = pr.multiProcessorCount;
+  }
+  return n[dev & 63];
+}
+// stream-K units per block (0: one tile per block).  PS_AMD_CONV_BIG_SK=0 never, =1 whenever the
+// pieces are >= 4 stages; default: when the last round of tiles would leave > 10 % of the CU-rounds idle
+static int sk_units_for(int tiles, int nk, int ncu) {
+  const char* me = std::getenv("PS_AMD_CONV_BIG_SK");  // per call: tests switch it in-process
+  const int mode = me == nullptr ? 0 : std::atoi(me);
+  if (mode == 0 || ncu <= 0) return 0;
+  const int rounds = (tiles + ncu - 1) / ncu;
+  if (mode == 2 && tiles >= static_cast<int64_t>(rounds) * ncu * 9 / 10) return 0;
+  const int64_t tot = static_cast<int64_t>(tiles) * nk;
+  const int units = static_cast<int>((tot + ncu - 1) / ncu);
+  return units >= 4 ? units : 0;
+}
+
+template <int E, int BK, int P, int C>
+static void big_launch(const ConvGemmArgs& a, hipStream_t s, int nblk) {
+  if constexpr (C == 0 && BK == 64) {
+    if (a.sk_units > 0) {
+      hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C, true>), dim3(nblk), dim3(512), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C, false>), dim3(nblk), dim3(64 * cfg_waves(C)), 0, s, a);
+}
+
+// the 256-channel-tile launches
 template <int C>
-static void launch_big256(const ConvGemmArgs& a, hipStream_t s, bool bwd, bool resp) {
-  const int nblk = conv_big_gm(a.M) * (a.N / 256);
-  const dim3 blk(64 * cfg_waves(C));
-#define PSAMD_BIG(E, BK, P) hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C>), dim3(nblk), blk, 0, s, a)
+static void launch_big256(const ConvGemmArgs& a0, hipStream_t s, bool bwd, bool resp) {
+  ConvGemmArgs a = a0;
+  int nblk = conv_big_gm(a.M) * (a.N / 256);
+  if (C == 0 && a.tbuf == nullptr && !(big_bk() == 32 && !bwd && !resp && a.pro == nullptr)) {
+    const int ncu = device_cus();
+    const int units = sk_units_for(nblk, a.K / 64, ncu);
+    if (units > 0) {
+      SkWorkspace& w = sk_workspace(s, ncu);
+      a.sk_ws = w.ws;
+      a.sk_flag = w.flag;
+      a.sk_units = units;
+      a.sk_epoch = ++w.epoch;
+      nblk = ncu;
+    }
+  }
+#define PSAMD_BIG(E, BK, P) big_launch<E, BK, P, C>(a, s, nblk)
   if (bwd) {
     switch (a.epi) {
       case 2: PSAMD_BIG(2, 64, 2); break;
@@ -737,8 +881,7 @@ void launch_conv_big(const ConvGemmArgs& a, hipStream_t s) {
 #undef PSAMD_BIG128
     return;
   }
-  if (big_w4()) launch_big256<2>(a, s, bwd, resp);
-  else launch_big256<0>(a, s, bwd, resp);
+  launch_big256<0>(a, s, bwd, resp);
 }
 
 

@@ -70,7 +70,7 @@ def main():
         torch.cuda.empty_cache()
 
 
-if __name__ == "__main__" and not any(a.startswith("--fold") or a in ("--pro", "--tn") for a in sys.argv):
+if __name__ == "__main__" and not any(a.startswith("--fold") or a in ("--pro", "--tn", "--blas") for a in sys.argv):
     main()
 
 
@@ -272,3 +272,27 @@ def main_tn():
 
 if __name__ == "__main__" and "--tn" in sys.argv:
     main_tn()
+
+
+def main_blas():
+    """The same GEMMs through torch.mm (hipBLASLt / rocBLAS): a ceiling check for the plain K loop."""
+    nat = native()
+    for name, h, k, co, s, epi in SHAPES:
+        if s != 1:
+            continue
+        M = 1024 * h * h
+        a = (torch.randn(M, k, device="cuda") * 0.5).bfloat16()
+        b = (torch.randn(co, k, device="cuda") * k ** -0.5).bfloat16()
+        bt = b.t()
+        t = timeit(lambda: torch.mm(a, bt))
+        gg = [M, 1, M, 1, 1, 1, 0]
+        t2 = timeit(lambda: nat.conv_gemm(a, b, gg))
+        print(json.dumps({"shape": name, "M": M, "K": k, "N": co, "torch_mm_ms": round(t, 4),
+                          "torch_TFs": round(2.0 * M * k * co / t / 1e9, 1), "ours_epi0_ms": round(t2, 4),
+                          "ours_TFs": round(2.0 * M * k * co / t2 / 1e9, 1)}), flush=True)
+        del a, b, bt
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__" and "--blas" in sys.argv:
+    main_blas()

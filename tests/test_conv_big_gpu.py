@@ -315,3 +315,53 @@ def test_big_tile_128_channel_tiles(monkeypatch, M, K, N, epi):
     cg = c.float()
     torch.testing.assert_close(part[0].sum(0), cg.sum(0), rtol=1e-4, atol=5e-2)
     torch.testing.assert_close(part[1].sum(0), (cg * ((z.float() - mean) * invstd)).sum(0), rtol=1e-3, atol=5e-2)
+
+
+@pytest.mark.parametrize("M,K,N,epi,kind", [(33001, 1024, 512, 1, "plain"), (16411, 2048, 1024, 3, "plain"),
+                                            (33001, 1024, 512, 3, "bwd"), (33001, 1024, 512, 1, "resp"),
+                                            (262213, 256, 256, 6, "plain")])
+def test_big_tile_stream_k_matches_one_tile_per_block(monkeypatch, M, K, N, epi, kind):
+    """Stream-K (a block per CU walking contiguous (tile, stage) units; a split tile finished by the
+    block holding its first stage, which adds the others' fp32 partials in block order) vs one tile
+    per block (PS_AMD_CONV_BIG_SK=0) and vs fp32: same outputs up to summation order, same partials,
+    the prologue's side outputs identical, and bitwise repeatable."""
+    g = _gen(M + K + epi)
+    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
+    gg = [M, 1, M, 1, 1, 1, 0]
+    pos, kw = (), {}
+    if epi == 1:
+        pos = (None, torch.zeros(N, device=DEV))
+    elif epi == 3:
+        pos = (_rnd(M, N, g=g), None, _coef(N, g), torch.randn(N, generator=g, device=DEV) * 0.1,
+               torch.rand(N, generator=g, device=DEV) + 0.5)
+    else:
+        bits = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
+        pos = (_rnd(M, N, g=g),)
+        kw = dict(bits=bits, aux2=_rnd(M, N, g=g), bits2=bits, mean=torch.zeros(N, device=DEV),
+                  invstd=torch.ones(N, device=DEV))
+    if kind == "bwd":
+        kw.update(a2=_rnd(M, K, g=g), bwd=torch.cat([torch.rand(K, generator=g, device=DEV) + 0.5,
+                                                     torch.randn(2 * K, generator=g, device=DEV) * 0.1]))
+    elif kind == "resp":
+        kw.update(a2=_rnd(M, K, g=g), aout=torch.empty(M, K, device=DEV, dtype=torch.bfloat16),
+                  abits=torch.empty(M * K // 8, device=DEV, dtype=torch.uint8))
+    pro = _coef(K, g) if kind == "resp" else None
+
+    def run():
+        kw2 = dict(kw)
+        if kind == "resp":
+            kw2["aout"], kw2["abits"] = torch.empty_like(kw["aout"]), torch.empty_like(kw["abits"])
+        r = native().conv_gemm(a, b, gg, pro, epi, *pos, **kw2)
+        return list(r) + ([kw2["aout"], kw2["abits"]] if kind == "resp" else [])
+
+    monkeypatch.setenv("PS_AMD_CONV_BIG_SK", "0")
+    ref = run()
+    monkeypatch.setenv("PS_AMD_CONV_BIG_SK", "1")
+    sk1, sk2 = run(), run()
+    for u, v in zip(sk1, sk2):
+        assert u is None or torch.equal(u, v)
+    _close(sk1[0], ref[0], tol=5e-3)
+    if ref[1] is not None:
+        torch.testing.assert_close(sk1[1].sum(1), ref[1].sum(1), rtol=1e-3, atol=5e-2)
+    for u, v in zip(sk1[2:], ref[2:]):  # the prologue's stored operand (dz or the block output, bits)
+        assert torch.equal(u, v)
