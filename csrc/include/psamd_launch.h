@@ -362,6 +362,7 @@ struct ConvGemmArgs {
   float* sk_ws = nullptr;
   int* sk_flag = nullptr;
   int sk_units = 0, sk_epoch = 0;
+  int krot = 0;  // conv_big: rotate each tile's K order by (tile mod stages)
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)

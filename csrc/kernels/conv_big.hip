@@ -176,6 +176,10 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   }
   const int mt = L / nN, n0 = (L - mt * nN) * kTN;
   const int m0 = mt * kTM;
+  // K-order rotation (p.krot): tile L walks its stages from (L mod nk), so the CUs of an XCD read
+  // different weight slices at a time instead of all the same 32 KiB of B
+  const int rot = p.krot ? L % nk : 0;
+  auto kmap = [&](int kt) { return kt + rot >= nk ? kt + rot - nk : kt + rot; };
   // per-thread indices from an opaque copy of threadIdx: nothing derived from them is hoisted out of
   // the SK item loop (kept live across the epilogue, it spilled)
   int tid = threadIdx.x;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
     bsrc[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + bswz<BK>(r, lch) * 8;
   }
   auto issue_z = [&](int kt) {
-    const int k0 = kt * BK;
+    const int k0 = kmap(kt) * BK;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const uint16_t* src = ((aok >> i) & 1u) ? p.a2 + abase[i] + k0 : kBigZero;
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   constexpr int NCO = PRO == 1 ? 4 : PRO == 2 ? 6 : 8;
   f32x4 co[NCO];
   auto load_coef = [&](int kt) {
-    const int cc = kt * BK + (t & 7) * 8;
+    const int cc = kmap(kt) * BK + (t & 7) * 8;
     const float* src[4] = {p.pro, p.pro, p.pro, p.pro};
     if constexpr (PRO == 2) {
       src[0] = p.bwd;
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   auto transform = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     const uint8_t* Zs = lds + Z_OFF;
-    const int lc = t & 7, tr0 = t >> 3, cc = kt * BK + lc * 8;
+    const int lc = t & 7, tr0 = t >> 3, cc = kmap(kt) * BK + lc * 8;
 #pragma unroll
     for (int i = 0; i < NCO; ++i) tie(co[i]);
     float c0[8], c1[8], c2[8], c3[8];
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   auto issue = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
-    const int k0 = kt * BK;
+    const int k0 = kmap(kt) * BK;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const uint16_t* src = ((aok >> i) & 1u) ? p.a + abase[i] + k0 : kBigZero;
@@ -455,44 +459,43 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   lds_bar();  // the output tile overlays the stage ring
 
   if constexpr (SK) {
-    // partial slots: [block][TI * 16 float4 groups][NT threads], coalesced per group
-    constexpr int NG = TI * 4 * 4;
+    // partial slots: [block][TI * 64 floats][NT threads], coalesced per float.  Written and read as
+    // agent-scope relaxed atomics (coherent across the XCDs' L2s without a release/acquire fence,
+    // which would write back / invalidate a whole L2 per piece: that made stream-K 2x slower)
+    constexpr int NF = TI * 4 * 16;
     if (kb > 0) {  // a continuation piece: fp32 partial to this block's slot, then its flag
-      f32x4* dst = reinterpret_cast<f32x4*>(p.sk_ws) + static_cast<int64_t>(cself) * NG * NT + t;
+      float* dst = p.sk_ws + static_cast<int64_t>(cself) * NF * NT + t;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4)
-            dst[((i * 4 + j) * 4 + q4) * NT] = f32x4{acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2],
-                                                    acc[i][j][4 * q4 + 3]};
-      __threadfence();
+          for (int q = 0; q < 16; ++q)
+            __hip_atomic_store(dst + ((i * 4 + j) * 16 + q) * NT, acc[i][j][q], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      wait_vm<0>();  // every store acknowledged before the flag
       __syncthreads();
-      if (t == 0) __hip_atomic_store(p.sk_flag + cself, p.sk_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) __hip_atomic_store(p.sk_flag + cself, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
     // the first piece finishes the tile: the following blocks' pieces, added in block order
     for (int c2 = cself + 1, done = ke; done < nk; ++c2) {
       if (t == 0) {  // bounded: a piece that never lands (a bug) gives a wrong tile, not a hung GPU
         const long long w0 = wall_clock64();
-        while (__hip_atomic_load(p.sk_flag + c2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+        while (__hip_atomic_load(p.sk_flag + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
                wall_clock64() - w0 < 50000000)
           __builtin_amdgcn_s_sleep(2);
       }
       __syncthreads();
-      __threadfence();
-      const f32x4* src = reinterpret_cast<const f32x4*>(p.sk_ws) + static_cast<int64_t>(c2) * NG * NT + t;
+      float* src = p.sk_ws + static_cast<int64_t>(c2) * NF * NT + t;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            const f32x4 v = __builtin_nontemporal_load(src + ((i * 4 + j) * 4 + q4) * NT);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][4 * q4 + e] += v[e];
-          }
+          for (int q = 0; q < 16; ++q)
+            acc[i][j][q] += __hip_atomic_load(src + ((i * 4 + j) * 16 + q) * NT, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
       done += min(nk - done, p.sk_units);
     }
   }
@@ -750,6 +753,8 @@ static void big_launch(const ConvGemmArgs& a, hipStream_t s, int nblk) {
 template <int C>
 static void launch_big256(const ConvGemmArgs& a0, hipStream_t s, bool bwd, bool resp) {
   ConvGemmArgs a = a0;
+  const char* kr = std::getenv("PS_AMD_CONV_BIG_KROT");
+  a.krot = kr != nullptr && kr[0] == '1' ? 1 : 0;
   int nblk = conv_big_gm(a.M) * (a.N / 256);
   if (C == 0 && a.tbuf == nullptr && !(big_bk() == 32 && !bwd && !resp && a.pro == nullptr)) {
     const int ncu = device_cus();
@@ -851,7 +856,11 @@ int conv_big_tn(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int e
   // prologue / epilogue outweigh the faster K loop unless K is deep (profiles/r5_conv_big_probe.txt:
   // at batch 256 the K = 256 / 512 shapes with 784 blocks ran 2-15 % slower, K >= 1024 faster)
   const int64_t nblk = mt * (N / 256);
-  return nblk >= 256 && (nblk >= 1024 || K >= 1024) ? 256 : 0;
+  if (nblk >= 256 && (nblk >= 1024 || K >= 1024)) return 256;
+  // with stream-K the last-round loss is gone: a deep K on fewer tiles (batch 256) can take them
+  const char* se = std::getenv("PS_AMD_CONV_BIG_SK_SMALL");
+  if (se != nullptr && se[0] == '1' && nblk >= 64 && K >= 512 && !(pro || src2 != 0)) return 256;
+  return 0;
 }
 
 bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {

@@ -17,4 +17,7 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 env PS_AMD_CONV_BIG_SK=0 timeout -k 10 300 python bench.py --steps 20 --warmup 8 > $O/bench_dp.json 2> $O/bench_dp.err && \
 timeout -k 10 300 python bench.py --steps 20 --warmup 8 > $O/bench_sk.json 2> $O/bench_sk.err && \
 timeout -k 10 300 python bench.py --batch-per-gpu 256 --steps 30 --warmup 10 > $O/bench256_sk.json 2> $O/bench256_sk.err && \
-env PS_AMD_CONV_BIG_SK=0 timeout -k 10 300 python bench.py --batch-per-gpu 256 --steps 30 --warmup 10 > $O/bench256_dp.json 2> $O/bench256_dp.err
+env PS_AMD_CONV_BIG_SK=0 timeout -k 10 300 python bench.py --batch-per-gpu 256 --steps 30 --warmup 10 > $O/bench256_dp.json 2> $O/bench256_dp.err && \
+# batch 256: deep-K GEMMs on fewer than 256 tiles through stream-K (PS_AMD_CONV_BIG_SK_SMALL=1)
+PS_AMD_CONV_BIG_SK_SMALL=1 timeout -k 10 300 python scripts/probe_conv_big.py > $O/big_sksmall.jsonl 2> $O/big_sksmall.err && \
+PS_AMD_CONV_BIG_SK_SMALL=1 timeout -k 10 300 python bench.py --batch-per-gpu 256 --steps 30 --warmup 10 > $O/bench256_sksmall.json 2> $O/bench256_sksmall.err
