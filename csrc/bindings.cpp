@@ -932,6 +932,7 @@ static void check_part_slabs(const Tensor& part) {
 
 static Tensor fold_partials(const Tensor& part, hipStream_t s) {
   const int G = static_cast<int>(part.size(1)), C = static_cast<int>(part.size(2));
+  if (psamd::bn_fin2_enabled(C)) return part;  // the one-launch finalize reads any G coalesced
   const int S = psamd::partials_fold_rows(G);
   if (S == 0) return part;
   auto f = torch::empty({2, S, C}, part.options());

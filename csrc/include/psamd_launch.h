@@ -229,6 +229,8 @@ int stem_wrw_blocks(int N, int OH);
 int partials_fold_rows(int G);
 void launch_partials_fold(const float* p, const float* q, int G, int C, float* op, float* oq, hipStream_t s);
 // BN finalize from producer-fused partial sums ps/pq: [G][C] of sum(x - k), sum((x - k)^2)
+// the one-launch coalesced finalize (bn_fin2_kernel) serves this C: callers skip the partials fold
+bool bn_fin2_enabled(int C);
 void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,
                              float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
