@@ -45,6 +45,8 @@ constexpr int kTM = 256;
 //      third less LDS read traffic per FLOP, but 7-24 % slower (the K loop is bound by the stage
 //      DMAs, not LDS reads, and one wave per SIMD hides less latency: profiles/r5_conv_big_kloop.txt);
 //      kept compilable, not launched.
+// (A register-staged ring -- global_load_dwordx4 -> VGPRs -> ds_write_b128 -- ran 0-12 % slower
+// than the LDS-DMA ring: profiles/r5_conv_big_kloop.txt.)
 constexpr int cfg_tn(int cfg) { return cfg == 1 ? 128 : 256; }
 constexpr int cfg_waves(int cfg) { return cfg == 0 ? 8 : 4; }
 constexpr int cfg_ring(int cfg) { return cfg == 1 ? 73728 : 131072; }
@@ -118,6 +120,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   static_assert(PRO == 0 || BK == 64, "the prologue variants run the 2 x 64-deep ring");
   static_assert(PRO != 2 || (EPI != 0 && EPI != 1), "the BN-backward prologue feeds a data-gradient GEMM");
   static_assert(CFG != 1 || (BK == 32 && PRO == 0), "128-channel tiles: plain 32-deep ring");
+
   constexpr int TN = cfg_tn(CFG), NW = cfg_waves(CFG), NT = 64 * NW;
   constexpr int WCH = CFG == 2 ? 128 : 64;        // channels per wave (2 waves along the pixels)
   constexpr int WN = TN / WCH, TI = WCH / 32;     // waves along the channels; 32-ch blocks per wave
