@@ -20,6 +20,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.dense import SplitKLinear
+from ..ops.linear import PsLinear
 from ..ops.transformer import (attention_causal_gqa, attention_qkv, cross_entropy, layer_norm_residual, rms_norm, rope_split,
                               rope_table, swiglu)
 
@@ -166,11 +167,12 @@ class LlamaBlock(nn.Module):
         self.c = c
         hd = c.hidden // c.heads
         self.attn_norm = RMSNorm(c.hidden, c.eps)
-        self.wqkv = nn.Linear(c.hidden, (c.heads + 2 * c.kv_heads) * hd, bias=False)
-        self.wo = nn.Linear(c.heads * hd, c.hidden, bias=False)
+        # PsLinear: the weight gradient lands straight in the PS gradient bucket (ops/linear.py)
+        self.wqkv = PsLinear(c.hidden, (c.heads + 2 * c.kv_heads) * hd, bias=False)
+        self.wo = PsLinear(c.heads * hd, c.hidden, bias=False)
         self.mlp_norm = RMSNorm(c.hidden, c.eps)
-        self.w13 = nn.Linear(c.hidden, 2 * c.ffn, bias=False)
-        self.w2 = nn.Linear(c.ffn, c.hidden, bias=False)
+        self.w13 = PsLinear(c.hidden, 2 * c.ffn, bias=False)
+        self.w2 = PsLinear(c.ffn, c.hidden, bias=False)
 
     def forward(self, x, r, cs):
         """Residual stream = x + r (r: the previous block's pending MLP output, None for the
@@ -198,7 +200,7 @@ class LlamaForCausalLM(nn.Module):
         self.embed = nn.Embedding(c.vocab, c.hidden)
         self.layers = nn.ModuleList(LlamaBlock(c) for _ in range(c.layers))
         self.norm = RMSNorm(c.hidden, c.eps)
-        self.lm_head = nn.Linear(c.hidden, c.vocab, bias=False)
+        self.lm_head = PsLinear(c.hidden, c.vocab, bias=False)
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)

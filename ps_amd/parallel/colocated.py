@@ -268,9 +268,20 @@ class ColocatedPS:
         return flat.view(ki.shape)
 
     def _bind(self, wslot: int, gslot: int) -> None:
+        from ..ops.linear import GradDst
+
         for n, p in self.params.items():
             p.data = self._view(self.wbuf, wslot, n)
             p.grad = None  # AccumulateGrad adopts the fresh gradient; _land() copies it in
+            if self.gpu and n not in self.cl_keys:
+                # where this step's gradient lives: a producer that knows it (ops/linear.py
+                # PsLinear) writes there directly and _land() has nothing to copy
+                ki = self.reg.keys[n]
+                d = getattr(p, "_ps_gdst", None)
+                if d is None:
+                    p._ps_gdst = GradDst(self.gbuf[ki.group][gslot], ki.offset, ki.numel, ki.shape)
+                else:
+                    d.buf, d.off, d.claimed = self.gbuf[ki.group][gslot], ki.offset, False
 
     def weight(self, name: str) -> torch.Tensor:
         """Current replica weights of key ``name`` (the pulled version)."""

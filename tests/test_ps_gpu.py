@@ -96,3 +96,42 @@ def test_ps_clip_norm():
     torch.cuda.synchronize()
     for p, q in zip(m.parameters(), ref.parameters()):
         torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
+
+
+def test_ps_linear_grads_land_in_bucket_and_match():
+    """Tiny Llama on the colocated PS: with PsLinear (ops/linear.py) the projection weights'
+    gradients are written into the bound gradient slot (p.grad IS the bucket view, nothing left
+    for the landing to copy) and the trained weights track an nn.Linear-only twin step for step."""
+    from ps_amd.models.transformer import LlamaConfig, LlamaForCausalLM
+    from ps_amd.ops.linear import PsLinear
+
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny()
+    a = LlamaForCausalLM(cfg).cuda()
+    b = copy.deepcopy(a)
+    for mod in b.modules():  # the twin: plain nn.Linear forwards
+        if isinstance(mod, PsLinear):
+            mod.forward = lambda x, _m=mod: F.linear(x, _m.weight, _m.bias)
+    pa = ColocatedPS(a, AdamUpdater(1e-3, 0.9, 0.95, 1e-8, bias_correction="step"), bucket_mb=0.05)
+    pb = ColocatedPS(b, AdamUpdater(1e-3, 0.9, 0.95, 1e-8, bias_correction="step"), bucket_mb=0.05)
+    ids = torch.randint(0, cfg.vocab, (2, 64), device="cuda")
+    in_place = []
+    for step in range(4):
+        la = a(ids, ids)
+        la.backward()
+        if step == 0:
+            for n, p in a.named_parameters():
+                if n.endswith(("wqkv.weight", "wo.weight", "w13.weight", "w2.weight", "lm_head.weight")):
+                    v = pa._view(pa.gbuf, pa.gslot, n)
+                    in_place.append(p.grad is not None and p.grad.data_ptr() == v.data_ptr())
+        pa.finish_step()
+        lb = b(ids, ids)
+        lb.backward()
+        pb.finish_step()
+        torch.testing.assert_close(la.float(), lb.float(), rtol=2e-2, atol=2e-2)
+    assert in_place and all(in_place), in_place
+    pa.synchronize()
+    pb.synchronize()
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        torch.testing.assert_close(p.float(), q.float(), rtol=2e-2, atol=2e-3)
