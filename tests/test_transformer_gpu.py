@@ -45,6 +45,28 @@ def test_rmsnorm_fwd_bwd(R, D, wdtype, residual):
     _close(w.grad, wr.grad)
 
 
+@pytest.mark.parametrize("used", ["y", "s"])
+def test_rmsnorm_residual_one_output_used(used):
+    """Only one of (stream s, normed y) feeds the loss (the final norm drops s): autograd hands the
+    backward None for the other (no zero-filled tensor) and the gradients match the reference."""
+    torch.manual_seed(3)
+    R, D = 96, 1024
+    x = torch.randn(R, D, device="cuda").bfloat16().requires_grad_(True)
+    r = torch.randn(R, D, device="cuda").bfloat16().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+    xr, rr, wr = (t.detach().float().requires_grad_(True) for t in (x, r, w))
+    s, y = T.rms_norm(x, w, 1e-5, residual=r)
+    sr = xr + rr
+    yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    g = torch.randn(R, D, device="cuda").bfloat16()
+    (y if used == "y" else s).backward(g)
+    (yr if used == "y" else sr).backward(g.float())
+    _close(x.grad, xr.grad)
+    _close(r.grad, rr.grad)
+    if used == "y":
+        _close(w.grad, wr.grad)
+
+
 @pytest.mark.parametrize("R,D", [(512, 768), (33, 1024), (8, 64)])
 @pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
 def test_layernorm_residual_no_dropout(R, D, wdtype):
