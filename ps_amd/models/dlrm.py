@@ -34,7 +34,10 @@ def mlp(dims: Sequence[int], last_act: bool = True) -> nn.Sequential:
         # nn.Linear with split-K weight gradients on GPU bf16 (batch-long reductions into small dW)
         layers.append(SplitKLinear(dims[i], dims[i + 1]))
         if i < len(dims) - 2 or last_act:
-            layers.append(nn.ReLU())
+            # the ReLU runs inside the linear (bias + ReLU GEMM epilogue); the Identity keeps the
+            # Sequential's indices, so state_dict keys are those of Linear / ReLU pairs
+            layers[-1].fuse_relu = True
+            layers.append(nn.Identity())
     return nn.Sequential(*layers)
 
 

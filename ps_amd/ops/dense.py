@@ -101,14 +101,23 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 
 class _SplitKLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+    def forward(ctx, x, w, b, relu=False):
         ctx.has_b = b is not None
+        ctx.relu = relu
+        if relu:  # bias + ReLU in the GEMM epilogue (hipBLASLt RELU_BIAS): no separate activation pass
+            y = torch._addmm_activation(b, x.reshape(-1, x.shape[-1]), w.t()).view(*x.shape[:-1], w.shape[0])
+            ctx.save_for_backward(x, w, y)
+            return y
+        ctx.save_for_backward(x, w)
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        if ctx.relu:
+            x, w, y = ctx.saved_tensors
+            dy = torch.ops.aten.threshold_backward(dy, y, 0)  # ReLU'(y), the pass nn.ReLU's backward was
+        else:
+            x, w = ctx.saved_tensors
         n, k = w.shape
         dy2 = dy.reshape(-1, n)
         dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
@@ -127,17 +136,27 @@ class _SplitKLinear(torch.autograd.Function):
             dw = dw.to(w.dtype)
         if want_db and db is None:
             db = dy2.sum(0).to(w.dtype)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class SplitKLinear(torch.nn.Linear):
     """nn.Linear (same parameters / state_dict) whose weight gradient runs split-K on GPU bf16
-    when the reduction (tokens) is long and the output small (``linear_wgrad``)."""
+    when the reduction (tokens) is long and the output small (``linear_wgrad``).  ``fuse_relu``:
+    the layer applies ReLU itself, in the GEMM epilogue on GPU bf16 (``mlp`` sets it and puts a
+    parameter-free ``nn.Identity`` where the ``nn.ReLU`` was, so state_dict keys do not move)."""
+
+    fuse_relu = False
 
     def forward(self, x):
         if x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled():
-            return _SplitKLinear.apply(x, self.weight, self.bias)
-        return super().forward(x)
+            relu = self.fuse_relu and self.bias is not None and _FUSED_RELU
+            y = _SplitKLinear.apply(x, self.weight, self.bias, relu)
+            return torch.relu(y) if self.fuse_relu and not relu else y
+        y = super().forward(x)
+        return torch.relu(y) if self.fuse_relu else y
+
+
+_FUSED_RELU = __import__("os").environ.get("PS_AMD_FUSED_RELU", "1") != "0"
 
 
 # ------------------------------------------------------------------------------ DLRM interaction

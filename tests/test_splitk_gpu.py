@@ -51,3 +51,32 @@ def test_splitk_linear_module_matches_linear():
     assert _rel(xa.grad, xb.grad) < 1e-2
     assert _rel(a.weight.grad, b.weight.grad) < 1e-2
     assert _rel(a.bias.grad, b.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T,K,N", [(65536, 512, 256), (8192, 256, 1024), (1000, 64, 32)])
+def test_splitk_linear_fused_relu_matches_linear_relu(T, K, N):
+    """SplitKLinear(fuse_relu): bias + ReLU in the GEMM epilogue, ReLU' before the split-K weight
+    gradient -- vs nn.Linear + ReLU in fp32 (forward, dx, dW, db)."""
+    from ps_amd.ops.dense import SplitKLinear
+
+    torch.manual_seed(T + K)
+    lin = SplitKLinear(K, N).cuda().bfloat16()
+    lin.fuse_relu = True
+    ref = torch.nn.Linear(K, N).cuda()
+    ref.weight.data.copy_(lin.weight.data.float())
+    ref.bias.data.copy_(lin.bias.data.float())
+    x = torch.randn(T, K, device="cuda").bfloat16().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    y = lin(x)
+    yr = torch.relu(ref(xr))
+    g = torch.randn(T, N, device="cuda").bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 2e-2
+    assert rel(lin.weight.grad, ref.weight.grad) < 2e-2
+    assert rel(lin.bias.grad, ref.bias.grad) < 2e-2
