@@ -54,11 +54,14 @@ class BertLayer(nn.Module):
     def forward(self, x, mask: Optional[torch.Tensor] = None):
         p = self.c.dropout if self.training else 0.0
         # fused MFMA attention over the qkv projection for S <= 128 (ops/transformer.py), SDPA else
-        a = attention_qkv(self.qkv(x), self.c.heads, p, mask)
+        # fork: x's residual gradient is added inside the qkv / fc1 data-gradient GEMM (ops/dense.py)
+        qkv, xr = self.qkv.fork(x)
+        a = attention_qkv(qkv, self.c.heads, p, mask)
         # post-LN epilogues: LN(x + dropout(sublayer)) as one fused HIP pass each way
-        x = layer_norm_residual(x, self.proj(a), self.ln1.weight, self.ln1.bias, self.c.eps, p, self.training)
-        f = self.fc2(F.gelu(self.fc1(x)))
-        return layer_norm_residual(x, f, self.ln2.weight, self.ln2.bias, self.c.eps, p, self.training)
+        x = layer_norm_residual(xr, self.proj(a), self.ln1.weight, self.ln1.bias, self.c.eps, p, self.training)
+        h, xr = self.fc1.fork(x)
+        f = self.fc2(F.gelu(h))
+        return layer_norm_residual(xr, f, self.ln2.weight, self.ln2.bias, self.c.eps, p, self.training)
 
 
 class BertForMLM(nn.Module):

@@ -139,6 +139,50 @@ class _SplitKLinear(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _SplitKLinearFork(torch.autograd.Function):
+    """(x W^T + b, x): the layer's input passed through as a second output, so a residual use of x
+    hands its gradient to THIS backward, which folds it into the data-gradient GEMM
+    (dxr += dy W, in place) -- autograd would otherwise sum the two branch gradients with a
+    separate add pass over [tokens, D] (25 per BERT-base step)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dxr):
+        x, w = ctx.saved_tensors
+        n, k = w.shape
+        dy2 = dy.reshape(-1, n)
+        dy2 = dy2 if dy2.is_contiguous() else dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if dxr is not None and dxr.is_contiguous() and dxr.dtype == dy2.dtype:
+                dx = dxr.view(-1, k).addmm_(dy2, w).view(x.shape)  # one GEMM with beta = 1
+            else:
+                dx = (dy2 @ w).view(x.shape)
+                if dxr is not None:
+                    dx = dx + dxr
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, k)
+            x2 = x2 if x2.is_contiguous() else x2.contiguous()
+            if want_db and _wgrad_ok(x2, dy2):
+                dw, db = native().linear_wgrad_db(dy2, x2)
+                db = db.to(w.dtype)
+            else:
+                dw = linear_wgrad(dy2, x2)
+            dw = dw.to(w.dtype)
+        if want_db and db is None:
+            db = dy2.sum(0).to(w.dtype)
+        return dx, dw, db
+
+
+_FORK = __import__("os").environ.get("PS_AMD_LINEAR_FORK", "1") != "0"
+
+
 class SplitKLinear(torch.nn.Linear):
     """nn.Linear (same parameters / state_dict) whose weight gradient runs split-K on GPU bf16
     when the reduction (tokens) is long and the output small (``linear_wgrad``).  ``fuse_relu``:
@@ -146,6 +190,14 @@ class SplitKLinear(torch.nn.Linear):
     parameter-free ``nn.Identity`` where the ``nn.ReLU`` was, so state_dict keys do not move)."""
 
     fuse_relu = False
+
+    def fork(self, x):
+        """(self(x), x) where the second output's gradient is added inside this layer's data-gradient
+        GEMM -- for an input that also feeds a residual (BertLayer)."""
+        if (_FORK and not self.fuse_relu and x.is_cuda and x.dtype == torch.bfloat16
+                and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()):
+            return _SplitKLinearFork.apply(x, self.weight, self.bias)
+        return self(x), x
 
     def forward(self, x):
         if x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled():

@@ -80,3 +80,27 @@ def test_splitk_linear_fused_relu_matches_linear_relu(T, K, N):
     assert rel(x.grad, xr.grad) < 2e-2
     assert rel(lin.weight.grad, ref.weight.grad) < 2e-2
     assert rel(lin.bias.grad, ref.bias.grad) < 2e-2
+
+
+def test_splitk_linear_fork_folds_residual_grad():
+    """SplitKLinear.fork: (x W^T + b, x) with the residual gradient added inside the data-gradient
+    GEMM -- vs nn.Linear + a residual use of x in fp32."""
+    from ps_amd.ops.dense import SplitKLinear
+
+    torch.manual_seed(7)
+    T, K, N = 8192, 768, 2304
+    lin = SplitKLinear(K, N).cuda().bfloat16()
+    ref = torch.nn.Linear(K, N).cuda()
+    ref.weight.data.copy_(lin.weight.data.float())
+    ref.bias.data.copy_(lin.bias.data.float())
+    x = torch.randn(T, K, device="cuda").bfloat16().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    y, xp = lin.fork(x)
+    yr = ref(xr)
+    gy, gx = torch.randn(T, N, device="cuda").bfloat16(), torch.randn(T, K, device="cuda").bfloat16()
+    (y.float() * gy.float()).sum().add_((xp.float() * gx.float()).sum()).backward()
+    ((yr * gy.float()).sum() + (xr * gx.float()).sum()).backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(lin.weight.grad, ref.weight.grad) < 2e-2
+    assert _rel(lin.bias.grad, ref.bias.grad) < 2e-2
