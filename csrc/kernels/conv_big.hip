@@ -13,10 +13,14 @@
 //     the ONE barrier of stage kt and waited for by a counted vmcnt, so NST - 1 stages stay in
 //     flight across the barrier (raw s_barrier: __syncthreads() would drain them);
 //   * fragment reads as inline asm, the next k-step's issued before this one's MFMAs;
-//   * the epilogue (plain store, BN statistics, or the data-gradient ReLU mask + BN-backward sums
-//     -- conv_gemm's epilogues 0 / 1 / 3) from a bf16 output tile in LDS, one 16-B column group
-//     per thread, rows coalesced.
+//   * the epilogue (plain store, BN statistics, the data-gradient ReLU mask + BN-backward sums,
+//     or the conv1 data gradients' residual / fold epilogues -- every conv_gemm epilogue 0-9) from
+//     a bf16 output tile in LDS, one 16-B column group per thread, rows coalesced.
 // Blocks are XCD-remapped so the channel tiles of one pixel tile share its A rows in one L2.
+// What bounds it (profiles/r5_conv_big_kloop.txt): the K loop runs at the memory system's stage
+// rate (~64 KiB per 1.8 us per CU); opt-in variants kept for the record: 256 x 128 tiles two per
+// CU, stream-K with fixed-order partials (PS_AMD_CONV_BIG_SK, r5_conv_big_stream_k.txt), a
+// per-tile K-order rotation (PS_AMD_CONV_BIG_KROT).
 #include <algorithm>
 #include <cstdlib>
 #include <map>
