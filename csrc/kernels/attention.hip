@@ -110,16 +110,31 @@ __device__ __forceinline__ bf16x8_t p_operand(const f32x16& blk, int s, int hl) 
   return __builtin_bit_cast(bf16x8_t, u32x4{a[0], b[0], a[1], b[1]});
 }
 
-// stage rows [0, S) of one head's 64-wide slice (row stride rs elements) into a [128][64] tile;
-// rows S..127 are zeroed
-__device__ __forceinline__ void stage64(uint16_t* T, const uint16_t* src, int64_t rs, int S) {
-  for (int id = threadIdx.x; id < kS * 8; id += blockDim.x) {
-    const int r = id >> 3, ch = id & 7;
-    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r < S) v = *reinterpret_cast<const u16x8*>(src + r * rs + ch * 8);
-    *reinterpret_cast<u16x8*>(T + off<64>(r, ch * 8)) = v;
-  }
+// stage rows [0, S) of N heads' 64-wide slices (row strides rs[i] elements) into [128][64] tiles,
+// rows S..127 zeroed; 256 threads: every chunk's global load is issued before any LDS store (a
+// load-store loop paid one HBM round trip per 4 KiB: the kernels ran at ~2.4 TB/s)
+template <int N>
+__device__ __forceinline__ void stage64n(uint16_t* const (&T)[N], const uint16_t* const (&src)[N],
+                                         const int64_t (&rs)[N], int S) {
+  constexpr int PER = kS * 8 / 256;  // 16-B chunks per thread per tile
+  u16x8 v[N][PER];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int id = threadIdx.x + i * 256, r = id >> 3, ch = id & 7;
+      v[n][i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (r < S) v[n][i] = *reinterpret_cast<const u16x8*>(src[n] + r * rs[n] + ch * 8);
+    }
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int id = threadIdx.x + i * 256, r = id >> 3, ch = id & 7;
+      *reinterpret_cast<u16x8*>(T[n] + off<64>(r, ch * 8)) = v[n][i];
+    }
 }
+
 
 // ------------------------------------------------------------------------------ forward
 template <bool DROP>
@@ -132,17 +147,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, c = lane & 31;
   const int64_t rs = 3LL * H * kD;
   const uint16_t* base = qkv + static_cast<int64_t>(b) * S * rs + h * kD;
-  stage64(Ks, base + H * kD, rs, S);
-  stage64(Vs, base + 2 * H * kD, rs, S);
-  __syncthreads();
   const int q0 = w * 32;
+  // Q^T as the B operand: lane holds Q[q0 + c][16 s + 8 hl + e] -- loaded before the K / V staging
+  // so its latency overlaps theirs
+  bf16x8_t qf[4];
+  const int qr = min(q0 + c, S - 1);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(base + qr * rs + 16 * s + 8 * hl);
+  {
+    uint16_t* const tt[2] = {Ks, Vs};
+    const uint16_t* const ss[2] = {base + H * kD, base + 2 * H * kD};
+    const int64_t rr[2] = {rs, rs};
+    stage64n<2>(tt, ss, rr, S);
+  }
+  __syncthreads();
   if (q0 >= S) return;  // no barrier below
   const int nkb = S >> 5;
-  // Q^T as the B operand: lane holds Q[q0 + c][16 s + 8 hl + e]
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = *reinterpret_cast<const bf16x8_t*>(base + (q0 + c) * rs + 16 * s + 8 * hl);
   f32x16 st[4];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
@@ -242,13 +262,32 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   const uint16_t* obase = o + static_cast<int64_t>(b) * S * ors + h * kD;
   const uint16_t* dobase = dout + static_cast<int64_t>(b) * S * ors + h * kD;
   uint16_t* gbase = dqkv + static_cast<int64_t>(b) * S * rs + h * kD;
-  stage64(Qs, base, rs, S);
-  stage64(Ks, base + H * kD, rs, S);
-  stage64(dOs, dobase, ors, S);
-  __syncthreads();
-  const int nkb = S >> 5;
   const int q0 = w * 32, q = q0 + c;
   const bool act = q0 < S;  // wave-uniform
+  // this lane's O / dO row halves and the row's log-sum-exp, loaded before the staging so their
+  // latency overlaps it (Dq = rowsum(dO * O) is formed after the barrier)
+  const int qq = min(q, S - 1);
+  u16x8 orow[4], drow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    orow[j] = *reinterpret_cast<const u16x8*>(obase + static_cast<int64_t>(qq) * ors + 32 * hl + 8 * j);
+    drow[j] = *reinterpret_cast<const u16x8*>(dobase + static_cast<int64_t>(qq) * ors + 32 * hl + 8 * j);
+  }
+  const float lse_q = lse[static_cast<int64_t>(bh) * S + qq];
+  {
+    uint16_t* const tt[3] = {Qs, Ks, dOs};
+    const uint16_t* const ss[3] = {base, base + H * kD, dobase};
+    const int64_t rr[3] = {rs, rs, ors};
+    stage64n<3>(tt, ss, rr, S);
+  }
+  __syncthreads();
+  const int nkb = S >> 5;
+  float dd = 0.f;  // formed right away: the row registers die before the MFMA accumulators live
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dd += bf16_to_f32(orow[j][e]) * bf16_to_f32(drow[j][e]);
+  dd += __shfl_xor(dd, 32, 64);
   f32x16 pt[4], ds[4];
   if (act) {
     // S^T = K Q^T and dP^T = V dO^T for this wave's 32 queries
@@ -273,17 +312,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
       }
     }
     // Dq = rowsum(dO * O) for query q: this lane's half of the 64 d, then the other half
-    float dd = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float x[8], y[8];
-      load8(obase + static_cast<int64_t>(q) * ors, 32 * hl + 8 * j, x);
-      load8(dobase + static_cast<int64_t>(q) * ors, 32 * hl + 8 * j, y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dd += x[e] * y[e];
-    }
-    dd += __shfl_xor(dd, 32, 64);
-    const float l2 = lse[static_cast<int64_t>(bh) * S + q] * kLog2e, k2 = scale * kLog2e;
+    const float l2 = lse_q * kLog2e, k2 = scale * kLog2e;
     const uint32_t rowbase = (static_cast<uint32_t>(bh) * S + q) * S;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
