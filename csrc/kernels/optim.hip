@@ -495,42 +495,10 @@ __global__ __launch_bounds__(256) void sparse_opt_vec_kernel(float* __restrict__
   const int per_wave = 64 >> lg;
   const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * blockDim.x / 64;
-  const int64_t stride = nwaves * per_wave;
-  // the row ids of the NEXT iteration are loaded at the top of this one, and each row's table
-  // (and state) entries are requested as soon as the id is known -- before the gradient run is
-  // walked -- so an iteration pays ~2 dependent round trips instead of ~4 (the kernel ran at
-  // ~1 TB/s on DLRM's pushed rows)
-  int64_t nid = -1, nprev = -2;
-  {
-    const int64_t r = wave * per_wave + sub;
-    if (r < nrows) {
-      nid = rows[r];
-      if (perm != nullptr && r > 0) nprev = rows[r - 1];
-    }
-  }
-  for (int64_t rb = wave * per_wave; rb < nrows; rb += stride) {  // wave-uniform loop
+  for (int64_t rb = wave * per_wave; rb < nrows; rb += nwaves * per_wave) {  // wave-uniform loop
     const int64_t r = rb + sub;
-    int64_t row = nid;
-    if (row >= 0 && perm != nullptr && r > 0 && nprev == row) row = -1;  // not a run head
-    {
-      const int64_t rn = r + stride;
-      nid = rn < nrows ? rows[rn] : -1;
-      nprev = perm != nullptr && rn > 0 && rn < nrows ? rows[rn - 1] : -2;
-    }
-    constexpr bool RW = KIND == kAdagrad;
-    const bool rowwise_ag = RW && rowwise;
-    const int64_t o = row >= 0 ? row * dim + c : 0;
-    f32x4 w = {0.f, 0.f, 0.f, 0.f}, a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-    float h0 = 0.f;
-    if (row >= 0) {
-      w = load4(table, o);
-      if (rowwise_ag) {
-        h0 = st0[row];
-      } else {
-        if (st0) a = load4(st0, o);
-        if (st1) b = load4(st1, o);
-      }
-    }
+    int64_t row = r < nrows ? rows[r] : -1;
+    if (row >= 0 && perm != nullptr && r > 0 && rows[r - 1] == row) row = -1;  // not a run head
     f32x4 g = {0.f, 0.f, 0.f, 0.f};
     if (row >= 0) {
       if (perm == nullptr) {
@@ -551,18 +519,23 @@ __global__ __launch_bounds__(256) void sparse_opt_vec_kernel(float* __restrict__
       }
       g *= scale;
     }
-    if (rowwise_ag) {
+    if (KIND == kAdagrad && rowwise) {
       const float ss = group_sum(g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w, lg) / static_cast<float>(dim);
       if (row < 0) continue;
-      const float h = h0 + ss;
+      const float h = st0[row] + ss;
       if (c == 0) st0[row] = h;
       const float k = p.lr / (sqrtf(h) + p.eps);
+      f32x4 w = load4(table, row * dim + c);
       w -= k * g;
-      store4(table, o, w);
+      store4(table, row * dim + c, w);
     } else {
       // skip_zero (FtrlUpdater.java:52-54): the row's first gradient element, from its lane 0
       const float g0 = __shfl(g.x, lane & ~((1 << lg) - 1), kWave);
       if (row < 0 || (p.skip_zero && g0 == 0.f)) continue;
+      const int64_t o = row * dim + c;
+      f32x4 w = load4(table, o);
+      f32x4 a = st0 ? load4(st0, o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 b = st1 ? load4(st1, o) : f32x4{0.f, 0.f, 0.f, 0.f};
       float wv[4] = {w.x, w.y, w.z, w.w}, av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
       const float gv[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll

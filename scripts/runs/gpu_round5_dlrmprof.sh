@@ -1,7 +1,7 @@
 #!/bin/bash
 # DLRM (1 GPU, batch 65536) kernel stats: where the 5.3 ms step goes
 set -o pipefail
-O=gpurun_out/r5dlrmprof
+O=${O:-gpurun_out/r5dlrmprof}
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
 R=$PWD
