@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-5 final: full GPU suite + smoke + every BASELINE config (driver flags: --warmup 5) on the final tree
 set -o pipefail
-O=gpurun_out/r5final2
+O=${O:-gpurun_out/r5final3}
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
