@@ -60,9 +60,14 @@ def _kv_body(tp, consistency, plane, steps, staleness=0, style="pushpull", mom=0
     xs, ys = x[tp.rank::tp.world], y[tp.rank::tp.world]
     names = list(KEYS)
     for _ in range(steps):
-        ws = dict(zip(names, kv.pull(names)))
+        if style == "async":  # reference prefetch idiom: queue every key, then wait for the views
+            for k in names:
+                kv.async_get(k)
+            ws = kv.async_wait()
+        else:
+            ws = dict(zip(names, kv.pull(names)))
         g = _grads(ws, xs, ys)
-        if style == "pushpull":
+        if style in ("pushpull", "async"):
             kv.push(names, [g[k] for k in names])
             kv.barrier()
         else:  # reference style: two half-contributions summed then averaged by update()
@@ -107,6 +112,15 @@ def test_ssp0_async_engine_is_bsp_exact():
 
 def test_bsp_staleness1_matches_delayed_oracle():
     res = dist_util.run(_kv_body, 2, ("bsp", "collective", 5, 1))
+    want = _oracle(2, 5, staleness=1)
+    for k in want:
+        torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-6)
+
+
+def test_async_get_wait_views_are_post_barrier_under_ssp1():
+    """async_get / async_wait (store/KVStore.java:109-111) under SSP(1): the views they return
+    must be the version the staleness gate allows after each barrier -- the delayed oracle."""
+    res = dist_util.run(_kv_body, 2, ("bsp", "collective", 5, 1, "async"))
     want = _oracle(2, 5, staleness=1)
     for k in want:
         torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-6)

@@ -19,7 +19,7 @@ def _data(n=48):
     return torch.randn(n, 12, generator=g), torch.randint(0, 4, (n,), generator=g)
 
 
-def _body(tp, consistency, steps, mom, staleness=0):
+def _body(tp, consistency, steps, mom, staleness=0, style="pull"):
     from ps_amd.parallel.gpu_kvstore import GpuKVStore
     from ps_amd.parallel.updaters import MomentumUpdater, SimpleUpdater
 
@@ -32,7 +32,12 @@ def _body(tp, consistency, steps, mom, staleness=0):
     xs, ys = x[tp.rank::tp.world].to(DEV), y[tp.rank::tp.world].to(DEV)
     names = list(KEYS)
     for _ in range(steps):
-        ws = dict(zip(names, kv.pull(names)))
+        if style == "async":
+            for k in names:
+                kv.async_get(k)
+            ws = kv.async_wait()
+        else:
+            ws = dict(zip(names, kv.pull(names)))
         g = _grads(ws, xs, ys)
         kv.push(names, [g[k] for k in names])
         kv.barrier()
@@ -58,6 +63,17 @@ def test_bsp_ssp1_xgmi_processes_match_delayed_oracle():
     want = _oracle(2, 5, staleness=1)
     for k in want:
         torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-5)
+
+
+def test_bsp_ssp1_async_get_wait_views_match_delayed_oracle():
+    """the views async_wait returns under SSP(1) on the xGMI plane are the
+    post-barrier version the gate allows (device pulls run on the engine's streams; the compute
+    stream reading the views must see them landed)."""
+    res = dist_util.run(_body, 2, ("bsp", 5, 0.9, 1, "async"))
+    want = _oracle(2, 5, staleness=1)
+    for k in want:
+        torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-5, atol=1e-5)
+        assert torch.equal(res[0][0][k], res[1][0][k])
 
 
 def test_async_ssp0_processes_match_oracle():
