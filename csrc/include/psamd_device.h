@@ -28,6 +28,16 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// two floats -> one dword of two bf16 (RNE): ONE v_cvt_pk_bf16_f32, not two conversions + shift / or
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
+// 2^x as the bare v_exp_f32: for softmax arguments (<= 0) a denormal result is as good as 0, so
+// exp2f's denormal-range fix-up (compare, select, scale, ldexp per element) is waste there
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // Grad / weight element loaders: T is float or uint16_t (bf16 storage).
 template <typename T> struct Elem;
 template <> struct Elem<float> {

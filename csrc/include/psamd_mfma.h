@@ -92,9 +92,7 @@ __device__ __forceinline__ void dma_tile128(uint16_t* T, const uint16_t* src, in
   }
 }
 
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f32_to_bf16(a)) | (static_cast<uint32_t>(f32_to_bf16(b)) << 16);
-}
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return pk_bf16(a, b); }
 
 // v_permlane32_swap(x, y): x's upper 32 lanes <-> y's lower 32 lanes (a VALU op: no LDS queue,
 // no lgkmcnt wait behind in-flight fragment reads, unlike a ds_bpermute shuffle).

@@ -91,7 +91,7 @@ __device__ __forceinline__ bool keep_lo(uint32_t h, uint32_t thr) { return (h & 
 __device__ __forceinline__ bool keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f32_to_bf16(a)) | (static_cast<uint32_t>(f32_to_bf16(b)) << 16);
+  return pk_bf16(a, b);
 }
 
 // B operand (keys 16 s + 8 hl + e, query = lane column) of P^T held in the accumulator layout
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const float p = kb < nkb ? exp2f((st[kb][e] - m) * k2) : 0.f;
+      const float p = kb < nkb ? fast_exp2((st[kb][e] - m) * k2) : 0.f;
       st[kb][e] = p;
       sum += p;
     }
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const float p = kb < nkb ? exp2f(pt[kb][e + u] * k2 - l2) : 0.f;
+          const float p = kb < nkb ? fast_exp2(pt[kb][e + u] * k2 - l2) : 0.f;
           float dp = ds[kb][e + u];
           float pd = p;
           if constexpr (DROP) {

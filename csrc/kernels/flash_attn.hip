@@ -197,7 +197,7 @@ __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restr
       mb = xhalf_max(mb) * k2;  // every processed tile holds >= 1 visible key per query
       if (!__all(mb - m2 <= kRescale)) {
         const float mn = fmaxf(m2, mb);
-        const float alpha = exp2f(m2 - mn);
+        const float alpha = fast_exp2(m2 - mn);
         l *= alpha;
 #pragma unroll
         for (int db = 0; db < 4; ++db)
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(NW * 64) void fa_fwd_kernel(const uint16_t* __restr
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const float p = exp2f(st[ks][e] * k2 - m2);
+          const float p = fast_exp2(st[ks][e] * k2 - m2);
           st[ks][e] = p;
           ls += p;
         }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(NW * 64) void fa_bwd_dq_kernel(const uint16_t* __re
         const bool diag = kk0 + 31 > q0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          float p = exp2f(st[e] * k2 - l2);
+          float p = fast_exp2(st[e] * k2 - l2);
           if (diag && kk0 + (e & 3) + 8 * (e >> 2) + 4 * hl > qi) p = 0.f;
           st[e] = p * (dp[e] - dd);  // dS^T
         }
@@ -453,13 +453,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const uint16_t* __rest
           ta[s2][db] = tfrag_a<128>(dO, sl * 2 + s2, db * 32, lane);
           tq[s2][db] = tfrag_a<128>(Q, sl * 2 + s2, db * 32, lane);
         }
-      const bool diag = k0 + 31 > qr0;
+      if (k0 + 31 > qr0) {  // wave-uniform: only slices on the diagonal need the causal mask
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float p = exp2f(sa[e] * k2 - lv[e >> 2][e & 3] * kLog2e);
-        if (diag && key > qr0 + (e & 3) + 8 * (e >> 2) + 4 * hl) p = 0.f;
-        sa[e] = p;
-        dp[e] = p * (dp[e] - dv4[e >> 2][e & 3]);  // dS
+        for (int e = 0; e < 16; ++e) {
+          float p = fast_exp2(sa[e] * k2 - lv[e >> 2][e & 3] * kLog2e);
+          if (key > qr0 + (e & 3) + 8 * (e >> 2) + 4 * hl) p = 0.f;
+          sa[e] = p;
+          dp[e] = p * (dp[e] - dv4[e >> 2][e & 3]);  // dS
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = fast_exp2(sa[e] * k2 - lv[e >> 2][e & 3] * kLog2e);
+          sa[e] = p;
+          dp[e] = p * (dp[e] - dv4[e >> 2][e & 3]);
+        }
       }
       lgkm_wait<0>();
 #pragma unroll
