@@ -121,6 +121,25 @@ def test_swiglu_fwd_bwd(R, F):
     _close(gu.grad, gr.grad)
 
 
+def test_swiglu_saturated_inputs_stay_finite():
+    """the fast sigmoid (bare exp2 + reciprocal) at |g| up to 120: exp overflows to inf and the
+    reciprocal to 0 -- silu and its gradient must still match the fp32 reference, no NaN."""
+    F = 1024
+    g = torch.linspace(-120, 120, 2 * F, device="cuda").reshape(2, F)
+    gu = torch.cat([g, torch.ones_like(g)], dim=-1).bfloat16().requires_grad_(True)
+    gr = gu.detach().float().requires_grad_(True)
+    h = T.swiglu(gu)
+    a, u = gr.chunk(2, dim=-1)
+    hr = F_silu(a) * u
+    assert torch.isfinite(h.float()).all()
+    _close(h, hr)
+    dh = torch.ones_like(hr).bfloat16()
+    h.backward(dh)
+    hr.backward(dh.float())
+    assert torch.isfinite(gu.grad.float()).all()
+    _close(gu.grad, gr.grad)
+
+
 def F_silu(t):
     return t * torch.sigmoid(t)
 
