@@ -159,6 +159,9 @@ def main():
         if not cpu:
             torch.cuda.synchronize()
 
+    from ps_amd.utils import gemm_tuning
+
+    gemm_table = gemm_tuning.load(args.config, dev)  # tuned hipBLASLt choices, lookups only
     torch.manual_seed(1234)
     bench = BC.SETUPS[args.config](args, tp, dev)
     step = bench.step
@@ -268,6 +271,7 @@ def main():
     if rank == 0:
         cfg = dict(bench.config)
         cfg["hip_graph"] = bool(use_graph)
+        cfg["gemm_table"] = os.path.basename(gemm_table) if gemm_table else None
         # the stream policy this run used (keyed on ranks sharing a GPU, not on WORLD_SIZE)
         images = bench.samples_per_step if args.config == "resnet50" else None
         cfg["ranks_per_device"] = rpd
