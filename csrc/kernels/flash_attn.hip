@@ -316,12 +316,16 @@ __global__ __launch_bounds__(NW * 64) void fa_bwd_dq_kernel(const uint16_t* __re
           st = mma(frag<128>(K, ks * 32 + c, 2 * s + hl), qf[s], st);
           dp = mma(frag<128>(V, ks * 32 + c, 2 * s + hl), df[s], dp);  // dP^T = V dO^T
         }
-        const bool diag = kk0 + 31 > q0;
+        if (kk0 + 31 > q0) {  // wave-uniform: only the diagonal half-tile needs the causal mask
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float p = fast_exp2(st[e] * k2 - l2);
-          if (diag && kk0 + (e & 3) + 8 * (e >> 2) + 4 * hl > qi) p = 0.f;
-          st[e] = p * (dp[e] - dd);  // dS^T
+          for (int e = 0; e < 16; ++e) {
+            float p = fast_exp2(st[e] * k2 - l2);
+            if (kk0 + (e & 3) + 8 * (e >> 2) + 4 * hl > qi) p = 0.f;
+            st[e] = p * (dp[e] - dd);  // dS^T
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) st[e] = fast_exp2(st[e] * k2 - l2) * (dp[e] - dd);
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
