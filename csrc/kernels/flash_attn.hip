@@ -18,6 +18,10 @@
 // backward is deterministic (no atomics, no partials).
 // Forward and dQ grids run their heaviest (latest) query blocks first, dK / dV its heaviest
 // (earliest) key blocks first.
+// The softmax is VALU work the MFMAs cannot hide in the one-wave-per-SIMD dK / dV kernel (PMC:
+// 15 VALU instructions per MFMA), so it is kept lean: bare v_exp_f32 (fast_exp2), one packed
+// bf16 convert per pair (pk_bf16), and the causal mask only on diagonal tiles / slices
+// (profiles/r5_flash_valu_trim.txt: bwd -18 %, fwd -17 %).
 #include "psamd_launch.h"
 #include "psamd_mfma.h"
 
