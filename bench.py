@@ -183,6 +183,7 @@ def main():
     sync()
     if bench.stats is not None:
         bench.stats()  # zero the counters at the start of the timed region
+    seg0 = None if cpu else torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -195,6 +196,14 @@ def main():
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
     timed_stats = bench.stats() if bench.stats is not None else None
+    # allocator steady state: a timed step that hipMallocs new segments means the host ran ahead of
+    # the GPU far enough that freed blocks still pending on another stream could not be reused --
+    # the mechanism behind the multi-second stall of an unbounded run-ahead
+    # (profiles/r6_stall_root_cause.txt); the engines' in-flight bound keeps this at 0
+    alloc_timed = None if cpu else torch.cuda.memory_stats(dev).get("num_device_alloc", 0) - seg0
+    if alloc_timed and rank == 0:
+        print(f"[bench] WARNING: {alloc_timed} new device segments allocated inside the timed region "
+              f"(allocator not in steady state; host run-ahead unbounded?)", file=sys.stderr, flush=True)
     value = bench.samples_per_step * world * args.steps / elapsed
     # after the timed region: per-phase PS timing (default 3 steps at world > 1, so the driver's
     # multi-GPU lines show how much of the push / pull the backward hides) and the collective
@@ -284,6 +293,9 @@ def main():
             cfg["plane_info"] = dict(bench.engine.plane.info)
         cfg["final_loss"] = round(float(loss.item()), 4)
         cfg["peak_mem_gb"] = None if cpu else round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        if not cpu:
+            cfg["reserved_gb"] = round(torch.cuda.memory_reserved(dev) / 2**30, 1)
+            cfg["device_allocs_timed"] = alloc_timed
         if timed_stats:
             cfg.update(timed_stats)
         if audit is not None:

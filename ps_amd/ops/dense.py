@@ -142,7 +142,7 @@ class _SplitKLinear(torch.autograd.Function):
 class _SplitKLinearFork(torch.autograd.Function):
     """(x W^T + b, x): the layer's input passed through as a second output, so a residual use of x
     hands its gradient to THIS backward, which folds it into the data-gradient GEMM
-    (dxr += dy W, in place) -- autograd would otherwise sum the two branch gradients with a
+    (dx = dxr + dy W as one beta = 1 GEMM) -- autograd would otherwise sum the two branch gradients with a
     separate add pass over [tokens, D] (25 per BERT-base step)."""
 
     @staticmethod
@@ -160,7 +160,9 @@ class _SplitKLinearFork(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if dxr is not None and dxr.is_contiguous() and dxr.dtype == dy2.dtype:
-                dx = dxr.view(-1, k).addmm_(dy2, w).view(x.shape)  # one GEMM with beta = 1
+                # one GEMM with beta = 1 into a NEW buffer: the incoming residual gradient is not
+                # guaranteed to be exclusively ours (hooks, retain_grad), so it is never written
+                dx = torch.addmm(dxr.view(-1, k), dy2, w).view(x.shape)
             else:
                 dx = (dy2 @ w).view(x.shape)
                 if dxr is not None:

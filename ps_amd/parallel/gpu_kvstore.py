@@ -257,8 +257,9 @@ class GpuKVStore:
         """Queue a key for ``async_wait`` (store/KVStore.java:109-111).  On the GPU engines a
         pull is already asynchronous -- the replica is written by the engines' pull kernels on
         their own streams and the compute stream waits on them -- so no prefetch thread is
-        needed: ``async_wait`` returns the views at once."""
-        if init is not None and not self.sealed and key not in self._decl:
+        needed: ``async_wait`` returns the views at once.  ``async_get(key, init)`` creates an
+        unknown key at any round, like ``get(key, init)`` (store/KVStore.java:109 -> create)."""
+        if init is not None and key not in self.params and key not in self._decl:
             self.init({key: init})
         self._async.append(key)
 

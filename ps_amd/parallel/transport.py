@@ -195,13 +195,27 @@ def ranks_per_device(refresh: bool = False, device=None) -> int:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         _RANKS_PER_DEVICE = 1
         return 1
-    if device is None and torch.cuda.is_available() and (dist.get_backend() == "nccl" or torch.cuda.is_initialized()
-                                                         or os.environ.get("PS_AMD_BENCH_ONE_GPU", "0") == "1"):
+    if not refresh:
+        # a policy query before the collective count (a process group not made by
+        # init_distributed): never gather lazily from inside model code -- estimate from the
+        # launcher's env (local ranks over visible devices) and leave the cache empty
+        return _local_share_estimate()
+    if device is None and torch.cuda.is_available():
         device = torch.device("cuda", torch.cuda.current_device())
     keys = [None] * dist.get_world_size()
     dist.all_gather_object(keys, device_key(device))
     _RANKS_PER_DEVICE = count_sharing(keys, dist.get_rank())
     return _RANKS_PER_DEVICE
+
+
+def _local_share_estimate() -> int:
+    """ceil(LOCAL_WORLD_SIZE / visible GPUs) without any collective (device_count does not
+    initialise the GPU); 1 for CPU ranks."""
+    if not torch.cuda.is_available():
+        return 1
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    ndev = max(1, torch.cuda.device_count())
+    return max(1, -(-local // ndev))
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> Transport:

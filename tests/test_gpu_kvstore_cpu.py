@@ -161,6 +161,13 @@ def test_single_rank_api_semantics():
     kv.async_get("w")
     got = kv.async_wait()
     assert set(got) == {"w"}
+    # async_get(new_key, init) after barriers creates the key (store/KVStore.java:109): async_wait
+    # returns its initial value, not None
+    kv.async_get("late_async", lambda: torch.full((2,), 7.0))
+    kv.async_get("w")
+    got = kv.async_wait()
+    torch.testing.assert_close(got["late_async"], torch.full((2,), 7.0))
+    assert "late_async" in kv
     # loss surface: s * w_init + (1 - s) * w
     prev = ctx.status
     ctx.status, ctx.weights_scale = Stat.LOSS_SURFACE_EVAL, 0.25

@@ -206,3 +206,4 @@ def test_auc_reference_fixture_and_bruteforce():
     assert abs(auc_exact(pt, yt) - tie_avg) < 1e-12 and abs(tie_avg - 0.84) < 1e-12
     # reference algorithm: ties broken by input order (stable sort), not averaged -> 0.88 here
     assert abs(AUC(pt, yt).calculate() - 0.88) < 1e-12
+

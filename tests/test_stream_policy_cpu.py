@@ -55,3 +55,16 @@ def _rpd_body(tp, shared):
 def test_ranks_per_device_gloo(shared):
     out = run(_rpd_body, 2, args=(shared,))
     assert out[0] == ([2, 2] if shared else [1, 1])
+
+
+def _lazy_body(tp):
+    # a process group made outside init_distributed: a policy query must not start a collective
+    # (rank 1 never calls it, so a lazy all_gather would hang the job)
+    transport._RANKS_PER_DEVICE = None
+    n = transport.ranks_per_device() if tp.rank == 0 else 1
+    return n, transport._RANKS_PER_DEVICE
+
+
+def test_ranks_per_device_policy_query_is_not_a_collective():
+    out = run(_lazy_body, 2)
+    assert out[0] == (1, None)  # CPU ranks: the env estimate, cache left for the collective count
