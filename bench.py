@@ -184,6 +184,7 @@ def main():
     if bench.stats is not None:
         bench.stats()  # zero the counters at the start of the timed region
     seg0 = None if cpu else torch.cuda.memory_stats(dev).get("num_device_alloc", 0)
+    res0 = None if cpu else torch.cuda.memory_reserved(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -201,9 +202,10 @@ def main():
     # the mechanism behind the multi-second stall of an unbounded run-ahead
     # (profiles/r6_stall_root_cause.txt); the engines' in-flight bound keeps this at 0
     alloc_timed = None if cpu else torch.cuda.memory_stats(dev).get("num_device_alloc", 0) - seg0
-    if alloc_timed and rank == 0:
-        print(f"[bench] WARNING: {alloc_timed} new device segments allocated inside the timed region "
-              f"(allocator not in steady state; host run-ahead unbounded?)", file=sys.stderr, flush=True)
+    grew_gb = None if cpu else (torch.cuda.memory_reserved(dev) - res0) / 2**30
+    if grew_gb is not None and grew_gb > 8 and rank == 0:  # (a bounded run adds one step's pending blocks at most)
+        print(f"[bench] WARNING: the allocator grew by {grew_gb:.1f} GB ({alloc_timed} segments) inside the timed "
+              f"region: the host ran far ahead of the GPU (PS_AMD_MAX_INFLIGHT=0?)", file=sys.stderr, flush=True)
     value = bench.samples_per_step * world * args.steps / elapsed
     # after the timed region: per-phase PS timing (default 3 steps at world > 1, so the driver's
     # multi-GPU lines show how much of the push / pull the backward hides) and the collective
@@ -296,6 +298,7 @@ def main():
         if not cpu:
             cfg["reserved_gb"] = round(torch.cuda.memory_reserved(dev) / 2**30, 1)
             cfg["device_allocs_timed"] = alloc_timed
+            cfg["reserved_growth_timed_gb"] = round(grew_gb, 2)
         if timed_stats:
             cfg.update(timed_stats)
         if audit is not None:

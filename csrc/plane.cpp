@@ -994,6 +994,20 @@ void register_plane(pybind11::module& m) {
     hip_ok(hipSetDevice(static_cast<int>(device)), "hipSetDevice");
     psamd::launch_plane_copy(c, reinterpret_cast<hipStream_t>(stream));
   });
+  // the owner-side read of the one-sided paths (remote_probe.py): n values at ``src`` into
+  // ``out`` (fp32) by the multi-source reduce kernel -- the system-scope acquire at entry and the
+  // loads of the async-PS serve (fused_opt_multi) and the plane serve, with one source
+  pm.def("read_acquire", [](int64_t src, int64_t n, bool bf16, torch::Tensor out, int64_t stream) {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() >= n,
+                "read_acquire: fp32 out of >= n elements");
+    TORCH_CHECK((src & 15) == 0 && n > 0, "read_acquire: 16-B aligned source");
+    psamd::MultiGrad m{};
+    m.nsrc = 1;
+    m.g[0] = reinterpret_cast<const void*>(src);
+    m.off = 0;
+    hip_ok(hipSetDevice(out.get_device()), "hipSetDevice");
+    psamd::launch_reduce_multi(m, bf16 ? 1 : 0, n, out.data_ptr<float>(), reinterpret_cast<hipStream_t>(stream));
+  });
   py::class_<PlaneEngine>(pm, "Engine")
       .def(py::init<uintptr_t, int64_t, int64_t, int64_t, int64_t, bool, int64_t, double, double, bool>())
       .def("set_bases", &PlaneEngine::set_bases)

@@ -91,23 +91,42 @@ def setup_resnet50(args, tp, dev) -> Bench:
                  feed=feed)
 
 
+def async_or_pipelined(model, upd, tp, stale: int, args, use_async: bool = True):
+    """The SSP(stale) engine of a model: the asynchronous PS (one-sided pushes into the owners'
+    mailboxes + native progress threads, async_ps.py) -- or, when its start-up remote-write probe
+    fails on any rank (remote_probe.py; every rank sees the same outcome), the pipelined
+    collective rounds of ColocatedPS with the same staleness.  -> (engine, async?, probe record)."""
+    from .parallel.colocated import ColocatedPS
+
+    probe = {}
+    if use_async:
+        from .parallel.async_ps import AsyncPS
+        from .parallel.remote_probe import RemoteWriteUnavailable
+
+        try:
+            ps = AsyncPS(model, upd, tp, staleness=stale)
+            probe = {k: v for k, v in ps.info.items() if k == "remote_write_probe"}
+            return ps, True, probe
+        except RemoteWriteUnavailable as e:
+            probe = {"remote_write_probe": "failed", "engine_fallback": "pipelined-collective: " + str(e)[:300]}
+            if tp.rank == 0:
+                print(f"[bench] {e}; falling back to the pipelined collective SSP", flush=True,
+                      file=__import__("sys").stderr)
+    ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
+                     staleness=stale, clip_norm=None)
+    return ps, False, probe
+
+
 def setup_bert_ssp(args, tp, dev) -> Bench:
     from .models.transformer import BertForMLM, mlm_batch
-    from .parallel.colocated import ColocatedPS
     from .parallel.updaters import AdamUpdater
 
     torch.manual_seed(0)
     model = BertForMLM().to(dev).to(torch.bfloat16)
     upd = AdamUpdater(1e-4, 0.9, 0.999, 1e-6, bias_correction="step", weight_decay=0.01, adamw=True)
     stale = 1 if args.staleness == 0 else args.staleness
-    use_async = os.environ.get("PS_AMD_BERT_ASYNC", "1") == "1"
-    if use_async:  # one-sided pushes into owner mailboxes + native progress threads (async_ps.py)
-        from .parallel.async_ps import AsyncPS
-
-        ps = AsyncPS(model, upd, tp, staleness=stale)
-    else:  # pipelined collective rounds (the bound enforced by the collective itself)
-        ps = ColocatedPS(model, upd, tp, bucket_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb,
-                         staleness=stale, clip_norm=None)
+    ps, use_async, probe = async_or_pipelined(model, upd, tp, stale, args,
+                                              os.environ.get("PS_AMD_BERT_ASYNC", "1") == "1")
     B, S = args.batch_per_gpu, args.seq_len
     pool = [mlm_batch(B, S, seed=tp.rank * 1000 + i, device=dev, with_positions=True) for i in range(POOL)]
     it = _cycle(pool)
@@ -122,7 +141,7 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
     return Bench(step, B, "sequences/sec (whole node) BERT-base MLM async bounded-staleness s=1", "sequences/s",
                  {"model": "BERT-base", "global_batch": B * tp.world, "seq_len": S,
                   "parallelism": f"ps-ssp{stale}-{'async' if use_async else 'pipelined'}-dp{tp.world}",
-                  "optimizer": upd.name}, ps)
+                  "optimizer": upd.name, **probe}, ps)
 
 
 def setup_dlrm(args, tp, dev) -> Bench:
@@ -175,7 +194,8 @@ def setup_dlrm(args, tp, dev) -> Bench:
                   "sparse_push_overlap": overlap,
                   # row exchange path at W > 1: "plane" (IPC arenas, parallel/row_plane.py) or
                   # "collective" (RCCL all-to-alls); "local" at W = 1
-                  "sparse_exchange": tbl.exchange}, ps, stats)
+                  "sparse_exchange": tbl.exchange, **({"sparse_exchange_info": tbl.exchange_info}
+                                                      if tbl.exchange_info else {})}, ps, stats)
 
 
 def setup_llama_onebit(args, tp, dev) -> Bench:
@@ -231,7 +251,7 @@ def setup_ctr_async(args, tp, dev) -> Bench:
     gen = torch.Generator().manual_seed(0)
     model = WideDeepNN.build_model(23, 10, 45, [150, 10, 1], 100000, gen=gen, emb_rows=100000, table_factory=tf,
                                    init_scale=0.2).to(dev)
-    ps = AsyncPS(model, model.get_updater(), tp, staleness=stale)
+    ps = AsyncPS(model, model.get_updater(), tp, staleness=stale)  # (a failed remote-write probe raises here)
     B = args.batch_per_gpu
     pool = []
     for i in range(POOL):
@@ -259,7 +279,9 @@ def setup_ctr_async(args, tp, dev) -> Bench:
                  "samples/s", {"model": "CTR-WideDeep-23x10", "global_batch": B * tp.world, "seq_len": None,
                                "parallelism": f"ps-ssp{stale}-async-rows-dp{tp.world}",
                                "row_tables": "device-resident (csrc/async_rows_gpu.cpp)" if dev.type == "cuda"
-                               else "host callbacks"}, _Engine(), dtype="fp32")
+                               else "host callbacks",
+                               **{k: v for k, v in ps.info.items() if k == "remote_write_probe"}},
+                 _Engine(), dtype="fp32")
 
 
 SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_dlrm,

@@ -263,6 +263,19 @@ class AsyncPS:
         self.A = A
         self.peer_mbox = self.share.exchange(self.mbox)
         self.peer_pub = self.share.exchange(self.pub)
+        # one-sided pushes write into the owners' HBM: prove the production write + read path on
+        # the mailbox lines themselves before relying on it (remote_probe.py); every rank raises
+        # RemoteWriteUnavailable together on a failure and the caller falls back
+        self.info = {"engine": "AsyncPS"}
+        if W > 1 and not self.threads:
+            try:
+                self.info["remote_write_probe"] = self._probe_remote_writes()
+            except Exception:
+                self.share.close(unlink=True)
+                self._ctl.close()
+                if me == 0:
+                    self._ctl.unlink()
+                raise
         # ---------------- native progress thread (owner) + completion thread (worker)
         if self.gpu:
             from .. import _C  # type: ignore
@@ -298,6 +311,69 @@ class AsyncPS:
         self._step_open = False
         self._hooks = ([p.register_post_accumulate_grad_hook(partial(self._on_ready, n)) for n, p in params]
                        if overlap else [])
+
+    def _probe_remote_writes(self) -> str:
+        """Every rank writes a pattern into the first 64 elements of its slot-0 mailbox row on every
+        owner by the push's copy kernel; the owner reads its W - 1 rows by the serve's acquire
+        kernel once the writers' completion was observed on the host (the control-block seq
+        protocol) -- three rounds over the same lines, then the lines are zeroed again."""
+        from .remote_probe import pattern, run_probe
+
+        W, me, MB, n = self.world, self.rank, self.MB, 64
+        peers = [w for w in range(W) if w != me]
+        if self.gpu:
+            from .. import _C  # type: ignore
+
+            P = _C.plane
+            ws, rs = torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device)
+            out = torch.zeros(W, n, dtype=torch.float32, device=self.device)
+            srcs = {}
+
+            def write(k):
+                src = srcs[k] = pattern(k, me, n).to(self.device, self.dtype)
+                ws.wait_stream(torch.cuda.current_stream(self.device))
+                es = src.element_size()
+                P.copy_many([(src.data_ptr(), self.peer_mbox[r][me * MB].data_ptr(), n * es) for r in peers],
+                            ws.cuda_stream, self.device.index)
+
+            def publish(k):
+                ws.synchronize()  # the host observed every copy's completion (as the notifier does)
+                self.t.barrier()
+
+            def read(k):
+                for w in peers:
+                    P.read_acquire(self.mbox[w * MB].data_ptr(), n, self.dtype == torch.bfloat16, out[w],
+                                   rs.cuda_stream)
+                rs.synchronize()
+                return out[peers].cpu()
+
+            def settle():
+                torch.cuda.synchronize(self.device)
+                self.t.barrier()
+        else:
+            def write(k):
+                src = pattern(k, me, n).to(self.dtype)
+                for r in peers:
+                    self.peer_mbox[r][me * MB][:n].copy_(src)
+
+            def publish(k):
+                self.t.barrier()
+
+            def read(k):
+                return torch.stack([self.mbox[w * MB][:n].float().clone() for w in peers])
+
+            def settle():
+                self.t.barrier()
+
+        rec = run_probe(self.t, "asyncps", 3, write, publish, read,
+                        lambda k: torch.stack([pattern(k, w, n) for w in peers]), settle)
+        with torch.no_grad():
+            for w in peers:
+                self.mbox[w * MB][:n].zero_()
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        self.t.barrier()
+        return rec
 
     def _segments(self, lo: int, hi: int) -> List[tuple]:
         """Updater segments of the shard [lo, hi): exact key -> longest prefix -> default per key

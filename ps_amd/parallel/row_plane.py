@@ -94,6 +94,52 @@ class RowPlane:
         self._tev: List[tuple] = []  # (phase, start event, end event)
         self._tsum: dict = {}
         self._tn = {"pulls": 0, "pushes": 0, "applies": 0}
+        # the response rows are written into the workers' arenas by the owners' kernels: prove the
+        # production write (row_plane_send) + publish (IPC events) + read (the worker's copy out)
+        # before the first pull (remote_probe.py); on a failure every rank raises together and
+        # the table falls back to the RCCL all-to-alls
+        self.info = {}
+        if self.W > 1 and not self.threads:
+            try:
+                self.info["remote_write_probe"] = self._probe_remote_writes()
+            except Exception:
+                self.close()
+                raise
+
+    def _probe_remote_writes(self, k: int = 16) -> str:
+        from ..ops._ext import native
+        from .remote_probe import pattern, run_probe
+
+        W, me, dim = self.W, self.me, self.dim
+        self._alloc(_round_cap(W * k))
+        cap = self.cap
+        rslots = torch.full((W * cap,), -1, dtype=torch.int64, device=self.device)
+        for w in range(W):
+            rslots[w * cap:w * cap + k] = torch.arange(k, device=self.device)
+        pmeta = torch.tensor([v for _ in range(W) for v in (me * k, k)], dtype=torch.int64, device=self.device)
+        tables = {}
+
+        def write(r):
+            tables[r] = pattern(r, me, k * dim).view(k, dim).to(self.device)
+            if self.gpu:
+                native().row_plane_send(tables[r], rslots, pmeta, [self._ptr(w, "rows") for w in range(W)], cap)
+            else:  # CPU ranks: the same rows into the peers' shared-memory arenas
+                for w in range(W):
+                    self._peer(w, "rows", torch.float32, cap * dim).view(cap, dim)[me * k:(me + 1) * k].copy_(tables[r])
+
+        def read(r):
+            return self.rows[:W * k].clone().cpu()
+
+        def settle():
+            if self.gpu:
+                torch.cuda.synchronize(self.device)
+            self.t.barrier()
+
+        rec = run_probe(self.t, "rowplane", 3, write, lambda r: self._stage("rows"), read,
+                        lambda r: torch.cat([pattern(r, o, k * dim).view(k, dim) for o in range(W)]), settle)
+        self.rows[:W * k].zero_()
+        settle()
+        return rec
 
     # ------------------------------------------------------------------ timing
     def _t0(self):

@@ -304,14 +304,23 @@ class ShardedSparseTable:
         # (``exchange`` "plane" | "collective"; default: PS_AMD_ROW_EXCHANGE, else auto)
         self.plane = None
         self._rowacc = None
+        self.exchange_info: dict = {}  # row-plane probe record / fallback reason (bench JSON)
         if self.world > 1:
             from . import row_plane as _rp
 
             if exchange not in (None, "auto", "plane", "collective"):
                 raise ValueError(exchange)
             if _rp.plane_rows_wanted(self.t, self.device, exchange):
-                self.plane = _rp.RowPlane(self.t, self.dim, self.device)
-                self._rowacc = _rp.RowAccumulator(self.shard)
+                from .remote_probe import RemoteWriteUnavailable
+
+                try:
+                    self.plane = _rp.RowPlane(self.t, self.dim, self.device)
+                    self._rowacc = _rp.RowAccumulator(self.shard)
+                    self.exchange_info.update(self.plane.info)
+                except RemoteWriteUnavailable as e:  # every rank: the collective all-to-alls instead
+                    if exchange == "plane":
+                        raise
+                    self.exchange_info["fallback"] = str(e)
         self.exchange = "plane" if self.plane is not None else ("collective" if self.world > 1 else "local")
 
     # ------------------------------------------------------------------ compat accessors
