@@ -10,7 +10,35 @@
 
 #include "psamd_launch.h"
 
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <string>
+
 namespace {
+
+// Dispatch log of the convolution routes (``route_log``): which kernel family / tile / prologue /
+// epilogue each conv call ran on -- tests assert that a whole-network run exercised the
+// production routes.  One relaxed load per call while disabled.
+std::atomic<bool> g_route_on{false};
+std::mutex g_route_mu;
+std::map<std::string, int64_t>& routes() {
+  static std::map<std::string, int64_t> r;
+  return r;
+}
+void route(const std::string& name) {
+  if (!g_route_on.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> g(g_route_mu);
+  routes()[name] += 1;
+}
+// -> the counts so far; then enables / disables logging and optionally clears the counts
+std::map<std::string, int64_t> route_log(bool enable, bool reset) {
+  std::lock_guard<std::mutex> g(g_route_mu);
+  auto out = routes();
+  if (reset) routes().clear();
+  g_route_on.store(enable, std::memory_order_relaxed);
+  return out;
+}
 
 using torch::Tensor;
 
@@ -1441,6 +1469,13 @@ std::vector<Tensor> conv_gemm(Tensor a, Tensor b, std::vector<int64_t> geo, c10:
     TORCH_CHECK(pl.bm == 256 && tbuf->numel() >= int64_t(8) * pl.gm * (N / pl.bn), "tbuf: [8 x blocks] on the big tiles");
     p.tbuf = reinterpret_cast<uint64_t*>(tbuf->data_ptr<int64_t>());
   }
+  if (g_route_on.load(std::memory_order_relaxed)) {
+    const auto pl = psamd::conv_fwd_plan_geo(p.M, p.N, p.K, has_pro || has_bwd, g, resp ? 1 : has_bwd ? 2 : 0, p.epi);
+    route((pl.bm == 256 && pl.bn == 256 ? std::string("conv_big") : "conv_fwd_" + std::to_string(pl.bm) + "x" +
+                                                                          std::to_string(pl.bn)) +
+          "/k" + std::to_string(g.ks) + (g.stride == 2 ? "s2" : "") + (has_pro ? "/pro" : "") + (has_bwd ? "/bnbwd" : "") +
+          (resp ? "/blockout" : "") + "/epi" + std::to_string(epi));
+  }
   psamd::launch_conv_fwd(p, cur_stream(a));
   if (has_bwd) return {c, part, bwd_out};
   return {c, part};
@@ -1510,6 +1545,7 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dz, std::vector<Tensor> wph, int64_t H,
         p.pgm = 4 * gm;
       }
     }
+    route("conv_dgrad_phases/epi" + std::to_string(epi));
     psamd::launch_conv_dgrad_phases(ps, cur_stream(dz));
     return {dx, part};
   }
@@ -1570,6 +1606,8 @@ Tensor conv_wgrad(Tensor dz, Tensor x, std::vector<int64_t> geo, c10::optional<T
   p.pro = prop;
   p.ws = ws.data_ptr<float>();
   p.dw = u16m(dw);
+  if (g_route_on.load(std::memory_order_relaxed))
+    route("conv_wgrad/k" + std::to_string(g.ks) + (g.stride == 2 ? "s2" : "") + (prop != nullptr ? "/pro" : ""));
   psamd::launch_conv_wgrad(p, cur_stream(dz));
   return dw;
 }
@@ -1625,6 +1663,8 @@ std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt
   a.ws = ws.data_ptr<float>();
   a.dw = u16m(dw);
   a.M = m;
+  route(std::string("conv11_bwd_fused/") + (plain ? "plain" : "bn2") + "/" + std::to_string(ci) + "x" +
+        std::to_string(co));
   psamd::launch_conv11_bwd_fused(a, ci, co, cur_stream(g));
   return {gy, part, dw};
 }
@@ -1786,6 +1826,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bwd") = py::none(), py::arg("aux3") = py::none(), py::arg("mean2") = py::none(),
         py::arg("invstd2") = py::none(), py::arg("pro2") = py::none(), py::arg("aout") = py::none(),
         py::arg("abits") = py::none(), py::arg("tbuf") = py::none());
+  m.def("route_log", &route_log, py::arg("enable") = true, py::arg("reset") = true);
   m.def("linear_wgrad_db", &linear_wgrad_db);
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("weight_prep", &weight_prep, py::arg("jobs"), py::arg("max_blocks") = 1024);
