@@ -224,7 +224,7 @@ void lerp(Tensor w0, Tensor w, double sc, Tensor out) {
 // ------------------------------------------------------------------------------ compression
 void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
   check_gpu(g, "g");
-  check_f32(err, "err");
+  check_gpu(err, "err");  // error feedback in fp32 or bf16
   check_gpu(words, "words");
   check_f32(scales, "scales");
   TORCH_CHECK(words.scalar_type() == torch::kInt64, "words must be int64 (bit-packed)");
@@ -233,7 +233,8 @@ void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
   TORCH_CHECK(words.numel() >= (n + 63) / 64, "words too small");
   TORCH_CHECK(scales.numel() >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
   const c10::DeviceGuard guard(g.device());
-  psamd::launch_onebit_pack(g.data_ptr(), dcode(g, "g"), err.data_ptr<float>(), n,
+  TORCH_CHECK(err.is_contiguous(), "err must be contiguous");
+  psamd::launch_onebit_pack(g.data_ptr(), dcode(g, "g"), err.data_ptr(), dcode(err, "err"), n,
                             reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), scales.data_ptr<float>(),
                             cur_stream(g));
 }

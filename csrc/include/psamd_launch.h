@@ -124,7 +124,7 @@ int sumsq_blocks(int64_t n);
 // ---------------------------------------------------------------- compress.hip
 // 1-bit sign compression with per-chunk scale and error feedback (K26).
 constexpr int kOnebitChunk = 1024;
-void launch_onebit_pack(const void* g, int gdtype, float* err, int64_t n, uint64_t* words, float* scales,
+void launch_onebit_pack(const void* g, int gdtype, void* err, int edtype, int64_t n, uint64_t* words, float* scales,
                         hipStream_t s);
 void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int nworkers, int64_t n,
                                  int64_t words_stride, int64_t scales_stride, void* out, int odtype, float mult,

@@ -6,12 +6,11 @@
 //
 //   c      = g + e                       (error feedback)
 //   scale  = mean(|c|) over a 1024-element chunk
-//   bit    = c >= 0                      packed 64 per word with a wave64 __ballot
+//   bit    = c >= 0                      packed 64 per word
 //   e      = c - (bit ? scale : -scale)
 //
-// Layout: element i lives in word i/64, bit i%64; the chunk scale for element i is
-// scales[i/1024].  A 256-thread block owns one chunk: thread t handles elements
-// t, t+256, t+512, t+768, so each wave's ballot produces one contiguous 64-element word.
+// Layout: element i lives in word i/64, bit i%64 (= byte i/8, bit i%8); the chunk scale for
+// element i is scales[i/1024].
 // unpack_reduce sums W workers' packed pushes in a fixed worker order (deterministic) and
 // optionally accumulates into the destination.
 #include "psamd_device.h"
@@ -19,37 +18,69 @@
 
 namespace psamd {
 
-template <typename G>
-__global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ g, float* __restrict__ err, int64_t n,
-                                                          uint64_t* __restrict__ words, float* __restrict__ scales) {
-  __shared__ float scratch[4];
-  const int64_t chunk = blockIdx.x;
+// E: the error-feedback buffer's element type -- fp32, or bf16 (uint16_t) to halve its footprint
+// on large models (Llama-3-8B: 16 GB instead of 32 GB per rank); c is formed in fp32 either way.
+// Vector layout: thread t of a 256-thread block owns 8 CONSECUTIVE elements of one of the block's
+// two 1024-element chunks (128 threads = 2 waves per chunk): 16-B loads / stores of g and e, and
+// its 8 sign bits are exactly one byte of the packed words (element i -> word i / 64, bit i % 64
+// == byte i / 8, bit i % 8 in little-endian memory), stored as a byte -- a wave writes 64
+// consecutive bytes.  The chunk's mean |c| is a 2-wave reduction through LDS.  (The previous
+// element-strided kernel with a wave64 ballot per word ran at ~0.4 TB/s: 0.49 ms per 64 MB
+// bf16 bucket, profiles/r5_llama_width_onebit.txt.)
+template <typename G, typename E>
+__global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ g, E* __restrict__ err, int64_t n,
+                                                          uint8_t* __restrict__ wbytes, float* __restrict__ scales) {
+  __shared__ float part[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t chunk = static_cast<int64_t>(blockIdx.x) * 2 + (t >> 7);
   const int64_t base = chunk * kOnebitChunk;
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  float c[4];
+  const int64_t i0 = base + static_cast<int64_t>(t & 127) * 8;
+  float c[8];
   float asum = 0.f;
+  const bool full = i0 + 8 <= n;
+  if (full) {
+    float gv[8], ev[8];
+    load8(g, i0, gv);
+    load8(err, i0, ev);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t i = base + j * 256 + threadIdx.x;
-    float v = 0.f;
-    if (i < n) v = Elem<G>::load(g, i) + err[i];
-    c[j] = v;
-    asum += fabsf(v);
+    for (int k = 0; k < 8; ++k) {
+      c[k] = gv[k] + ev[k];
+      asum += fabsf(c[k]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = i0 + k;
+      c[k] = i < n ? Elem<G>::load(g, i) + Elem<E>::load(err, i) : 0.f;
+      asum += fabsf(c[k]);
+    }
   }
+  asum = wave_sum(asum);
+  if (lane == 0) part[wid] = asum;
+  __syncthreads();
+  if (base >= n) return;  // (a block's second chunk past the end: after the barrier)
+  const float tot = part[(wid & ~1)] + part[(wid & ~1) + 1];
   const int64_t valid = (n - base) < kOnebitChunk ? (n - base) : kOnebitChunk;
-  asum = block_sum(asum, scratch);
-  const float scale = asum / static_cast<float>(valid);
-  if (threadIdx.x == 0) scales[chunk] = scale;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t i = base + j * 256 + threadIdx.x;
-    const bool pos = (i < n) && c[j] >= 0.f;  // padded lanes contribute 0 bits
-    const uint64_t m = __ballot(pos);
-    if (i < n) err[i] = c[j] - (pos ? scale : -scale);
-    const int64_t wbase = base + j * 256 + wid * 64;
-    if (lane == 0 && wbase < n) words[wbase / 64] = m;
+  const float scale = tot / static_cast<float>(valid);
+  if ((t & 127) == 0) scales[chunk] = scale;
+  if (i0 >= n) {  // past the end inside the last word: zero bits, as the host layout pads
+    if (i0 < ((n + 63) & ~int64_t(63))) wbytes[i0 >> 3] = 0;
+    return;
   }
+  unsigned byte = 0;
+  float e[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool pos = (i0 + k < n) && c[k] >= 0.f;  // padded elements contribute 0 bits
+    byte |= (pos ? 1u : 0u) << k;
+    e[k] = c[k] - (pos ? scale : -scale);
+  }
+  if (full) {
+    store8(err, i0, e);
+  } else {
+    for (int k = 0; k < 8 && i0 + k < n; ++k) Elem<E>::store(err, i0 + k, e[k]);
+  }
+  wbytes[i0 >> 3] = static_cast<uint8_t>(byte);
 }
 
 // 8 consecutive elements per thread (one byte of a packed word, one 16-B / 32-B output store):
@@ -95,16 +126,20 @@ __global__ __launch_bounds__(256) void onebit_unpack_reduce_kernel(const uint64_
   }
 }
 
-void launch_onebit_pack(const void* g, int gdtype, float* err, int64_t n, uint64_t* words, float* scales,
+void launch_onebit_pack(const void* g, int gdtype, void* err, int edtype, int64_t n, uint64_t* words, float* scales,
                         hipStream_t s) {
   if (n <= 0) return;
   const int64_t nchunks = (n + kOnebitChunk - 1) / kOnebitChunk;
-  if (gdtype == 1)
-    hipLaunchKernelGGL(onebit_pack_kernel<uint16_t>, dim3(nchunks), dim3(256), 0, s, static_cast<const uint16_t*>(g),
-                       err, n, words, scales);
-  else
-    hipLaunchKernelGGL(onebit_pack_kernel<float>, dim3(nchunks), dim3(256), 0, s, static_cast<const float*>(g), err,
-                       n, words, scales);
+  const int64_t nblk = (nchunks + 1) / 2;
+  uint8_t* wb = reinterpret_cast<uint8_t*>(words);
+#define PSAMD_PACK(G, E)                                                                                           \
+  hipLaunchKernelGGL((onebit_pack_kernel<G, E>), dim3(nblk), dim3(256), 0, s, static_cast<const G*>(g),            \
+                     static_cast<E*>(err), n, wb, scales)
+  if (gdtype == 1 && edtype == 1) PSAMD_PACK(uint16_t, uint16_t);
+  else if (gdtype == 1) PSAMD_PACK(uint16_t, float);
+  else if (edtype == 1) PSAMD_PACK(float, uint16_t);
+  else PSAMD_PACK(float, float);
+#undef PSAMD_PACK
 }
 
 void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int nworkers, int64_t n,

@@ -905,6 +905,145 @@ class Arena {
   std::vector<void*> opened_;
 };
 
+// An arena built from physical chunks of at most ``chunk`` bytes (HIP virtual memory management),
+// mapped back to back into ONE virtual range, so the local view is contiguous like Arena's.  Why:
+// on this stack hipIpcOpenMemHandle hangs for any allocation above 2 GiB (1.99 GiB opens at once,
+// 2.01 GiB never returns: profiles/r6_plane_ipc_2gib.txt), and a Llama-3-8B plane arena is ~34 GB.
+// Each chunk is exported as a dma-buf file descriptor (the fds travel to the peers over a Unix
+// socket, ps_amd/parallel/plane.py); a peer imports every chunk and maps them back to back into a
+// virtual range of its own, so it also sees one contiguous arena -- the plane engine's (base +
+// offset) addressing is unchanged.
+class VmmArena {
+ public:
+  VmmArena(int64_t nbytes, int64_t device, int64_t chunk) : dev_(static_cast<int>(device)) {
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    hipMemAllocationProp prop = props(dev_);
+    size_t gran = 0;
+    hip_ok(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum), "granularity");
+    gran_ = gran;
+    const size_t ch = round_up(static_cast<size_t>(chunk), gran);
+    size_t left = round_up(static_cast<size_t>(nbytes), gran);
+    while (left > 0) {
+      const size_t sz = left < ch ? left : ch;
+      sizes_.push_back(sz);
+      left -= sz;
+    }
+    total_ = 0;
+    for (size_t sz : sizes_) total_ += sz;
+    hip_ok(hipMemAddressReserve(&base_, total_, gran, nullptr, 0), "hipMemAddressReserve");
+    size_t off = 0;
+    for (size_t sz : sizes_) {
+      hipMemGenericAllocationHandle_t h;
+      hip_ok(hipMemCreate(&h, sz, &prop, 0), "hipMemCreate");
+      handles_.push_back(h);
+      hip_ok(hipMemMap(static_cast<char*>(base_) + off, sz, 0, h, 0), "hipMemMap");
+      off += sz;
+    }
+    set_access(base_, total_);
+    hip_ok(hipMemset(base_, 0, total_), "hipMemset");
+    hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    n_ = nbytes;
+  }
+  ~VmmArena() { close(); }
+
+  // one dma-buf fd per chunk (the caller sends them to the peers, then closes them)
+  std::vector<int64_t> export_fds() {
+    std::vector<int64_t> fds;
+    for (auto h : handles_) {
+      int fd = -1;
+      hip_ok(hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0),
+             "hipMemExportToShareableHandle");
+      fds.push_back(fd);
+    }
+    return fds;
+  }
+  std::vector<int64_t> chunk_sizes() const { return std::vector<int64_t>(sizes_.begin(), sizes_.end()); }
+
+  // map a peer's chunks (received fds, its chunk sizes) back to back; -> the peer arena's base here
+  int64_t open(std::vector<int64_t> fds, std::vector<int64_t> sizes, int64_t peer_device) {
+    TORCH_CHECK(fds.size() == sizes.size() && !fds.empty(), "one fd per chunk");
+    hip_ok(hipSetDevice(dev_), "hipSetDevice");
+    if (peer_device != dev_) {
+      int can = 0;
+      hip_ok(hipDeviceCanAccessPeer(&can, dev_, static_cast<int>(peer_device)), "hipDeviceCanAccessPeer");
+      TORCH_CHECK(can, "GPU ", dev_, " cannot access peer GPU ", peer_device);
+    }
+    size_t total = 0;
+    for (auto sz : sizes) total += static_cast<size_t>(sz);
+    Peer pr;
+    pr.size = total;
+    hip_ok(hipMemAddressReserve(&pr.base, total, gran_, nullptr, 0), "hipMemAddressReserve(peer)");
+    size_t off = 0;
+    for (size_t i = 0; i < fds.size(); ++i) {
+      hipMemGenericAllocationHandle_t h;
+      // this HIP reads the descriptor THROUGH the pointer (passing the fd value as a pointer, the
+      // CUDA convention, faults at that address)
+      int fdv = static_cast<int>(fds[i]);
+      hip_ok(hipMemImportFromShareableHandle(&h, &fdv, hipMemHandleTypePosixFileDescriptor),
+             "hipMemImportFromShareableHandle");
+      pr.handles.push_back(h);
+      hip_ok(hipMemMap(static_cast<char*>(pr.base) + off, static_cast<size_t>(sizes[i]), 0, h, 0), "hipMemMap(peer)");
+      off += static_cast<size_t>(sizes[i]);
+    }
+    set_access(pr.base, total);
+    peers_.push_back(pr);
+    return reinterpret_cast<int64_t>(pr.base);
+  }
+
+  void close() {
+    if (dev_ < 0) return;
+    hipSetDevice(dev_);
+    hipDeviceSynchronize();
+    for (auto& pr : peers_) release(pr.base, pr.size, pr.handles);
+    peers_.clear();
+    if (base_ != nullptr) release(base_, total_, handles_);
+    base_ = nullptr;
+    handles_.clear();
+    dev_ = -1;
+  }
+  torch::Tensor tensor() {
+    auto opts = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, dev_);
+    return torch::from_blob(base_, {n_}, [](void*) {}, opts);
+  }
+  int64_t base() const { return reinterpret_cast<int64_t>(base_); }
+
+ private:
+  struct Peer {
+    void* base = nullptr;
+    size_t size = 0;
+    std::vector<hipMemGenericAllocationHandle_t> handles;
+  };
+  static hipMemAllocationProp props(int dev) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    return prop;
+  }
+  static size_t round_up(size_t n, size_t g) { return (n + g - 1) / g * g; }
+  void set_access(void* p, size_t n) {
+    hipMemAccessDesc d{};
+    d.location.type = hipMemLocationTypeDevice;
+    d.location.id = dev_;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    hip_ok(hipMemSetAccess(p, n, &d, 1), "hipMemSetAccess");
+  }
+  static void release(void* base, size_t size, std::vector<hipMemGenericAllocationHandle_t>& hs) {
+    hipMemUnmap(base, size);
+    for (auto h : hs) hipMemRelease(h);
+    hs.clear();
+    hipMemAddressFree(base, size);
+  }
+  int dev_;
+  int64_t n_ = 0;
+  size_t gran_ = 0, total_ = 0;
+  void* base_ = nullptr;
+  std::vector<size_t> sizes_;
+  std::vector<hipMemGenericAllocationHandle_t> handles_;
+  std::vector<Peer> peers_;
+};
+
 // ------------------------------------------------------------------ IPC events
 // An event another process on the node can make its streams wait on (hipEventInterprocess):
 // the owner records it after a kernel, a peer that opened the handle enqueues
@@ -1036,6 +1175,14 @@ void register_plane(pybind11::module& m) {
       .def("query", &IpcEvent::query)
       .def("synchronize", &IpcEvent::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("ptr", &IpcEvent::ptr);
+  py::class_<VmmArena>(pm, "VmmArena")
+      .def(py::init<int64_t, int64_t, int64_t>())
+      .def("tensor", &VmmArena::tensor)
+      .def_property_readonly("base", &VmmArena::base)
+      .def("export_fds", &VmmArena::export_fds)
+      .def("chunk_sizes", &VmmArena::chunk_sizes)
+      .def("open", &VmmArena::open)
+      .def("close", &VmmArena::close);
   py::class_<Arena>(pm, "Arena")
       .def(py::init<int64_t, int64_t>())
       .def("tensor", &Arena::tensor)

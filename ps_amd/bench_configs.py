@@ -216,6 +216,7 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
     # A/B that prices the serve's HBM traffic stretching backward (profiles/r4_llama_serve_overlap.txt)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
                      compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None),
+                     ef_dtype=torch.bfloat16,  # bf16 error feedback: 16 GB instead of 32 GB per rank at 8B
                      overlap=os.environ.get("PS_AMD_OVERLAP", "1") == "1")
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)

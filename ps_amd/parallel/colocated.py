@@ -42,6 +42,8 @@ arbitrary per-key-prefix updaters (resolve_updater).
 """
 from __future__ import annotations
 
+import contextlib
+
 import time
 from collections import deque
 from functools import partial
@@ -64,7 +66,8 @@ class ColocatedPS:
                  staleness: int = 0, clip_norm: Optional[float] = None, compress: Optional[str] = None,
                  average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
                  compress_warmup: int = 0, split_comm: Optional[bool] = None, plane: Optional[str] = None,
-                 timeout_s: float = 600.0, reduce_fp32: Optional[bool] = None):
+                 timeout_s: float = 600.0, reduce_fp32: Optional[bool] = None,
+                 ef_dtype: Optional[torch.dtype] = None):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -177,12 +180,21 @@ class ColocatedPS:
                 self.gshard.append(torch.empty(b.chunk, dtype=gdt, device=self.device))
             else:
                 self.gshard.append(None)
-        # 1-bit compression state: error-feedback buffer per bucket (full bucket, fp32); with the
-        # plane the packed words / scales live in its arena (one per gradient slot)
+        # 1-bit compression state: error-feedback buffer per bucket (full bucket; fp32, or bf16 via
+        # ``ef_dtype`` -- Llama-3-8B: 16 instead of 32 GB per rank); with the plane the packed words
+        # / scales live in its arena (one per gradient slot)
+        self.ef_dtype = ef_dtype or torch.float32
+        if self.ef_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"error-feedback dtype {ef_dtype} (fp32 or bf16)")
+        # the plane path packs on its own stream behind each bucket's landing event, so the
+        # 1-bit pack + error feedback never sits in the backward's stream
+        self.pack_stream = None
         if compress == "onebit" and self.plane is not None:
-            self.err = [torch.zeros(b.size, dtype=torch.float32, device=self.device) for b in R.buckets]
+            self.err = [torch.zeros(b.size, dtype=self.ef_dtype, device=self.device) for b in R.buckets]
+            if self.gpu:
+                self.pack_stream = torch.cuda.Stream(device=self.device)
         elif compress == "onebit":
-            self.err = [torch.zeros(b.size, dtype=torch.float32, device=self.device) for b in R.buckets]
+            self.err = [torch.zeros(b.size, dtype=self.ef_dtype, device=self.device) for b in R.buckets]
             self.cwords = []
             self.cscales = []
             for b in R.buckets:
@@ -361,9 +373,18 @@ class ColocatedPS:
                 bk = self.reg.buckets[b]
                 gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
                 words, scales = self.plane.words(b, self.gslot)
-                self._mark("pack0")
-                _cmp.onebit_pack(gin, self.err[b], words, scales)  # sign bits + scales + error feedback
-                self._mark("pack1")
+                if self.pack_stream is not None:  # behind the landing, off the backward's stream
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.device))
+                    self.pack_stream.wait_event(ev)
+                with (torch.cuda.stream(self.pack_stream) if self.pack_stream is not None
+                      else contextlib.nullcontext()):
+                    self._mark("pack0")
+                    _cmp.onebit_pack(gin, self.err[b], words, scales)  # sign bits + scales + error feedback
+                    self._mark("pack1")
+                    with _trace.range(f"ps.push.b{b}"):  # the push's landing event: after the pack
+                        self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
+                return
             with _trace.range(f"ps.push.b{b}"):
                 self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
             return
@@ -573,6 +594,10 @@ class ColocatedPS:
     def _finish_plane_round(self) -> None:
         """Round bookkeeping of the xGMI plane: the engine runs serve / pull on its own streams;
         the compute stream waits only for the round the next forward must see."""
+        if self.pack_stream is not None:
+            # the next round's gradients (PsLinear writes them straight into the buckets during
+            # backward) overwrite what this round's packs read: order them after every pack
+            torch.cuda.current_stream(self.device).wait_stream(self.pack_stream)
         self.round += 1
         self.stats["rounds"] += 1
         v = max(0, self.round - self.staleness)

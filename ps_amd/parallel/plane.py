@@ -49,6 +49,7 @@ from ..ops import compress as _cmp
 from ..ops import optim as _o
 from ..ops import reduce as _red
 from .async_ps import _addr, _ShmSeg
+from .ipc_arena import IpcArena
 from .transport import Transport
 
 _ALIGN = 256
@@ -136,7 +137,7 @@ class XgmiPlane:
         if self.gpu:
             err = None
             try:
-                self._arena = P.Arena(self.nbytes, device.index)
+                self._arena = IpcArena(self.nbytes, device.index)  # VMM chunks above 1 GiB (ipc_arena.py)
                 self.arena = self._arena.tensor()
                 mine = (self._arena.handle() if not self.threads else self._arena.base, device.index)
             except Exception as e:  # noqa: BLE001 -- reported through the agreement

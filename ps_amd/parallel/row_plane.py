@@ -240,10 +240,9 @@ class RowPlane:
         self.cap = cap
         self.off, nbytes = self._layout(cap)
         if self.gpu and not self.threads:
-            from .. import _C  # type: ignore
+            from .ipc_arena import IpcArena
 
-            P = _C.plane
-            self._arena = P.Arena(nbytes, self.device.index)
+            self._arena = IpcArena(nbytes, self.device.index)
             mine = self._arena.tensor()
             hs = self.t.all_gather_object((self._arena.handle(), self.device.index))
             bases = [self._arena.base if r == self.me else self._arena.open(h, d) for r, (h, d) in enumerate(hs)]

@@ -122,7 +122,7 @@ def test_lerp():
     torch.testing.assert_close(out.cpu(), 0.3 * w0 + 0.7 * w)
 
 
-@pytest.mark.parametrize("n", [64, 1024, 3000, 70000])
+@pytest.mark.parametrize("n", [64, 1024, 3000, 3001, 70000])
 def test_onebit(n):
     torch.manual_seed(n)
     g = torch.randn(n)
@@ -145,6 +145,25 @@ def test_onebit(n):
     out = torch.zeros(n, device=DEV)
     C.onebit_unpack_reduce(W.to(DEV), Sc.to(DEV), out, 0.5)
     torch.testing.assert_close(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_onebit_bf16_error_feedback(gdt):
+    """The error-feedback buffer in bf16 (colocated.py ef_dtype): c = g + e is formed in fp32 and the
+    new residual is rounded to bf16 -- the CPU oracle does the same."""
+    n = 5000
+    torch.manual_seed(7)
+    g = torch.randn(n).to(gdt)
+    err = (torch.randn(n) * 0.1).bfloat16()
+    nw, ns = C.packed_sizes(n)
+    rw, rs, re = torch.zeros(nw, dtype=torch.int64), torch.zeros(ns), err.clone()
+    C.onebit_pack(g, re, rw, rs)
+    gw, gs, ge = torch.zeros(nw, dtype=torch.int64, device=DEV), torch.zeros(ns, device=DEV), err.to(DEV)
+    C.onebit_pack(g.to(DEV), ge, gw, gs)
+    assert ge.dtype == torch.bfloat16
+    assert torch.equal(gw.cpu(), rw)
+    torch.testing.assert_close(gs.cpu(), rs, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ge.cpu().float(), re.float(), rtol=1e-2, atol=1e-3)
 
 
 def test_sparse_rows():

@@ -382,7 +382,7 @@ def test_world8_collective_fp32_reduction_closer_to_fp32_oracle():
     assert errs[True] < 0.05, errs
 
 
-def _llama_body(tp, steps):
+def _llama_body(tp, steps, ef_dtype=None):
     from ps_amd.models.transformer import LlamaConfig, LlamaForCausalLM
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import AdamUpdater
@@ -392,7 +392,8 @@ def _llama_body(tp, steps):
     cfg = LlamaConfig.tiny()
     model = LlamaForCausalLM(cfg).cuda().to(torch.bfloat16)
     ps = ColocatedPS(model, AdamUpdater(3e-3, 0.9, 0.95, 1e-8, bias_correction="step"), tp, bucket_mb=0.05,
-                     compress="onebit", compress_warmup=2, plane="xgmi", timeout_s=60)
+                     compress="onebit", compress_warmup=2, plane="xgmi", timeout_s=60, ef_dtype=ef_dtype)
+    assert ps.pack_stream is not None  # the pack runs off the backward's stream
     g = torch.Generator(device="cuda").manual_seed(tp.rank)
     ids = torch.randint(0, 64, (4, 64), device="cuda", generator=g)  # a small learnable vocabulary
     losses = []
@@ -408,10 +409,12 @@ def _llama_body(tp, steps):
     return out, losses
 
 
-def test_tiny_llama_onebit_two_processes_on_the_plane():
+@pytest.mark.parametrize("ef_dtype", [None, torch.bfloat16])
+def test_tiny_llama_onebit_two_processes_on_the_plane(ef_dtype):
     """the Llama config's 1-bit push (owner decodes the W packed pushes inside
-    the fused Adam kernel) with 2 processes: replicas stay identical, the loss falls."""
-    res = dist_util.run(_llama_body, 2, (25,))
+    the fused Adam kernel) with 2 processes: replicas stay identical, the loss falls -- with the
+    error feedback in fp32 and in bf16 (the 8B bench's choice), packed on the pack stream."""
+    res = dist_util.run(_llama_body, 2, (25, ef_dtype))
     for k in res[0][0]:
         assert torch.equal(res[0][0][k], res[1][0][k])
     for _, losses in res:
