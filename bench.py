@@ -49,22 +49,23 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("PS_AMD_BUCKET_MB", "25")))
     ap.add_argument("--last-bucket-mb", type=float, default=2.0)
     ap.add_argument("--staleness", type=int, default=0)
+    ap.add_argument("--async-ps", type=int, default=1,
+                    help="bert: the asynchronous PS (one-sided pushes); 0: the pipelined collective SSP engine")
     ap.add_argument("--plane", default=os.environ.get("PS_AMD_PLANE", "auto"), choices=["auto", "xgmi", "collective"],
                     help="PS data plane at world > 1: one-sided xGMI plane (IPC) or RCCL collectives")
     ap.add_argument("--bn-fp32", type=int, default=1)
-    ap.add_argument("--fused-bn", type=int, default=int(os.environ.get("PS_AMD_FUSED_BN", "1")),
+    ap.add_argument("--fused-bn", type=int, default=1,
                     help="HIP fused BatchNorm+residual+ReLU kernels (ops/bn.py) instead of MIOpen BN")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--dlrm-rows", type=int, default=1000000)
     ap.add_argument("--tiny", type=int, default=0, help="llama-onebit: tiny config (smoke only)")
-    ap.add_argument("--graph", type=str, default=os.environ.get("PS_AMD_GRAPH", "0"),
-                    help="capture the whole step in a HIP graph: 1/0/auto (measured slower on ROCm 7 for "
-                         "ResNet-50: 32.7 vs 31.6 ms, profiles/archive/r1_graph_vs_eager.txt)")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler over N extra steps (rank 0)")
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--comm-probe", type=int, default=1,
                     help="world > 1: after the timed region, measure RS / AG / AR bandwidth (ps_amd/parallel/"
                          "comm_probe.py) and report it in the JSON config")
+    ap.add_argument("--compute-priority", choices=["auto", "high", "normal"], default="auto",
+                    help="stream priority of forward / backward (auto: high for ResNet-50 with one rank per GPU)")
     ap.add_argument("--checkpoint-dir", type=str, default=os.environ.get("PS_AMD_CHECKPOINT_DIR", ""),
                     help="after the timed region: one sharded checkpoint of every rank's server shard (timed, "
                          "reported on stderr) -- utils/checkpoint.py")
@@ -148,9 +149,10 @@ def main():
         # measured on (bs1024 +0.15 %, three interleaved pairs, profiles/r4_wgrad_stream_policy.txt),
         # which a one-process-per-GPU node reproduces whatever WORLD_SIZE is; normal when ranks
         # share a GPU, and for the asynchronous configs, whose owner service threads launch on
-        # normal-priority streams (PS_AMD_COMPUTE_PRIORITY forces it)
-        prio = os.environ.get("PS_AMD_COMPUTE_PRIORITY",
-                              "high" if (rpd == 1 and args.config == "resnet50") else "normal")
+        # normal-priority streams (--compute-priority forces it)
+        prio = args.compute_priority
+        if prio == "auto":
+            prio = "high" if (rpd == 1 and args.config == "resnet50") else "normal"
         if prio == "high":
             torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     dev = torch.device("cpu") if cpu else torch.device("cuda", local)
@@ -159,22 +161,13 @@ def main():
         if not cpu:
             torch.cuda.synchronize()
 
-    from ps_amd.utils import gemm_tuning
-
-    gemm_table = gemm_tuning.load(args.config, dev)  # tuned hipBLASLt choices, lookups only
     torch.manual_seed(1234)
     bench = BC.SETUPS[args.config](args, tp, dev)
     step = bench.step
 
-    use_graph = args.graph == "1" or (args.graph == "auto" and world == 1)
     tw0 = time.perf_counter()
-    if use_graph:
-        from ps_amd.train.graphs import GraphedStep
-
-        step = GraphedStep(step, warmup=max(1, args.warmup - 1), feed=bench.feed)
-    else:
-        for _ in range(args.warmup):
-            step()
+    for _ in range(args.warmup):
+        step()
     sync()
     if rank == 0:
         print(f"[bench] {args.config}: warmup {args.warmup} steps took {time.perf_counter() - tw0:.1f}s "
@@ -212,7 +205,7 @@ def main():
     # bandwidth curve of this node's RCCL / xGMI plane
     tsum = comm = None
     n_timing = args.timing if args.timing else (3 if world > 1 else 0)
-    if n_timing and getattr(bench.engine, "timing_summary", None) is not None and not use_graph:
+    if n_timing and getattr(bench.engine, "timing_summary", None) is not None:
         eng = bench.engine
         try:
             eng.timing = True
@@ -234,7 +227,7 @@ def main():
             print("[bench-timing] " + json.dumps(tsum), file=sys.stderr, flush=True)
     audit = None
     n_audit = args.sync_audit if args.sync_audit >= 0 else (2 if args.config in ("dlrm", "ctr-async") else 0)
-    if n_audit and not cpu and not use_graph:
+    if n_audit and not cpu:
         import warnings
 
         try:
@@ -281,8 +274,6 @@ def main():
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     if rank == 0:
         cfg = dict(bench.config)
-        cfg["hip_graph"] = bool(use_graph)
-        cfg["gemm_table"] = os.path.basename(gemm_table) if gemm_table else None
         # the stream policy this run used (keyed on ranks sharing a GPU, not on WORLD_SIZE)
         images = bench.samples_per_step if args.config == "resnet50" else None
         cfg["ranks_per_device"] = rpd

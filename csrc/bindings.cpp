@@ -961,7 +961,6 @@ static void check_part_slabs(const Tensor& part) {
 
 static Tensor fold_partials(const Tensor& part, hipStream_t s) {
   const int G = static_cast<int>(part.size(1)), C = static_cast<int>(part.size(2));
-  if (psamd::bn_fin2_enabled(C)) return part;  // the one-launch finalize reads any G coalesced
   const int S = psamd::partials_fold_rows(G);
   if (S == 0) return part;
   auto f = torch::empty({2, S, C}, part.options());
@@ -1511,12 +1510,9 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dz, std::vector<Tensor> wph, int64_t H,
   }
   const c10::DeviceGuard guard(dz.device());
   auto dx = torch::empty({imgs * H * W, C1}, dz.options());
-  static const bool merged = [] {
-    const char* e = std::getenv("PS_AMD_DGRAD_S2_MERGED");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (merged) {  // the four phases in one grid (csrc convgemm.hip conv_dgrad_phases_kernel)
-    std::vector<Tensor> ws;  // (stream-ordered lifetime, as in the per-phase path)
+  // the four phases in one grid (csrc convgemm.hip conv_dgrad_phases_kernel)
+  {
+    std::vector<Tensor> ws;  // (temporary contiguous weights are freed stream-ordered)
     ws.reserve(4);
     psamd::ConvGemmArgs ps[4] = {};
     const int gm = psamd::conv_dgrad_phase_gm(static_cast<int>(M));
@@ -1550,35 +1546,6 @@ std::vector<Tensor> conv_dgrad_s2(Tensor dz, std::vector<Tensor> wph, int64_t H,
     psamd::launch_conv_dgrad_phases(ps, cur_stream(dz));
     return {dx, part};
   }
-  std::vector<Tensor> parts;
-  for (int ph = 0; ph < 4; ++ph) {
-    const int a = ph >> 1, b = ph & 1, nh = a ? 2 : 1, nw = b ? 2 : 1;
-    Tensor w = wph[ph].contiguous();
-    check_rows(w, "phase weight");
-    TORCH_CHECK(w.dim() == 2 && w.size(0) == C1 && w.size(1) == nh * nw * C2, "phase weight [C1, nh*nw*C2]");
-    psamd::ConvGemmArgs p{};
-    p.a = u16(dz);
-    p.b = u16(w);
-    p.c = u16m(dx);
-    p.M = static_cast<int>(M);
-    p.N = static_cast<int>(C1);
-    p.K = static_cast<int>(nh * nw * C2);
-    p.g = psamd::ConvGeo{static_cast<int>(OH), static_cast<int>(OW), static_cast<int>(OH), static_cast<int>(OW),
-                         static_cast<int>(C2), nh, 1, 0, nw, static_cast<int>(H), static_cast<int>(W), a, b};
-    p.epi = static_cast<int>(epi);
-    if (epi == 3) {
-      const int G = psamd::conv_fwd_plan(p.M, p.N, p.K, false).gm;
-      parts.push_back(torch::empty({2, G, C1}, dz.options().dtype(torch::kFloat32)));
-      p.aux = zp;
-      p.mc = f32_opt(mc, 2 * C1, "mc");
-      p.mean = f32_opt(mean, C1, "mean");
-      p.invstd = f32_opt(invstd, C1, "invstd");
-      p.part = parts.back().data_ptr<float>();
-    }
-    psamd::launch_conv_fwd(p, cur_stream(dz));  // (a temporary contiguous w is freed stream-ordered)
-  }
-  Tensor part = epi == 3 ? torch::cat(parts, 1) : Tensor();
-  return {dx, part};
 }
 
 // dW [N, ks*ks*C] (bf16) = sum_m dz[m, :]^T f(x[src(m, k)])
@@ -1668,28 +1635,6 @@ std::vector<Tensor> conv11_bwd_fused(Tensor g, Tensor z3, Tensor cbwd, Tensor wt
         std::to_string(co));
   psamd::launch_conv11_bwd_fused(a, ci, co, cur_stream(g));
   return {gy, part, dw};
-}
-
-// A stream whose kernels may only run on n_cus of the device's CUs (hipExtStreamCreateWithCUMask),
-// spread evenly over the CU index space (every (CUs / n)-th CU, so every XCD keeps a share) or the
-// first n.  The PS serve of a single-GPU Llama step runs on it beside backward
-// (parallel/colocated.py, PS_AMD_SERVE_CUS): the serve keeps a bounded slice of the chip instead
-// of contending for all of it.  Returned as the raw handle for torch.cuda.ExternalStream; it lives
-// for the process.
-int64_t cu_mask_stream(int64_t device, int64_t n_cus, bool spread) {
-  hipDeviceProp_t prop;
-  TORCH_CHECK(hipGetDeviceProperties(&prop, static_cast<int>(device)) == hipSuccess, "hipGetDeviceProperties");
-  const int ncu = prop.multiProcessorCount;
-  TORCH_CHECK(n_cus >= 1 && n_cus <= ncu, "n_cus must be in 1..", ncu);
-  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  const int step = spread ? std::max(1, ncu / static_cast<int>(n_cus)) : 1;
-  int set = 0;
-  for (int c = 0; c < ncu && set < n_cus; c += step, ++set) mask[c / 32] |= 1u << (c % 32);
-  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, static_cast<c10::DeviceIndex>(device)));
-  hipStream_t st = nullptr;
-  TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess,
-              "hipExtStreamCreateWithCUMask");
-  return reinterpret_cast<int64_t>(st);
 }
 
 bool conv11_bwd_fused_supported(int64_t ci, int64_t co, bool plain) {
@@ -1841,7 +1786,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cf2") = py::none(), py::arg("mean2") = py::none(), py::arg("invstd2") = py::none());
   m.def("conv11_bwd_fused_supported", &conv11_bwd_fused_supported, py::arg("ci"), py::arg("co"),
         py::arg("plain") = false);
-  m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("n_cus"), py::arg("spread") = true);
   m.def("bn_apply_coef", &bn_apply_coef, py::arg("x"), py::arg("coef"), py::arg("res") = py::none(),
         py::arg("rcoef") = py::none(), py::arg("act") = 1, py::arg("want_mask") = false);
   m.def("bn_bwd_partials", &bn_bwd_partials);

@@ -229,8 +229,6 @@ int stem_wrw_blocks(int N, int OH);
 int partials_fold_rows(int G);
 void launch_partials_fold(const float* p, const float* q, int G, int C, float* op, float* oq, hipStream_t s);
 // BN finalize from producer-fused partial sums ps/pq: [G][C] of sum(x - k), sum((x - k)^2)
-// the one-launch coalesced finalize (bn_fin2_kernel) serves this C: callers skip the partials fold
-bool bn_fin2_enabled(int C);
 void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,
                              float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
@@ -358,18 +356,10 @@ struct ConvGemmArgs {
   FastDiv fd_ohw, fd_ow;  // set by launch_conv_fwd (OH * OW, OW)
   int pgm;                // rows per partial slab (0: the launch's gm); several GEMMs share one part
   uint64_t* tbuf = nullptr;  // conv_big only, diagnostics: 8 wall-clock stamps per block (nullable)
-  // conv_big stream-K (set by its launcher): block c owns (tile, stage) units [c sk_units, ..);
-  // a tile split across blocks is finished by the block holding its first stage, which adds the
-  // others' fp32 partials (sk_ws, one slot per block) once their flag reads sk_epoch
-  float* sk_ws = nullptr;
-  int* sk_flag = nullptr;
-  int sk_units = 0, sk_epoch = 0;
-  int krot = 0;  // conv_big: rotate each tile's K order by (tile mod stages)
 };
 struct ConvFwdPlan {
   int bm, bn, gm;       // tile pixels / channels, pixel-tile groups (partial-sum rows)
 };
-// epi: the fold epilogues (6-9) may run on one-tile-per-block LDS-DMA grids (PS_AMD_FOLD_GLDS)
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi = 0);
 // conv_big.hip: 256 x 256 tiles, one 512-thread block per CU, for deep-K 1x1 GEMMs (every epilogue);
 // conv_fwd_plan_geo / launch_conv_fwd route there when conv_big_ok holds (gm = conv_big_gm(M))
@@ -386,12 +376,6 @@ int conv_dgrad_phase_gm(int M);
 // src2: the launch's two-source prologue (0 none, 1 block output, 2 BN backward)
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2 = 0, int epi = 0);
 void launch_conv_fwd(const ConvGemmArgs& a, hipStream_t s);
-// the planar resident-weight 3x3 64 -> 64 kernel (conv3x3_c64.hip): epi 1 / 3, gm = the plan's blocks
-void launch_conv3x3_c64s(const ConvGemmArgs& a, int gm, hipStream_t s);
-// mode 3: the 64 x 576 weight held in registers by every wave (PS_AMD_CONV_C64=3)
-void launch_conv3x3_c64r(const ConvGemmArgs& a, int gm, hipStream_t s);
-// mode 4: the weight in registers + a rolling 8-row window over contiguous 2-row tiles (PS_AMD_CONV_C64=4)
-void launch_conv3x3_c64v(const ConvGemmArgs& a, int gm, hipStream_t s);
 // Backward layouts of many conv weights in one launch: jobs = device array of
 // {src, dst, kind (0 1x1 transpose, 1 3x3 flip-transpose, 2 3x3 stride-2 phases), A, B} (32 B each)
 void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t s);

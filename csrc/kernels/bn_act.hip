@@ -15,8 +15,6 @@
 // kernel that sums them in fixed order.  act: 0 none, 1 relu.
 #include <algorithm>
 #include <cstdlib>
-#include <map>
-#include <mutex>
 #include <utility>
 
 #include "psamd_device.h"
@@ -52,11 +50,7 @@ int bn_red_blocks(int64_t R, int C) {
   const int64_t want = (2048 + ctiles - 1) / ctiles;
   if (g < want) g = std::min<int64_t>(want, (R + 7) / 8);
   if (g < 1) g = 1;
-  static const int64_t cap = [] {
-    const char* e = std::getenv("PS_AMD_BN_RED_MAXG");  // A/B knob for the block cap
-    return static_cast<int64_t>(e ? std::atoi(e) : 2048);
-  }();
-  if (g > cap) g = cap;
+  if (g > 2048) g = 2048;
   return static_cast<int>(g);
 }
 
@@ -524,175 +518,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
   }
 }
 
-// ------------------------------------------------------------------------------ one-launch finalize
-// The BN statistics / backward coefficients from a producer's partial sums [2][G][C] in ONE launch
-// with coalesced reads: block (cg, chunk) sums rows [chunk rows] of 64 channels (a wave reads one
-// row's 64 floats, 8 rows in flight per wave), publishes its 2 x 64 sums with agent-coherent stores,
-// and the last block of the channel group (a counter) adds the chunks in chunk order -- fixed-order,
-// so deterministic -- and runs the per-channel math of bn_finalize_kernel (MODE 0) or
-// bn_bwd_finalize_kernel (MODE 1).  Replaces the fold + 8-channel finalize pair (latency-bound:
-// 9-24 us per call with C / 8 blocks of strided 32-B reads; ~100 calls per ResNet-50 step).
-struct BnFin2Args {
-  const float* p;  // [G][C] first sums (stats: sum(x - k); backward: sum(dz))
-  const float* q;  // [G][C] second sums (stats: sum((x - k)^2); backward: sum(dz * xhat))
-  int G, C, nchunk, rows;  // rows per chunk
-  int64_t R;
-  float* ws;      // [C / 64][nchunk][2][64] chunk sums
-  int* cnt;       // [C / 64] arrival counters (zero between launches)
-  // MODE 0
-  const float* kshift;
-  float eps, momentum;
-  const float *gamma, *beta;
-  float *rmean, *rvar, *mean, *invstd, *scale, *shift;
-  // MODE 1 (mean / invstd read, gamma as above)
-  const float *bmean, *binvstd;
-  float *dgamma, *dbeta, *ca, *cb, *cc;
-};
-
-template <int MODE>
-__global__ __launch_bounds__(256) void bn_fin2_kernel(const BnFin2Args a) {
-  __shared__ float red[2][4][64];
-  __shared__ int last;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int cgp = blockIdx.x, chunk = blockIdx.y, c = cgp * 64 + lane;
-  const int g0 = chunk * a.rows, g1 = min(a.G, g0 + a.rows);
-  float s1 = 0.f, s2 = 0.f;
-  constexpr int U = 8;
-  for (int g = g0 + w; g < g1; g += 4 * U) {
-    float u[U], v[U];
-#pragma unroll
-    for (int i = 0; i < U; ++i) {
-      const int gg = g + 4 * i;
-      const int64_t o = static_cast<int64_t>(gg < g1 ? gg : g1 - 1) * a.C + c;
-      u[i] = gg < g1 ? a.p[o] : 0.f;
-      v[i] = gg < g1 ? a.q[o] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < U; ++i) {
-      s1 += u[i];
-      s2 += v[i];
-    }
-  }
-  red[0][w][lane] = s1;
-  red[1][w][lane] = s2;
-  __syncthreads();
-  if (a.nchunk > 1) {
-    if (t < 128) {  // this chunk's sums, published agent-coherently (sc1) for the last block
-      const int k = t >> 6;
-      const float v = red[k][0][lane] + red[k][1][lane] + red[k][2][lane] + red[k][3][lane];
-      __hip_atomic_store(a.ws + (static_cast<int64_t>(cgp) * a.nchunk + chunk) * 128 + t, v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) last = atomicAdd(a.cnt + cgp, 1) == a.nchunk - 1;
-    __syncthreads();
-    if (!last) return;
-    // the last block: every chunk's sums in chunk order (wave w: chunks w, w + 4, ..; then waves 0-3)
-    float x1 = 0.f, x2 = 0.f;
-    const float* base = a.ws + static_cast<int64_t>(cgp) * a.nchunk * 128;
-    for (int k = w; k < a.nchunk; k += 4) {
-      x1 += __hip_atomic_load(base + k * 128 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      x2 += __hip_atomic_load(base + k * 128 + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    red[0][w][lane] = x1;
-    red[1][w][lane] = x2;
-    __syncthreads();
-    if (t == 0) __hip_atomic_store(a.cnt + cgp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (t >= 64) return;
-  const float S1 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
-  const float S2 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
-  const float inv_n = 1.f / static_cast<float>(a.R);
-  if constexpr (MODE == 0) {
-    const float dm = S1 * inv_n;  // mean - K
-    const float mean = a.kshift[c] + dm;
-    float var = S2 * inv_n - dm * dm;
-    if (var < 0.f) var = 0.f;
-    const float invstd = rsqrtf(var + a.eps);
-    const float ga = a.gamma ? a.gamma[c] : 1.f, be = a.beta ? a.beta[c] : 0.f;
-    a.mean[c] = mean;
-    a.invstd[c] = invstd;
-    a.scale[c] = ga * invstd;
-    a.shift[c] = be - mean * ga * invstd;
-    if (a.rmean) {
-      const float unbiased = a.R > 1 ? var * static_cast<float>(a.R) / static_cast<float>(a.R - 1) : var;
-      a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * mean;
-      a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * unbiased;
-    }
-  } else {
-    if (a.dgamma) a.dgamma[c] = S2;
-    if (a.dbeta) a.dbeta[c] = S1;
-    const float ga = a.gamma ? a.gamma[c] : 1.f;
-    const float is = a.binvstd[c];
-    const float k = ga * is;
-    const float md = S1 * inv_n, mx = S2 * inv_n;
-    a.ca[c] = k;
-    a.cb[c] = -k * is * mx;
-    a.cc[c] = -k * md + k * is * mx * a.bmean[c];
-  }
-}
-
-namespace {
-struct Fin2Ws {
-  float* ws = nullptr;
-  int* cnt = nullptr;
-  size_t ws_floats = 0;
-  int ncnt = 0;
-};
-// per (device, stream) scratch: chunk sums + counters (counters return to zero after every launch)
-Fin2Ws& fin2_ws(hipStream_t s, size_t ws_floats, int ncnt) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, Fin2Ws> all;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(mu);
-  Fin2Ws& w = all[{dev, s}];
-  if (w.ws_floats < ws_floats || w.ncnt < ncnt) {
-    if (w.ws != nullptr) {
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(w.ws);
-      (void)hipFree(w.cnt);
-    }
-    w.ws_floats = std::max(ws_floats, w.ws_floats);
-    w.ncnt = std::max(ncnt, w.ncnt);
-    (void)hipMalloc(reinterpret_cast<void**>(&w.ws), w.ws_floats * sizeof(float));
-    (void)hipMalloc(reinterpret_cast<void**>(&w.cnt), static_cast<size_t>(w.ncnt) * sizeof(int));
-    (void)hipMemsetAsync(w.cnt, 0, static_cast<size_t>(w.ncnt) * sizeof(int), s);
-  }
-  return w;
-}
-// opt-in (PS_AMD_BN_FIN2=1): per call it is 20-30 % faster at C >= 256 with thousands of partial rows
-// but 1.5-2x slower at C = 64 / 128 (the last block's serial walk over 256 chunk sums), and in
-// the bench the difference is within box noise (profiles/r5_bn_fin2_ab.txt)
-bool fin2_on(int C) {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_BN_FIN2");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on && C % 64 == 0;
-}
-// chunks per channel group: ~512 blocks in all, >= 16 rows per chunk, <= 256 chunks
-void fin2_shape(int G, int C, BnFin2Args& a) {
-  const int groups = C / 64;
-  int nchunk = std::max(1, std::min(256, 512 / groups));
-  nchunk = std::min(nchunk, std::max(1, (G + 15) / 16));
-  a.rows = (G + nchunk - 1) / nchunk;
-  a.nchunk = (G + a.rows - 1) / a.rows;
-}
-template <int MODE>
-void fin2_launch(BnFin2Args& a, hipStream_t s) {
-  fin2_shape(a.G, a.C, a);
-  if (a.nchunk > 1) {
-    Fin2Ws& w = fin2_ws(s, static_cast<size_t>(a.C / 64) * a.nchunk * 128, a.C / 64);
-    a.ws = w.ws;
-    a.cnt = w.cnt;
-  }
-  hipLaunchKernelGGL((bn_fin2_kernel<MODE>), dim3(a.C / 64, a.nchunk), dim3(256), 0, s, a);
-}
-}  // namespace
-
 // ------------------------------------------------------------------------------ launchers
 void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
   const int C = a.C;
@@ -734,32 +559,9 @@ void launch_bn_fwd(const BnFwdArgs& a, hipStream_t s) {
 void launch_bn_finalize_sums(const float* ps, const float* pq, const float* kshift, int G, int C, int64_t R,
                              float eps, float momentum, const float* gamma, const float* beta, float* rmean,
                              float* rvar, float* mean, float* invstd, float* scale, float* shift, hipStream_t s) {
-  if (fin2_on(C) && kshift != nullptr) {
-    BnFin2Args f{};
-    f.p = ps;
-    f.q = pq;
-    f.G = G;
-    f.C = C;
-    f.R = R;
-    f.kshift = kshift;
-    f.eps = eps;
-    f.momentum = momentum;
-    f.gamma = gamma;
-    f.beta = beta;
-    f.rmean = rmean;
-    f.rvar = rvar;
-    f.mean = mean;
-    f.invstd = invstd;
-    f.scale = scale;
-    f.shift = shift;
-    fin2_launch<0>(f, s);
-    return;
-  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, ps, pq, nullptr, kshift, G, C, R, eps,
                      momentum, gamma, beta, rmean, rvar, mean, invstd, scale, shift);
 }
-
-bool bn_fin2_enabled(int C) { return fin2_on(C); }
 
 void launch_bn_bwd(const BnBwdArgs& a, hipStream_t s) {
   const int C = a.C;
@@ -881,26 +683,8 @@ void launch_bn_apply_coef(const uint16_t* x, const uint16_t* res, const float* c
 void launch_bn_bwd_partials(const float* pd, const float* px, int G, const uint16_t* g, const uint16_t* x,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
                             float* coef, uint16_t* dx, int64_t R, int C, hipStream_t s) {
-  if (fin2_on(C)) {
-    BnFin2Args f{};
-    f.p = pd;
-    f.q = px;
-    f.G = G;
-    f.C = C;
-    f.R = R;
-    f.gamma = gamma;
-    f.bmean = mean;
-    f.binvstd = invstd;
-    f.dgamma = dgamma;
-    f.dbeta = dbeta;
-    f.ca = coef;
-    f.cb = coef + C;
-    f.cc = coef + 2 * C;
-    fin2_launch<1>(f, s);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, pd, px, G, C, R, gamma, mean,
-                       invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C);
-  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(fin_threads(G)), 0, s, pd, px, G, C, R, gamma, mean,
+                     invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C);
   const int64_t nvec = R * C / 8;
   if (nvec <= 0 || dx == nullptr) return;  // dx null: coefficients only (a GEMM prologue applies them)
   const int grid = apply_grid(nvec);

@@ -18,14 +18,11 @@
 //     a bf16 output tile in LDS, one 16-B column group per thread, rows coalesced.
 // Blocks are XCD-remapped so the channel tiles of one pixel tile share its A rows in one L2.
 // What bounds it (profiles/r5_conv_big_kloop.txt): the K loop runs at the memory system's stage
-// rate (~64 KiB per 1.8 us per CU); opt-in variants kept for the record: 256 x 128 tiles two per
-// CU, stream-K with fixed-order partials (PS_AMD_CONV_BIG_SK, r5_conv_big_stream_k.txt), a
-// per-tile K-order rotation (PS_AMD_CONV_BIG_KROT).
+// rate (~64 KiB per 1.8 us per CU).  Variants measured and removed (round 6): 256 x 128 tiles two
+// per CU, 4 waves of 128 x 128, a 4 x 32-deep ring, stream-K with fixed-order partials, a per-tile
+// K-order rotation -- none faster on the ResNet-50 shapes (profiles/r5_conv_big_kloop.txt,
+// r5_conv_big_stream_k.txt).
 #include <algorithm>
-#include <cstdlib>
-#include <map>
-#include <mutex>
-#include <utility>
 
 #include "psamd_device.h"
 #include "psamd_launch.h"
@@ -41,19 +38,6 @@ typedef __attribute__((address_space(3))) const char lds_char;
 __device__ __attribute__((aligned(16))) uint16_t kBigZero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
 constexpr int kTM = 256;
-// block shapes (CFG):
-//   0  256 x 256 tile, 8 waves of 128 px x 64 ch, one 512-thread block per CU, 128 KiB ring;
-//   1  256 x 128 tile, 4 waves of 128 x 64, 256-thread blocks two per CU, a 72 KiB ring of three
-//      32-deep stages (one block's epilogue can overlap the other's K loop);
-//   2  256 x 256 tile, 4 waves of 128 px x 128 ch (256 accumulators each, one wave per SIMD): a
-//      third less LDS read traffic per FLOP, but 7-24 % slower (the K loop is bound by the stage
-//      DMAs, not LDS reads, and one wave per SIMD hides less latency: profiles/r5_conv_big_kloop.txt);
-//      kept compilable, not launched.
-// (A register-staged ring -- global_load_dwordx4 -> VGPRs -> ds_write_b128 -- ran 0-12 % slower
-// than the LDS-DMA ring: profiles/r5_conv_big_kloop.txt.)
-constexpr int cfg_tn(int cfg) { return cfg == 1 ? 128 : 256; }
-constexpr int cfg_waves(int cfg) { return cfg == 0 ? 8 : 4; }
-constexpr int cfg_ring(int cfg) { return cfg == 1 ? 73728 : 131072; }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_char*)p));
@@ -99,14 +83,10 @@ __device__ __forceinline__ int xcd_remap_big(int b, int nblk) {
 }
 __device__ __forceinline__ uint32_t fdiv_big(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
 
-// Stage tile rows of BK bf16 (2 BK bytes).  BK = 64: 128-B rows, chunk c of row r at c ^ ((r >> 1)
-// & 7); BK = 32: 64-B rows, chunk c at c ^ ((r >> 2) & 3).  Either way the 16 rows of a
+// Stage tile rows of 64 bf16 (128 B): chunk c of row r at c ^ ((r >> 1) & 7), so the 16 rows of a
 // ds_read_b128 lane group land on 16 distinct 16-B bank slots, and the swizzle of a 32-row
 // fragment block depends on fr = r & 31 only.
-template <int BK>
-__device__ __forceinline__ int bswz(int r, int c) {
-  return BK == 64 ? c ^ ((r >> 1) & 7) : c ^ ((r >> 2) & 3);
-}
+__device__ __forceinline__ int bswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
 // PRO (conv_gemm's A prologues, applied by ONE in-place pass over each landed A stage):
 //   0 none; 1 relu(bf16(a sc + sh)) (the previous BN + ReLU); 2 the BN backward
@@ -117,23 +97,20 @@ __device__ __forceinline__ int bswz(int r, int c) {
 // once the pass over stage kt has read it.  With a 256-wide channel tile the A rows are staged
 // (and transformed) once per channel tile -- once in all for N = 256, and for wider N the other
 // channel tiles of the pixel tile run on the same XCD (L2 re-reads, not HBM).
-template <int EPI, int BK, int PRO, int CFG, bool SK = false>
-__global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_big_kernel(const ConvGemmArgs p) {
+template <int EPI, int PRO>
+__global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) {
   static_assert(EPI >= 0 && EPI <= 9, "conv_gemm's epilogues");
-  static_assert(BK == 64 || BK == 32, "stage depth");
-  static_assert(PRO == 0 || BK == 64, "the prologue variants run the 2 x 64-deep ring");
   static_assert(PRO != 2 || (EPI != 0 && EPI != 1), "the BN-backward prologue feeds a data-gradient GEMM");
-  static_assert(CFG != 1 || (BK == 32 && PRO == 0), "128-channel tiles: plain 32-deep ring");
 
-  constexpr int TN = cfg_tn(CFG), NW = cfg_waves(CFG), NT = 64 * NW;
-  constexpr int WCH = CFG == 2 ? 128 : 64;        // channels per wave (2 waves along the pixels)
+  constexpr int BK = 64, TN = 256, NW = 8, NT = 64 * NW;
+  constexpr int WCH = 64;                         // channels per wave (2 waves along the pixels)
   constexpr int WN = TN / WCH, TI = WCH / 32;     // waves along the channels; 32-ch blocks per wave
-  constexpr int kRing = cfg_ring(CFG);
+  constexpr int kRing = 131072;
   constexpr int kTN = TN, kCS = TN + 4;          // output tile row stride (elements)
   constexpr bool TWO = PRO == 2 || PRO == 3;
   constexpr int RB = 2 * BK;                    // bytes per stage row
   constexpr int A_BYTES = kTM * RB, STAGE = (kTM + kTN) * RB;
-  constexpr int NST = kRing / STAGE;            // TN 256: 2 (BK 64) or 4 (BK 32); TN 128: 3
+  constexpr int NST = kRing / STAGE;            // 2
   static_assert(NST >= 2, "ring depth");
   constexpr int CPR = RB / 16;                  // 16-B chunks per row
   constexpr int RPI = 64 / CPR;                 // rows per DMA wave-instruction
@@ -158,40 +135,13 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
     if (p.tbuf != nullptr && threadIdx.x == 0) p.tbuf[static_cast<int64_t>(blockIdx.x) * 8 + i] = wall_clock64();
   };
   stamp(0);
-  // ---- work: one tile over all of K, or (SK) the contiguous (tile, stage) units of this block --
-  // the last round of a grid with few tiles per CU leaves most CUs idle; stream-K spreads the units
-  const int cself = xcd_remap_big(blockIdx.x, gridDim.x);
-  int u = 0, u_end = 1;
-  if constexpr (SK) {
-    const int tot = mtiles * nN * nk;
-    u = min(tot, cself * p.sk_units);
-    u_end = min(tot, (cself + 1) * p.sk_units);
-  }
-  while (u < u_end) {
-  int L, kb, ke;
-  if constexpr (SK) {
-    L = u / nk;
-    kb = u - L * nk;
-    ke = min(nk, kb + (u_end - u));
-    u += ke - kb;
-    lds_bar();  // the previous item's epilogue is done with the LDS
-  } else {
-    L = cself;
-    kb = 0;
-    ke = nk;
-    u = u_end;
-  }
+  // ---- one 256 x 256 tile per block, over all of K
+  const int L = xcd_remap_big(blockIdx.x, gridDim.x);
+  constexpr int kb = 0;
+  const int ke = nk;
   const int mt = L / nN, n0 = (L - mt * nN) * kTN;
   const int m0 = mt * kTM;
-  // K-order rotation (p.krot): tile L walks its stages from (L mod nk), so the CUs of an XCD read
-  // different weight slices at a time instead of all the same 32 KiB of B
-  const int rot = p.krot ? L % nk : 0;
-  auto kmap = [&](int kt) { return kt + rot >= nk ? kt + rot - nk : kt + rot; };
-  // per-thread indices from an opaque copy of threadIdx: nothing derived from them is hoisted out of
-  // the SK item loop (kept live across the epilogue, it spilled)
-  int tid = threadIdx.x;
-  if constexpr (SK) asm volatile("" : "+v"(tid));
-  const int t = tid, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int fr = lane & 31, fh = lane >> 5;
 
   // ---- DMA sources: lane-linear LDS rows, swizzled source chunk; A rows past M read zeros
@@ -213,16 +163,16 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
       }
       aok |= 1u << i;
     }
-    abase[i] = off + bswz<BK>(r, lch) * 8;
+    abase[i] = off + bswz(r, lch) * 8;
   }
   const uint16_t* bsrc[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
     const int r = (wave * PB + i) * RPI + lrow;
-    bsrc[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + bswz<BK>(r, lch) * 8;
+    bsrc[i] = p.b + static_cast<int64_t>(n0 + r) * p.K + bswz(r, lch) * 8;
   }
   auto issue_z = [&](int kt) {
-    const int k0 = kmap(kt) * BK;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const uint16_t* src = ((aok >> i) & 1u) ? p.a2 + abase[i] + k0 : kBigZero;
@@ -236,7 +186,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   constexpr int NCO = PRO == 1 ? 4 : PRO == 2 ? 6 : 8;
   f32x4 co[NCO];
   auto load_coef = [&](int kt) {
-    const int cc = kmap(kt) * BK + (t & 7) * 8;
+    const int cc = kt * BK + (t & 7) * 8;
     const float* src[4] = {p.pro, p.pro, p.pro, p.pro};
     if constexpr (PRO == 2) {
       src[0] = p.bwd;
@@ -262,7 +212,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   auto transform = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     const uint8_t* Zs = lds + Z_OFF;
-    const int lc = t & 7, tr0 = t >> 3, cc = kmap(kt) * BK + lc * 8;
+    const int lc = t & 7, tr0 = t >> 3, cc = kt * BK + lc * 8;
 #pragma unroll
     for (int i = 0; i < NCO; ++i) tie(co[i]);
     float c0[8], c1[8], c2[8], c3[8];
@@ -289,14 +239,14 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
     u16x8 va[HB], za[HB];
 #pragma unroll
     for (int i = 0; i < HB; ++i) {  // the rows' reads before any use (one LDS latency per group)
-      const int r = tr0 + TRP * (h + i), off = r * RB + bswz<BK>(r, lc) * 16;
+      const int r = tr0 + TRP * (h + i), off = r * RB + bswz(r, lc) * 16;
       va[i] = *reinterpret_cast<const u16x8*>(As + off);
       if constexpr (TWO) za[i] = *reinterpret_cast<const u16x8*>(Zs + off);
     }
 #pragma unroll
     for (int i = 0; i < HB; ++i) {
       const int r = tr0 + TRP * (h + i), m = m0 + r;
-      const int off = r * RB + bswz<BK>(r, lc) * 16;
+      const int off = r * RB + bswz(r, lc) * 16;
       u16x8 v = va[i];
       unsigned ob = 0;
       if constexpr (PRO == 1) {
@@ -336,7 +286,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   auto issue = [&](int kt, int buf) {
     uint8_t* As = lds + buf * STAGE;
     uint8_t* Bs = As + A_BYTES;
-    const int k0 = kmap(kt) * BK;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const uint16_t* src = ((aok >> i) & 1u) ? p.a + abase[i] + k0 : kBigZero;
@@ -354,7 +304,7 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   uint32_t fa[KSTEPS], fb[KSTEPS];
 #pragma unroll
   for (int s = 0; s < KSTEPS; ++s) {
-    const int ch = bswz<BK>(fr, 2 * s + fh) * 16;
+    const int ch = bswz(fr, 2 * s + fh) * 16;
     fa[s] = static_cast<uint32_t>((128 * wm + fr) * RB + ch);
     fb[s] = static_cast<uint32_t>(A_BYTES + (WCH * wn + fr) * RB + ch);
   }
@@ -376,10 +326,6 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
     xa[set][3] = ld_b128o<3 * OJ>(a);
     wb[set][0] = ld_b128o<0>(b);
     wb[set][1] = ld_b128o<OJ>(b);
-    if constexpr (TI == 4) {
-      wb[set][2] = ld_b128o<2 * OJ>(b);
-      wb[set][3] = ld_b128o<3 * OJ>(b);
-    }
   };
   constexpr int FR = 4 + TI;  // fragment reads per k-step
   auto mfma_set = [&](int set) {
@@ -464,48 +410,6 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   stamp(2);
   wait_vm<0>();
   lds_bar();  // the output tile overlays the stage ring
-
-  if constexpr (SK) {
-    // partial slots: [block][TI * 64 floats][NT threads], coalesced per float.  Written and read as
-    // agent-scope relaxed atomics (coherent across the XCDs' L2s without a release/acquire fence,
-    // which would write back / invalidate a whole L2 per piece: that made stream-K 2x slower)
-    constexpr int NF = TI * 4 * 16;
-    if (kb > 0) {  // a continuation piece: fp32 partial to this block's slot, then its flag
-      float* dst = p.sk_ws + static_cast<int64_t>(cself) * NF * NT + t;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            __hip_atomic_store(dst + ((i * 4 + j) * 16 + q) * NT, acc[i][j][q], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      wait_vm<0>();  // every store acknowledged before the flag
-      __syncthreads();
-      if (t == 0) __hip_atomic_store(p.sk_flag + cself, p.sk_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      continue;
-    }
-    // the first piece finishes the tile: the following blocks' pieces, added in block order
-    for (int c2 = cself + 1, done = ke; done < nk; ++c2) {
-      if (t == 0) {  // bounded: a piece that never lands (a bug) gives a wrong tile, not a hung GPU
-        const long long w0 = wall_clock64();
-        while (__hip_atomic_load(p.sk_flag + c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
-               wall_clock64() - w0 < 50000000)
-          __builtin_amdgcn_s_sleep(2);
-      }
-      __syncthreads();
-      float* src = p.sk_ws + static_cast<int64_t>(c2) * NF * NT + t;
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            acc[i][j][q] += __hip_atomic_load(src + ((i * 4 + j) * 16 + q) * NT, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-      done += min(nk - done, p.sk_units);
-    }
-  }
 
   // ---- accumulators -> bf16 output tile [256 px][kCS]: register q of acc[i][j] is channel
   // 64 wn + 32 i + 8 (q >> 2) + 4 fh + (q & 3) of pixel 128 wm + 32 j + fr
@@ -669,7 +573,6 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
       if constexpr (FOLD_DS) p.part[(2 * PG + mt) * p.N + n0 + t] = c3;
     }
   }
-  }  // work items
   if (p.tbuf != nullptr) {
     stamp(4);  // stores issued
     wait_vm<0>();
@@ -678,196 +581,69 @@ __global__ __launch_bounds__(64 * cfg_waves(CFG), CFG == 1 ? 2 : 1) void conv_bi
   }
 }
 
-// auto choice of the 128-channel tiles (PS_AMD_CONV_BIG_TN unset): not yet (probe first)
-bool big_tn128(int M, int N, int K, const ConvGeo& g, int epi) {
-  (void)M, (void)N, (void)K, (void)g, (void)epi;
-  return false;
-}
-
-int big_bk() {
-  static const int bk = [] {
-    const char* e = std::getenv("PS_AMD_CONV_BIG_BK");
-    return e != nullptr && std::atoi(e) == 32 ? 32 : 64;
-  }();
-  return bk;
-}
-
 }  // namespace
 
-// stream-K workspace of one (device, stream): a partial slot (256 KiB) and a flag per block
-struct SkWorkspace {
-  float* ws = nullptr;
-  int* flag = nullptr;
-  int nslots = 0, epoch = 0;
-};
-static SkWorkspace& sk_workspace(hipStream_t s, int nslots) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWorkspace> all;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(mu);
-  SkWorkspace& w = all[{dev, s}];
-  if (w.nslots < nslots) {
-    if (w.ws != nullptr) {
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(w.ws);
-      (void)hipFree(w.flag);
-    }
-    (void)hipMalloc(reinterpret_cast<void**>(&w.ws), static_cast<size_t>(nslots) * 512 * 32 * 16);
-    (void)hipMalloc(reinterpret_cast<void**>(&w.flag), static_cast<size_t>(nslots) * sizeof(int));
-    (void)hipMemsetAsync(w.flag, 0, static_cast<size_t>(nslots) * sizeof(int), s);
-    w.nslots = nslots;
-    w.epoch = 0;
-  }
-  return w;
-}
-static int device_cus() {
-  static int n[64] = {0};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (n[dev & 63] == 0) {
-    hipDeviceProp_t pr;
-    (void)hipGetDeviceProperties(&pr, dev);
-    n[dev & 63] = pr.multiProcessorCount;
-  }
-  return n[dev & 63];
-}
-// stream-K units per block (0: one tile per block).  PS_AMD_CONV_BIG_SK=0 never, =1 whenever the
-// pieces are >= 4 stages; default: when the last round of tiles would leave > 10 % of the CU-rounds idle
-static int sk_units_for(int tiles, int nk, int ncu) {
-  const char* me = std::getenv("PS_AMD_CONV_BIG_SK");  // per call: tests switch it in-process
-  const int mode = me == nullptr ? 0 : std::atoi(me);
-  if (mode == 0 || ncu <= 0) return 0;
-  const int rounds = (tiles + ncu - 1) / ncu;
-  if (mode == 2 && tiles >= static_cast<int64_t>(rounds) * ncu * 9 / 10) return 0;
-  const int64_t tot = static_cast<int64_t>(tiles) * nk;
-  const int units = static_cast<int>((tot + ncu - 1) / ncu);
-  return units >= 4 ? units : 0;
-}
-
-template <int E, int BK, int P, int C>
-static void big_launch(const ConvGemmArgs& a, hipStream_t s, int nblk) {
-  if constexpr (C == 0 && BK == 64) {
-    if (a.sk_units > 0) {
-      hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C, true>), dim3(nblk), dim3(512), 0, s, a);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((conv_big_kernel<E, BK, P, C, false>), dim3(nblk), dim3(64 * cfg_waves(C)), 0, s, a);
-}
-
 // the 256-channel-tile launches
-template <int C>
-static void launch_big256(const ConvGemmArgs& a0, hipStream_t s, bool bwd, bool resp) {
-  ConvGemmArgs a = a0;
-  const char* kr = std::getenv("PS_AMD_CONV_BIG_KROT");
-  a.krot = kr != nullptr && kr[0] == '1' ? 1 : 0;
-  int nblk = conv_big_gm(a.M) * (a.N / 256);
-  if (C == 0 && a.tbuf == nullptr && !(big_bk() == 32 && !bwd && !resp && a.pro == nullptr)) {
-    const int ncu = device_cus();
-    const int units = sk_units_for(nblk, a.K / 64, ncu);
-    if (units > 0) {
-      SkWorkspace& w = sk_workspace(s, ncu);
-      a.sk_ws = w.ws;
-      a.sk_flag = w.flag;
-      a.sk_units = units;
-      a.sk_epoch = ++w.epoch;
-      nblk = ncu;
-    }
-  }
-#define PSAMD_BIG(E, BK, P) big_launch<E, BK, P, C>(a, s, nblk)
+static void launch_big256(const ConvGemmArgs& a, hipStream_t s, bool bwd, bool resp) {
+  const int nblk = conv_big_gm(a.M) * (a.N / 256);
+#define PSAMD_BIG(E, P) hipLaunchKernelGGL((conv_big_kernel<E, P>), dim3(nblk), dim3(512), 0, s, a)
   if (bwd) {
     switch (a.epi) {
-      case 2: PSAMD_BIG(2, 64, 2); break;
-      case 4: PSAMD_BIG(4, 64, 2); break;
-      case 5: PSAMD_BIG(5, 64, 2); break;
-      case 6: PSAMD_BIG(6, 64, 2); break;
-      case 7: PSAMD_BIG(7, 64, 2); break;
-      case 8: PSAMD_BIG(8, 64, 2); break;
-      case 9: PSAMD_BIG(9, 64, 2); break;
-      default: PSAMD_BIG(3, 64, 2); break;
+      case 2: PSAMD_BIG(2, 2); break;
+      case 4: PSAMD_BIG(4, 2); break;
+      case 5: PSAMD_BIG(5, 2); break;
+      case 6: PSAMD_BIG(6, 2); break;
+      case 7: PSAMD_BIG(7, 2); break;
+      case 8: PSAMD_BIG(8, 2); break;
+      case 9: PSAMD_BIG(9, 2); break;
+      default: PSAMD_BIG(3, 2); break;
     }
   } else if (resp) {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 3);
-    else PSAMD_BIG(0, 64, 3);
+    if (a.epi == 1) PSAMD_BIG(1, 3);
+    else PSAMD_BIG(0, 3);
   } else if (a.pro != nullptr) {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 1);
-    else PSAMD_BIG(0, 64, 1);
-  } else if (a.epi == 2 || a.epi >= 4) {
-    switch (a.epi) {
-      case 2: PSAMD_BIG(2, 64, 0); break;
-      case 4: PSAMD_BIG(4, 64, 0); break;
-      case 5: PSAMD_BIG(5, 64, 0); break;
-      case 6: PSAMD_BIG(6, 64, 0); break;
-      case 7: PSAMD_BIG(7, 64, 0); break;
-      case 8: PSAMD_BIG(8, 64, 0); break;
-      default: PSAMD_BIG(9, 64, 0); break;
-    }
-  } else if (C == 0 && big_bk() == 32) {
-    if constexpr (C == 0) {
-      if (a.epi == 1) PSAMD_BIG(1, 32, 0);
-      else if (a.epi == 3) PSAMD_BIG(3, 32, 0);
-      else PSAMD_BIG(0, 32, 0);
-    }
+    if (a.epi == 1) PSAMD_BIG(1, 1);
+    else PSAMD_BIG(0, 1);
   } else {
-    if (a.epi == 1) PSAMD_BIG(1, 64, 0);
-    else if (a.epi == 3) PSAMD_BIG(3, 64, 0);
-    else PSAMD_BIG(0, 64, 0);
+    switch (a.epi) {
+      case 1: PSAMD_BIG(1, 0); break;
+      case 2: PSAMD_BIG(2, 0); break;
+      case 3: PSAMD_BIG(3, 0); break;
+      case 4: PSAMD_BIG(4, 0); break;
+      case 5: PSAMD_BIG(5, 0); break;
+      case 6: PSAMD_BIG(6, 0); break;
+      case 7: PSAMD_BIG(7, 0); break;
+      case 8: PSAMD_BIG(8, 0); break;
+      case 9: PSAMD_BIG(9, 0); break;
+      default: PSAMD_BIG(0, 0); break;
+    }
   }
 #undef PSAMD_BIG
 }
 
-// Eligible: a 1x1 GEMM (rows in order) with K = C.  The 256-channel tiles: N a multiple of 256,
-// K >= 256, and >= 1024 blocks or K >= 1024 (with >= 256 blocks); epilogues 0 / 1 / 3 with or
-// without a stride-1 prologue, the residual / fold epilogues 2, 4-9 without one (or with the BN
-// backward one).  The 128-channel tiles (two blocks per CU): no prologue, N a multiple of 128,
-// K a multiple of 32, >= 512 blocks, where big_tn128 picks them.  PS_AMD_CONV_BIG=0 disables;
-// PS_AMD_CONV_BIG_FOLD=0 keeps 2, 4-9 on the 128-pixel tiles; PS_AMD_CONV_BIG_BK=32 selects the
-// 4-stage ring of 32-deep stages (256-channel tiles, epilogues 0 / 1 / 3); PS_AMD_CONV_BIG_TN=128 /
-// 256 forces one channel tile where it is eligible.
+// Eligible: a 1x1 GEMM (rows in order) with K = C, N a multiple of 256, K >= 256, and >= 1024
+// blocks or K >= 1024 (with >= 256 blocks); epilogues 0 / 1 / 3 with or without a stride-1
+// prologue, the residual / fold epilogues 2, 4-9 without one (or with the BN backward one).
 int conv_big_tn(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_CONV_BIG");
-    return e == nullptr || e[0] != '0';
-  }();
-  static const bool pro_on = [] {
-    const char* e = std::getenv("PS_AMD_CONV_BIG_PRO");
-    return e == nullptr || e[0] != '0';
-  }();
-  static const bool fold_on = [] {
-    const char* e = std::getenv("PS_AMD_CONV_BIG_FOLD");
-    return e == nullptr || e[0] != '0';
-  }();
-  const char* tne = std::getenv("PS_AMD_CONV_BIG_TN");  // read per call: tests switch it in-process
-  const int tn_env = tne == nullptr ? 0 : std::atoi(tne);
-  if (!on || g.RH != 0) return 0;
+  if (g.RH != 0) return 0;
   if (g.ks != 1 || g.ksw > 1 || g.pad != 0 || g.C != K) return 0;
   if (epi < 0 || epi > 9) return 0;
-  const bool plain_epi = epi == 0 || epi == 1 || epi == 3;
-  if (!plain_epi && !fold_on) return 0;
-  const int64_t mt = (M + kTM - 1) / kTM;
-  if (tn_env != 256 && !pro && src2 == 0 && N % 128 == 0 && K % 32 == 0 && K >= 64 && mt * (N / 128) >= 512) {
-    if (tn_env == 128 || big_tn128(M, N, K, g, epi)) return 128;
-  }
   if (N % 256 != 0 || K % 64 != 0 || K < 256) return 0;
+  const bool plain_epi = epi == 0 || epi == 1 || epi == 3;
   // the residual / fold epilogues (2, 4-9: the conv1 data gradients): no prologue, or the BN
   // backward one (the conv1 data gradient with bn1's backward applied)
   if (!plain_epi && ((pro && src2 != 2) || src2 == 1)) return 0;
   // prologues (PRO 1: pro, src2 0; PRO 3: src2 1; PRO 2: src2 2 + a data-gradient epilogue): stride 1 only
   if (pro || src2 != 0) {
-    if (!pro_on || g.stride != 1) return 0;
+    if (g.stride != 1) return 0;
     if (src2 == 2 && (epi == 0 || epi == 1)) return 0;
     if (src2 == 1 && epi == 3) return 0;
   }
   // one block per CU: below ~4 rounds of blocks the last round's idle CUs and the per-tile
   // prologue / epilogue outweigh the faster K loop unless K is deep (profiles/r5_conv_big_probe.txt:
   // at batch 256 the K = 256 / 512 shapes with 784 blocks ran 2-15 % slower, K >= 1024 faster)
-  const int64_t nblk = mt * (N / 256);
-  if (nblk >= 256 && (nblk >= 1024 || K >= 1024)) return 256;
-  // with stream-K the last-round loss is gone: a deep K on fewer tiles (batch 256) can take them
-  const char* se = std::getenv("PS_AMD_CONV_BIG_SK_SMALL");
-  if (se != nullptr && se[0] == '1' && nblk >= 64 && K >= 512 && !(pro || src2 != 0)) return 256;
-  return 0;
+  const int64_t nblk = static_cast<int64_t>(conv_big_gm(M)) * (N / 256);
+  return nblk >= 256 && (nblk >= 1024 || K >= 1024) ? 256 : 0;
 }
 
 bool conv_big_ok(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
@@ -878,27 +654,7 @@ int conv_big_gm(int M) { return (M + kTM - 1) / kTM; }
 
 void launch_conv_big(const ConvGemmArgs& a, hipStream_t s) {
   const bool bwd = a.bwd != nullptr, resp = a.pro != nullptr && a.a2 != nullptr && !bwd;
-  const int tn = conv_big_tn(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, resp ? 1 : bwd ? 2 : 0, a.epi);
-  if (tn == 128) {
-    const int nb = conv_big_gm(a.M) * (a.N / 128);
-#define PSAMD_BIG128(E) hipLaunchKernelGGL((conv_big_kernel<E, 32, 0, 1>), dim3(nb), dim3(256), 0, s, a)
-    switch (a.epi) {
-      case 0: PSAMD_BIG128(0); break;
-      case 1: PSAMD_BIG128(1); break;
-      case 2: PSAMD_BIG128(2); break;
-      case 3: PSAMD_BIG128(3); break;
-      case 4: PSAMD_BIG128(4); break;
-      case 5: PSAMD_BIG128(5); break;
-      case 6: PSAMD_BIG128(6); break;
-      case 7: PSAMD_BIG128(7); break;
-      case 8: PSAMD_BIG128(8); break;
-      default: PSAMD_BIG128(9); break;
-    }
-#undef PSAMD_BIG128
-    return;
-  }
-  launch_big256<0>(a, s, bwd, resp);
+  launch_big256(a, s, bwd, resp);
 }
-
 
 }  // namespace psamd

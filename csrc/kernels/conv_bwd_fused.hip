@@ -425,279 +425,6 @@ __global__ __launch_bounds__(512, 1) void conv11_bwd_fused_kernel(const Conv11Bw
   }
 }
 
-// The layer-2 shape (CI = 128 -> CO = 512): 64-pixel tiles, 8 waves (2 per SIMD), the per-block
-// dW (512 x 128 fp32) spread over all 512 lanes (128 VGPRs each), and the transposed weight
-// (128 KiB) streamed per stage from L2 through its own 3-slot ring (two stages ahead) instead of
-// staying resident.  Waves: data gradient pb = wave & 1 (32-pixel block) x cb = wave >> 1
-// (32-channel block) -- ONE output channel per lane; weight gradient nb = wave & 1 (32-row n block
-// of the stage) x cw = wave >> 1 (32-column c block).  z2 tile [64 px][128 c]: 256-B rows, chunk c
-// of row r at c ^ ((r & 3) << 2) (a transposed read's four rows land in four 64-B bank quarters).
-template <int CI, int CO>
-__global__ __launch_bounds__(512, 1) void conv11_bwd_fused_w128_kernel(const Conv11BwdArgs p) {
-  static_assert(CI == 128 && CO == 512, "the layer-2 conv3 shape (128 -> 512)");
-  constexpr int TM = 64;                    // pixels per tile
-  constexpr int NS = CO / kKS;              // 8 stages per tile
-  constexpr int GSL = TM * kKS * 2;         // 8 KiB: g / dz3 stage tile [64 px][64 n]
-  constexpr int WSL = CI * kKS * 2;         // 16 KiB: W3t stage slice [128 c][64 n]
-  constexpr int ZSL = TM * CI * 2;          // 16 KiB: z2 tile [64 px][128 c]
-  constexpr int NRG = 5, PDG = NRG - 1;     // g ring: stage q + 4 issued during stage q
-  constexpr int NRW = 3, PDW = NRW - 1;     // W ring: stage q + 2 issued during stage q
-  // A2: per-wave a2 fragments of the tile ([8 waves][4 ks][64 lanes] x 16 B), written and read
-  // back by the same wave in order (no barrier); in registers they pushed the kernel into spills
-  constexpr int GR = 0, WR = GR + NRG * GSL, ZR = WR + NRW * WSL, A2 = ZR + 2 * ZSL, PAR = A2 + 8 * 4096;
-  constexpr int NPAR = 3 * CO + 4 * CI;
-  constexpr int LDS_BYTES = PAR + NPAR * 4;
-  static_assert(LDS_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-  float* const par = reinterpret_cast<float*>(lds + PAR);
-  const uint32_t L0 = lds_addr(lds);
-
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int fr = lane & 31, fh = lane >> 5;
-  const int GM = gridDim.x, mg = blockIdx.x;
-  const int ntiles = (p.M + TM - 1) / TM;
-  const int my_tiles = mg < ntiles ? (ntiles - mg + GM - 1) / GM : 0;  // block-uniform
-  const int nq = my_tiles * NS;
-  auto stage_m0 = [&](int q) { return q < nq ? (mg + (q / NS) * GM) * TM : p.M; };
-
-  for (int i = t; i < NPAR; i += 512) {
-    float v;
-    if (i < 3 * CO) v = p.cbwd[i];
-    else if (i < 3 * CO + 2 * CI) v = p.cf2[i - 3 * CO];
-    else if (i < 3 * CO + 3 * CI) v = p.mean2[i - 3 * CO - 2 * CI];
-    else v = p.invstd2[i - 3 * CO - 3 * CI];
-    par[i] = v;
-  }
-  // g stage [64][64]: 8 pieces of 8 rows, one per wave; rows past M read the zero row
-  auto issue_g = [&](int q, int sl) {
-    const int m0 = stage_m0(q), col0 = (q % NS) * kKS;
-    const int r = 8 * wave + (lane >> 3), m = m0 + r;
-    const uint16_t* src = m < p.M ? p.g + static_cast<int64_t>(m) * CO + col0 + ((lane & 7) ^ swf(r)) * 8 : kZeroRow;
-    __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + GR + sl * GSL + wave * 1024), 16, 0, 0);
-  };
-  // W3t slice of stage q (columns 64 (q % NS) ..): [128 c][64 n], 16 pieces, 2 per wave
-  auto issue_w = [&](int q, int sl) {
-    const int col0 = (q % NS) * kKS;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = wave * 2 + i, r = 8 * k + (lane >> 3);
-      __builtin_amdgcn_global_load_lds((gptr_t*)(p.wt + static_cast<int64_t>(r) * CO + col0 + ((lane & 7) ^ swf(r)) * 8),
-                                       (lptr_t*)(lds + WR + sl * WSL + k * 1024), 16, 0, 0);
-    }
-  };
-  // z2 tile [64][128]: 16 pieces of 4 rows, 2 per wave
-  auto issue_z2 = [&](int m0, int sl) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = wave * 2 + i, r = 4 * k + (lane >> 4), m = m0 + r;
-      const uint16_t* src =
-          m < p.M ? p.z2 + static_cast<int64_t>(m) * CI + ((lane & 15) ^ ((r & 3) << 2)) * 8 : kZeroRow;
-      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + ZR + sl * ZSL + k * 1024), 16, 0, 0);
-    }
-  };
-  const int zr = t >> 3, zc = t & 7;  // z3: logical chunk zc of row zr (one chunk per thread)
-  u16x8 z3r[2];
-  auto load_z3 = [&](int q, u16x8& dst) {
-    const int m = stage_m0(q) + zr, col = (q % NS) * kKS + zc * 8;
-    dst = m < p.M ? *reinterpret_cast<const u16x8*>(p.z3 + static_cast<int64_t>(m) * CO + col)
-                  : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  };
-  issue_z2(stage_m0(0), 0);
-#pragma unroll
-  for (int i = 0; i < PDG; ++i) issue_g(i, i);
-#pragma unroll
-  for (int i = 0; i < PDW; ++i) issue_w(i, i);
-  load_z3(0, z3r[0]);
-  load_z3(1, z3r[1]);
-  wait_vm<0>();
-  lds_bar();
-
-  const int pb = wave & 1, cb = wave >> 1;  // data gradient block; weight gradient: nb = pb, cw = cb
-  const int dpx = 32 * pb + fr, dsw = swf(dpx);
-  const int ec = 32 * cb + fr;              // this lane's output channel (data gradient) / dW column
-  const int gi = lane >> 4, i16 = lane & 15;
-  const int trow = 8 * (gi >> 1) + (i16 >> 2), tcol = 16 * (gi & 1) + 4 * (i16 & 3);
-  // dz3 stage tile, transposed read of the n block pb (A operand of the weight gradient)
-  auto trD = [&](int h) {
-    const int r = trow + 4 * h;
-    return static_cast<uint32_t>(r * 128 + ((((32 * pb + tcol) >> 3) ^ swf(r)) << 4) + (tcol & 7) * 2);
-  };
-  const uint32_t tD0 = trD(0), tD1 = trD(1);
-  // z2 tile, transposed read at column block cbk, row r (256-B rows)
-  auto trZ = [&](int cbk, int r) {
-    const int col = 32 * cbk + tcol;
-    return static_cast<uint32_t>(r * 256 + (((col >> 3) ^ ((r & 3) << 2)) << 4) + (col & 7) * 2);
-  };
-  const float asc = par[3 * CO + ec], ash = par[3 * CO + CI + ec];
-  const float emc = asc, esh = ash, emu = par[3 * CO + 2 * CI + ec], eis = par[3 * CO + 3 * CI + ec];
-  const uint32_t wrow_off = static_cast<uint32_t>(ec * 128);  // W slice row of this lane's channel
-  const int wsw = swf(ec);
-
-  f32x16 acc_dg, accW[NS];
-  auto zero16 = [](f32x16& a) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) a[i] = 0.f;
-  };
-  zero16(acc_dg);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) zero16(accW[s]);
-  float s1 = 0.f, s2 = 0.f;
-  const uint32_t a2s = L0 + A2 + wave * 4096 + lane * 16;
-  auto make_a2 = [&](int ti) {
-    const uint32_t zs = L0 + ZR + (ti & 1) * ZSL;
-    s16x4 lo[4], hi[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      lo[ks] = ld_tr(zs + trZ(cb, 16 * ks + trow));
-      hi[ks] = ld_tr(zs + trZ(cb, 16 * ks + trow + 4));
-    }
-    lgkm0();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      tie(lo[ks]);
-      tie(hi[ks]);
-      u16x8 v = __builtin_bit_cast(u16x8, cat8(lo[ks], hi[ks]));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = f32_to_bf16(bf16_to_f32(v[j]) * asc + ash);
-      const s16x8i z = {0, 0, 0, 0, 0, 0, 0, 0};
-      st_b128(a2s + ks * 1024, __builtin_bit_cast(bf16x8_t, __builtin_elementwise_max(__builtin_bit_cast(s16x8i, v), z)));
-    }
-  };
-  auto transform = [&](int sl, int s, int m0, const u16x8& z8) {
-    const uint32_t ds = L0 + GR + sl * GSL;
-    const uint32_t pa = L0 + PAR + (s * kKS + zc * 8) * 4;
-    const f32x4 ca0 = ld_f4(pa), ca1 = ld_f4(pa + 16);
-    const f32x4 cb0 = ld_f4(pa + CO * 4), cb1 = ld_f4(pa + CO * 4 + 16);
-    const f32x4 cc0 = ld_f4(pa + 2 * CO * 4), cc1 = ld_f4(pa + 2 * CO * 4 + 16);
-    const uint32_t ga = ds + zr * 128 + ((zc ^ swf(zr)) << 4);
-    bf16x8_t gv = ld_b128(ga);
-    lgkm0();
-    f32x4 c0a = ca0, c0b = ca1, c1a = cb0, c1b = cb1, c2a = cc0, c2b = cc1;
-    tie(c0a); tie(c0b); tie(c1a); tie(c1b); tie(c2a); tie(c2b);
-    tie(gv);
-    const u16x8 g8 = __builtin_bit_cast(u16x8, gv);
-    u16x8 d;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float a = j < 4 ? c0a[j] : c0b[j - 4], b = j < 4 ? c1a[j] : c1b[j - 4], c = j < 4 ? c2a[j] : c2b[j - 4];
-      d[j] = f32_to_bf16(a * bf16_to_f32(g8[j]) + b * bf16_to_f32(z8[j]) + c);
-    }
-    if (m0 + zr >= p.M) d = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    st_b128(ga, __builtin_bit_cast(bf16x8_t, d));
-  };
-  auto compute = [&](int gsl, int wsl, f32x16& aw) {
-    const uint32_t ds = L0 + GR + gsl * GSL, ws = L0 + WR + wsl * WSL;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two k-steps at a time (register budget)
-      bf16x8_t xa[2], wb[2], af[2];
-      s16x4 dl[2], dh[2];
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        const int ks = 2 * h + k2;
-        af[k2] = ld_b128(a2s + ks * 1024);
-        xa[k2] = ld_b128(ds + dpx * 128 + (((2 * ks + fh) ^ dsw) << 4));
-        wb[k2] = ld_b128(ws + wrow_off + (((2 * ks + fh) ^ wsw) << 4));
-        dl[k2] = ld_tr(ds + ks * 2048 + tD0);
-        dh[k2] = ld_tr(ds + ks * 2048 + tD1);
-      }
-      lgkm0();
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        tie(xa[k2]);
-        tie(wb[k2]);
-        tie(af[k2]);
-        tie(dl[k2]);
-        tie(dh[k2]);
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-        acc_dg = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[k2], wb[k2], acc_dg, 0, 0, 0);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-        aw = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat8(dl[k2], dh[k2]), af[k2], aw, 0, 0, 0);
-    }
-  };
-  auto epilogue = [&](int ti) {
-    const int m0 = (mg + ti * GM) * TM;
-    const uint32_t zs = L0 + ZR + (ti & 1) * ZSL;
-    s16x4 zv[4];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) zv[q4] = ld_tr(zs + trZ(cb, 32 * pb + 8 * q4 + 4 * (gi >> 1) + (i16 >> 2)));
-    lgkm0();
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      tie(zv[q4]);
-      const u16x4 z4 = __builtin_bit_cast(u16x4, zv[q4]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint16_t val = f32_to_bf16(acc_dg[4 * q4 + e]);
-        const float z = bf16_to_f32(z4[e]);
-        const bool on = z * emc + esh > 0.f;
-        const float gv = on ? bf16_to_f32(val) : 0.f;
-        s1 += gv;
-        s2 += gv * ((z - emu) * eis);
-        const int m = m0 + 32 * pb + 8 * q4 + 4 * fh + e;
-        if (m < p.M) p.gy[static_cast<int64_t>(m) * CI + ec] = on ? val : static_cast<uint16_t>(0);
-      }
-    }
-    zero16(acc_dg);
-  };
-
-  int slg = 0, slw = 0, q = 0;
-  for (int ti = 0; ti < my_tiles; ++ti) {
-    const int m0 = (mg + ti * GM) * TM;
-#pragma unroll
-    for (int s = 0; s < NS; ++s, ++q) {
-      // the stage counter through an opaque copy: per-stage DMA / load addresses are computed here
-      // instead of being hoisted for all 8 unrolled stages
-      int qo = q;
-      asm volatile("" : "+s"(qo));
-      if (s == 0) make_a2(ti);
-      transform(slg, s, m0, z3r[s & 1]);
-      lds_bar();  // dz3 of stage q complete; stage q - 1's g and W slots are free
-      issue_g(qo + PDG, slg == 0 ? NRG - 1 : slg - 1);
-      issue_w(qo + PDW, slw == 0 ? NRW - 1 : slw - 1);
-      load_z3(qo + 2, z3r[s & 1]);
-      if (s == 0) issue_z2(ti + 1 < my_tiles ? m0 + GM * TM : p.M, (ti + 1) & 1);
-      compute(slg, slw, accW[s]);
-      if (s == NS - 1) epilogue(ti);
-      // W(q + 1) (issued in stage q - 1) and G(q + 1) (stage q - 3) landed: younger than W(q + 1)
-      // are at least this stage's G + W DMAs (3) and the z2 tile if issued in stage q - 1 or q (2)
-      if (s <= 1) wait_vm<5>();
-      else wait_vm<3>();
-      lds_bar();
-      slg = slg == NRG - 1 ? 0 : slg + 1;
-      slw = slw == NRW - 1 ? 0 : slw + 1;
-    }
-  }
-  wait_vm<0>();
-  lds_bar();
-
-  // bn2 partial sums: lanes l / l + 32 (pixel halves), then the two pixel-block waves of a channel
-  // block in fixed order
-  s1 += __shfl_xor(s1, 32, 64);
-  s2 += __shfl_xor(s2, 32, 64);
-  float* red = reinterpret_cast<float*>(lds);  // [2][2 pb][CI]
-  if (fh == 0) {
-    red[pb * CI + ec] = s1;
-    red[(2 + pb) * CI + ec] = s2;
-  }
-  __syncthreads();
-  if (t < CI) {
-    p.part[static_cast<int64_t>(mg) * CI + t] = red[t] + red[CI + t];
-    p.part[static_cast<int64_t>(GM + mg) * CI + t] = red[2 * CI + t] + red[3 * CI + t];
-  }
-  // dW slab: rows n of every stage's n block pb, column ec
-  float* slab = p.ws + static_cast<int64_t>(mg) * CO * CI;
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int n = s * kKS + 32 * pb + 8 * (i >> 2) + 4 * fh + (i & 3);
-      slab[n * CI + ec] = accW[s][i];
-    }
-}
-
 // out[y][e] = sum_{b in [y*per, y*per + per)} in[b][e], fixed order (bf16 or fp32 out)
 template <bool BF16>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ in, int nslab, int per, int64_t E,
@@ -723,25 +450,18 @@ int slab_levels(int nslab) { return nslab > 16 ? (nslab + 15) / 16 : 0; }
 
 }  // namespace
 
-// The layer-2 variant (CI = 128) is built but opt-in (PS_AMD_CONV3_FUSED_W128=1): with the weight
-// streamed per stage it ran 0.78 ms (4 waves) / 0.96 ms (8 waves) against the two-kernel chain's
-// 0.76 ms at batch 1024 (profiles/r5_conv3_bwd_fused_probe_w128.jsonl)
-bool conv11_bwd_fused_ok(int CI, int CO) {
-  static const bool w128 = [] {
-    const char* e = std::getenv("PS_AMD_CONV3_FUSED_W128");
-    return e != nullptr && e[0] == '1';
-  }();
-  return (CI == 64 && CO == 256) || (w128 && CI == 128 && CO == 512);
-}
+// Layer 1 only (64 -> 256).  A layer-2 variant (128 -> 512, 64-pixel tiles, the weight streamed
+// per stage) ran 0.78 ms against the two-kernel chain's 0.76 ms at batch 1024
+// (profiles/r5_conv3_bwd_fused_probe_w128.jsonl) and was removed in round 6.
+bool conv11_bwd_fused_ok(int CI, int CO) { return CI == 64 && CO == 256; }
 
 bool conv11_bwd_plain_ok(int CI, int CO) { return CI == 64 && CO == 256; }
 
-bool conv11_bwd_built(int CI, int CO) { return (CI == 64 && CO == 256) || (CI == 128 && CO == 512); }
+bool conv11_bwd_built(int CI, int CO) { return CI == 64 && CO == 256; }
 
 int conv11_bwd_blocks(int M, int CI, int CO) {
-  (void)CO;
-  const int tm = CI == 128 ? 64 : kTM;
-  const int ntiles = (M + tm - 1) / tm;
+  (void)CI, (void)CO;
+  const int ntiles = (M + kTM - 1) / kTM;
   return std::max(1, std::min(ntiles, 256));  // one block per CU (LDS-bound)
 }
 
@@ -757,8 +477,6 @@ void launch_conv11_bwd_fused(const Conv11BwdArgs& a, int CI, int CO, hipStream_t
     hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256, true>), dim3(gm), dim3(512), 0, s, a);
   else if (CI == 64 && CO == 256) hipLaunchKernelGGL((conv11_bwd_fused_kernel<64, 256, false>), dim3(gm), dim3(512), 0, s, a);
   else if (a.cf2 == nullptr) return;  // PLAIN: the 64 -> 256 kernel only
-  else if (CI == 128 && CO == 512)
-    hipLaunchKernelGGL((conv11_bwd_fused_w128_kernel<128, 512>), dim3(gm), dim3(512), 0, s, a);
   else return;
   const int64_t E = static_cast<int64_t>(CI) * CO;
   const unsigned eb = static_cast<unsigned>((E + 255) / 256);

@@ -230,8 +230,8 @@ struct StageRegs {
 template <int BN>
 constexpr int patch_bytes() { return BN == 64 ? 65536 : 40960; }  // 8 channel planes of 8 / 5 KiB
 
-// VAR: 0 the plain paths, 1 PATCH (3x3 patch-staged tiles), 2 the plain LDS-DMA path with a
-// 3-stage ring (two stages in flight behind the MFMAs; one block per CU by LDS)
+// VAR: 0 the plain paths, 1 PATCH (3x3 patch-staged tiles).  (A 3-stage ring for the plain
+// LDS-DMA path measured no faster: profiles/r4_deep_ring_graph_ab.txt; removed in round 6.)
 // The kernel body takes its logical block id L (XCD-remapped) from the launching kernel: conv_fwd_kernel
 // (one GEMM per launch) or conv_dgrad_phases_kernel (the four stride-2 data-gradient phases in one grid).
 template <int BM, int BN, int PRO, int EPI, bool KS1, bool GLDS, int VAR = 0>
@@ -276,8 +276,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int
   constexpr int RED_ELEMS = 4 * NSUM * BN * 2 > (FOLD_DS ? 256 * 8 * 2 : 0) ? 4 * NSUM * BN * 2 : 256 * 8 * 2;
   constexpr int EPI_ELEMS = BM * CS + RED_ELEMS;
   constexpr bool PATCH = VAR == 1;
-  constexpr int NST = VAR == 2 ? 3 : 2;  // plain LDS-DMA ring depth
-  static_assert(VAR != 2 || (GLDS && !PRO), "the deep ring is the plain LDS-DMA path");
+  constexpr int NST = 2;  // LDS-DMA ring depth
+  static_assert(VAR == 0 || VAR == 1, "plain or patch");
   constexpr int A_ELEMS = PATCH ? patch_bytes<BN>() / 2 : (TWO_GLDS ? 3 : NST) * BM * kBK;
   constexpr int Z_BASE = 2 * BM * kBK;  // TWO_GLDS: the second source's stage tile
   constexpr int B_BASE = ((A_ELEMS > EPI_ELEMS ? A_ELEMS : EPI_ELEMS) + 7) & ~7;
@@ -925,31 +925,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int
         epi_load(mg);
         epilogue(mg);
       }
-    } else if (VAR == 2 && mg < mtiles) {  // 3-stage ring: issue kt + 2, wait for kt
-      issue(0, 0);
-      if (nk > 1) issue(1, 1);
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // refills compute(kt - 1)'s buffer
-        const int ahead = min(2, nk - 1 - kt);         // stages issued after kt, in flight
-        if (ahead == 2) {
-          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-          else if constexpr (AI + BI == 10) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-          else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (ahead == 1) {
-          if constexpr (AI + BI == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else if constexpr (AI + BI == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-          else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        lds_barrier();  // every wave's stage-kt DMAs landed
-        compute(kt % 3);
-        lds_barrier();  // stage kt read out before stage kt + 3 is issued into its buffer
-      }
-      epi_load(mg);
-      epilogue(mg);
     } else if (mg < mtiles) {  // block-uniform
       issue(0, 0);
       for (int kt = 0; kt < nk; ++kt) {
@@ -1047,257 +1022,6 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_phases_kernel(const ConvPha
   const int ph = P.order[i];
   conv_fwd_body<128, BN, 0, EPI, false, true, 0>(P.ph[ph], P.gm[ph],
                                                  xcd_remap(b - P.start[i], P.start[i + 1] - P.start[i]));
-}
-
-// ------------------------------------------------------------------------------ conv3x3 64 -> 64
-// The 64-channel 3x3 stride-1 layers (ResNet-50 layer 1: forward and data gradient at 56 x 56):
-// a persistent block per CU keeps the WHOLE weight (9 taps x 64 x 64 = 72 KiB) resident in LDS
-// and walks row-aligned tiles of two image rows (112 of 128 MFMA rows used).  Each tile's input is
-// staged once as a zero-haloed patch of 4 x 58 slots (eight 16-B channel planes) by LDS-DMA, two
-// patch slots deep: the next tile's patch streams in while this one computes, and the nine taps
-// read their A fragments from the same patch at shifted slots -- no per-tap barrier, no im2col
-// re-read of the input.  The im2col tile (256 x 64, LDS-DMA per tap) moved nine copies of every
-// input pixel through L2 per layer and ran at 0.55-0.6 PF/s.
-// Epilogues: 0 (store), 1 (+ the next BN's statistics about kshift), 3 (ReLU mask from z * mc +
-// shift and the BN-backward sums) -- partials [2][gridDim.x][64] like the persistent conv_fwd grid.
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 63, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int W, int EPI>
-__global__ __launch_bounds__(256, 1) void conv3x3_c64_kernel(const ConvGemmArgs p) {
-  constexpr int C = 64, N = 64, RT = 128 / W, TP = RT * W;  // image rows / pixels per tile
-  constexpr int PW = W + 2, PR = RT + 2, NSL = PR * PW;       // patch slots (rows x cols)
-  constexpr int PPP = (NSL + 63) / 64;                         // 1-KiB pieces per plane
-  constexpr int PLB = PPP * 1024;                              // bytes per 16-B channel plane
-  constexpr int SLOT = 8 * PLB;                                // bytes per patch
-  constexpr int NPIECE = 8 * PPP, PPW = NPIECE / 4;            // pieces, per wave
-  static_assert(NPIECE % 4 == 0 && RT >= 1, "patch pieces over 4 waves");
-  constexpr int BTAP = N * 64 * 2;                             // bytes per tap of the weight
-  constexpr int CS = N + 4;                                    // output tile row stride (bf16)
-  constexpr int B_OFF = 2 * SLOT, CS_OFF = B_OFF + 9 * BTAP, RED_OFF = CS_OFF + 128 * CS * 2;
-  constexpr int LDS_BYTES = RED_OFF + 8 * N * 4;
-  static_assert(LDS_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-  uint16_t* const Cs = reinterpret_cast<uint16_t*>(lds + CS_OFF);
-  float* const red = reinterpret_cast<float*>(lds + RED_OFF);
-
-  const ConvGeo& g = p.g;
-  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int GM = gridDim.x, mg = blockIdx.x;
-  const int tpi = g.OH / RT, ntiles = (p.M / (g.OH * g.OW)) * tpi;
-  const int fr = lane & 31, fh = lane >> 5;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 32;  // 2 x 2 waves of 64 px x 32 ch
-
-  // the resident weight: tap k-slab [64 n][64 k] with chunk c of row n at swz(n, c)
-  {
-    const int lrow = lane >> 3, lch = lane & 7;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int n = (wave * 2 + i) * 8 + lrow;
-        __builtin_amdgcn_global_load_lds((gptr_t*)(p.b + static_cast<int64_t>(n) * p.K + tap * C + swz(n, lch) * 8),
-                                         (lptr_t*)(lds + B_OFF + tap * BTAP + (wave * 2 + i) * 8 * 128), 16, 0, 0);
-      }
-  }
-  // patch of tile mt into slot sl: plane pl, piece k = 64 lane-linear slots of row-major (row, col)
-  auto issue_patch = [&](int mt, int sl) {
-    const int img = mt / tpi, oh0 = (mt - img * tpi) * RT;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int pc = wave + 4 * i, pl = pc / PPP, sq = (pc - pl * PPP) * 64 + lane;
-      const int pr = sq / PW, pcol = sq - pr * PW, ih = oh0 - 1 + pr, iw = pcol - 1;
-      const bool ok = sq < NSL && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
-      const uint16_t* src = ok ? p.a + ((static_cast<int64_t>(img) * g.H + ih) * W + iw) * C + pl * 8 : kZeroPage;
-      __builtin_amdgcn_global_load_lds((gptr_t*)src, (lptr_t*)(lds + sl * SLOT + pl * PLB + (pc - pl * PPP) * 1024), 16,
-                                       0, 0);
-    }
-  };
-  // A-fragment slot of this lane's pixel rows (tap (0, 0)); pixels past the tile read slot 0
-  uint32_t abase[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int px = wm + 32 * j + fr;
-    const int pr = px / W, pcol = px - pr * W;
-    abase[j] = static_cast<uint32_t>(fh * PLB + (px < TP ? pr * PW + pcol : 0) * 16);
-  }
-  const int brow = wn + fr;
-  // two accumulator sets by k-step parity: four independent MFMA chains per wave (one wave per
-  // SIMD here, so the chains -- not a partner wave -- cover the MFMA dependency latency)
-  f32x16 acc[2], acc2[2];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[j][q] = acc2[j][q] = 0.f;
-  };
-  auto compute = [&](int sl) {
-    const uint8_t* P = lds + sl * SLOT;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int tap = kh * 3 + kw, toff = (kh * PW + kw) * 16;
-        const uint8_t* B = lds + B_OFF + tap * BTAP;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const int ch = 2 * s2 + fh;
-          const bf16x8_t wb = *reinterpret_cast<const bf16x8_t*>(B + brow * 128 + swz(brow, ch) * 16);
-          bf16x8_t xa[2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            xa[j] = *reinterpret_cast<const bf16x8_t*>(P + abase[j] + toff + 2 * s2 * PLB);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            if (s2 & 1) acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc2[j], 0, 0, 0);
-            else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, xa[j], acc[j], 0, 0, 0);
-          }
-        }
-      }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[j] += acc2[j];
-  };
-  // epilogue: thread t owns channels [8 cg, 8 cg + 8) of tile rows r0 + 32 i
-  const int cg = t & 7, r0 = t >> 3, nc = cg * 8;
-  float s1[8], s2[8], e0[8], e1[8], e2[8], e3[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = e0[j] = e1[j] = e2[j] = e3[j] = 0.f;
-  if constexpr (EPI == 1) {
-    if (p.kshift) load8(p.kshift, nc, e0);
-  } else if constexpr (EPI == 3) {
-    load8(p.mc, nc, e0);
-    load8(p.mc + N, nc, e1);
-    load8(p.mean, nc, e2);
-    load8(p.invstd, nc, e3);
-  }
-  u16x8 ra[4];
-  auto epi_load = [&](int m0) {
-    if constexpr (EPI == 3) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = r0 + 32 * i;
-        ra[i] = *reinterpret_cast<const u16x8*>(p.aux + static_cast<int64_t>(m0 + (rr < TP ? rr : 0)) * N + nc);
-      }
-    }
-  };
-  auto acc_to_lds = [&]() {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const int nl = wn + 8 * q4 + 4 * fh, ml = wm + 32 * j + fr;
-        const u16x4 v = {f32_to_bf16(acc[j][4 * q4]), f32_to_bf16(acc[j][4 * q4 + 1]),
-                         f32_to_bf16(acc[j][4 * q4 + 2]), f32_to_bf16(acc[j][4 * q4 + 3])};
-        *reinterpret_cast<u16x4*>(Cs + ml * CS + nl) = v;
-      }
-  };
-  auto epilogue_rows = [&](int m0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rr = r0 + 32 * i;
-      if (rr >= TP) break;
-      const u16x4 lo = *reinterpret_cast<const u16x4*>(Cs + rr * CS + nc);
-      const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * CS + nc + 4);
-      u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if constexpr (EPI == 1) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = bf16_to_f32(v[j]) - e0[j];
-          s1[j] += d;
-          s2[j] += d * d;
-        }
-      } else if constexpr (EPI == 3) {
-        const u16x8 z8 = ra[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float z = bf16_to_f32(z8[j]);
-          const bool on = z * e0[j] + e1[j] > 0.f;
-          const float gv = on ? bf16_to_f32(v[j]) : 0.f;
-          s1[j] += gv;
-          s2[j] += gv * ((z - e2[j]) * e3[j]);
-          if (!on) v[j] = 0;
-        }
-      }
-      *reinterpret_cast<u16x8*>(p.c + static_cast<int64_t>(m0 + rr) * N + nc) = v;
-    }
-  };
-
-  // prologue: weight + the first two patches in flight; wait for the weight and patch 0
-  zero_acc();
-  const bool has0 = mg < ntiles, has1 = mg + GM < ntiles;
-  if (has0) issue_patch(mg, 0);
-  if (has1) issue_patch(mg + GM, 1);
-  if (has1) wait_vm<PPW>();
-  else wait_vm<0>();
-  lds_barrier();
-  for (int ti = 0, mt = mg; mt < ntiles; ++ti, mt += GM) {
-    const int sl = ti & 1, m0 = mt * TP;
-    epi_load(m0);
-    compute(sl);
-    acc_to_lds();
-    lds_barrier();  // the output tile is complete; every wave is done with patch slot sl
-    const bool more2 = mt + 2 * GM < ntiles;
-    if (more2) issue_patch(mt + 2 * GM, sl);  // streams in during this epilogue and the next tile
-    epilogue_rows(m0);
-    zero_acc();
-    // the next tile's patch landed (this wave's pieces): the just-issued patch and the epilogue's
-    // row stores (3 or 4 per thread; vmcnt retires in issue order, so counting the smaller is
-    // safe) may stay in flight
-    if (more2) wait_vm<PPW + 3>();
-    else wait_vm<3>();
-    lds_barrier();  // every wave's pieces landed; the output tile was read out
-  }
-  if constexpr (EPI == 1 || EPI == 3) {
-#pragma unroll
-    for (int off = 8; off < 64; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s1[j] += __shfl_xor(s1[j], off, 64);
-        s2[j] += __shfl_xor(s2[j], off, 64);
-      }
-    if (lane < 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[wave * N + nc + j] = s1[j];
-        red[(4 + wave) * N + nc + j] = s2[j];
-      }
-    }
-    lds_barrier();
-    if (t < N) {
-      p.part[static_cast<int64_t>(mg) * N + t] = (red[t] + red[N + t]) + (red[2 * N + t] + red[3 * N + t]);
-      p.part[(static_cast<int64_t>(GM) + mg) * N + t] =
-          (red[4 * N + t] + red[5 * N + t]) + (red[6 * N + t] + red[7 * N + t]);
-    }
-  }
-}
-
-// PS_AMD_CONV_C64: "1" the round-4 resident-weight kernel above (0.476 / 0.507 ms vs the tall
-// im2col tile's 0.451 / 0.456, profiles/r4_conv3x3_c64_probe.txt), "2" the planar-LDS kernel of
-// conv3x3_c64.hip (asm fragment reads, no compiler vmcnt at the loop edge), "0" / unset the tall
-// im2col tile
-int c64_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("PS_AMD_CONV_C64");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  return m;
-}
-bool c64_enabled() { return c64_mode() != 0; }
-
-// the layers conv3x3_c64_kernel takes: 3x3 / stride 1 / pad 1, 64 -> 64 channels, 56-wide maps
-// with an even row count, no prologue
-bool c64_ok(const ConvGeo& g, int N, bool pro) {
-  return c64_enabled() && !pro && g.ks == 3 && (g.ksw == 0 || g.ksw == 3) && g.stride == 1 && g.pad == 1 &&
-         g.RH == 0 && g.C == 64 && N == 64 && g.W == 56 && g.OW == 56 && g.OH == g.H && g.OH % 2 == 0;
-}
-
-int c64_blocks(int M, const ConvGeo& g) {
-  const int ntiles = (M / (g.OH * g.OW)) * (g.OH / 2);
-  return std::max(1, std::min(ntiles, 256));
 }
 
 // ------------------------------------------------------------------------------ conv_wgrad
@@ -2028,70 +1752,29 @@ void launch_weight_prep(const void* jobs, int njobs, int max_blocks, hipStream_t
 // register staging gains most from the cross-tile prefetch: scripts/probe_conv_fwd.py) run a
 // persistent grid of 2 blocks per CU (statistics kept in registers); deeper K runs one block per
 // tile so the hardware balances the tail.
-int persist_nk_pro() {
-  static const int v = [] {
-    const char* e = std::getenv("PS_AMD_PERSIST_NK_PRO");
-    return e ? std::atoi(e) : 4;  // 4-stage PRO layers: cross-tile prefetch pays (L3 conv3 -8%)
-  }();
-  return v;
-}
-
-bool tall_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_CONV_TALL");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
-bool patch_fwd_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_CONV_PATCH");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
+constexpr int kPersistNkPro = 4;  // 4-stage PRO layers: cross-tile prefetch pays (L3 conv3 -8%)
 
 // 3x3 / stride 1 / pad 1 forward (or data gradient) whose 128-pixel tiles' patch fits the LDS
 // budget and spans at most two images
 bool patch_fwd_ok(const ConvGeo& g, int N, bool pro) {
-  if (pro || !patch_fwd_enabled() || g.ks != 3 || (g.ksw != 0 && g.ksw != 3) || g.stride != 1 || g.pad != 1 ||
+  if (pro || g.ks != 3 || (g.ksw != 0 && g.ksw != 3) || g.stride != 1 || g.pad != 1 ||
       g.RH != 0 || g.OH != g.H || g.OW != g.W || g.C % 64 != 0 || g.OH * g.OW < 128)
     return false;
   // 64-channel outputs keep the tall 256 x 64 im2col tile: the 128 x 64 patch tile (64 x 32 per
   // wave, 1.5 fragment reads per MFMA) measured 9-14 % slower there (profiles/r3_conv_patch_fwd_ab.txt)
-  if (N % 128 != 0 && std::getenv("PS_AMD_CONV_PATCH64") == nullptr) return false;
+  if (N % 128 != 0) return false;
   const int bn = N % 128 == 0 ? 128 : 64;
   const int span = (g.OW - 1 + 128 + g.OW - 1) / g.OW, rmax = span + 4;
   const int plane = (rmax * (g.W + 2) * 16 + 1023) / 1024 * 1024;  // one 16-B channel plane, whole pieces
   return 8 * plane <= (bn == 64 ? patch_bytes<64>() : patch_bytes<128>());
 }
 
-int twosrc_glds_min_nk() {
-  static const int v = [] {
-    const char* e = std::getenv("PS_AMD_TWOSRC_GLDS_MIN_NK");
-    return e ? std::atoi(e) : 4;  // K >= 256 (profiles/r4_twosrc_probe.txt: LDS-DMA ahead at every K)
-  }();
-  return v;
-}
+// two-source prologues with K >= 64 x this run on the LDS-DMA variant (profiles/r4_twosrc_probe.txt:
+// LDS-DMA ahead at every K >= 256)
+constexpr int kTwosrcGldsMinNk = 4;
 
 // src2: two-source prologue of the launch (0 none, 1 block output, 2 BN backward)
-bool twosrc_glds(int K, int src2) { return src2 != 0 && K / kBK >= twosrc_glds_min_nk(); }
-
-int pro_glds_min_nk() {
-  static const int v = [] {
-    const char* e = std::getenv("PS_AMD_PRO_GLDS_MIN_NK");
-    // off by default: slower than the persistent register-staged prologue at every ResNet-50
-    // depth (layer 2: 0.41 vs 0.33 ms, profiles/r4_twosrc_probe.txt)
-    return e ? std::atoi(e) : 1 << 20;
-  }();
-  return v;
-}
-
-// the one-source BN + ReLU prologue (1x1) on the LDS-DMA path from this K depth
-bool pro_glds(int K, bool pro, int src2, const ConvGeo& g) {
-  return pro && src2 == 0 && g.ks == 1 && g.ksw <= 1 && g.stride == 1 && g.pad == 0 && K / kBK >= pro_glds_min_nk();
-}
+bool twosrc_glds(int K, int src2) { return src2 != 0 && K / kBK >= kTwosrcGldsMinNk; }
 
 ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, int src2, int epi) {
   if (const int tn = conv_big_tn(M, N, K, pro, g, src2, epi)) {  // 256 x TN tiles (conv_big.hip)
@@ -2101,14 +1784,7 @@ ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, i
     pl.gm = conv_big_gm(M);
     return pl;
   }
-  if (src2 == 0 && c64_ok(g, N, pro)) {  // persistent row-tile patch kernel, one block per CU
-    ConvFwdPlan pl;
-    pl.bm = 128;
-    pl.bn = 64;
-    pl.gm = c64_blocks(M, g);
-    return pl;
-  }
-  if (twosrc_glds(K, src2) || pro_glds(K, pro, src2, g)) {  // LDS-DMA prologue: one 128-pixel tile per block
+  if (twosrc_glds(K, src2)) {  // LDS-DMA two-source prologue: one 128-pixel tile per block
     ConvFwdPlan pl;
     pl.bm = 128;
     pl.bn = N % 128 == 0 ? 128 : 64;
@@ -2131,20 +1807,9 @@ ConvFwdPlan conv_fwd_plan_geo(int M, int N, int K, bool pro, const ConvGeo& g, i
   return conv_fwd_plan(M, N, K, pro, epi);
 }
 
-// The fold epilogues (6-9: residual + mask + the previous block's BN-backward sums) over shallow K
-// on one-tile-per-block LDS-DMA grids instead of the persistent register-staged grid, whose
-// epilogue-9 variant spills (PS_AMD_FOLD_GLDS=1)
-bool fold_glds(int epi, bool pro) {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_FOLD_GLDS");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on && epi >= 6 && !pro;
-}
-
 ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi) {
   ConvFwdPlan pl;
-  if (!pro && N == 64 && K / kBK >= 8 && tall_enabled()) {  // 64-channel 3x3 (K = 576): 256 x 64 tiles
+  if (!pro && N == 64 && K / kBK >= 8) {  // 64-channel 3x3 (K = 576): 256 x 64 tiles
     pl.bm = 256;
     pl.bn = 64;
     pl.gm = (M + 255) / 256;
@@ -2156,7 +1821,7 @@ ConvFwdPlan conv_fwd_plan(int M, int N, int K, bool pro, int epi) {
   const int nk = K / kBK;
   // (a persistent grid for the read-heavy data-gradient epilogues measured no faster at 4-16
   // stages: scripts/probe_dgrad_epi.py)
-  const bool persist = !fold_glds(epi, pro) && (nk <= 2 || (pro && nk <= persist_nk_pro()));
+  const bool persist = nk <= 2 || (pro && nk <= kPersistNkPro);
   pl.gm = !persist ? (M + 127) / 128 : std::max(1, std::min((M + 127) / 128, 512 / nN));
   return pl;
 }
@@ -2174,40 +1839,6 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
   const int nblk = GM * (a.N / pl.bn);
   if (conv_big_ok(a.M, a.N, a.K, a.pro != nullptr || bwd, a.g, src2, a.epi)) {
     launch_conv_big(a, s);
-    return;
-  }
-  if (src2 == 0 && c64_ok(a.g, a.N, a.pro != nullptr) && (a.epi == 0 || a.epi == 1 || a.epi == 3)) {
-    if (c64_mode() == 2 && (a.epi == 1 || a.epi == 3)) {
-      launch_conv3x3_c64s(a, GM, s);
-      return;
-    }
-    if (c64_mode() == 3 && (a.epi == 1 || a.epi == 3)) {
-      launch_conv3x3_c64r(a, GM, s);
-      return;
-    }
-    if (c64_mode() == 4 && (a.epi == 1 || a.epi == 3)) {
-      launch_conv3x3_c64v(a, GM, s);
-      return;
-    }
-    if (a.epi == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 1>), dim3(GM), dim3(256), 0, s, a);
-    else if (a.epi == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<56, 3>), dim3(GM), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv3x3_c64_kernel<56, 0>), dim3(GM), dim3(256), 0, s, a);
-    return;
-  }
-  if (pro_glds(a.K, a.pro != nullptr, src2, a.g)) {
-    if (pl.bn == 128) {
-      if (a.epi == 1) {
-        hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, 1, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
-      } else {
-        hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 1, 0, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
-      }
-    } else {
-      if (a.epi == 1) {
-        hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, 1, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
-      } else {
-        hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 1, 0, true, true>), dim3(nblk), dim3(256), 0, s, a, GM);
-      }
-    }
     return;
   }
   if (twosrc_glds(a.K, src2)) {  // (1x1: the binding checks)
@@ -2237,29 +1868,13 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
     return;
   }
   const bool ks1 = a.g.ks == 1 && a.g.ksw <= 1;
-  // deep K without the BN prologue: LDS-DMA staging (one tile per block); PS_AMD_GLDS_STAGES=3:
-  // a 3-stage ring (one block per CU) for K >= 64 x PS_AMD_GLDS_DEEP_MIN_NK
-  const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm &&
-                    (a.K / kBK > 2 || fold_glds(a.epi, false));
-  static const int stages = [] {
-    const char* e = std::getenv("PS_AMD_GLDS_STAGES");
-    return e ? std::atoi(e) : 2;
-  }();
-  static const int deep_min_nk = [] {
-    const char* e = std::getenv("PS_AMD_GLDS_DEEP_MIN_NK");
-    return e ? std::atoi(e) : 8;
-  }();
-  const bool deep = stages == 3 && a.K / kBK >= deep_min_nk;
+  // deep K without the BN prologue: LDS-DMA staging (one tile per block)
+  const bool glds = !a.pro && !bwd && pl.gm == (a.M + pl.bm - 1) / pl.bm && a.K / kBK > 2;
 #define PSAMD_CF3(BM, BN, PRO, EPI, GL)                                                                          \
   if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, GL>), dim3(nblk), dim3(256), 0, s, a, GM); \
   else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, GL>), dim3(nblk), dim3(256), 0, s, a, GM)
-#define PSAMD_CF3V(BM, BN, PRO, EPI)                                                                          \
-  if (ks1) hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, true, true, 2>), dim3(nblk), dim3(256), 0, s, a, \
-                              GM);                                                                              \
-  else hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, PRO, EPI, false, true, 2>), dim3(nblk), dim3(256), 0, s, a, GM)
 #define PSAMD_CF2(BM, BN, PRO, EPI)                        \
   if constexpr (PRO) { PSAMD_CF3(BM, BN, PRO, EPI, false); } \
-  else if (glds && deep) { PSAMD_CF3V(BM, BN, PRO, EPI); }   \
   else if (glds) { PSAMD_CF3(BM, BN, PRO, EPI, true); }       \
   else { PSAMD_CF3(BM, BN, PRO, EPI, false); }
 #define PSAMD_CF(BN, PRO, EPI) PSAMD_CF2(128, BN, PRO, EPI)
@@ -2277,8 +1892,7 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
     default: PSAMD_CF(BN, PRO, 0); break; \
   }
   if (pl.bm == 256) {  // LDS-DMA only (no prologue, deep K)
-#define PSAMD_CFT(EPI) \
-  if (deep) { PSAMD_CF3V(256, 64, false, EPI); } else { PSAMD_CF3(256, 64, false, EPI, true); }
+#define PSAMD_CFT(EPI) PSAMD_CF3(256, 64, false, EPI, true)
     switch (a.epi) {
       case 1: PSAMD_CFT(1); break;
       case 2: PSAMD_CFT(2); break;
@@ -2323,7 +1937,6 @@ void launch_conv_fwd(const ConvGemmArgs& a0, hipStream_t s) {
 #undef PSAMD_CF
 #undef PSAMD_CF2
 #undef PSAMD_CF3
-#undef PSAMD_CF3V
 }
 
 int conv_dgrad_phase_gm(int M) { return (M + 127) / 128; }
@@ -2362,14 +1975,6 @@ struct WPlan {
   int wide;  // 0: conv_wgrad_kernel; wide tiles 1: 256 x 256, 2: 256 x 128, 3: 128 x 256, 4: 128 x 384
 };
 
-bool wide_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("PS_AMD_WGRAD_WIDE");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
 // Slab reduction levels: > 16 slabs reduce in two fixed-order levels (16 slabs per first-level
 // group) unless the weight has >= 256K elements -- then one thread per element over every slab
 // already fills the chip, and the second launch (plus its gap) is saved.
@@ -2404,7 +2009,7 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
   const bool ks1 = K == C;
   int bno = N % 256 == 0 ? 256 : 128, bko = K % 256 == 0 ? 256 : 128;
   if (bno == 128 && bko == 128 && K % 384 == 0) bko = 384;  // 3x3 at C = 128: 3 taps per k-tile
-  if (wide_enabled() && (!pro || ks1) && N % 128 == 0 && K % 128 == 0 && C % 8 == 0 && (bno == 256 || bko > 128)) {
+  if ((!pro || ks1) && N % 128 == 0 && K % 128 == 0 && C % 8 == 0 && (bno == 256 || bko > 128)) {
     w.wide = bno == 256 ? (bko == 256 ? 1 : 2) : bko == 256 ? 3 : 4;
     w.tiles = (N / bno) * (K / bko);
     const int chunks = (M + kWP - 1) / kWP;
@@ -2426,18 +2031,12 @@ WPlan wplan(int M, int N, int K, int C, bool pro) {
 
 namespace {
 // The patch kernel's shapes: 3x3 / pad 1, stride 1 on 56- or 28-wide maps, stride 2 on a 56-wide map
-// (the ResNet-50 64- and 128-channel stages), channels up to PS_AMD_WGRAD_PATCH_MAX_C (default 128; 0 = never).
-int patch_max_c() {
-  static const int v = [] {
-    const char* e = std::getenv("PS_AMD_WGRAD_PATCH_MAX_C");
-    return e ? std::atoi(e) : 128;
-  }();
-  return v;
-}
+// (the ResNet-50 64- and 128-channel stages), channels up to 128.
+constexpr int kPatchMaxC = 128;
 
 bool patch_ok(const ConvGeo& g, int M, int N, bool pro) {
   if (pro || g.ks != 3 || !(g.ksw == 0 || g.ksw == 3) || g.pad != 1 || g.C % 64 != 0 || N % 64 != 0 ||
-      g.C > patch_max_c() || M % kPP != 0 || g.RH != 0)
+      g.C > kPatchMaxC || M % kPP != 0 || g.RH != 0)
     return false;
   if (g.stride == 1)  // 56- / 28-wide maps
     return g.H == g.OH && g.W == g.OW && (g.W == 56 || g.W == 28) && g.OH % (kPP / g.W) == 0;
@@ -2509,11 +2108,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a0, hipStream_t s) {
   const int nblk = w.tiles * w.nsplit;
   // LIN: 1x1 stride-1 pad-0 geometry (X row m = pixel m), DMA sources without the pixel decode
   const bool lin = a.g.ks == 1 && a.g.stride == 1 && a.g.pad == 0;
-  static const bool prol_env = [] {
-    const char* e = std::getenv("PS_AMD_WGRAD_PRO_LDS");
-    return e == nullptr || e[0] != '0';
-  }();
-  const bool prol = prol_env && a.g.ks == 1;  // the LDS pass maps k to the channel directly
+  const bool prol = a.g.ks == 1;  // the LDS pass maps k to the channel directly
 #define PSAMD_CWW3(TN, TK, WN, WK, L)                                                                             \
   if (a.pro && prol && (WK * 32 * TK == 128 || WK * 32 * TK == 256))                                            \
     hipLaunchKernelGGL((conv_wgrad_wide_kernel<TN, TK, WN, WK, true, false, L, (WK * 32 * TK == 128 ||          \

@@ -22,18 +22,9 @@
 
 namespace psamd {
 
-// Dense optimizer grid: stream_grid capped by PS_AMD_OPT_MAX_BLOCKS (default 2048 = uncapped).  A
-// serve that overlaps a backward takes fewer CUs' worth of HBM bandwidth when capped; it runs
-// longer but stays hidden (profiles/r4_llama_serve_overlap.txt).
-static int opt_grid(int64_t work_items, int block) {
-  static const int cap = [] {
-    const char* e = std::getenv("PS_AMD_OPT_MAX_BLOCKS");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 2048;
-  }();
-  const int g = stream_grid(work_items, block);
-  return g < cap ? g : cap;
-}
+// Dense optimizer grid: stream_grid (a cap on the grid, to leave CUs to an overlapping backward,
+// measured no better: profiles/r4_llama_serve_overlap.txt).
+static int opt_grid(int64_t work_items, int block) { return stream_grid(work_items, block); }
 
 enum OptKind : int { kSGD = 0, kAdam = 1, kAdagrad = 2, kFtrl = 3 };
 

@@ -24,7 +24,7 @@ import torch
 import torch.nn.functional as F
 
 
-POOL = int(os.environ.get("PS_AMD_BENCH_POOL", "8"))  # distinct GPU-resident synthetic batches cycled
+POOL = 8  # distinct GPU-resident synthetic batches cycled
 
 
 def _cycle(pool):
@@ -42,9 +42,6 @@ class Bench:
     engine: object = None
     stats: Optional[Callable[[], Dict]] = None  # extra counters for the JSON line (read after timing)
     dtype: str = "bf16"  # compute dtype reported in the JSON line
-    # HIP-graph mode: the step reads static input buffers and ``feed`` copies the next batch of the
-    # pool into them before every replay (the graph never sees a Python-side batch change)
-    feed: Optional[Callable[[], None]] = None
 
 
 def setup_resnet50(args, tp, dev) -> Bench:
@@ -62,33 +59,18 @@ def setup_resnet50(args, tp, dev) -> Bench:
         memory_format=torch.channels_last), torch.randint(0, 1000, (B,), device=dev, generator=g))
         for _ in range(POOL)]
     it = _cycle(pool)
-    feed = None
-    if str(getattr(args, "graph", "0")) != "0":
-        xs, ys = pool[0][0].clone(), pool[0][1].clone()
 
-        def feed():
-            x, y = next(it)
-            xs.copy_(x)
-            ys.copy_(y)
-
-        def step():
-            loss = F.cross_entropy(model(xs).float(), ys)
-            loss.backward()
-            ps.finish_step()
-            return loss
-    else:
-        def step():
-            x, y = next(it)
-            loss = F.cross_entropy(model(x).float(), y)
-            loss.backward()
-            ps.finish_step()
-            return loss
+    def step():
+        x, y = next(it)
+        loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        ps.finish_step()
+        return loss
 
     return Bench(step, B, "samples/sec (whole node) ResNet-50 sync-BSP at 1/2/4/8 MI355X workers", "samples/s",
                  {"model": "ResNet-50", "global_batch": B * tp.world, "seq_len": None, "image_size": S,
                   "parallelism": f"ps-bsp-colocated-dp{tp.world}", "optimizer": upd.name,
-                  "bucket_mb": args.bucket_mb, "staleness": args.staleness, "fused_bn": bool(args.fused_bn)}, ps,
-                 feed=feed)
+                  "bucket_mb": args.bucket_mb, "staleness": args.staleness, "fused_bn": bool(args.fused_bn)}, ps)
 
 
 def async_or_pipelined(model, upd, tp, stale: int, args, use_async: bool = True):
@@ -125,8 +107,7 @@ def setup_bert_ssp(args, tp, dev) -> Bench:
     model = BertForMLM().to(dev).to(torch.bfloat16)
     upd = AdamUpdater(1e-4, 0.9, 0.999, 1e-6, bias_correction="step", weight_decay=0.01, adamw=True)
     stale = 1 if args.staleness == 0 else args.staleness
-    ps, use_async, probe = async_or_pipelined(model, upd, tp, stale, args,
-                                              os.environ.get("PS_AMD_BERT_ASYNC", "1") == "1")
+    ps, use_async, probe = async_or_pipelined(model, upd, tp, stale, args, bool(getattr(args, "async_ps", 1)))
     B, S = args.batch_per_gpu, args.seq_len
     pool = [mlm_batch(B, S, seed=tp.rank * 1000 + i, device=dev, with_positions=True) for i in range(POOL)]
     it = _cycle(pool)
@@ -151,9 +132,8 @@ def setup_dlrm(args, tp, dev) -> Bench:
 
     torch.manual_seed(0)
     rows = [args.dlrm_rows] * 26
-    overlap = os.environ.get("PS_AMD_SPARSE_OVERLAP", "1") == "1"  # A/B knob for the hook-driven push
     model = DLRM(table_rows=rows, transport=tp, device=dev,
-                 sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True), overlap=overlap).to(dev)
+                 sparse_updater=AdagradUpdater(0.01, 1e-8, rowwise=True), overlap=True).to(dev)
     # bf16 compute for the MLPs + interaction (fp32 master weights live in the PS shards);
     # embedding tables and their Adagrad state stay fp32, rows are cast inside the gather
     model.bottom.to(torch.bfloat16)
@@ -212,12 +192,12 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
         model = LlamaForCausalLM(cfg, checkpointing=bool(int(os.environ.get("PS_AMD_LLAMA_CKPT", "0")))).to(
             torch.bfloat16)
     upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
-    # PS_AMD_OVERLAP=0: every bucket's serve after backward instead of overlapped with it -- the
-    # A/B that prices the serve's HBM traffic stretching backward (profiles/r4_llama_serve_overlap.txt)
+    # every bucket's serve overlapped with backward (serving after backward instead was the A/B
+    # that priced the serve's HBM traffic stretching backward: profiles/r4_llama_serve_overlap.txt)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
                      compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None),
                      ef_dtype=torch.bfloat16,  # bf16 error feedback: 16 GB instead of 32 GB per rank at 8B
-                     overlap=os.environ.get("PS_AMD_OVERLAP", "1") == "1")
+                     overlap=True)
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)
     pool = [torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g) for _ in range(POOL)]
@@ -289,7 +269,7 @@ SETUPS = {"resnet50": setup_resnet50, "bert-ssp": setup_bert_ssp, "dlrm": setup_
           "llama-onebit": setup_llama_onebit, "ctr-async": setup_ctr_async}
 
 DEFAULTS = {  # per-config defaults for --batch-per-gpu / --seq-len when not given
-    "resnet50": dict(batch=int(os.environ.get("PS_AMD_BENCH_BATCH", "1024")), seq=0),
+    "resnet50": dict(batch=1024, seq=0),
     # per-GPU batches sized for the 288 GB HBM (weak scaling; profiles/r2_bert_dlrm_batch_sweep.txt):
     # BERT 1024 x 128 (8.41K vs 7.22K seq/s at 256, 45.7 GB peak); DLRM 65536 (12.3M vs 6.9M
     # samples/s at 16384: the per-step sparse exchange / row optimizer cost amortises)

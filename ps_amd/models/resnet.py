@@ -11,11 +11,11 @@ the reference has no BN at all).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 
+from .. import knobs
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1, StemConv, stem_bn_relu_maxpool
 from ..ops.convgemm import (deferred_bn_counters, flush_deferred, fused_block_ok, fused_bottleneck,
@@ -113,7 +113,7 @@ class ResNet(nn.Module):
                 prepare_backward_weights(blks)  # all data-grad weight layouts, one kernel
                 # a block followed by a fused block leaves its output to that block's conv1 prologue
                 # where that pays (ops/convgemm.py resp_consumer_ok)
-                on = os.environ.get("PS_AMD_RESP", "1") != "0"
+                on = knobs.enabled("block_out")
                 h, w = x.shape[2], x.shape[3]
                 for a, b in zip(blks, blks[1:] + [None]):
                     s = a.conv2.stride[0]

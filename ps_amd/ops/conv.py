@@ -10,11 +10,12 @@ zero-fill / cast side kernels.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import knobs
 
 FWD_GEMM_MIN_CIN = 1024
 BWD_DATA_GEMM_MIN_CIN = 256
@@ -168,8 +169,8 @@ class _StemBnReluMaxPool(torch.autograd.Function):
         n, oh, ow, c = z.shape
         dyn = dy.permute(0, 2, 3, 1)
         dyn = dyn if dyn.is_contiguous() else dyn.contiguous()
-        fusable = oh % 2 == 0 and ow % 2 == 0 and 256 % (c // 8) == 0 and os.environ.get("PS_AMD_POOL_BN_BWD", "1") != "0"
-        if fusable and c == 64 and os.environ.get("PS_AMD_STEM_BWD_FUSED", "1") != "0":
+        fusable = oh % 2 == 0 and ow % 2 == 0 and 256 % (c // 8) == 0 and knobs.enabled("pool_bn_bwd")
+        if fusable and c == 64 and knobs.enabled("stem_bwd_fused"):
             # statistics pass, then the weight gradient computing each dz row itself from the
             # pooled gradient (csrc/kernels/stem.hip FUSED): dz is never written
             dwp, dg, db = native().stem_bwd_fused(xin, dyn, idx, z, coef, gamma, mean, invstd)

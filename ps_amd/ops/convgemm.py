@@ -34,12 +34,12 @@ Per block that removes the statistics passes of bn1 / bn3 / bn_d, bn2's output w
 bn2's backward reduce pass and the residual-gradient add, and replaces MIOpen's 1x1 solvers (and
 their zero-fill / cast side kernels).  Anything else -- CPU tensors, eval mode, fp32, channel
 counts that are not multiples of 64 -- runs the module-by-module path, which is also the numerics
-oracle in tests/test_convgemm_gpu.py.  ``PS_AMD_FUSED_BLOCK=0`` disables the fused path.
+oracle in tests/test_convgemm_gpu.py.  ``PS_AMD_DISABLE=fused_block`` turns the fused path off
+(ps_amd/knobs.py).
 """
 from __future__ import annotations
 
 import contextlib
-import os
 import threading
 import weakref
 from typing import List
@@ -48,6 +48,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import knobs
 from . import side_stream as _side
 from ._ext import native
 
@@ -143,12 +144,11 @@ def _phase_weights(w: torch.Tensor) -> List[torch.Tensor]:
 
 
 def _dgrad_s2_min_c() -> int:
-    """Stride-2 data gradients on the phase GEMMs from this many channels up (PS_AMD_DGRAD_S2_MIN_C,
-    0 = never): at 256 / 512 channels they beat MIOpen's kernel alone; at 128 (56x56) the four
-    phases (747 us) trail its kernel (728 us) but not its zero fill + the separate bn1 reduce
-    (profiles/r2_probe_dgrad_s2.jsonl: bench A/B 13.53-13.56K vs 13.52K img/s)."""
-    v = int(os.environ.get("PS_AMD_DGRAD_S2_MIN_C", "128"))
-    return v if v > 0 else 1 << 30
+    """Stride-2 data gradients on the phase GEMMs from 128 channels up: at 256 / 512 channels they
+    beat MIOpen's kernel alone; at 128 (56x56) the four phases (747 us) trail its kernel (728 us)
+    but not its zero fill + the separate bn1 reduce (profiles/r2_probe_dgrad_s2.jsonl: bench A/B
+    13.53-13.56K vs 13.52K img/s)."""
+    return 128
 
 
 WGRAD3X3_MIN_C = 256
@@ -157,9 +157,8 @@ WGRAD3X3_MIN_C = 256
 def _patch_wgrad_ok(h: int, w: int, c1: int, c2: int, s: int) -> bool:
     """The shapes csrc conv_wgrad_patch_kernel takes (mirrors convgemm.hip patch_ok): 3x3 / pad 1,
     stride 1 on 56- or 28-wide input maps, stride 2 on a 56-wide one (whole 112-pixel stages),
-    c1 <= PS_AMD_WGRAD_PATCH_MAX_C (128)."""
-    cap = int(os.environ.get("PS_AMD_WGRAD_PATCH_MAX_C", "128"))
-    if not (c1 % 64 == 0 and c2 % 64 == 0 and c1 <= cap):
+    c1 <= 128."""
+    if not (c1 % 64 == 0 and c2 % 64 == 0 and c1 <= 128):
         return False
     if s == 1:
         return w in (56, 28) and h % (112 // w) == 0
@@ -167,7 +166,7 @@ def _patch_wgrad_ok(h: int, w: int, c1: int, c2: int, s: int) -> bool:
 
 
 def _conv3x3_enabled() -> bool:
-    return os.environ.get("PS_AMD_CONV3X3", "1") != "0"
+    return knobs.enabled("conv3x3")
 
 
 class _Link:
@@ -211,15 +210,15 @@ class _Deferred:
 
 
 def _resp_enabled(c: int) -> bool:
-    """Block outputs of up to PS_AMD_RESP_MAX_C channels (0: never) are applied in the consumer's
-    conv1 prologue (which consumers take it: models/resnet.py ResNet.forward, resp_consumer_ok)."""
-    return c <= int(os.environ.get("PS_AMD_RESP_MAX_C", "4096"))
+    """Block outputs are applied in the consumer's conv1 prologue (which consumers take it:
+    models/resnet.py ResNet.forward, resp_consumer_ok) unless PS_AMD_DISABLE=block_out."""
+    return knobs.enabled("block_out")
 
 
 def twosrc_glds_min_nk() -> int:
-    """Mirror of csrc convgemm.hip twosrc_glds_min_nk: two-source prologues with K >= 64 x this run
+    """Mirror of csrc convgemm.hip kTwosrcGldsMinNk: two-source prologues with K >= 64 x this run
     on the LDS-DMA variant."""
-    return int(os.environ.get("PS_AMD_TWOSRC_GLDS_MIN_NK", "4"))
+    return 4
 
 
 def big_tile(m: int, n: int, k: int, src2: int = 0, epi: int = 1, pro: bool = False) -> bool:
@@ -255,58 +254,50 @@ def _twosrc_max_n() -> int:
     """Two-source prologues pay while the GEMM has ONE channel tile (N <= 128): every further tile
     re-reads both row sources (scripts/probe_twosrc.py, profiles/r4_twosrc_probe.txt: conv3 data
     grad 0.51 vs 0.64 ms at N = 128, 0.36 vs 0.25 ms at N = 512)."""
-    return int(os.environ.get("PS_AMD_TWOSRC_MAX_N", "128"))
+    return 128
 
 
 def _bwd_prologue_enabled(c3: int, n: int = 0) -> bool:
-    """bn3 backward applied in the conv3 data-gradient prologue, up to PS_AMD_BN_BWD_PROLOGUE_MAX_C
-    bn3 channels (0: never, the separate apply pass).  At 256 channels (4 K-stages, persistent
+    """bn3 backward applied in the conv3 data-gradient prologue (one channel tile).  At 256 channels (4 K-stages, persistent
     grid) the prologue stages A through registers from TWO row sources and replaces the apply
     pass + the LDS-DMA GEMM (1.29 -> 1.05-1.08 ms per layer-1 block); deeper K (512-2048
     channels, where the register-staged GEMM was 2-6x slower: profiles/r3_bn_bwd_prologue_ab.txt)
     runs the LDS-DMA two-source variant: both row sources land in LDS by DMA and one in-place pass
     per stage applies the BN backward (csrc convgemm.hip TWO_GLDS, scripts/probe_twosrc.py)."""
-    return c3 <= int(os.environ.get("PS_AMD_BN_BWD_PROLOGUE_MAX_C", "4096")) and n <= _twosrc_max_n()
+    return n <= _twosrc_max_n()
 
 
 def _pro_fuse_max_k() -> int:
     """conv3's forward applies bn2 + ReLU while staging up to this many input channels; deeper
     (layer 4, 512) the apply pass + plain GEMM is faster: 0.16 vs 0.21 ms (layer 3: 0.26 either
     way; profiles/r4_twosrc_probe.txt, bn_relu_prologue rows)."""
-    return int(os.environ.get("PS_AMD_PRO_FUSE_MAX_K", "256"))
+    return 256
 
 
 def _conv3_bwd_fused(ci: int, co: int) -> bool:
     """conv3's data AND weight gradient in one pass with bn3's backward in the prologue
     (csrc/kernels/conv_bwd_fused.hip): dz3 never reaches HBM and z2 is read once.
-    PS_AMD_CONV3_BWD_FUSED=0 keeps the two-kernel chain (prologue data gradient storing dz3 + the
-    weight-gradient GEMM re-reading it)."""
-    return os.environ.get("PS_AMD_CONV3_BWD_FUSED", "1") != "0" and bool(native().conv11_bwd_fused_supported(ci, co))
+    PS_AMD_DISABLE=conv3_bwd_fused keeps the two-kernel chain (prologue data gradient storing dz3 +
+    the weight-gradient GEMM re-reading it)."""
+    return knobs.enabled("conv3_bwd_fused") and bool(native().conv11_bwd_fused_supported(ci, co))
 
 
 def _ds_bwd_fused(ci: int, co: int, s: int) -> bool:
     """The downsample branch's data AND weight gradient in one pass with its BN backward in the
     prologue (the PLAIN mode of conv_bwd_fused.hip; stride 1, layer 1's 64 -> 256): dzd never
-    reaches HBM and the block input is read once.  PS_AMD_DS_BWD_FUSED=0 keeps the apply pass +
-    weight-gradient GEMM + data-gradient GEMM."""
-    return (s == 1 and os.environ.get("PS_AMD_DS_BWD_FUSED", "1") != "0"
+    reaches HBM and the block input is read once.  PS_AMD_DISABLE=ds_bwd_fused keeps the apply
+    pass + weight-gradient GEMM + data-gradient GEMM."""
+    return (s == 1 and knobs.enabled("ds_bwd_fused")
             and bool(native().conv11_bwd_fused_supported(ci, co, True)))
 
 
-def _conv1_bwd_prologue() -> bool:
-    """bn1's backward as the conv1 data-gradient GEMM's prologue where that GEMM runs on the 256 x 256
-    tiles: opt-in (PS_AMD_CONV1_BWD_PRO=1) -- at K = 256 / 512 the prologue (A and z1 re-read per channel
-    tile, transform pass per stage) costs more than the apply pass it removes (profiles/r5_conv1_dgrad_big.txt)."""
-    return os.environ.get("PS_AMD_CONV1_BWD_PRO", "0") != "0"
-
-
 def _fold_enabled() -> bool:
-    return os.environ.get("PS_AMD_FOLD_BN3", "1") != "0"
+    return knobs.enabled("fold_bn3")
 
 
 def _fold_ds_enabled() -> bool:
     """Downsample BN's backward reduce in the consumer block's conv1 data-gradient epilogue (9)."""
-    return os.environ.get("PS_AMD_FOLD_BN_DS", "1") != "0"
+    return knobs.enabled("fold_bn_ds")
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -462,23 +453,15 @@ class _BottleneckFn(torch.autograd.Function):
             e1 = (8 if s == 2 else 7) if fold else (4 if s == 2 else 2)
         else:
             e1 = (9 if li.zd is not None else 6) if fold else 5
-        # bn1's backward in the conv1 data-gradient prologue (256 x 256 tiles, layers 3-4): the
-        # GEMM also stores dz1 for the weight gradient -- no apply pass over gy1 / z1
-        pro1 = ours_dgrad and _conv1_bwd_prologue() and big_tile(x2.shape[0], x2.shape[1], w1.shape[0], src2=2,
-                                                                 epi=e1)
-        dw1 = None
-        if pro1:
-            dg1, db1, cb1 = nat.bn_bwd_coef(p1b, g1, m1, i1, gy1.shape[0])
-            bkw = dict(a2=z1, bwd=cb1)
+        # (bn1's backward as the conv1 data-gradient prologue on the 256 x 256 tiles cost more than
+        # the apply pass it removes at K = 256 / 512: profiles/r5_conv1_dgrad_big.txt; removed)
+        if ours_dgrad:
+            dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
-            if ours_dgrad:
-                dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
-            else:
-                dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
-            sd.fork()
-            dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
-            bkw = {}
-        a1 = gy1 if pro1 else dz1
+            dz1, _, dg1, db1 = nat.bn_act_bwd(rows(dy1), None, z1, g1, m1, i1, 1, False, True, cf1)
+        sd.fork()
+        dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
+        a1 = dz1
         w1t = pw[0] if pw else _mat(w1).t()
         dwd = dgd = dbd = None
         if wd is not None:
@@ -498,18 +481,13 @@ class _BottleneckFn(torch.autograd.Function):
                 sd.fork()
                 dwd = sd.run(lambda: nat.conv_wgrad(dzd, x2, geo(h, w, 1, s)), dzd, x2, like=wd)
                 t = nat.conv_gemm(dzd, wdt, go)[0]
-            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, t, **fkw, **bkw)
+            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, t, **fkw)
         elif e1 == 9:  # the producer has a downsample BN: its sum rides along
             r1 = nat.conv_gemm(a1, w1t, gi, None, 9, d2, bits=obits, aux3=li.zd, mean2=li.md, invstd2=li.idd,
-                               **fkw, **bkw)
+                               **fkw)
         else:
-            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, d2, bits=obits, **fkw, **bkw)
+            r1 = nat.conv_gemm(a1, w1t, gi, None, e1, d2, bits=obits, **fkw)
         dx2, part = r1[0], r1[1]
-        if pro1:
-            dz1 = r1[2]
-            FOLD_STATS["conv1_pro"] = FOLD_STATS.get("conv1_pro", 0) + 1
-            sd.fork()
-            dw1 = sd.run(lambda: nat.conv_wgrad(dz1, x2, gi), dz1, x2, like=w1)
         if fold:
             # dx_keep pins a second reference on dx2's storage, so autograd cannot sum another
             # consumer's gradient into it in place (it would not bump the version): a summed
@@ -521,7 +499,7 @@ class _BottleneckFn(torch.autograd.Function):
 
 def fused_block_ok(blk: nn.Module, x: torch.Tensor) -> bool:
     """True when ``blk`` (models.resnet.Bottleneck) can run the fused path on ``x``."""
-    if os.environ.get("PS_AMD_FUSED_BLOCK", "1") == "0" or not getattr(blk, "fuse_block", False):
+    if knobs.disabled("fused_block") or not getattr(blk, "fuse_block", False):
         return False
     if not (blk.training and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
@@ -572,7 +550,7 @@ def prepare_backward_weights(blocks) -> None:
     """Build the backward weight layouts of ``blocks`` (the fused bottlenecks of one forward) in
     one launch; _BottleneckFn picks them up through the thread-local set (cleared when the
     enclosing ``deferred_bn_counters`` context ends)."""
-    if os.environ.get("PS_AMD_WEIGHT_PREP", "1") == "0":
+    if knobs.disabled("weight_prep"):
         return
     blks = [b for b in blocks if _prep_ok(b)]
     if not blks:

@@ -14,6 +14,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from ._ext import native
 
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_SIGMOID = 0, 1, 2, 3
@@ -88,7 +89,7 @@ def _wgrad_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
     N = dy2.shape[1]
     return (x2.is_cuda and x2.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16 and N % 128 == 0
             and K % 128 == 0 and (N % 256 == 0 or K % 256 == 0) and T >= 4096 and T < 2 ** 31
-            and (N // 256 + 1) * (K // 256 + 1) < 256 and os.environ.get("PS_AMD_SPLITK_WGRAD", "1") != "0")
+            and (N // 256 + 1) * (K // 256 + 1) < 256 and knobs.enabled("splitk_wgrad"))
 
 
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
@@ -182,9 +183,6 @@ class _SplitKLinearFork(torch.autograd.Function):
         return dx, dw, db
 
 
-_FORK = __import__("os").environ.get("PS_AMD_LINEAR_FORK", "1") != "0"
-
-
 class SplitKLinear(torch.nn.Linear):
     """nn.Linear (same parameters / state_dict) whose weight gradient runs split-K on GPU bf16
     when the reduction (tokens) is long and the output small (``linear_wgrad``).  ``fuse_relu``:
@@ -196,21 +194,18 @@ class SplitKLinear(torch.nn.Linear):
     def fork(self, x):
         """(self(x), x) where the second output's gradient is added inside this layer's data-gradient
         GEMM -- for an input that also feeds a residual (BertLayer)."""
-        if (_FORK and not self.fuse_relu and x.is_cuda and x.dtype == torch.bfloat16
+        if (knobs.enabled("linear_fork") and not self.fuse_relu and x.is_cuda and x.dtype == torch.bfloat16
                 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled()):
             return _SplitKLinearFork.apply(x, self.weight, self.bias)
         return self(x), x
 
     def forward(self, x):
         if x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16 and torch.is_grad_enabled():
-            relu = self.fuse_relu and self.bias is not None and _FUSED_RELU
+            relu = self.fuse_relu and self.bias is not None and knobs.enabled("fused_relu")
             y = _SplitKLinear.apply(x, self.weight, self.bias, relu)
             return torch.relu(y) if self.fuse_relu and not relu else y
         y = super().forward(x)
         return torch.relu(y) if self.fuse_relu else y
-
-
-_FUSED_RELU = __import__("os").environ.get("PS_AMD_FUSED_RELU", "1") != "0"
 
 
 # ------------------------------------------------------------------------------ DLRM interaction

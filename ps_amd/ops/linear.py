@@ -20,12 +20,13 @@ Reference: the reference computes the same product in its FC layer's backward
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import knobs
 
 __all__ = ["GradDst", "PsLinear", "ps_linear"]
 
@@ -39,11 +40,8 @@ class GradDst:
         self.buf, self.off, self.numel, self.shape, self.claimed = buf, off, numel, tuple(shape), False
 
 
-_ENABLED = os.environ.get("PS_AMD_PS_LINEAR", "1") != "0"  # 0: always the ordinary weight gradient
-
-
 def _claim(w: torch.Tensor) -> Optional[torch.Tensor]:
-    if not _ENABLED:
+    if knobs.disabled("ps_linear"):  # the ordinary weight gradient
         return None
     d = getattr(w, "_ps_gdst", None)
     if d is None or d.claimed or w.grad is not None or d.buf.dtype != w.dtype or d.buf.device != w.device:

@@ -69,20 +69,13 @@ def enabled(images: Optional[int] = None) -> bool:
 
 
 def side_stream(device: torch.device) -> torch.cuda.Stream:
-    """PS_AMD_WGRAD_CUS=N: the side stream's kernels may only use N of the CUs (spread over the
-    XCDs, hipExtStreamCreateWithCUMask), so the compute stream's small kernels (BN finalizes,
-    folds) find free CUs instead of queueing behind weight-gradient blocks."""
+    """The device's weight-gradient side stream (created on first use).  A CU-masked variant
+    (hipExtStreamCreateWithCUMask) was measured and removed: no gain (README, round-6 prune)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     with _lock:
         s = _STREAMS.get(idx)
         if s is None:
-            cus = int(os.environ.get("PS_AMD_WGRAD_CUS", "0"))
-            if cus > 0:
-                from ._ext import native as _nat
-
-                s = torch.cuda.ExternalStream(_nat().cu_mask_stream(idx, cus, True), device=idx)
-            else:
-                s = torch.cuda.Stream(device=idx)
+            s = torch.cuda.Stream(device=idx)
             _STREAMS[idx] = s
         return s
 

@@ -14,12 +14,12 @@ runs the plain torch composition, which is also the numerics oracle in the GPU t
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from ._ext import native
 
 
@@ -179,7 +179,7 @@ def attention_qkv_ok(qkv: torch.Tensor, heads: int, mask) -> bool:
     """The fused kernel's domain: GPU bf16, head dim 64, S a multiple of 32 up to 128, no mask."""
     return (mask is None and _hip(qkv) and qkv.dim() == 3 and qkv.shape[2] == 3 * heads * 64
             and qkv.shape[1] % 32 == 0 and 0 < qkv.shape[1] <= 128
-            and os.environ.get("PS_AMD_FUSED_ATTN", "1") != "0")
+            and knobs.enabled("fused_attn"))
 
 
 class _FusedAttention(torch.autograd.Function):
@@ -212,11 +212,11 @@ def attention_qkv(qkv: torch.Tensor, heads: int, p: float = 0.0, mask: Optional[
 
 # ------------------------------------------------------------------------------ causal GQA flash attention
 def flash_ok(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> bool:
-    """The in-house causal GQA flash kernels are the default for head dim 128 (PS_AMD_FLASH_ATTN=0
+    """The in-house causal GQA flash kernels are the default for head dim 128 (PS_AMD_DISABLE=flash_attn
     falls back to SDPA): on the Llama-3-8B shape they beat SDPA's library kernels forward and
     backward (profiles/r3_flash_v3_probe.jsonl) and end to end (profiles/r3_llama_flash_vs_sdpa.jsonl)."""
     return (_hip(q, k, v) and q.dim() == 4 and q.shape[3] == 128 and k.shape == v.shape and q.shape[2] % 128 == 0
-            and q.shape[1] % k.shape[1] == 0 and os.environ.get("PS_AMD_FLASH_ATTN", "1") != "0")
+            and q.shape[1] % k.shape[1] == 0 and knobs.enabled("flash_attn"))
 
 
 class _FlashCausal(torch.autograd.Function):
@@ -268,9 +268,9 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
     """Mean softmax cross-entropy of ``logits`` [..., V] against ``labels`` [...] (ignore_index rows
     excluded), as F.cross_entropy.  GPU bf16 logits take the fused HIP kernels (csrc/kernels/xent.hip):
     the forward reads the logits once (per-row log-sum-exp), the backward reads them once and writes
-    the bf16 gradient -- no fp32 copy of the vocab-sized activations.  PS_AMD_FUSED_XENT=0 falls back."""
+    the bf16 gradient -- no fp32 copy of the vocab-sized activations.  PS_AMD_DISABLE=fused_xent falls back."""
     V = logits.shape[-1]
-    if _hip(logits) and logits.dtype == torch.bfloat16 and os.environ.get("PS_AMD_FUSED_XENT", "1") != "0":
+    if _hip(logits) and logits.dtype == torch.bfloat16 and knobs.enabled("fused_xent"):
         x = logits.reshape(-1, V)
         x = x if x.is_contiguous() else x.contiguous()
         return _FusedXent.apply(x, labels.reshape(-1).long().contiguous(), int(ignore_index))

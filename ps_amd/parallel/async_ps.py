@@ -581,8 +581,11 @@ class AsyncPS:
     def snapshot(self) -> dict:
         return self.A.snapshot(self.ctl)
 
-    def synchronize(self) -> None:
-        """Wait until every push of THIS worker has been applied by every owner, then pull."""
+    def synchronize(self, collective: bool = False) -> None:
+        """Wait until every push of THIS worker has been applied by every owner, then pull.
+        ``collective`` (every rank calls it): then a barrier and a second pull, so the replica
+        holds every worker's pushes -- without it a faster rank's replica may still miss a slower
+        rank's last push."""
         if self.gpu:
             torch.cuda.current_stream(self.device).synchronize()
             self.push_stream.synchronize()
@@ -601,6 +604,12 @@ class AsyncPS:
         if self.gpu:
             torch.cuda.current_stream(self.device).synchronize()
             self.notifier.drain()
+        if collective and self.world > 1:
+            self.t.barrier()  # every rank's pushes are applied everywhere
+            self._pull(gate=False)
+            if self.gpu:
+                torch.cuda.current_stream(self.device).synchronize()
+                self.notifier.drain()
 
     # ------------------------------------------------------------------ checkpoint
     def _state_list(self) -> List[torch.Tensor]:

@@ -43,6 +43,7 @@ arbitrary per-key-prefix updaters (resolve_updater).
 from __future__ import annotations
 
 import contextlib
+import os
 
 import time
 from collections import deque
@@ -85,12 +86,8 @@ class ColocatedPS:
         self.compress_warmup = int(compress_warmup)
         self.average = average
         self.overlap = overlap
-        import os as _os0
-
-        # collective plane: reduce-scatter bf16 buckets in fp32 (the W-way sum is otherwise rounded
-        # in bf16 by RCCL); the xGMI plane always sums in fp32 on the owner
-        if reduce_fp32 is None:
-            reduce_fp32 = _os0.environ.get("PS_AMD_REDUCE_FP32", "0") == "1"
+        # collective plane: reduce-scatter bf16 buckets in fp32 when reduce_fp32 (the W-way sum is
+        # otherwise rounded in bf16 by RCCL); the xGMI plane always sums in fp32 on the owner
         self.reduce_fp32 = bool(reduce_fp32)
         self.accumulating = False  # micro-batch accumulation: hooks stay quiet until the last one
         params = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
@@ -216,27 +213,10 @@ class ColocatedPS:
         self._key_bucket = {n: R.keys[n].bucket for n in self.params}
         self._landing: List[Dict[str, torch.Tensor]] = [dict() for _ in R.buckets]  # parked grads
         self.comm = torch.cuda.Stream(device=self.device) if self.gpu else None
-        # PS_AMD_SERVE_CUS=N: the comm stream -- where a single-GPU step's optimizer serve runs
-        # beside backward -- only gets N of the CUs (spread over every XCD), so the serve takes a
-        # bounded slice of the chip instead of contending with the backward GEMMs for all of it
-        # (profiles/r5_llama_serve_overlap.txt)
-        import os as _os
-
-        self.serve_cus = int(_os.environ.get("PS_AMD_SERVE_CUS", "0")) if self.gpu else 0
-        if self.serve_cus > 0:
-            from ..ops._ext import native as _nat
-
-            h = _nat().cu_mask_stream(self.device.index if self.device.index is not None
-                                      else torch.cuda.current_device(), self.serve_cus, True)
-            self.comm = torch.cuda.ExternalStream(h, device=self.device)
         # separate push / pull communicators: the all-gather of bucket b runs on
         # its own communicator + stream, so the reduce-scatter of bucket b+1 need not wait behind
-        # it; opt-in (PS_AMD_SPLIT_COMM=1) -- the default single communicator is what the
-        # measured multi-GPU configs use
-        import os as _os
-
-        if split_comm is None:
-            split_comm = _os.environ.get("PS_AMD_SPLIT_COMM", "0") == "1"
+        # it; opt-in (split_comm=True) -- the default single communicator is what the measured
+        # multi-GPU configs use
         self.split_comm = bool(split_comm) and self.world > 1
         self.tpull = self.t.split() if self.split_comm else self.t
         self.comm_pull = torch.cuda.Stream(device=self.device) if (self.gpu and self.split_comm) else self.comm
@@ -247,7 +227,7 @@ class ColocatedPS:
         # then, once per process at a random point in the first ~30 steps, the runtime stalls for
         # 2-4 s (2 of 3 runs with --warmup 5 timed 6.2-6.9K img/s instead of 16.5K; with the
         # bound at 2: 3 of 3 normal, and no steady-state cost -- profiles/r5_run_ahead_ab.txt).
-        self.max_inflight = int(_os.environ.get("PS_AMD_MAX_INFLIGHT", "2"))
+        self.max_inflight = int(os.environ.get("PS_AMD_MAX_INFLIGHT", "2"))
         self._host_events: deque = deque()
         self.stats = {"exposed_wait_ms": 0.0, "rounds": 0}
         # fault injection (PS_AMD_FAULT / HIPPS_FAULT): kill at a step, delay pushes
@@ -257,9 +237,7 @@ class ColocatedPS:
         self.fault = fi if fi.spec else None
         # per-step phase timing: device events on the comm stream around push /
         # serve / pull of every bucket, plus backward-end vs round-end for the exposed tail
-        import os as _os
-
-        self.timing = timing or _os.environ.get("PS_AMD_TIMING", "0") == "1"
+        self.timing = timing or os.environ.get("PS_AMD_TIMING", "0") == "1"
         self._marks: List[tuple] = []  # (name, event or perf_counter) of the current step
         self._tsum: Dict[str, float] = {}
         self._tsteps = 0

@@ -348,9 +348,15 @@ class GpuKVStore:
                 self.sum(n, p.grad)
 
     # ------------------------------------------------------------------ lifecycle
-    def synchronize(self) -> None:
+    def synchronize(self, collective: bool = False) -> None:
+        """Drain every engine.  ``collective=True`` (every rank calls it, e.g. before reading the
+        final weights): the asynchronous engine's replicas then also hold every OTHER worker's
+        pushes, not just this rank's."""
         for eng in self.engines:
-            eng.synchronize()
+            if collective and getattr(eng, "info", {}).get("engine") == "AsyncPS":
+                eng.synchronize(collective=True)
+            else:
+                eng.synchronize()
         for t in self.tables.values():
             t.synchronize()
 

@@ -105,7 +105,7 @@ RESP = [(3211264, 256, 64), (3211264, 256, 128), (802816, 512, 128), (802816, 51
         (200704, 1024, 512), (50176, 2048, 512)]
 def c64_case(M, K, N):
     """3x3 64 -> 64 at 56 x 56: forward (epi 1) and data gradient (epi 3); 'fused' = the default
-    routing (conv3x3_c64_kernel unless PS_AMD_CONV_C64=0), 'split' = forward + data gradient sum."""
+    routing (the default 3x3 route), 'split' = forward + data gradient sum."""
     n = M // (56 * 56)
     x, w = rnd(M, 64), rnd(64, 576, scale=576 ** -0.5)
     z1, cf = rnd(M, 64), coef(64)
@@ -141,7 +141,7 @@ def plain_case(M, K, N):
 PLAIN = [(802816, 512, 128), (200704, 1024, 256), (50176, 2048, 512), (200704, 512, 1024), (3211264, 576, 64),
          (200704, 256, 1024), (802816, 128, 512)]
 C64 = [(1024 * 56 * 56, 576, 64), (256 * 56 * 56, 576, 64)]
-CASES = [("plain_gemm", PLAIN, plain_case), ("conv3x3_c64 (fwd_ms, dgrad_ms)", C64, c64_case), ("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
+CASES = [("plain_gemm", PLAIN, plain_case), ("conv3x3_64 (fwd_ms, dgrad_ms)", C64, c64_case), ("bn_relu_prologue", PRO, pro_case), ("bn_bwd_prologue", BWD, bwd_case),
          ("block_output_prologue", RESP, resp_case)]
 only = os.environ.get("PROBE_ONLY")
 for kind, shapes, fn in CASES:

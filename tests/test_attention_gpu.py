@@ -61,7 +61,7 @@ def test_bert_layer_fused_attention_matches_sdpa(monkeypatch):
     wl = torch.randn(4, 128, 256, device=DEV)  # (mean(y^2) after a LayerNorm has zero gradient)
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("PS_AMD_FUSED_ATTN", flag)
+        monkeypatch.setenv("PS_AMD_DISABLE", "" if flag == "1" else "fused_attn")
         layer.zero_grad()
         xi = x.clone().requires_grad_()
         y = layer(xi)

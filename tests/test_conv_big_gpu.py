@@ -265,103 +265,3 @@ def test_big_tile_residual_and_fold_epilogues(epi):
     torch.testing.assert_close(part[1].sum(0), (cg * ((z3.float() - mean) * invstd)).sum(0), rtol=1e-3, atol=5e-2)
     if epi == 9:
         torch.testing.assert_close(part[2].sum(0), (cg * ((zd.float() - m2) * i2)).sum(0), rtol=1e-3, atol=5e-2)
-
-
-@pytest.mark.parametrize("M,K,N,epi", [(131101, 64, 256, 1), (131101, 128, 512, 0), (65613, 256, 1024, 3),
-                                       (65613, 256, 512, 6), (65613, 256, 512, 9), (70000, 512, 256, 1)])
-def test_big_tile_128_channel_tiles(monkeypatch, M, K, N, epi):
-    """256 x 128 tiles (256-thread blocks, two per CU, 3-deep ring of 32-deep stages) vs fp32: the
-    store, BN statistics, data-gradient and fold epilogues, K from 64 up."""
-    monkeypatch.setenv("PS_AMD_CONV_BIG_TN", "128")
-    g = _gen(M + K + N + epi)
-    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
-    gg = [M, 1, M, 1, 1, 1, 0]
-    bm, bn, gm = native().conv_gemm_plan(M, N, K, gg, False, epi)
-    assert (bm, bn, gm) == (256, 128, (M + 255) // 256)
-    ref = a.float() @ b.float().t()
-    if epi == 0:
-        _close(native().conv_gemm(a, b, gg)[0], ref)
-        return
-    if epi == 1:
-        kshift = torch.randn(N, generator=g, device=DEV) * 0.1
-        c, part = native().conv_gemm(a, b, gg, None, 1, None, kshift)
-        _close(c, ref)
-        cb = c.float() - kshift
-        torch.testing.assert_close(part[0].sum(0), cb.sum(0), rtol=1e-4, atol=5e-2)
-        torch.testing.assert_close(part[1].sum(0), (cb * cb).sum(0), rtol=1e-4, atol=5e-2)
-        return
-    mean, invstd = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
-    if epi == 3:
-        z = _rnd(M, N, g=g)
-        mc = _coef(N, g)
-        c, part = native().conv_gemm(a, b, gg, None, 3, z, None, mc, mean, invstd)
-        _close(c, ref * ((z.float() * mc[:N] + mc[N:]) > 0))
-    else:
-        aux, z = _rnd(M, N, g=g), _rnd(M, N, g=g)
-        bits = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
-        bits2 = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
-        kw = dict(bits=bits, aux2=z, bits2=bits2, mean=mean, invstd=invstd)
-        if epi == 9:
-            zd = _rnd(M, N, g=g)
-            m2, i2 = torch.randn(N, generator=g, device=DEV) * 0.1, torch.rand(N, generator=g, device=DEV) + 0.5
-            kw.update(aux3=zd, mean2=m2, invstd2=i2)
-        c, part = native().conv_gemm(a, b, gg, None, epi, aux, **kw)
-        r = ref.bfloat16().float()
-        want = torch.where(_unpack(bits, M, N), r + aux.float(), r) * _unpack(bits2, M, N)
-        _close(c, want)
-        if epi == 9:
-            torch.testing.assert_close(part[2].sum(0), (c.float() * ((zd.float() - m2) * i2)).sum(0),
-                                       rtol=1e-3, atol=5e-2)
-    cg = c.float()
-    torch.testing.assert_close(part[0].sum(0), cg.sum(0), rtol=1e-4, atol=5e-2)
-    torch.testing.assert_close(part[1].sum(0), (cg * ((z.float() - mean) * invstd)).sum(0), rtol=1e-3, atol=5e-2)
-
-
-@pytest.mark.parametrize("M,K,N,epi,kind", [(33001, 1024, 512, 1, "plain"), (16411, 2048, 1024, 3, "plain"),
-                                            (33001, 1024, 512, 3, "bwd"), (33001, 1024, 512, 1, "resp"),
-                                            (262213, 256, 256, 6, "plain")])
-def test_big_tile_stream_k_matches_one_tile_per_block(monkeypatch, M, K, N, epi, kind):
-    """Stream-K (a block per CU walking contiguous (tile, stage) units; a split tile finished by the
-    block holding its first stage, which adds the others' fp32 partials in block order) vs one tile
-    per block (PS_AMD_CONV_BIG_SK=0) and vs fp32: same outputs up to summation order, same partials,
-    the prologue's side outputs identical, and bitwise repeatable."""
-    g = _gen(M + K + epi)
-    a, b = _rnd(M, K, g=g), _rnd(N, K, g=g, scale=K ** -0.5)
-    gg = [M, 1, M, 1, 1, 1, 0]
-    pos, kw = (), {}
-    if epi == 1:
-        pos = (None, torch.zeros(N, device=DEV))
-    elif epi == 3:
-        pos = (_rnd(M, N, g=g), None, _coef(N, g), torch.randn(N, generator=g, device=DEV) * 0.1,
-               torch.rand(N, generator=g, device=DEV) + 0.5)
-    else:
-        bits = torch.randint(0, 256, (M * N // 8,), generator=g, device=DEV, dtype=torch.uint8)
-        pos = (_rnd(M, N, g=g),)
-        kw = dict(bits=bits, aux2=_rnd(M, N, g=g), bits2=bits, mean=torch.zeros(N, device=DEV),
-                  invstd=torch.ones(N, device=DEV))
-    if kind == "bwd":
-        kw.update(a2=_rnd(M, K, g=g), bwd=torch.cat([torch.rand(K, generator=g, device=DEV) + 0.5,
-                                                     torch.randn(2 * K, generator=g, device=DEV) * 0.1]))
-    elif kind == "resp":
-        kw.update(a2=_rnd(M, K, g=g), aout=torch.empty(M, K, device=DEV, dtype=torch.bfloat16),
-                  abits=torch.empty(M * K // 8, device=DEV, dtype=torch.uint8))
-    pro = _coef(K, g) if kind == "resp" else None
-
-    def run():
-        kw2 = dict(kw)
-        if kind == "resp":
-            kw2["aout"], kw2["abits"] = torch.empty_like(kw["aout"]), torch.empty_like(kw["abits"])
-        r = native().conv_gemm(a, b, gg, pro, epi, *pos, **kw2)
-        return list(r) + ([kw2["aout"], kw2["abits"]] if kind == "resp" else [])
-
-    monkeypatch.setenv("PS_AMD_CONV_BIG_SK", "0")
-    ref = run()
-    monkeypatch.setenv("PS_AMD_CONV_BIG_SK", "1")
-    sk1, sk2 = run(), run()
-    for u, v in zip(sk1, sk2):
-        assert u is None or torch.equal(u, v)
-    _close(sk1[0], ref[0], tol=5e-3)
-    if ref[1] is not None:
-        torch.testing.assert_close(sk1[1].sum(1), ref[1].sum(1), rtol=1e-3, atol=5e-2)
-    for u, v in zip(sk1[2:], ref[2:]):  # the prologue's stored operand (dz or the block output, bits)
-        assert torch.equal(u, v)

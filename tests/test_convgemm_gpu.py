@@ -335,14 +335,14 @@ def test_bn_apply_coef_and_backward_from_partials():
 @pytest.mark.parametrize("conv3x3", ["1", "0"])
 @pytest.mark.parametrize("inplanes,planes,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2), (512, 128, 1)])
 def test_fused_bottleneck_matches_module_path(inplanes, planes, stride, conv3x3, monkeypatch):
-    """Fused block (3x3 conv on our GEMMs or, PS_AMD_CONV3X3=0, on MIOpen) vs module path."""
+    """Fused block (3x3 conv on our GEMMs or, PS_AMD_DISABLE=conv3x3, on MIOpen) vs module path."""
     import torch.nn as nn
 
     from ps_amd.models.resnet import Bottleneck, prepare_for_mi355x
     from ps_amd.ops.bn import BatchNormAct2d
     from ps_amd.ops.convgemm import fused_block_ok
 
-    monkeypatch.setenv("PS_AMD_CONV3X3", conv3x3)
+    monkeypatch.setenv("PS_AMD_DISABLE", "" if conv3x3 == "1" else "conv3x3")
     torch.manual_seed(0)
     ds = None
     if stride != 1 or inplanes != planes * 4:
@@ -437,7 +437,7 @@ def test_fold_epilogues_previous_block_bn3_reduce(epi, K):
 def test_chained_blocks_fold_bn3_backward(extra_consumer, wide, monkeypatch):
     """Three fused bottlenecks (downsample first) inside the ResNet forward context: block i's
     conv1 data-grad epilogue reduces block i-1's bn3 backward.  Checked against the same fused
-    chain with the fold disabled (PS_AMD_FOLD_BN3=0: every block runs its own reduce pass).
+    chain with the fold disabled (PS_AMD_DISABLE=fold_bn3: every block runs its own reduce pass).
     With a second consumer of a block output autograd sums the gradients and that block must
     fall back to its own reduce.  (Fused vs module path per block: the test above.)"""
     import torch.nn as nn
@@ -480,12 +480,12 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, wide, monkeypatch):
     assert cg.FOLD_STATS["used"] - before == (1 if extra_consumer else 2)
     # the downsample block's BN sum rides in block 1's epilogue 9 unless y1 has a second consumer
     assert cg.FOLD_STATS["ds"] - before_ds == (0 if extra_consumer else 1)
-    monkeypatch.setenv("PS_AMD_FOLD_BN_DS", "0")  # bn3 folded, the downsample BN reduced on its own
+    monkeypatch.setenv("PS_AMD_DISABLE", "fold_bn_ds")  # bn3 folded, the downsample BN reduced on its own
     gc, pc = run()
     _close(ga, gc, tol=1e-2, amax=0.05)
     for n in pc:
         _close(pa[n], pc[n], tol=1e-2, amax=0.05)
-    monkeypatch.delenv("PS_AMD_FOLD_BN_DS")
+    monkeypatch.delenv("PS_AMD_DISABLE")
     # block outputs applied in the next block's conv1 prologue (PRO 3): same gradients, and the
     # forward outputs / ReLU bits they store equal the apply pass's
     before = cg.FOLD_STATS["resp"]
@@ -494,7 +494,7 @@ def test_chained_blocks_fold_bn3_backward(extra_consumer, wide, monkeypatch):
     _close(ga, gr, tol=1e-2, amax=0.05)
     for n in pr:
         _close(pa[n], pr[n], tol=1e-2, amax=0.05)
-    monkeypatch.setenv("PS_AMD_FOLD_BN3", "0")
+    monkeypatch.setenv("PS_AMD_DISABLE", "fold_bn3")
     before = cg.FOLD_STATS["used"]
     gb, pb = run()
     assert cg.FOLD_STATS["used"] == before
@@ -590,7 +590,7 @@ def test_weight_prep_matches_reference_layouts(monkeypatch):
     y = torch.randint(0, 10, (8,), device=DEV, generator=g)
     grads = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("PS_AMD_WEIGHT_PREP", flag)
+        monkeypatch.setenv("PS_AMD_DISABLE", "" if flag == "1" else "weight_prep")
         mm = copy.deepcopy(m)
         F.cross_entropy(mm(x).float(), y).backward()
         grads[flag] = {n: p.grad.clone() for n, p in mm.named_parameters()}
@@ -604,10 +604,7 @@ def test_conv3x3_patch_forward_statistics_and_data_grad(n, hw, cin, cout):
     """3x3 stride-1 forward on the patch-staged tiles (PS_AMD_CONV_PATCH, default on: the tile's
     input rows staged once per 64-channel chunk, tiles straddling two images) with the BN
     statistics epilogue, and the data gradient (flipped weight) with epilogue 3 -- vs fp32 torch.
-    56 x 56 at 64 -> 64 channels runs conv3x3_c64_kernel (persistent row tiles, resident weight;
-    n = 10: 280 tiles over 256 blocks, so blocks walk several tiles through both patch slots; n = 20:
-    three tiles per block, some crossing an image boundary -- the rolling row window of mode 4
-    restarts there)."""
+    n = 10 / 20 at 56 x 56: tiles crossing image boundaries and grids of several waves."""
     from ps_amd.ops.convgemm import _mat3_dgrad
 
     g = _gen(n * hw + cin + cout)
@@ -731,8 +728,7 @@ def test_layer1_chain_single_pass_backwards_match_unfused(monkeypatch):
     ga, pa = run()
     assert cg.FOLD_STATS.get("conv3_fused", 0) - c3 == 2  # blocks 0 and 1 (block 2 has no consumer)
     assert cg.FOLD_STATS.get("ds_fused", 0) - dsf == 1
-    monkeypatch.setenv("PS_AMD_DS_BWD_FUSED", "0")
-    monkeypatch.setenv("PS_AMD_CONV3_BWD_FUSED", "0")
+    monkeypatch.setenv("PS_AMD_DISABLE", "ds_bwd_fused,conv3_bwd_fused")
     gb, pb = run()
     _close(ga, gb, tol=1e-2, amax=0.05)
     for n in pb:

@@ -57,7 +57,7 @@ def test_llama_block_flash_matches_sdpa(monkeypatch):
     cs = rope_table(256, 128, c.rope_theta, x.device)
     outs = []
     for flag in ("1", "0"):  # flash kernel (the default) vs SDPA
-        monkeypatch.setenv("PS_AMD_FLASH_ATTN", flag)
+        monkeypatch.setenv("PS_AMD_DISABLE", "" if flag == "1" else "flash_attn")
         blk.zero_grad()
         xi = x.clone().requires_grad_()
         y, r = blk(xi, None, cs)

@@ -48,6 +48,14 @@ def _oracle(world, steps, lr=0.1, mom=0.9, staleness=0):
     return versions[max(0, steps - staleness)] if staleness else w
 
 
+def _lockstep(tp):
+    """The SSP gate is a LOWER bound: a pull waits for every worker's earlier pushes but may also
+    see a fast worker's NEXT push, applied in the meantime.  A collective barrier after each round
+    (the pull inside ``kv.barrier()`` comes first, behind the gate) keeps the workers in lockstep,
+    which with apply-on-arrival and plain SGD makes SSP(0) the BSP trajectory exactly."""
+    tp.barrier()
+
+
 def _kv_body(tp, consistency, plane, steps, staleness=0, style="pushpull", mom=0.9):
     from ps_amd.parallel.gpu_kvstore import GpuKVStore
     from ps_amd.parallel.updaters import MomentumUpdater, SimpleUpdater
@@ -70,13 +78,15 @@ def _kv_body(tp, consistency, plane, steps, staleness=0, style="pushpull", mom=0
         if style in ("pushpull", "async"):
             kv.push(names, [g[k] for k in names])
             kv.barrier()
+            if consistency == "ssp":
+                _lockstep(tp)
         else:  # reference style: two half-contributions summed then averaged by update()
             for k in names:
                 kv.sum(k, g[k] * 0.5)
                 kv.sum(k, g[k] * 1.5)
             kv.update()
             kv.clear()
-    kv.synchronize()
+    kv.synchronize(collective=True)  # the final weights hold every worker's pushes
     out = {k: kv.get(k).detach().clone() for k in names}
     st = kv.stats()
     kv.close()
@@ -297,7 +307,9 @@ def _late_body(tp, consistency, plane, steps, t_new, mom=0.9):
             lw = kv.pull(LATE)
             kv.push(LATE, 0.2 * (lw - 1.0))
         kv.barrier()
-    kv.synchronize()
+        if consistency == "ssp":
+            _lockstep(tp)
+    kv.synchronize(collective=True)
     out = {k: kv.get(k).detach().float().cpu().clone() for k in names + [LATE]}
     st = kv.stats()
     kv.close()
@@ -309,8 +321,8 @@ def test_key_created_after_seal_matches_oracle(consistency, plane):
     """VERDICT r4 Next #6: a dense key first appears in round 3, after the store sealed -- it
     becomes a second key group (its own engine on the same ranks) and trains like the others."""
     steps, t_new = 6, 3
-    # the async owners apply each worker's push on arrival (gradient / W): with plain SGD and the
-    # SSP(0) gate that is the BSP trajectory (test_ssp0_async_engine_is_bsp_exact)
+    # the async owners apply each worker's push on arrival (gradient / W): with plain SGD, the
+    # SSP(0) gate and lockstep rounds that is the BSP trajectory (test_ssp0_async_engine_is_bsp_exact)
     mom = 0.9 if consistency == "bsp" else 0.0
     res = dist_util.run(_late_body, 2, (consistency, plane, steps, t_new, mom))
     want = _late_oracle(2, steps, t_new, mom=mom)
