@@ -454,7 +454,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             e1 = (9 if li.zd is not None else 6) if fold else 5
         # (bn1's backward as the conv1 data-gradient prologue on the 256 x 256 tiles cost more than
-        # the apply pass it removes at K = 256 / 512: profiles/r5_conv1_dgrad_big.txt; removed)
+        # the apply pass it removes at K = 256 / 512 in the round-5 A/B, scripts/probe_conv_big.py; removed)
         if ours_dgrad:
             dz1, dg1, db1 = nat.bn_bwd_partials(gy1, z1, p1b, g1, m1, i1)
         else:
