@@ -1223,7 +1223,12 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const ConvWgradArgs 
 // fragments in registers -- a fragment is 8 pixels of ONE channel, so one scale / shift per lane;
 // rows past the split read zeros from dz, so their transformed X never contributes.
 constexpr int kWP = 32;  // pixels per stage
-constexpr int kWS = 4;   // LDS ring depth
+// LDS ring depth: 3 stages (96 KiB at the 256 x 256 tile) rather than 4 (128 KiB), so smaller
+// compute-stream blocks can share a CU with a weight-gradient block running on the side stream:
+// ResNet-50 bs1024 +0.4 %, bs256 +0.8 % (2 stages: no further gain; the LDS-pass prologue needs 3,
+// its pass runs one stage ahead of the MFMAs -- profiles/r6_wgrad_ring_depth_ab.txt)
+constexpr int kWS = 3;
+constexpr int kWSP = 3;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -1245,12 +1250,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
   constexpr int BNO = WN * 32 * TN, BKO = WK * 32 * TK;
   static_assert(!PROL || (PRO && (BKO == 128 || BKO == 256)), "LDS-pass prologue: 16-B chunks tile 512 threads");
   static_assert(WN * WK == 8, "8 waves");
+  constexpr int WS = PROL ? kWSP : kWS;
   constexpr int STAGE = kWP * (BNO + BKO);
   constexpr int GCPR = BNO / 8, XCPR = BKO / 8;                // 16-B chunks per tile row
   constexpr int GI = kWP * GCPR / 512, XI = kWP * XCPR / 512;  // DMA instructions per wave per stage
   constexpr int PER = GI + XI;
   static_assert(GI >= 1 && XI >= 1 && kWP * GCPR % 512 == 0 && kWP * XCPR % 512 == 0, "tile / stage shape");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kWS * STAGE];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[WS * STAGE];
 
   const ConvGeo& g = p.g;
   // wave id through readfirstlane: provably uniform, so LDS-DMA destinations (M0) and other
@@ -1416,7 +1422,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
       }
     }
   };
-  const int pre = nst < kWS - 1 ? nst : kWS - 1;
+  const int pre = nst < WS - 1 ? nst : WS - 1;
   for (int st = 0; st < pre; ++st) issue(st, st);
   if constexpr (PROL) {
     // the LDS pass runs one stage ahead (stage st + 1 while stage st computes), so the barrier
@@ -1430,7 +1436,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
   for (int st = 0; st < nst; ++st) {
     // this wave's DMAs of stage st landed (later stages may stay in flight), then everyone's
     // (PROL: of stage st + 1, whose LDS pass runs in this iteration)
-    const int ahead = min(kWS - 2, nst - 1 - st);
+    const int ahead = min(WS - 2, nst - 1 - st);
     if constexpr (PROL) {
       if (ahead >= 2) wait_vmcnt<PER>();
       else wait_vmcnt<0>();
@@ -1440,13 +1446,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
       else wait_vmcnt<0>();
     }
     lds_barrier();  // also: every wave finished stage st - 1, whose buffer the next issue refills
-    if (st + kWS - 1 < nst) issue(st + kWS - 1, (st + kWS - 1) % kWS);
+    if (st + WS - 1 < nst) issue(st + WS - 1, (st + WS - 1) % WS);
     if constexpr (PROL) {
-      if (st + 1 < nst) xform((st + 1) % kWS);  // published by the next iteration's barrier
+      if (st + 1 < nst) xform((st + 1) % WS);  // published by the next iteration's barrier
     }
     if constexpr (DB) {
       if (dbt) {
-        const uint16_t* Gs = lds + (st % kWS) * STAGE;
+        const uint16_t* Gs = lds + (st % WS) * STAGE;
         const int cc = t % GCPR;
 #pragma unroll
         for (int r = t / GCPR; r < kWP; r += DBR) {
@@ -1456,7 +1462,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_wide_kernel(const ConvWgrad
         }
       }
     }
-    mma(st % kWS);
+    mma(st % WS);
   }
   if constexpr (DB) {
     if (dbt) {
