@@ -222,7 +222,7 @@ void lerp(Tensor w0, Tensor w, double sc, Tensor out) {
 }
 
 // ------------------------------------------------------------------------------ compression
-void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
+void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales, c10::optional<Tensor> mom, double beta1) {
   check_gpu(g, "g");
   check_gpu(err, "err");  // error feedback in fp32 or bf16
   check_gpu(words, "words");
@@ -234,9 +234,25 @@ void onebit_pack(Tensor g, Tensor err, Tensor words, Tensor scales) {
   TORCH_CHECK(scales.numel() >= (n + psamd::kOnebitChunk - 1) / psamd::kOnebitChunk, "scales too small");
   const c10::DeviceGuard guard(g.device());
   TORCH_CHECK(err.is_contiguous(), "err must be contiguous");
+  void* mp = nullptr;
+  if (mom.has_value() && mom->defined()) {  // 1-bit Adam: the worker momentum, err's dtype
+    check_gpu(*mom, "mom");
+    TORCH_CHECK(mom->numel() == n && mom->is_contiguous() && mom->scalar_type() == err.scalar_type(),
+                "mom: contiguous, err's size and dtype");
+    mp = mom->data_ptr();
+  }
   psamd::launch_onebit_pack(g.data_ptr(), dcode(g, "g"), err.data_ptr(), dcode(err, "err"), n,
                             reinterpret_cast<uint64_t*>(words.data_ptr<int64_t>()), scales.data_ptr<float>(),
-                            cur_stream(g));
+                            cur_stream(g), mp, static_cast<float>(beta1));
+}
+
+void onebit_momentum(Tensor g, Tensor mom, double beta1) {
+  check_gpu(g, "g");
+  check_gpu(mom, "mom");
+  TORCH_CHECK(g.is_contiguous() && mom.is_contiguous() && g.numel() == mom.numel(), "g, mom: contiguous, same size");
+  const c10::DeviceGuard guard(g.device());
+  psamd::launch_onebit_momentum(g.data_ptr(), dcode(g, "g"), mom.data_ptr(), dcode(mom, "mom"), g.numel(),
+                                static_cast<float>(beta1), cur_stream(g));
 }
 
 void onebit_unpack_reduce(Tensor words, Tensor scales, Tensor out, double mult, bool accumulate) {
@@ -1801,7 +1817,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("axpy_", &axpy_);
   m.def("reduce_n", &reduce_n);
   m.def("lerp", &lerp);
-  m.def("onebit_pack", &onebit_pack);
+  m.def("onebit_pack", &onebit_pack, py::arg("g"), py::arg("err"), py::arg("words"), py::arg("scales"),
+        py::arg("mom") = py::none(), py::arg("beta1") = 0.0);
+  m.def("onebit_momentum", &onebit_momentum);
   m.def("onebit_unpack_reduce", &onebit_unpack_reduce);
   m.def("gather_rows", &gather_rows);
   m.def("segment_reduce_rows", &segment_reduce_rows);

@@ -124,8 +124,10 @@ int sumsq_blocks(int64_t n);
 // ---------------------------------------------------------------- compress.hip
 // 1-bit sign compression with per-chunk scale and error feedback (K26).
 constexpr int kOnebitChunk = 1024;
+// mom (nullable, err's dtype): 1-bit Adam -- compress the worker momentum beta1 m + (1 - beta1) g
 void launch_onebit_pack(const void* g, int gdtype, void* err, int edtype, int64_t n, uint64_t* words, float* scales,
-                        hipStream_t s);
+                        hipStream_t s, void* mom = nullptr, float beta1 = 0.f);
+void launch_onebit_momentum(const void* g, int gdtype, void* mom, int mdtype, int64_t n, float beta1, hipStream_t s);
 void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int nworkers, int64_t n,
                                  int64_t words_stride, int64_t scales_stride, void* out, int odtype, float mult,
                                  int accumulate, hipStream_t s);

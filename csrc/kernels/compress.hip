@@ -27,9 +27,13 @@ namespace psamd {
 // consecutive bytes.  The chunk's mean |c| is a 2-wave reduction through LDS.  (The previous
 // element-strided kernel with a wave64 ballot per word ran at ~0.4 TB/s: 0.49 ms per 64 MB
 // bf16 bucket, profiles/r5_llama_width_onebit.txt.)
-template <typename G, typename E>
+// MOM (1-bit Adam, compressing the worker's MOMENTUM instead of its gradient): m = beta1 m + (1 - beta1) g
+// first (m in E, stored back), then c = m + e; the owner runs Adam with beta1 = 0 and a frozen variance
+// on the decoded momenta (parallel/updaters.py OneBitAdamUpdater).
+template <typename G, typename E, bool MOM>
 __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ g, E* __restrict__ err, int64_t n,
-                                                          uint8_t* __restrict__ wbytes, float* __restrict__ scales) {
+                                                          uint8_t* __restrict__ wbytes, float* __restrict__ scales,
+                                                          E* __restrict__ mom, float beta1) {
   __shared__ float part[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int64_t chunk = static_cast<int64_t>(blockIdx.x) * 2 + (t >> 7);
@@ -42,6 +46,13 @@ __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ 
     float gv[8], ev[8];
     load8(g, i0, gv);
     load8(err, i0, ev);
+    if constexpr (MOM) {
+      float mv[8];
+      load8(mom, i0, mv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[k] = beta1 * mv[k] + (1.f - beta1) * gv[k];
+      store8(mom, i0, gv);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       c[k] = gv[k] + ev[k];
@@ -51,7 +62,15 @@ __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int64_t i = i0 + k;
-      c[k] = i < n ? Elem<G>::load(g, i) + Elem<E>::load(err, i) : 0.f;
+      float gk = 0.f;
+      if (i < n) {
+        gk = Elem<G>::load(g, i);
+        if constexpr (MOM) {
+          gk = beta1 * Elem<E>::load(mom, i) + (1.f - beta1) * gk;
+          Elem<E>::store(mom, i, gk);
+        }
+      }
+      c[k] = i < n ? gk + Elem<E>::load(err, i) : 0.f;
       asum += fabsf(c[k]);
     }
   }
@@ -81,6 +100,28 @@ __global__ __launch_bounds__(256) void onebit_pack_kernel(const G* __restrict__ 
     for (int k = 0; k < 8 && i0 + k < n; ++k) Elem<E>::store(err, i0 + k, e[k]);
   }
   wbytes[i0 >> 3] = static_cast<uint8_t>(byte);
+}
+
+// m = beta1 m + (1 - beta1) g: the worker momentum of 1-bit Adam during the full-precision warm-up
+// rounds (the push itself is the uncompressed gradient then), so the compressed phase starts from it.
+template <typename G, typename E>
+__global__ __launch_bounds__(256) void onebit_momentum_kernel(const G* __restrict__ g, E* __restrict__ mom, int64_t n,
+                                                              float beta1) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t * 8 < n; t += stride) {
+    const int64_t i0 = t * 8;
+    if (i0 + 8 <= n) {
+      float gv[8], mv[8];
+      load8(g, i0, gv);
+      load8(mom, i0, mv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mv[k] = beta1 * mv[k] + (1.f - beta1) * gv[k];
+      store8(mom, i0, mv);
+    } else {
+      for (int64_t i = i0; i < n; ++i)
+        Elem<E>::store(mom, i, beta1 * Elem<E>::load(mom, i) + (1.f - beta1) * Elem<G>::load(g, i));
+    }
+  }
 }
 
 // 8 consecutive elements per thread (one byte of a packed word, one 16-B / 32-B output store):
@@ -127,19 +168,36 @@ __global__ __launch_bounds__(256) void onebit_unpack_reduce_kernel(const uint64_
 }
 
 void launch_onebit_pack(const void* g, int gdtype, void* err, int edtype, int64_t n, uint64_t* words, float* scales,
-                        hipStream_t s) {
+                        hipStream_t s, void* mom, float beta1) {
   if (n <= 0) return;
   const int64_t nchunks = (n + kOnebitChunk - 1) / kOnebitChunk;
   const int64_t nblk = (nchunks + 1) / 2;
   uint8_t* wb = reinterpret_cast<uint8_t*>(words);
-#define PSAMD_PACK(G, E)                                                                                           \
-  hipLaunchKernelGGL((onebit_pack_kernel<G, E>), dim3(nblk), dim3(256), 0, s, static_cast<const G*>(g),            \
-                     static_cast<E*>(err), n, wb, scales)
+#define PSAMD_PACK(G, E)                                                                                             \
+  if (mom != nullptr)                                                                                                \
+    hipLaunchKernelGGL((onebit_pack_kernel<G, E, true>), dim3(nblk), dim3(256), 0, s, static_cast<const G*>(g),      \
+                       static_cast<E*>(err), n, wb, scales, static_cast<E*>(mom), beta1);                            \
+  else                                                                                                               \
+    hipLaunchKernelGGL((onebit_pack_kernel<G, E, false>), dim3(nblk), dim3(256), 0, s, static_cast<const G*>(g),     \
+                       static_cast<E*>(err), n, wb, scales, static_cast<E*>(nullptr), 0.f)
   if (gdtype == 1 && edtype == 1) PSAMD_PACK(uint16_t, uint16_t);
   else if (gdtype == 1) PSAMD_PACK(uint16_t, float);
   else if (edtype == 1) PSAMD_PACK(float, uint16_t);
   else PSAMD_PACK(float, float);
 #undef PSAMD_PACK
+}
+
+void launch_onebit_momentum(const void* g, int gdtype, void* mom, int mdtype, int64_t n, float beta1, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = stream_grid((n + 7) / 8, 256);
+#define PSAMD_MOM(G, E)                                                                                       \
+  hipLaunchKernelGGL((onebit_momentum_kernel<G, E>), dim3(grid), dim3(256), 0, s, static_cast<const G*>(g), \
+                     static_cast<E*>(mom), n, beta1)
+  if (gdtype == 1 && mdtype == 1) PSAMD_MOM(uint16_t, uint16_t);
+  else if (gdtype == 1) PSAMD_MOM(uint16_t, float);
+  else if (mdtype == 1) PSAMD_MOM(float, uint16_t);
+  else PSAMD_MOM(float, float);
+#undef PSAMD_MOM
 }
 
 void launch_onebit_unpack_reduce(const uint64_t* words, const float* scales, int nworkers, int64_t n,

@@ -13,13 +13,20 @@ def packed_sizes(n: int) -> tuple[int, int]:
     return (n + 63) // 64, (n + CHUNK - 1) // CHUNK
 
 
-def onebit_pack(g: torch.Tensor, err: torch.Tensor, words: torch.Tensor, scales: torch.Tensor) -> None:
-    """Compress ``g + err`` into sign bits ``words`` (int64) and per-chunk ``scales``; update ``err``."""
+def onebit_pack(g: torch.Tensor, err: torch.Tensor, words: torch.Tensor, scales: torch.Tensor,
+                mom: torch.Tensor = None, beta1: float = 0.0) -> None:
+    """Compress ``g + err`` into sign bits ``words`` (int64) and per-chunk ``scales``; update ``err``.
+    With ``mom`` (1-bit Adam): first ``mom = beta1 mom + (1 - beta1) g`` (stored in mom's dtype), then
+    compress ``mom + err`` -- the worker's momentum, not its gradient, crosses the wire."""
     n = g.numel()
     if use_native(g, err):
-        native().onebit_pack(g.contiguous(), err, words, scales)
+        native().onebit_pack(g.contiguous(), err, words, scales, mom, float(beta1))
         return
-    c = g.float().reshape(-1) + err.reshape(-1)
+    x = g.float().reshape(-1)
+    if mom is not None:
+        x = beta1 * mom.float().reshape(-1) + (1.0 - beta1) * x
+        mom.reshape(-1).copy_(x)
+    c = x + err.float().reshape(-1)
     nw, ns = packed_sizes(n)
     pad = ns * CHUNK - n
     cp = torch.nn.functional.pad(c, (0, pad))
@@ -38,6 +45,14 @@ def onebit_pack(g: torch.Tensor, err: torch.Tensor, words: torch.Tensor, scales:
     for b in range(64):
         w |= bits[:, b] << shifts[b]
     words[:nw].copy_(w)
+
+
+def onebit_momentum(g: torch.Tensor, mom: torch.Tensor, beta1: float) -> None:
+    """mom = beta1 mom + (1 - beta1) g: the 1-bit Adam worker momentum during full-precision rounds."""
+    if use_native(g, mom):
+        native().onebit_momentum(g.contiguous(), mom, float(beta1))
+        return
+    mom.copy_((beta1 * mom.float() + (1.0 - beta1) * g.float().reshape(mom.shape)).to(mom.dtype))
 
 
 def onebit_unpack_reduce(words: torch.Tensor, scales: torch.Tensor, out: torch.Tensor, mult: float = 1.0,

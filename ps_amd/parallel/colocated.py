@@ -68,7 +68,7 @@ class ColocatedPS:
                  average: bool = True, broadcast_init: bool = True, overlap: bool = True, timing: bool = False,
                  compress_warmup: int = 0, split_comm: Optional[bool] = None, plane: Optional[str] = None,
                  timeout_s: float = 600.0, reduce_fp32: Optional[bool] = None,
-                 ef_dtype: Optional[torch.dtype] = None):
+                 ef_dtype: Optional[torch.dtype] = None, onebit_momentum: Optional[float] = None):
         self.model = model
         self.t = transport or Transport()
         self.world, self.rank = self.t.world, self.t.rank
@@ -84,6 +84,21 @@ class ColocatedPS:
         # full-precision rounds before the 1-bit push takes over: the
         # error-feedback state starts from zero at the switch
         self.compress_warmup = int(compress_warmup)
+        # 1-bit Adam (updaters.OneBitAdamUpdater): every worker keeps its momentum
+        # m = beta1 m + (1 - beta1) g from round 0 and, after the warm-up, pushes the error-compensated
+        # 1-bit MOMENTUM; the owners' Adam runs with beta1 = 0 and a frozen variance from then on
+        self.onebit_momentum = None if onebit_momentum is None else float(onebit_momentum)
+        if self.onebit_momentum is not None:
+            from .updaters import OneBitAdamUpdater
+
+            if compress != "onebit":
+                raise ValueError("onebit_momentum needs compress='onebit'")
+            bad = [k for k, u in self.updaters.items()
+                   if not isinstance(u, OneBitAdamUpdater) or u.warmup != self.compress_warmup
+                   or u.beta1 != self.onebit_momentum]
+            if bad:
+                raise ValueError(f"onebit_momentum: every updater must be OneBitAdamUpdater(warmup=compress_warmup="
+                                 f"{self.compress_warmup}, beta1={self.onebit_momentum}); not {bad}")
         self.average = average
         self.overlap = overlap
         # collective plane: reduce-scatter bf16 buckets in fp32 when reduce_fp32 (the W-way sum is
@@ -186,6 +201,9 @@ class ColocatedPS:
         # the plane path packs on its own stream behind each bucket's landing event, so the
         # 1-bit pack + error feedback never sits in the backward's stream
         self.pack_stream = None
+        # worker momenta of 1-bit Adam, in the error-feedback dtype (the pack kernel reads both alike)
+        self.wmom = ([torch.zeros(b.size, dtype=self.ef_dtype, device=self.device) for b in R.buckets]
+                     if self.onebit_momentum is not None else None)
         if compress == "onebit" and self.plane is not None:
             self.err = [torch.zeros(b.size, dtype=self.ef_dtype, device=self.device) for b in R.buckets]
             if self.gpu:
@@ -347,10 +365,9 @@ class ColocatedPS:
             self.fault.before_push()
         if self.plane is not None:
             onebit = self.compress == "onebit" and self.round >= self.compress_warmup
-            if onebit:
+            if onebit or self.wmom is not None:
                 bk = self.reg.buckets[b]
                 gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
-                words, scales = self.plane.words(b, self.gslot)
                 if self.pack_stream is not None:  # behind the landing, off the backward's stream
                     ev = torch.cuda.Event()
                     ev.record(torch.cuda.current_stream(self.device))
@@ -358,7 +375,12 @@ class ColocatedPS:
                 with (torch.cuda.stream(self.pack_stream) if self.pack_stream is not None
                       else contextlib.nullcontext()):
                     self._mark("pack0")
-                    _cmp.onebit_pack(gin, self.err[b], words, scales)  # sign bits + scales + error feedback
+                    if onebit:  # sign bits + scales + error feedback (of the momentum, 1-bit Adam)
+                        words, scales = self.plane.words(b, self.gslot)
+                        _cmp.onebit_pack(gin, self.err[b], words, scales,
+                                         None if self.wmom is None else self.wmom[b], self.onebit_momentum or 0.0)
+                    else:  # 1-bit Adam warm-up: the momentum only, the push is the full gradient
+                        _cmp.onebit_momentum(gin, self.wmom[b], self.onebit_momentum)
                     self._mark("pack1")
                     with _trace.range(f"ps.push.b{b}"):  # the push's landing event: after the pack
                         self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
@@ -449,10 +471,17 @@ class ColocatedPS:
         bk = self.reg.buckets[b]
         gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
         if self.world == 1:
+            if self.wmom is not None:  # 1-bit Adam with nothing to push: the owner still gets the momentum
+                _cmp.onebit_momentum(gin, self.wmom[b], self.onebit_momentum)
+                if self.round >= self.compress_warmup:
+                    gin.copy_(self.wmom[b])
             return
         if self.compress == "onebit" and self.round >= self.compress_warmup:
             self._push_onebit(b, gin)
-        elif self.gshard[b].dtype != gin.dtype:  # fp32 reduction of a bf16 bucket
+            return
+        if self.wmom is not None:  # 1-bit Adam warm-up: keep the worker momentum, push the gradient
+            _cmp.onebit_momentum(gin, self.wmom[b], self.onebit_momentum)
+        if self.gshard[b].dtype != gin.dtype:  # fp32 reduction of a bf16 bucket
             self.t.reduce_scatter(self.gshard[b], gin.float())
         else:
             self.t.reduce_scatter(self.gshard[b], gin)
@@ -463,7 +492,8 @@ class ColocatedPS:
         bk = self.reg.buckets[b]
         words, rwords = self.cwords[b]
         scales, rscales = self.cscales[b]
-        _cmp.onebit_pack(gin, self.err[b], words, scales)
+        _cmp.onebit_pack(gin, self.err[b], words, scales, None if self.wmom is None else self.wmom[b],
+                         self.onebit_momentum or 0.0)
         self.t.all_to_all(rwords, words)
         self.t.all_to_all(rscales, scales)
         nw_chunk = bk.chunk // 64

@@ -201,6 +201,36 @@ class AdamUpdater(Updater):
         self.step_flat(master, states, g, step=t[key])
 
 
+class OneBitAdamUpdater(AdamUpdater):
+    """The owner side of 1-bit Adam (Tang et al. 2021): ``warmup`` full-precision rounds of plain
+    Adam, then the variance is FROZEN and the workers push their error-compensated 1-bit MOMENTUM
+    (ColocatedPS ``compress="onebit"`` + ``onebit_momentum``: ops/compress.onebit_pack with ``mom``).
+    On the owner that is Adam with beta1 = 0 (m := the decoded average of the workers' momenta),
+    beta2 = 1 (v unchanged) and the bias correction of the last warm-up step -- the same fused
+    kernel, only the per-round hyper-parameters change.  Compressing gradients into an owner Adam
+    with a live variance learns far more slowly at 8B depth (profiles/r6_llama8b_full_onebit_w2.txt);
+    freezing the variance with gradients compressed diverges."""
+
+    prefix = "onebitadam"
+
+    def __init__(self, alfa: float = 0.001, beta1: float = 0.9, beta2: float = 0.999, epsilon: float = 1e-8,
+                 bias_correction: str = "step", weight_decay: float = 0.0, adamw: bool = True, warmup: int = 100):
+        super().__init__(alfa, beta1, beta2, epsilon, bias_correction, weight_decay, adamw)
+        if warmup < 1:
+            raise ValueError("1-bit Adam needs >= 1 full-precision warm-up round to form the variance")
+        self.warmup = int(warmup)
+
+    def spec_items(self):
+        return super().spec_items() + [("warmup", float(self.warmup))]
+
+    def hyper(self, step):
+        if step <= self.warmup:
+            return super().hyper(step)
+        h = super().hyper(self.warmup)
+        h.update(beta1=0.0, beta2=1.0, bc1=1.0)
+        return h
+
+
 class AdagradUpdater(Updater):
     """h += g^2; w -= lr g / (sqrt(h) + eps) (north-star DLRM tables, K24)."""
 

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--ckpt", type=int, default=0, help="activation checkpointing per block")
     ap.add_argument("--ef", default="fp32", choices=["fp32", "bf16"], help="error-feedback buffer dtype")
     ap.add_argument("--warmup", type=int, default=0, help="full-precision rounds before the 1-bit push")
+    ap.add_argument("--adam1bit", type=int, default=0,
+                    help="1-bit Adam: push the worker momentum, owners freeze the variance after --warmup")
     a = ap.parse_args()
     import faulthandler
 
@@ -40,7 +42,7 @@ def main():
     from ps_amd.models.transformer import LlamaConfig, LlamaForCausalLM
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.transport import init_distributed
-    from ps_amd.parallel.updaters import AdamUpdater
+    from ps_amd.parallel.updaters import AdamUpdater, OneBitAdamUpdater
     import torch.distributed as dist
 
     torch.cuda.set_device(0)
@@ -58,10 +60,15 @@ def main():
     torch.cuda.synchronize()
     say(f"model built, {torch.cuda.memory_allocated(dev) / 2**30:.1f} GB")
     nparam = sum(p.numel() for p in model.parameters())
-    upd = AdamUpdater(a.lr, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
+    if a.adam1bit:
+        upd = OneBitAdamUpdater(a.lr, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True,
+                                warmup=a.warmup)
+    else:
+        upd = AdamUpdater(a.lr, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
     ps = ColocatedPS(model, upd, tp, bucket_mb=64.0, last_bucket_mb=2.0,
                      compress=None if a.compress == "none" else "onebit", plane="xgmi",
-                     ef_dtype=torch.bfloat16 if a.ef == "bf16" else torch.float32, compress_warmup=a.warmup)
+                     ef_dtype=torch.bfloat16 if a.ef == "bf16" else torch.float32, compress_warmup=a.warmup,
+                     onebit_momentum=0.9 if a.adam1bit else None)
     torch.cuda.synchronize()
     say(f"PS built ({len(ps.reg.buckets)} buckets, plane {ps.plane_kind}), {torch.cuda.memory_allocated(dev) / 2**30:.1f} GB")
     g = torch.Generator(device=dev).manual_seed(100 + tp.rank)
@@ -100,7 +107,7 @@ def main():
                "phase_ms_per_step": {k: round(v, 3) for k, v in tsum.items()},
                "pack_ms_per_bucket": round(tsum.get("pack_ms", 0.0) / packs, 4) if packs else None,
                "plane": {k: round(float(v), 3) for k, v in pst.items()},
-               "checkpointing": bool(a.ckpt), "ef_dtype": a.ef, "compress_warmup": a.warmup,
+               "checkpointing": bool(a.ckpt), "ef_dtype": a.ef, "compress_warmup": a.warmup, "adam1bit": bool(a.adam1bit),
                "peak_allocated_reserved_gb_per_rank": peaks,
                "device_free_total_gb": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info(dev)]}
         print(json.dumps(out), flush=True)

@@ -166,6 +166,29 @@ def test_onebit_bf16_error_feedback(gdt):
     torch.testing.assert_close(ge.cpu().float(), re.float(), rtol=1e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("n,mdt", [(3001, torch.float32), (5000, torch.bfloat16), (70000, torch.float32)])
+def test_onebit_momentum_pack(n, mdt):
+    """1-bit Adam's pack (colocated.py onebit_momentum): m = 0.9 m + 0.1 g stored back in m's dtype,
+    then c = m + e packed -- vs the CPU oracle of the same op; and the warm-up momentum-only kernel."""
+    torch.manual_seed(n)
+    g = torch.randn(n).bfloat16()
+    err = (torch.randn(n) * 0.1).to(mdt)
+    mom = torch.randn(n).to(mdt)
+    nw, ns = C.packed_sizes(n)
+    rw, rs, re, rm = torch.zeros(nw, dtype=torch.int64), torch.zeros(ns), err.clone(), mom.clone()
+    C.onebit_pack(g, re, rw, rs, rm, 0.9)
+    gw, gs, ge, gm = torch.zeros(nw, dtype=torch.int64, device=DEV), torch.zeros(ns, device=DEV), err.to(DEV), mom.to(DEV)
+    C.onebit_pack(g.to(DEV), ge, gw, gs, gm, 0.9)
+    tol = dict(rtol=1e-2, atol=1e-3) if mdt == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gm.cpu().float(), rm.float(), **tol)
+    assert (gw.cpu() != rw).sum() <= (0 if mdt == torch.float32 else nw // 50)  # bf16 m: rare sign ties differ
+    torch.testing.assert_close(gs.cpu(), rs, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(ge.cpu().float(), re.float(), **tol)
+    m2 = mom.to(DEV)
+    C.onebit_momentum(g.to(DEV), m2, 0.5)
+    torch.testing.assert_close(m2.cpu().float(), (0.5 * mom.float() + 0.5 * g.float()), **tol)
+
+
 def test_sparse_rows():
     torch.manual_seed(1)
     table = torch.randn(1000, 16)
