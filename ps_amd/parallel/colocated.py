@@ -96,9 +96,10 @@ class ColocatedPS:
             bad = [k for k, u in self.updaters.items()
                    if not isinstance(u, OneBitAdamUpdater) or u.warmup != self.compress_warmup
                    or u.beta1 != self.onebit_momentum]
-            if bad:
+            if bad or len({u.refresh for u in self.updaters.values()}) != 1:
                 raise ValueError(f"onebit_momentum: every updater must be OneBitAdamUpdater(warmup=compress_warmup="
-                                 f"{self.compress_warmup}, beta1={self.onebit_momentum}); not {bad}")
+                                 f"{self.compress_warmup}, beta1={self.onebit_momentum}), one refresh; not {bad}")
+            self._full_round = next(iter(self.updaters.values())).full_round
         self.average = average
         self.overlap = overlap
         # collective plane: reduce-scatter bf16 buckets in fp32 when reduce_fp32 (the W-way sum is
@@ -364,7 +365,7 @@ class ColocatedPS:
         if self.fault is not None:
             self.fault.before_push()
         if self.plane is not None:
-            onebit = self.compress == "onebit" and self.round >= self.compress_warmup
+            onebit = self._onebit_round()
             if onebit or self.wmom is not None:
                 bk = self.reg.buckets[b]
                 gin = self.gbuf[bk.group][self.gslot][bk.start:bk.start + bk.size]
@@ -473,10 +474,10 @@ class ColocatedPS:
         if self.world == 1:
             if self.wmom is not None:  # 1-bit Adam with nothing to push: the owner still gets the momentum
                 _cmp.onebit_momentum(gin, self.wmom[b], self.onebit_momentum)
-                if self.round >= self.compress_warmup:
+                if self._onebit_round(any_world=True):
                     gin.copy_(self.wmom[b])
             return
-        if self.compress == "onebit" and self.round >= self.compress_warmup:
+        if self._onebit_round():
             self._push_onebit(b, gin)
             return
         if self.wmom is not None:  # 1-bit Adam warm-up: keep the worker momentum, push the gradient
@@ -485,6 +486,14 @@ class ColocatedPS:
             self.t.reduce_scatter(self.gshard[b], gin.float())
         else:
             self.t.reduce_scatter(self.gshard[b], gin)
+
+    def _onebit_round(self, any_world: bool = False) -> bool:
+        """This round's push is 1-bit: past the warm-up, and (1-bit Adam) not a variance-refresh round."""
+        if self.compress != "onebit" and not (any_world and self.wmom is not None):
+            return False
+        if self.wmom is not None:
+            return not self._full_round(self.round + 1)
+        return self.round >= self.compress_warmup
 
     def _push_onebit(self, b: int, gin: torch.Tensor) -> None:
         """Compressed push: sign bits + chunk scales, all-to-all to the owners, owner decodes

@@ -203,31 +203,50 @@ class AdamUpdater(Updater):
 
 class OneBitAdamUpdater(AdamUpdater):
     """The owner side of 1-bit Adam (Tang et al. 2021): ``warmup`` full-precision rounds of plain
-    Adam, then the variance is FROZEN and the workers push their error-compensated 1-bit MOMENTUM
-    (ColocatedPS ``compress="onebit"`` + ``onebit_momentum``: ops/compress.onebit_pack with ``mom``).
-    On the owner that is Adam with beta1 = 0 (m := the decoded average of the workers' momenta),
-    beta2 = 1 (v unchanged) and the bias correction of the last warm-up step -- the same fused
-    kernel, only the per-round hyper-parameters change.  Compressing gradients into an owner Adam
-    with a live variance learns far more slowly at 8B depth (profiles/r6_llama8b_full_onebit_w2.txt);
-    freezing the variance with gradients compressed diverges."""
+    Adam, then the workers push their error-compensated 1-bit MOMENTUM (ColocatedPS
+    ``compress="onebit"`` + ``onebit_momentum``: ops/compress.onebit_pack with ``mom``) and the
+    variance is frozen.  On the owner that is Adam with beta1 = 0 (m := the decoded average of the
+    workers' momenta) and beta2 = 1 (v unchanged) -- the same fused kernel, only the per-round
+    hyper-parameters change.  ``refresh = k``: every k-th round after the warm-up is again a
+    full-precision round (the workers push their gradient) in which the owners' Adam continues
+    from the last decoded momentum and updates the variance -- a frozen variance from a short
+    warm-up goes stale and the run diverges (profiles/r6_llama8b_onebit_adam.txt).  Compressing
+    gradients into an owner Adam with a live variance instead learns far more slowly at 8B depth
+    (profiles/r6_llama8b_full_onebit_w2.txt)."""
 
     prefix = "onebitadam"
 
     def __init__(self, alfa: float = 0.001, beta1: float = 0.9, beta2: float = 0.999, epsilon: float = 1e-8,
-                 bias_correction: str = "step", weight_decay: float = 0.0, adamw: bool = True, warmup: int = 100):
+                 bias_correction: str = "step", weight_decay: float = 0.0, adamw: bool = True, warmup: int = 100,
+                 refresh: int = 0):
         super().__init__(alfa, beta1, beta2, epsilon, bias_correction, weight_decay, adamw)
         if warmup < 1:
             raise ValueError("1-bit Adam needs >= 1 full-precision warm-up round to form the variance")
-        self.warmup = int(warmup)
+        if refresh < 0:
+            raise ValueError("refresh >= 0")
+        self.warmup, self.refresh = int(warmup), int(refresh)
 
     def spec_items(self):
-        return super().spec_items() + [("warmup", float(self.warmup))]
+        return super().spec_items() + [("warmup", float(self.warmup)), ("refresh", float(self.refresh))]
+
+    def full_round(self, step: int) -> bool:
+        """Whether step (1-based; round r is step r + 1) pushes full-precision gradients."""
+        return step <= self.warmup or (self.refresh > 0 and (step - self.warmup) % self.refresh == 0)
+
+    def _n_full(self, step: int) -> int:
+        return step if step <= self.warmup else self.warmup + (
+            (step - self.warmup) // self.refresh if self.refresh else 0)
 
     def hyper(self, step):
         if step <= self.warmup:
             return super().hyper(step)
         h = super().hyper(self.warmup)
-        h.update(beta1=0.0, beta2=1.0, bc1=1.0)
+        nf = self._n_full(step)
+        if self.bias_correction == "step":
+            h["bc2"] = 1.0 / (1.0 - self.beta2 ** nf)  # v has seen nf updates
+        h["bc1"] = 1.0  # m continues from the workers' momenta, past its start-up bias
+        if not self.full_round(step):
+            h.update(beta1=0.0, beta2=1.0)
         return h
 
 

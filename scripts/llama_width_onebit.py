@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=0, help="full-precision rounds before the 1-bit push")
     ap.add_argument("--adam1bit", type=int, default=0,
                     help="1-bit Adam: push the worker momentum, owners freeze the variance after --warmup")
+    ap.add_argument("--refresh", type=int, default=0, help="1-bit Adam: every k-th round full precision (variance refresh)")
     a = ap.parse_args()
     import faulthandler
 
@@ -62,7 +63,7 @@ def main():
     nparam = sum(p.numel() for p in model.parameters())
     if a.adam1bit:
         upd = OneBitAdamUpdater(a.lr, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True,
-                                warmup=a.warmup)
+                                warmup=a.warmup, refresh=a.refresh)
     else:
         upd = AdamUpdater(a.lr, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
     ps = ColocatedPS(model, upd, tp, bucket_mb=64.0, last_bucket_mb=2.0,
@@ -107,7 +108,7 @@ def main():
                "phase_ms_per_step": {k: round(v, 3) for k, v in tsum.items()},
                "pack_ms_per_bucket": round(tsum.get("pack_ms", 0.0) / packs, 4) if packs else None,
                "plane": {k: round(float(v), 3) for k, v in pst.items()},
-               "checkpointing": bool(a.ckpt), "ef_dtype": a.ef, "compress_warmup": a.warmup, "adam1bit": bool(a.adam1bit),
+               "checkpointing": bool(a.ckpt), "ef_dtype": a.ef, "compress_warmup": a.warmup, "adam1bit": bool(a.adam1bit), "refresh": a.refresh,
                "peak_allocated_reserved_gb_per_rank": peaks,
                "device_free_total_gb": [round(v / 2**30, 1) for v in torch.cuda.mem_get_info(dev)]}
         print(json.dumps(out), flush=True)

@@ -22,14 +22,14 @@ def _data(n=64):
     return torch.randn(n, 12, generator=g), torch.randint(0, 4, (n,), generator=g)
 
 
-def _body(tp, plane, steps, warm):
+def _body(tp, plane, steps, warm, refresh=0):
     import torch.nn.functional as F
 
     from ps_amd.parallel.colocated import ColocatedPS
     from ps_amd.parallel.updaters import OneBitAdamUpdater
 
     m = _model(seed=tp.rank)  # rank 0's broadcast wins
-    u = OneBitAdamUpdater(LR, B1, B2, EPS, warmup=warm)
+    u = OneBitAdamUpdater(LR, B1, B2, EPS, warmup=warm, refresh=refresh)
     ps = ColocatedPS(m, u, tp, bucket_mb=0.01, last_bucket_mb=0.01, compress="onebit", compress_warmup=warm,
                      onebit_momentum=B1, plane=plane)
     assert len({b.group for b in ps.reg.buckets}) == 1 and all(b.start % 1024 == 0 for b in ps.reg.buckets)
@@ -46,7 +46,7 @@ def _body(tp, plane, steps, warm):
     return {n: p.detach().clone() for n, p in m.named_parameters()}, losses, ps.plane_kind, layout
 
 
-def _oracle(steps, warm, layout, world=2):
+def _oracle(steps, warm, layout, world=2, refresh=0):
     import torch.nn.functional as F
 
     offs, n = layout
@@ -69,11 +69,15 @@ def _oracle(steps, warm, layout, world=2):
         gs = [flat_grad(x[w::world], y[w::world]) for w in range(world)]
         for w in range(world):
             mw[w] = B1 * mw[w] + (1 - B1) * gs[w]
-        if t < warm:
+        step = t + 1
+        full = step <= warm or (refresh and (step - warm) % refresh == 0)
+        nfull = step if step <= warm else warm + ((step - warm) // refresh if refresh else 0)
+        if full:
             g = sum(gs) / world
             s0 = B1 * s0 + (1 - B1) * g
             s1 = B2 * s1 + (1 - B2) * g * g
-            bc1, bc2 = 1 / (1 - B1 ** (t + 1)), 1 / (1 - B2 ** (t + 1))
+            bc1 = 1 / (1 - B1 ** step) if step <= warm else 1.0
+            bc2 = 1 / (1 - B2 ** nfull)
             upd = (s0 * bc1) / ((s1 * bc2).sqrt() + EPS)
         else:
             dec = []
@@ -84,7 +88,7 @@ def _oracle(steps, warm, layout, world=2):
                 ew[w] = c - d
                 dec.append(d)
             s0 = sum(dec) / world  # beta1 = 0: m := the decoded average of the worker momenta
-            bc2 = 1 / (1 - B2 ** warm)  # variance frozen at the warm-up's last step
+            bc2 = 1 / (1 - B2 ** nfull)  # variance frozen since the last full-precision round
             upd = s0 / ((s1 * bc2).sqrt() + EPS)
         with torch.no_grad():
             for nm, p in named:
@@ -122,16 +126,21 @@ def test_updater_freezes_variance_after_warmup():
         assert u.hyper(s) == a.hyper(s)
     h = u.hyper(6)
     assert h["beta1"] == 0.0 and h["beta2"] == 1.0 and h["bc1"] == 1.0 and h["bc2"] == a.hyper(5)["bc2"]
+    r = OneBitAdamUpdater(1e-3, 0.9, 0.999, warmup=5, refresh=3)
+    assert [r.full_round(s) for s in range(1, 13)] == [True] * 5 + [False, False, True] * 2 + [False]
+    h8, h9 = r.hyper(8), r.hyper(9)  # step 8: a refresh round (live betas, v's 6th update)
+    assert h8["beta1"] == 0.9 and h8["beta2"] == 0.999 and h8["bc1"] == 1.0 and h8["bc2"] == a.hyper(6)["bc2"]
+    assert h9["beta1"] == 0.0 and h9["bc2"] == h8["bc2"]
     with pytest.raises(ValueError):
         OneBitAdamUpdater(warmup=0)
 
 
-@pytest.mark.parametrize("plane", ["collective", "xgmi"])
-def test_onebit_adam_world2_matches_oracle(plane):
-    steps, warm = 8, 3
-    res = dist_util.run(_body, 2, (plane, steps, warm))
+@pytest.mark.parametrize("plane,refresh", [("collective", 0), ("xgmi", 0), ("collective", 2), ("xgmi", 3)])
+def test_onebit_adam_world2_matches_oracle(plane, refresh):
+    steps, warm = 9, 3
+    res = dist_util.run(_body, 2, (plane, steps, warm, refresh))
     assert res[0][2] == plane
-    want = _oracle(steps, warm, res[0][3])
+    want = _oracle(steps, warm, res[0][3], refresh=refresh)
     for k in want:
         torch.testing.assert_close(res[0][0][k], res[1][0][k], rtol=0, atol=0)  # replicas identical
         torch.testing.assert_close(res[0][0][k], want[k], rtol=1e-4, atol=1e-5)
