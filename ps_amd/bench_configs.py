@@ -181,7 +181,7 @@ def setup_dlrm(args, tp, dev) -> Bench:
 def setup_llama_onebit(args, tp, dev) -> Bench:
     from .models.transformer import LlamaConfig, LlamaForCausalLM
     from .parallel.colocated import ColocatedPS
-    from .parallel.updaters import AdamUpdater
+    from .parallel.updaters import AdamUpdater, OneBitAdamUpdater
 
     cfg = LlamaConfig.tiny() if args.tiny else LlamaConfig.llama3_8b()
     torch.manual_seed(0)
@@ -191,13 +191,21 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
         # HBM -- recomputing the forward would cost ~25 % of the step
         model = LlamaForCausalLM(cfg, checkpointing=bool(int(os.environ.get("PS_AMD_LLAMA_CKPT", "0")))).to(
             torch.bfloat16)
-    upd = AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True)
+    # W > 1: 1-bit Adam -- the workers push their error-compensated 1-bit momentum, the owners
+    # freeze the variance after 10 full-precision rounds and refresh it every 4th round (at 8B depth
+    # this tracks the uncompressed run; compressed gradients into a live-variance Adam do not:
+    # profiles/r6_llama8b_onebit_adam.txt)
+    onebit = tp.world > 1
+    warm, refresh = 10, 4
+    upd = (OneBitAdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True,
+                             warmup=warm, refresh=refresh) if onebit
+           else AdamUpdater(3e-4, 0.9, 0.95, 1e-8, bias_correction="step", weight_decay=0.1, adamw=True))
     # every bucket's serve overlapped with backward (serving after backward instead was the A/B
     # that priced the serve's HBM traffic stretching backward: profiles/r4_llama_serve_overlap.txt)
     ps = ColocatedPS(model, upd, tp, bucket_mb=max(args.bucket_mb, 64.0), last_bucket_mb=args.last_bucket_mb,
-                     compress="onebit" if tp.world > 1 else None, plane=getattr(args, "plane", None),
-                     ef_dtype=torch.bfloat16,  # bf16 error feedback: 16 GB instead of 32 GB per rank at 8B
-                     overlap=True)
+                     compress="onebit" if onebit else None, plane=getattr(args, "plane", None),
+                     ef_dtype=torch.bfloat16,  # bf16 error feedback (and momentum): 16 GB each per rank at 8B
+                     overlap=True, compress_warmup=warm if onebit else 0, onebit_momentum=0.9 if onebit else None)
     B, S = args.batch_per_gpu, args.seq_len
     g = torch.Generator(device=dev).manual_seed(tp.rank)
     pool = [torch.randint(0, cfg.vocab, (B, S), device=dev, generator=g) for _ in range(POOL)]
@@ -213,7 +221,9 @@ def setup_llama_onebit(args, tp, dev) -> Bench:
     return Bench(step, B * S, "tokens/sec (whole node) Llama-3-8B bf16 1-bit compressed push", "tokens/s",
                  {"model": "Llama-3-8B" if not args.tiny else "Llama-tiny", "global_batch": B * tp.world,
                   "seq_len": S, "parallelism": f"ps-bsp-onebit-colocated-dp{tp.world}",
-                  "compression": "onebit+error-feedback" if tp.world > 1 else "none (1 worker: nothing to push)"},
+                  "compression": (f"1-bit Adam: 1-bit momentum + error feedback, {warm} full-precision warm-up rounds, "
+                                  f"variance refresh every {refresh}th round") if onebit
+                  else "none (1 worker: nothing to push)"},
                  ps)
 
 
