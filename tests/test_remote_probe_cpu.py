@@ -127,3 +127,39 @@ def test_row_plane_probe_failure_falls_back_to_collective_all_to_alls():
         _assert_same(res[r][:2], single)
     ok = dist_util.run(_rows_body, 2, (None,))
     assert all(ex == "plane" for ex, _, _ in ok[0][2].values())
+
+
+def _async_rows_body(tp, fail):
+    import os
+
+    if fail:
+        os.environ["PS_AMD_PROBE_FAIL"] = fail
+    from ps_amd.parallel.async_rows import AsyncRowTable
+    from ps_amd.parallel.updaters import AdagradUpdater
+
+    try:
+        t = AsyncRowTable("emb", 8, 1000, tp, AdagradUpdater(0.1, 1e-8), init=(-0.1, 0.1), staleness=1,
+                          capacity=256, timeout_s=60)
+    except RP.RemoteWriteUnavailable as e:
+        return "raised", str(e), None
+    ids = torch.arange(0, 40)
+    before = t.pull(ids)
+    t.push(ids, torch.ones(40, 8))
+    t.synchronize()
+    after = t.pull(ids)
+    info = dict(t.info)
+    t.close()
+    return "ok", info, bool((after < before).all())
+
+
+def test_async_rows_probe_passes_and_rows_train():
+    res = dist_util.run(_async_rows_body, 2, (None,))
+    for kind, info, dec in res:
+        assert kind == "ok" and info["remote_write_probe"].startswith("ok") and dec
+    # the probe's lines were zeroed: a push after it is applied as pushed (rows decrease, above)
+
+
+def test_async_rows_probe_failure_is_agreed_by_every_rank():
+    res = dist_util.run(_async_rows_body, 2, ("asyncrows@0",))
+    for kind, msg, _ in res:
+        assert kind == "raised" and "ranks [0]" in msg and "asyncrows" in msg

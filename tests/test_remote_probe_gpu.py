@@ -101,3 +101,43 @@ def test_row_plane_probe_two_processes(fail):
             assert ex == "plane" and info["remote_write_probe"].startswith("ok"), info
         else:
             assert ex == "collective" and "ranks [0]" in info["fallback"], info
+
+
+def _async_rows_body(tp, fail):
+    import os
+
+    if fail:
+        os.environ["PS_AMD_PROBE_FAIL"] = fail
+    from ps_amd.parallel import remote_probe as RP
+    from ps_amd.parallel.async_rows import AsyncRowTable
+    from ps_amd.parallel.updaters import AdagradUpdater
+
+    torch.cuda.set_device(0)
+    try:
+        t = AsyncRowTable("emb", 8, 1000, tp, AdagradUpdater(0.1, 1e-8), init=(-0.1, 0.1), staleness=1,
+                          capacity=256, device=DEV, timeout_s=60)
+    except RP.RemoteWriteUnavailable as e:
+        return "raised", str(e), None
+    ids = torch.arange(0, 40, device=DEV)
+    before = t.pull(ids)
+    t.push(ids, torch.ones(40, 8, device=DEV))
+    t.synchronize()
+    after = t.pull(ids)
+    torch.cuda.synchronize()
+    info = dict(t.info)
+    ok = bool((after < before).all())
+    t.close()
+    return "ok", info, ok
+
+
+@pytest.mark.parametrize("fail", [None, "asyncrows@1"])
+def test_async_rows_probe_two_processes(fail):
+    """The asynchronous row tables' mailbox writes (rows.to_peers into IPC-mapped owner mailboxes,
+    read back through an acquiring kernel): the probe passes and the rows train; an injected
+    failure on one rank raises on both."""
+    res = dist_util.run(_async_rows_body, 2, (fail,))
+    for kind, info, dec in res:
+        if fail:
+            assert kind == "raised" and "ranks [1]" in info
+        else:
+            assert kind == "ok" and info["remote_write_probe"].startswith("ok") and dec
