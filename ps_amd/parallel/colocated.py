@@ -239,6 +239,13 @@ class ColocatedPS:
         self.split_comm = bool(split_comm) and self.world > 1
         self.tpull = self.t.split() if self.split_comm else self.t
         self.comm_pull = torch.cuda.Stream(device=self.device) if (self.gpu and self.split_comm) else self.comm
+        # one worker: nothing crosses a wire, so each bucket's serve runs inline on the stream that
+        # landed it (compute, or the side stream for weight gradients).  A separate comm stream
+        # only adds cross-queue event waits at the step boundary: the last serve and the next
+        # forward each waited 0.1-0.6 ms for an event already signalled on another queue
+        # (ResNet-50 bs1024, profiles/r6_step_boundary_gap.txt)
+        self.inline_serve = (self.gpu and self.world == 1 and self.plane is None and clip_norm is None
+                             and os.environ.get("PS_AMD_INLINE_SERVE", "1") != "0")
         self.round_events: deque = deque()
         # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT (0 = unbounded): finish_step waits on the
         # host until the step max_inflight - 1 steps back is done.  The host issues a ResNet-50
@@ -340,11 +347,15 @@ class ColocatedPS:
             torch._foreach_copy_(dst, src)
         self._landing[b] = {}
 
-    def _launch(self, b: int) -> None:
+    def _launch(self, b: int, in_backward: bool = True) -> None:
         if self.launched[b]:
             return
         self.launched[b] = True
-        side = _side.active(self.device) if self.gpu else None
+        # after backward (finish_step) the compute stream has already joined the side stream
+        # (ops/side_stream.py end-of-backward callback): a bucket launched then lands on the compute
+        # stream directly -- routing it through the side stream cost two cross-queue event waits
+        # at the step boundary (0.56 + 0.12 ms per ResNet-50 step, profiles/r6_step_boundary_gap.txt)
+        side = _side.active(self.device) if (self.gpu and in_backward) else None
         if side is not None:
             # some of the bucket's gradients are weight gradients still in flight on the side
             # stream (ops/side_stream.py): land and push from that stream, after the compute
@@ -388,6 +399,10 @@ class ColocatedPS:
                 return
             with _trace.range(f"ps.push.b{b}"):
                 self.plane.push(b, self.round, self.gslot, (self.round + 1) % self.nslots, onebit)
+            return
+        if self.gpu and self.inline_serve:
+            with _trace.range(f"ps.serve_pull.b{b}"):
+                self._serve_pull(b)
             return
         if self.gpu:
             ev = torch.cuda.Event()
@@ -555,7 +570,7 @@ class ColocatedPS:
             self._mark("bwd_end")
         for b in range(len(self.reg.buckets)):
             if not self.launched[b]:
-                self._launch(b)
+                self._launch(b, in_backward=False)
         if self.plane is not None:
             self._finish_plane_round()
             return
@@ -570,11 +585,11 @@ class ColocatedPS:
             if self.comm_pull is not self.comm:
                 self.comm_pull.wait_stream(self.comm)  # the round ends when both streams are done
             ev = torch.cuda.Event()
-            ev.record(self.comm_pull)
+            ev.record(torch.cuda.current_stream(self.device) if self.inline_serve else self.comm_pull)
             self.round_events.append(ev)
         if self.timing:
             if self.gpu:
-                with torch.cuda.stream(self.comm_pull):
+                with torch.cuda.stream(torch.cuda.current_stream(self.device) if self.inline_serve else self.comm_pull):
                     self._mark("round_end")
             else:
                 self._mark("round_end")
