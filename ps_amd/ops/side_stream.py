@@ -39,6 +39,15 @@ import torch
 
 _STREAMS: Dict[int, torch.cuda.Stream] = {}
 _lock = threading.Lock()
+# storage of the gradients produced on a side stream during the current backward (cleared by the
+# end-of-backward join): the parameter server lands a bucket from the side stream only when one of
+# its gradients is among them -- a cross-queue hop costs ~0.1-0.6 ms at the step boundary
+_SIDE_PTRS: set = set()
+
+
+def produced_on_side(t: Optional[torch.Tensor]) -> bool:
+    """Whether ``t`` (a gradient) was written by a side-stream weight gradient of this backward."""
+    return t is not None and t.device.type == "cuda" and t.data_ptr() in _SIDE_PTRS
 
 
 def _ranks_per_device() -> int:
@@ -129,7 +138,12 @@ class Fork:
         if not self.queued:  # one end-of-backward join per Fork (no state across passes)
             self.queued = True
             main, side = self.main, self.side
-            torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+
+            def _join():
+                main.wait_stream(side)
+                _SIDE_PTRS.clear()
+
+            torch.autograd.Variable._execution_engine.queue_callback(_join)
 
     def run(self, fn: Callable, *inputs: torch.Tensor, like: Optional[torch.Tensor] = None):
         """``fn()`` on the side stream (inputs protected from reuse); with ``like`` the result is
@@ -144,4 +158,6 @@ class Fork:
             out = fn()
             if like is not None:
                 out = _match_layout(out, like)
+        if isinstance(out, torch.Tensor):
+            _SIDE_PTRS.add(out.data_ptr())
         return out

@@ -244,8 +244,7 @@ class ColocatedPS:
         # only adds cross-queue event waits at the step boundary: the last serve and the next
         # forward each waited 0.1-0.6 ms for an event already signalled on another queue
         # (ResNet-50 bs1024, profiles/r6_step_boundary_gap.txt)
-        self.inline_serve = (self.gpu and self.world == 1 and self.plane is None and clip_norm is None
-                             and os.environ.get("PS_AMD_INLINE_SERVE", "1") != "0")
+        self.inline_serve = self.gpu and self.world == 1 and self.plane is None and clip_norm is None
         self.round_events: deque = deque()
         # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT (0 = unbounded): finish_step waits on the
         # host until the step max_inflight - 1 steps back is done.  The host issues a ResNet-50
@@ -356,6 +355,8 @@ class ColocatedPS:
         # stream directly -- routing it through the side stream cost two cross-queue event waits
         # at the step boundary (0.56 + 0.12 ms per ResNet-50 step, profiles/r6_step_boundary_gap.txt)
         side = _side.active(self.device) if (self.gpu and in_backward) else None
+        if side is not None and not any(_side.produced_on_side(g) for g in self._landing[b].values()):
+            side = None  # every gradient of the bucket came from the compute stream
         if side is not None:
             # some of the bucket's gradients are weight gradients still in flight on the side
             # stream (ops/side_stream.py): land and push from that stream, after the compute
