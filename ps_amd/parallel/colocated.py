@@ -357,6 +357,12 @@ class ColocatedPS:
         side = _side.active(self.device) if (self.gpu and in_backward) else None
         if side is not None and not any(_side.produced_on_side(g) for g in self._landing[b].values()):
             side = None  # every gradient of the bucket came from the compute stream
+        if side is not None and all(self.launched) and os.environ.get("PS_AMD_LASTJOIN", "1") != "0":
+            # the step's last bucket: the compute stream has nothing left to overlap, so it joins the
+            # side stream (whose weight gradients are done by now) and serves the bucket itself --
+            # the side stream serving it left the next forward waiting ~0.1 ms on a cross-queue event
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            side = None
         if side is not None:
             # some of the bucket's gradients are weight gradients still in flight on the side
             # stream (ops/side_stream.py): land and push from that stream, after the compute

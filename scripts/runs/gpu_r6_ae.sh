@@ -7,9 +7,9 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -1 $O/pytest.log
 for i in 1 2; do
 for v in 0 1; do
-PS_AMD_INLINE_SERVE=$v timeout -k 10 300 python bench.py --steps 30 --warmup 10 > $O/b1024_i${v}_$i.json 2> $O/b1024_i${v}_$i.err || { tail -5 $O/b1024_i${v}_$i.err; exit 1; }
-python -c "import json;r=json.loads(open('$O/b1024_i${v}_$i.json').read().strip().splitlines()[-1]);print('bs1024 inline=$v', r['value'], r['ms_per_step'])"
-PS_AMD_INLINE_SERVE=$v timeout -k 10 300 python bench.py --steps 60 --warmup 15 --batch-per-gpu 256 > $O/b256_i${v}_$i.json 2> $O/b256_i${v}_$i.err || { tail -5 $O/b256_i${v}_$i.err; exit 1; }
-python -c "import json;r=json.loads(open('$O/b256_i${v}_$i.json').read().strip().splitlines()[-1]);print('bs256 inline=$v', r['value'], r['ms_per_step'])"
+PS_AMD_LASTJOIN=$v timeout -k 10 300 python bench.py --steps 30 --warmup 10 > $O/b1024_i${v}_$i.json 2> $O/b1024_i${v}_$i.err || { tail -5 $O/b1024_i${v}_$i.err; exit 1; }
+python -c "import json;r=json.loads(open('$O/b1024_i${v}_$i.json').read().strip().splitlines()[-1]);print('bs1024 lastjoin=$v', r['value'], r['ms_per_step'])"
+PS_AMD_LASTJOIN=$v timeout -k 10 300 python bench.py --steps 60 --warmup 15 --batch-per-gpu 256 > $O/b256_i${v}_$i.json 2> $O/b256_i${v}_$i.err || { tail -5 $O/b256_i${v}_$i.err; exit 1; }
+python -c "import json;r=json.loads(open('$O/b256_i${v}_$i.json').read().strip().splitlines()[-1]);print('bs256 lastjoin=$v', r['value'], r['ms_per_step'])"
 done
 done
