@@ -245,6 +245,12 @@ class ColocatedPS:
         # forward each waited 0.1-0.6 ms for an event already signalled on another queue
         # (ResNet-50 bs1024, profiles/r6_step_boundary_gap.txt)
         self.inline_serve = self.gpu and self.world == 1 and self.plane is None and clip_norm is None
+        # per parameter group, the bucket that holds its first layers (backward order: it fires last)
+        last = {}
+        for i, bk in enumerate(R.buckets):
+            if bk.group not in last or bk.start > R.buckets[last[bk.group]].start:
+                last[bk.group] = i
+        self._group_last = set(last.values())
         self.round_events: deque = deque()
         # host run-ahead bound (GPU), PS_AMD_MAX_INFLIGHT (0 = unbounded): finish_step waits on the
         # host until the step max_inflight - 1 steps back is done.  The host issues a ResNet-50
@@ -357,10 +363,11 @@ class ColocatedPS:
         side = _side.active(self.device) if (self.gpu and in_backward) else None
         if side is not None and not any(_side.produced_on_side(g) for g in self._landing[b].values()):
             side = None  # every gradient of the bucket came from the compute stream
-        if side is not None and all(self.launched) and os.environ.get("PS_AMD_LASTJOIN", "1") != "0":
-            # the step's last bucket: the compute stream has nothing left to overlap, so it joins the
-            # side stream (whose weight gradients are done by now) and serves the bucket itself --
-            # the side stream serving it left the next forward waiting ~0.1 ms on a cross-queue event
+        if side is not None and b in self._group_last:
+            # the last bucket of its group holds the first layers: its gradients complete the
+            # backward, so the compute stream has nothing left to overlap -- it joins the side stream
+            # (whose weight gradients are done by now) and serves the bucket itself; the side stream
+            # serving it left the next forward waiting ~0.1 ms on a cross-queue event
             torch.cuda.current_stream(self.device).wait_stream(side)
             side = None
         if side is not None:
