@@ -43,6 +43,12 @@ _lock = threading.Lock()
 # end-of-backward join): the parameter server lands a bucket from the side stream only when one of
 # its gradients is among them -- a cross-queue hop costs ~0.1-0.6 ms at the step boundary
 _SIDE_PTRS: set = set()
+# side-stream work enqueued / joined so far, per side stream: every Fork of a backward queues an
+# end-of-backward callback, but only the first one that finds unjoined work makes the compute stream
+# wait (16 fused blocks queued 16 waits -- 16 barrier packets, a 0.09 ms bubble before the next
+# forward: profiles/r6_step_boundary_gap.txt)
+_WORK: Dict[int, int] = {}
+_JOINED: Dict[int, int] = {}
 
 
 def produced_on_side(t: Optional[torch.Tensor]) -> bool:
@@ -140,7 +146,10 @@ class Fork:
             main, side = self.main, self.side
 
             def _join():
-                main.wait_stream(side)
+                k = id(side)
+                if _JOINED.get(k, 0) < _WORK.get(k, 0):
+                    main.wait_stream(side)
+                    _JOINED[k] = _WORK[k]
                 _SIDE_PTRS.clear()
 
             torch.autograd.Variable._execution_engine.queue_callback(_join)
@@ -160,4 +169,5 @@ class Fork:
                 out = _match_layout(out, like)
         if isinstance(out, torch.Tensor):
             _SIDE_PTRS.add(out.data_ptr())
+        _WORK[id(self.side)] = _WORK.get(id(self.side), 0) + 1
         return out
