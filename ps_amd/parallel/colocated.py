@@ -244,7 +244,10 @@ class ColocatedPS:
         # only adds cross-queue event waits at the step boundary: the last serve and the next
         # forward each waited 0.1-0.6 ms for an event already signalled on another queue
         # (ResNet-50 bs1024, profiles/r6_step_boundary_gap.txt)
-        self.inline_serve = self.gpu and self.world == 1 and self.plane is None and clip_norm is None
+        # Large models keep the comm stream: their serve (Llama-3-8B: ~50-130 ms of AdamW over 8B
+        # masters) is worth overlapping with backward (profiles/r4_llama_serve_overlap.txt).
+        self.inline_serve = (self.gpu and self.world == 1 and self.plane is None and clip_norm is None
+                             and sum(b.size for b in R.buckets) <= (1 << 28))
         # per parameter group, the bucket that holds its first layers (backward order: it fires last)
         last = {}
         for i, bk in enumerate(R.buckets):
