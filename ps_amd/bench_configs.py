@@ -171,7 +171,7 @@ def setup_dlrm(args, tp, dev) -> Bench:
     return Bench(step, B, "samples/sec (whole node) DLRM sparse push/pull + server row-wise Adagrad", "samples/s",
                  {"model": "DLRM-26x128", "global_batch": B * tp.world, "seq_len": None,
                   "table_rows": args.dlrm_rows, "parallelism": f"ps-bsp-sparse-sharded-dp{tp.world}",
-                  "sparse_push_overlap": overlap,
+                  "sparse_push_overlap": True,
                   # row exchange path at W > 1: "plane" (IPC arenas, parallel/row_plane.py) or
                   # "collective" (RCCL all-to-alls); "local" at W = 1
                   "sparse_exchange": tbl.exchange, **({"sparse_exchange_info": tbl.exchange_info}

@@ -42,3 +42,23 @@ def test_bench_json_contract_cpu(world, tmp_path):
         assert set(rec["config"]["ps_phase_ms_per_step"]) >= {"push_ms", "serve_ms", "pull_ms"}
         if rec["config"].get("data_plane") == "xgmi":  # mapping mode / self-test / round end reported
             assert {"mode", "self_test", "round_end"} <= set(rec["config"]["plane_info"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config,extra", [("dlrm", ["--dlrm-rows", "2000", "--batch-per-gpu", "32"]),
+                                          ("ctr-async", ["--batch-per-gpu", "32"]),
+                                          ("llama-onebit", ["--tiny", "1", "--batch-per-gpu", "2", "--seq-len", "32"])])
+def test_other_bench_configs_build_and_step_cpu(config, extra, tmp_path):
+    """Every non-default bench config builds and times a step on CPU (world 1): a config that no
+    longer constructs fails here, not on the GPU box."""
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--config", config, "--steps", "1",
+           "--warmup", "1"] + extra
+    out = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert KEYS <= set(rec) and rec["value"] > 0
