@@ -134,6 +134,13 @@ __device__ __forceinline__ void stage_window(const uint16_t* __restrict__ x, uin
     if (i < 7 * kPairs) store_pair(lds_in, ih0 + i / kPairs, i % kPairs, v[k]);
   }
 }
+
+// Forward output staging (OW <= 112): pixel p of output row oh goes to the ring slots that row
+// oh's MFMAs (input rows 2oh-3 .. 2oh+3) and its prefetch (2oh+4, 2oh+5) leave free -- slots
+// 2oh+6 .. 2oh+12, 16 pixels x 128 B each -- so the row leaves as whole 128-B pixel rows.
+__device__ __forceinline__ uint16_t* stage_at(uint16_t* lds_in, int oh, int p) {
+  return lds_in + ((2 * oh + 6 + (p >> 4)) & (kSlots - 1)) * kRS + (p & 15) * 64;
+}
 }  // namespace
 
 // grid = N * splits blocks of 256 threads; block b: image b / splits, output rows
@@ -145,7 +152,10 @@ __device__ __forceinline__ void stage_window(const uint16_t* __restrict__ x, uin
 // Wave w owns output channels [16w, 16w + 16) of every pixel tile of the row: its weight
 // fragments are 28 VGPRs (a 2 x 2 wave grid held 56) and the kernel fits 128 VGPRs, i.e. four
 // blocks per CU instead of two -- the row loop is latency-bound, so rows in flight per CU set
-// the rate (0.79 ms -> see profiles/r4_stem_fwd_occupancy_ab.txt at bs1024).
+// the rate (0.79 ms -> see profiles/r4_stem_fwd_occupancy_ab.txt at bs1024).  Each wave's
+// accumulators hold 32 B of every pixel (its 16 channels); for OW <= 112 they pass through free
+// LDS ring slots (stage_at) so every global store writes whole 128-B pixel rows instead of 32-B
+// quarters that four waves complete at different times.
 __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ wp,
                                                                uint16_t* __restrict__ z, int N, int H, int W, int OH,
@@ -171,6 +181,7 @@ __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* _
   if (oh0 < oh1) stage_window(x, lds_in, n, oh0, H, W, cin);  // block-uniform
   __syncthreads();
   const int mtiles = (OW + 15) / 16;  // <= 8
+  const bool staged = OW <= 112;      // block-uniform: 7 free ring slots hold the row
   for (int oh = oh0; oh < oh1; ++oh) {
     RowPrefetch<256> pf;
     const bool more = oh + 1 < oh1;
@@ -207,11 +218,29 @@ __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* _
             s2[r] += d * d;
           }
         }
-        *reinterpret_cast<uint2*>(zo + ow * 64 + c0) =
-            make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+        const uint2 v = make_uint2(h[0] | (uint32_t(h[1]) << 16), h[2] | (uint32_t(h[3]) << 16));
+        if (staged) {  // 8-B unit u = c0 / 4 of pixel ow, XOR-swizzled by the pixel's low 4 bits
+          *reinterpret_cast<uint2*>(stage_at(lds_in, oh, ow) + ((c0 >> 2) ^ (ow & 15)) * 4) = v;
+        } else {
+          *reinterpret_cast<uint2*>(zo + ow * 64 + c0) = v;
+        }
       }
     }
     lds_barrier();
+    if (staged) {
+      // whole 128-B pixel rows: thread -> 16-B chunk k of pixel p, consecutive lanes consecutive chunks
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = threadIdx.x + 256 * i, p = c >> 3, k = c & 7;
+        if (p < OW) {
+          const int s = p & 15;
+          uint4 v = *reinterpret_cast<const uint4*>(stage_at(lds_in, oh, p) + ((2 * k) ^ (s & 14)) * 4);
+          if (s & 1) v = make_uint4(v.z, v.w, v.x, v.y);
+          *reinterpret_cast<uint4*>(zo + p * 64 + 8 * k) = v;
+        }
+      }
+      lds_barrier();  // the staging slots are the next row's prefetch / staging targets
+    }
   }
   if (part) {  // fixed-order combine over the 16 pixel lanes (xor shuffles); waves own disjoint channels
 #pragma unroll
