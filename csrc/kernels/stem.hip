@@ -156,6 +156,9 @@ __device__ __forceinline__ uint16_t* stage_at(uint16_t* lds_in, int oh, int p) {
 // accumulators hold 32 B of every pixel (its 16 channels); for OW <= 112 they pass through free
 // LDS ring slots (stage_at) so every global store writes whole 128-B pixel rows instead of 32-B
 // quarters that four waves complete at different times.
+// MT > 0: OW == 16 MT exactly (ResNet's 112: MT = 7), the tile loop and its guards compile away --
+// the runtime-mtiles version spends SGPRs on per-tile exec masks (24 spilled to VGPR lanes).
+template <int MT>
 __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ wp,
                                                                uint16_t* __restrict__ z, int N, int H, int W, int OH,
@@ -180,8 +183,8 @@ __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* _
   for (int kh = 0; kh < 7; ++kh) bw[kh] = *reinterpret_cast<const bf16x8_t*>(wp + (16 * wave + fr) * kKp + kh * 32 + 8 * g);
   if (oh0 < oh1) stage_window(x, lds_in, n, oh0, H, W, cin);  // block-uniform
   __syncthreads();
-  const int mtiles = (OW + 15) / 16;  // <= 8
-  const bool staged = OW <= 112;      // block-uniform: 7 free ring slots hold the row
+  const int mtiles = MT > 0 ? MT : (OW + 15) / 16;  // <= 8
+  const bool staged = MT > 0 || OW <= 112;         // block-uniform: 7 free ring slots hold the row
   for (int oh = oh0; oh < oh1; ++oh) {
     RowPrefetch<256> pf;
     const bool more = oh + 1 < oh1;
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(256, 4) void stem_conv_fwd_kernel(const uint16_t* _
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int ow = 16 * t + fr;
-      if (t < mtiles && ow < OW) {
+      if (MT > 0 ? t < MT : (t < mtiles && ow < OW)) {
         // C layout: row (channel) = 16 wave + 4 g + r, col (pixel) = fr -> one 8-B store per tile
         uint16_t h[4];
 #pragma unroll
@@ -367,11 +370,16 @@ __device__ __forceinline__ void dz_row_to_lds(uint16_t* lds_dz, const ZPair& z, 
       for (int e = 0; e < 8; ++e) {
         const float zf = bf16_to_f32(z.v[k][d][e]);
         const float g = zf * sc[e] + sh[e] > 0.f ? bf16_to_f32(f32_to_bf16(acc[e])) : 0.f;
-        o[e] = px < OW ? f32_to_bf16(A[e] * g + B[e] * zf + Cc[e]) : static_cast<uint16_t>(0);
+        o[e] = f32_to_bf16(A[e] * g + B[e] * zf + Cc[e]);
       }
+      // pixels >= OW (finite: z read at pixel 0) are zeroed by one select per word AFTER the math:
+      // a per-element `px < OW ? ... : 0` compiled to 8 divergent branches per pixel
+      const uint32_t keep = px < OW ? ~0u : 0u;
       uint16_t* dst = lds_dz + px * kDzLd + ch * 8;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16));
-      *reinterpret_cast<uint2*>(dst + 4) = make_uint2(o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16));
+      *reinterpret_cast<uint2*>(dst) =
+          make_uint2((o[0] | (uint32_t(o[1]) << 16)) & keep, (o[2] | (uint32_t(o[3]) << 16)) & keep);
+      *reinterpret_cast<uint2*>(dst + 4) =
+          make_uint2((o[4] | (uint32_t(o[5]) << 16)) & keep, (o[6] | (uint32_t(o[7]) << 16)) & keep);
     }
 }
 
@@ -525,7 +533,11 @@ void launch_stem_conv_fwd(const uint16_t* x, int cin, const uint16_t* wp, uint16
                           int OW, const float* kshift, float* part, hipStream_t s) {
   if (N <= 0 || OH <= 0) return;
   const int rpb = (OH + kFwdSplits - 1) / kFwdSplits;
-  hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(N * kFwdSplits), dim3(256), 0, s, x, wp, z, N, H, W, OH, OW,
+  if (OW == 112)
+    hipLaunchKernelGGL(stem_conv_fwd_kernel<7>, dim3(N * kFwdSplits), dim3(256), 0, s, x, wp, z, N, H, W, OH, OW,
+                       kFwdSplits, rpb, cin, kshift, part);
+  else
+    hipLaunchKernelGGL(stem_conv_fwd_kernel<0>, dim3(N * kFwdSplits), dim3(256), 0, s, x, wp, z, N, H, W, OH, OW,
                      kFwdSplits, rpb, cin, kshift, part);
 }
 

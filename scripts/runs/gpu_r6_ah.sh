@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6: stem forward with LDS-staged whole-pixel-row stores -- numerics + in-step kernel time + bench
-O=gpurun_out/${OUT:-r6ah2}
+O=gpurun_out/${OUT:-r6ah3}
 mkdir -p $O
 export TMPDIR=/tmp PYTHONPATH=$PWD:$PYTHONPATH
 R=$PWD
