@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void maxpool_s2k3_bwd_quad_kernel(const uint16
 // unfused path stored it.  The grid stride is a multiple of C / 8 (launcher), so every thread
 // keeps one channel group and the partials stay in registers.
 template <bool APPLY>
-__global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const uint16_t* __restrict__ dy,
+__global__ __launch_bounds__(256, 3) void pool_bn_bwd_kernel(const uint16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           const uint16_t* __restrict__ z,
                                                           const float* __restrict__ mc,
@@ -331,7 +331,6 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const uint16_t* __rest
     load8(coef + 2 * C, c8 * 8, Cc);
   } else {
     load8(mean, c8 * 8, mu);
-    load8(invstd, c8 * 8, is);
   }
   float sd[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (uint32_t v = v0; v < total; v += stride) {
@@ -379,7 +378,7 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const uint16_t* __rest
             out[e] = A[e] * g + B[e] * zf + Cc[e];
           } else {
             sd[e] += g;
-            sx[e] += g * (zf - mu[e]) * is[e];
+            sx[e] += g * (zf - mu[e]);  // x invstd once per channel at the end
           }
         }
         if constexpr (APPLY)
@@ -403,6 +402,9 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const uint16_t* __rest
           sd[e] += lds_d[k * 8 + e];
           sx[e] += lds_x[k * 8 + e];
         }
+      load8(invstd, t * 8, is);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sx[e] *= is[e];
       float* od = pd + static_cast<int64_t>(blockIdx.x) * C + t * 8;
       float* ox = px + static_cast<int64_t>(blockIdx.x) * C + t * 8;
 #pragma unroll
