@@ -34,6 +34,37 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   typedef __bf16 b2v __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
 }
+// Per-element bit masks over 8 x bf16 (bit e of `bits` -> element e), branch-free: an
+// `if ((bits >> e) & 1) v[e] = ...` compiles to one exec-mask branch per element (saveexec /
+// restore + the arm), which made the data-gradient epilogues issue-bound.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// 16-bit lane mask of dword w (elements 2w, 2w + 1): one signed 1-bit extract per half + a bitfield insert
+__device__ __forceinline__ uint32_t bf16_pair_mask(unsigned bits, int w) {
+  const uint32_t lo = static_cast<uint32_t>(static_cast<int32_t>(bits << (31 - 2 * w)) >> 31);
+  const uint32_t hi = static_cast<uint32_t>(static_cast<int32_t>(bits << (30 - 2 * w)) >> 31);
+  return (lo & 0xffffu) | (hi & 0xffff0000u);
+}
+// v[e] + r[e] (one bf16 rounding of the fp32 sum) where bit e is set, v[e] elsewhere
+__device__ __forceinline__ u16x8 bf16_add_where(u16x8 v, u16x8 r, unsigned bits) {
+  const u32x4_t vw = __builtin_bit_cast(u32x4_t, v), rw = __builtin_bit_cast(u32x4_t, r);
+  u32x4_t o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float a0 = __uint_as_float(vw[w] << 16), a1 = __uint_as_float(vw[w] & 0xffff0000u);
+    const float b0 = __uint_as_float(rw[w] << 16), b1 = __uint_as_float(rw[w] & 0xffff0000u);
+    const uint32_t m = bf16_pair_mask(bits, w);
+    o[w] = (pk_bf16(a0 + b0, a1 + b1) & m) | (vw[w] & ~m);
+  }
+  return __builtin_bit_cast(u16x8, o);
+}
+// v[e] where bit e is set, 0 elsewhere
+__device__ __forceinline__ u16x8 bf16_keep_where(u16x8 v, unsigned bits) {
+  u32x4_t o = __builtin_bit_cast(u32x4_t, v);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) o[w] &= bf16_pair_mask(bits, w);
+  return __builtin_bit_cast(u16x8, o);
+}
+
 // 2^x as the bare v_exp_f32: for softmax arguments (<= 0) a denormal result is as good as 0, so
 // exp2f's denormal-range fix-up (compare, select, scale, ldexp per element) is waste there
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

@@ -499,9 +499,7 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
       const u16x4 hi = *reinterpret_cast<const u16x4*>(Cs + rr * kCS + cg * 8 + 4);
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if ((rb[i] >> e) & 1u) v[e] = f32_to_bf16(bf16_to_f32(v[e]) + bf16_to_f32(ra[i][e]));
+        v = bf16_add_where(v, ra[i], rb[i]);
       } else if constexpr (BASE == 2 || BASE == 4) {
         if (BASE == 2 || !((rodd >> i) & 1u)) {
 #pragma unroll
@@ -526,9 +524,9 @@ __global__ __launch_bounds__(512, 1) void conv_big_kernel(const ConvGemmArgs p) 
         }
       }
       if constexpr (FOLD) {  // previous block's bn3: ReLU mask from its output bits + reduce sums
+        v = bf16_keep_where(v, rp[i]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          if (!((rp[i] >> e) & 1u)) v[e] = 0;
           const float gv = bf16_to_f32(v[e]);
           s1[e] += gv;
           s2[e] += gv * ((bf16_to_f32(rz[i][e]) - e2[e]) * e3[e]);

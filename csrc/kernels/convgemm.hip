@@ -485,8 +485,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int
   // data-gradient epilogues ran at ~2.8 TB/s).  Rows past M read row M - 1 (in bounds, unused).
   constexpr int NPASS = BM / RPP;
   // destination row of output pixel m (a stride-2 data-gradient phase scatters to every other row)
+  // (only the phase launches -- epilogues 0 / 3, bindings conv_dgrad_s2 -- carry RH > 0: the
+  // other epilogues compile the scatter away)
   auto orow = [&](int m) -> int64_t {
-    if (g.RH == 0) return m;
+    if (!(EPI == 0 || EPI == 3) || g.RH == 0) return m;
     const int ohw = g.OH * g.OW, im = static_cast<int>(fdiv(static_cast<uint32_t>(m), p.fd_ohw)), r = m - im * ohw,
               i = static_cast<int>(fdiv(static_cast<uint32_t>(r), p.fd_ow)), j = r - i * g.OW;
     return (static_cast<int64_t>(im) * g.RH + 2 * i + g.ra) * g.RW + 2 * j + g.rb;
@@ -549,11 +551,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int
       u16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       const int64_t o = orow(m) * p.N + nc;
       if constexpr (BASE == 5) {  // identity-branch gradient = dout * relu'(block output), from bits
-        const u16x8 r8 = ra[i];
-        const unsigned bits = rb[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if ((bits >> j) & 1u) v[j] = f32_to_bf16(bf16_to_f32(v[j]) + bf16_to_f32(r8[j]));
+        v = bf16_add_where(v, ra[i], rb[i]);
       } else if constexpr (BASE == 2 || BASE == 4) {
         if (BASE == 2 || !((rodd >> i) & 1u)) {
           const u16x8 r8 = ra[i];
@@ -581,11 +579,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvGemmArgs& p, int GM, int
       }
       if constexpr (FOLD) {  // previous block's bn3: ReLU mask from its output bits + reduce sums
         const u16x8 z8 = rz[i];
-        const unsigned pb = rp[i];
+        v = bf16_keep_where(v, rp[i]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const bool on = (pb >> j) & 1u;
-          if (!on) v[j] = 0;
           const float gv = bf16_to_f32(v[j]);
           s1[j] += gv;
           s2[j] += gv * ((bf16_to_f32(z8[j]) - e2[j]) * e3[j]);
